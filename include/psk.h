@@ -1,0 +1,157 @@
+/*
+ * psk.h — C ABI of libpsk.so, the MI355X (gfx950) Krylov engine behind
+ * pysolvers_amd.Linear (a drop-in for krlong014/PySolvers' PySolvers/Linear).
+ *
+ * Plain C: pointers, sizes and PODs only; no torch/HIP types cross this line.
+ * Every entry point returns PSK_OK (0) or a negative PSK_ERR_* code; the text
+ * of the last error of the calling thread is available from psk_last_error().
+ * NUMERICAL failure (breakdown, maxiter, GMRES true-residual miss) is NOT an
+ * error: it is reported in psk_result.status exactly as the reference reports
+ * it through SolveStatus(success=False, ...) (IterativeSolver.py:101-129).
+ *
+ * Reference interfaces each group replaces (paths relative to the reference root):
+ *   psk_csr_*        scipy.sparse CSR handed to LinearSolver.solve(A, b)
+ *                    (LinearSolver.py:30-33) — uploaded once, kept in HBM.
+ *   psk_spmv         mvmult(A, x)                 IterativeLinearSolver.py:94-106
+ *   psk_dot/nrm2     np.dot / IterativeSolver.norm (npla.norm)  IterativeSolver.py:86-88
+ *   psk_axpy         x + alpha*p style updates    PCGSolver.py:121-122,138
+ *   psk_prec_*       PreconditionerType.form(A) -> applyRight(vec)
+ *                    PreconditionerType.py:4-19, Preconditioner.py:3-68;
+ *                    JACOBI = DInv*v with DInv = reciprocal(diag(A)) (ClassicSmoothers.py:8,14)
+ *   psk_pcg          PCGSolver.solve              PCGSolver.py:64-142
+ *   psk_gmres        GMRESSolver.solve            GMRESSolver.py:55-180 (restart==0)
+ *   psk_comm_*, psk_csr_create_fd2d_dist: row-block sharding across GPUs (RCCL over
+ *                    xGMI); no reference counterpart (the reference is single-process).
+ *   psk_csr_create_fd2d: examples/FDLaplacian2D.py:5-23 generated on the device,
+ *                    bit-identical arrays and entry order.
+ */
+#ifndef PSK_H
+#define PSK_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PSK_ABI_VERSION 1
+
+/* return codes */
+#define PSK_OK               0
+#define PSK_ERR_ARG         -1   /* bad argument (AssertionError in the reference, PCGSolver.py:79-83) */
+#define PSK_ERR_HIP         -2
+#define PSK_ERR_RCCL        -3
+#define PSK_ERR_ALLOC       -4
+#define PSK_ERR_UNSUPPORTED -5
+
+/* psk_result.status */
+#define PSK_CONVERGED        0   /* handleConvergence            IterativeSolver.py:101-107 */
+#define PSK_MAXITER          1   /* handleMaxiter                IterativeSolver.py:115-129 */
+#define PSK_BREAKDOWN        2   /* handleBreakdown              IterativeSolver.py:109-113 */
+#define PSK_TRUE_RESID_FAIL  3   /* GMRES true residual missed   GMRESSolver.py:167-174 */
+
+/* where the vector pointers of a call live */
+#define PSK_HOST   0
+#define PSK_DEVICE 1
+
+/* preconditioner kinds */
+#define PSK_PREC_IDENTITY 0      /* IdentityPreconditionerType   PreconditionerType.py:13-19 */
+#define PSK_PREC_JACOBI   1      /* DInv*v                        ClassicSmoothers.py:5-16 pattern */
+
+typedef struct psk_csr  psk_csr;    /* device CSR (int32 rowptr/colidx, f64 vals), library-owned */
+typedef struct psk_prec psk_prec;   /* formed preconditioner, library-owned */
+typedef struct psk_comm psk_comm;   /* RCCL communicator + rank geometry */
+
+/* CommonSolverArgs (IterativeSolver.py:42-57) minus the print/norm knobs. */
+typedef struct psk_ctl {
+    int64_t maxiter;          /* CommonSolverArgs.maxiter */
+    double  tau;              /* relative residual tolerance */
+    int32_t fail_on_maxiter;  /* CommonSolverArgs.failOnMaxiter */
+    int32_t restart;          /* GMRES only: 0 = reference non-restarted (Krylov dim = maxiter) */
+    int32_t check_every;      /* host polls the device status every N iterations; 0 = auto */
+    int32_t time_kernels;     /* 1 = HIP-event timing of the SpMV launches (psk_result.spmv_ms) */
+} psk_ctl;
+
+typedef struct psk_result {
+    int32_t status;           /* PSK_CONVERGED / MAXITER / BREAKDOWN / TRUE_RESID_FAIL */
+    int32_t success;          /* SolveStatus.success() */
+    int64_t iters;            /* SolveStatus.iters() (reference conventions, incl. k on maxiter) */
+    double  resid;            /* SolveStatus.resid(): PCG recursive ||r||; GMRES true ||b-Ax|| */
+    double  resid_recursive;  /* last recursive residual estimate */
+    double  norm_b;           /* ||b|| */
+    double  loop_ms;          /* device wall time of the solve (HIP events) */
+    double  spmv_ms;          /* mean SpMV launch duration when ctl.time_kernels */
+    int64_t spmv_launches;    /* number of SpMV launches (timed ones when ctl.time_kernels) */
+    int64_t hist_len;         /* valid entries written to hist */
+    char    msg[256];         /* SolveStatus.msg() */
+} psk_result;
+
+/* ---- library / device ---------------------------------------------------------------- */
+int         psk_abi_version(void);
+const char *psk_last_error(void);
+int         psk_device_count(int32_t *n);
+int         psk_set_device(int32_t dev);
+int         psk_synchronize(void);
+/* device memory helpers (so a host binding can keep vectors resident in HBM) */
+int psk_dmalloc(int64_t bytes, void **dptr);
+int psk_dfree(void *dptr);
+int psk_h2d(void *dst, const void *src, int64_t bytes);
+int psk_d2h(void *dst, const void *src, int64_t bytes);
+int psk_dmemset0(void *dst, int64_t bytes);
+
+/* ---- CSR matrices ---------------------------------------------------------------------- */
+/* Copy a CSR matrix (rowptr[n+1], colidx[nnz], vals[nnz]; stored entry order is kept,
+ * sorted or not) into HBM. loc says where the three arrays live. */
+int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
+                   const double *vals, int32_t loc, psk_csr **out);
+/* FDLaplacian2D(a, b, m) generated on the device (examples/FDLaplacian2D.py:5-23). */
+int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out);
+int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
+/* Copy the arrays back to host buffers (any pointer may be NULL). */
+int psk_csr_download(const psk_csr *A, int32_t *rowptr, int32_t *colidx, double *vals);
+int psk_csr_destroy(psk_csr *A);
+
+/* ---- kernels on the hot path ------------------------------------------------------------ */
+/* y = A x, per-row stored-order sum from 0.0, product rounded before the add:
+ * bit-identical to scipy csr_matvec. For a distributed matrix x is the local
+ * [owned | halo] vector and the halo is refreshed first (collective). */
+int psk_spmv(const psk_csr *A, const double *x, double *y, int32_t loc);
+int psk_dot(int64_t n, const double *x, const double *y, int32_t loc, double *out);
+int psk_nrm2(int64_t n, const double *x, int32_t loc, double *out);
+/* y = y + alpha*x (two roundings, as numpy's y + alpha*x) */
+int psk_axpy(int64_t n, double alpha, const double *x, double *y, int32_t loc);
+
+/* ---- preconditioners (PreconditionerType.form / applyRight) ---------------------------- */
+int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out);
+int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *out, int32_t loc);
+int psk_prec_destroy(psk_prec *M);
+
+/* ---- solvers ------------------------------------------------------------------------------ */
+/* M == NULL means identity. b, x: length n (local length for a distributed A). hist: nullable
+ * HOST array of ctl->maxiter doubles receiving the per-iteration residual norms reportIter
+ * sees (PCG ||r_k||, GMRES |g[k+1]|); entries past res->iters+1 are left untouched.
+ * x is overwritten with the solution (SolveStatus.soln()). */
+int psk_pcg(const psk_csr *A, const psk_prec *M, const double *b, double *x, const psk_ctl *ctl,
+            psk_result *res, double *hist, int32_t loc);
+int psk_gmres(const psk_csr *A, const psk_prec *M, const double *b, double *x, const psk_ctl *ctl,
+              psk_result *res, double *hist, int32_t loc);
+
+/* ---- multi-GPU (one process per GPU, RCCL over xGMI) ------------------------------------- */
+#define PSK_UNIQUE_ID_BYTES 128
+int psk_comm_unique_id(uint8_t *id /* PSK_UNIQUE_ID_BYTES */);
+int psk_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, psk_comm **out);
+int psk_comm_destroy(psk_comm *c);
+/* Rank `rank`'s row block of FDLaplacian2D(a,b,m): rows [row_begin,row_end) split on
+ * whole grid lines; local columns are [owned | halo_lo | halo_hi]. */
+int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *c, psk_csr **out,
+                             int64_t *row_begin, int64_t *row_end);
+/* Row block [row_begin,row_end) of a global CSR given with GLOBAL column indices
+ * (host arrays of the local rows only: rowptr[nloc+1] starting anywhere, colidx, vals). */
+int psk_csr_create_dist(int64_t n_global, int64_t row_begin, int64_t row_end,
+                        const int64_t *rowptr, const int32_t *colidx, const double *vals,
+                        psk_comm *c, psk_csr **out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PSK_H */

@@ -1,0 +1,66 @@
+"""ORACLE — test infrastructure only (see oracle/__init__.py).
+
+Vectorised restatement of the reference's problem generators.
+
+``fd_laplacian_2d`` reproduces ``examples/FDLaplacian2D.py:5-23`` bit for bit,
+including the CSR entry order that ``dok_matrix.tocsr()`` leaves behind.  The
+reference inserts, for grid point k = m*iy + ix, the keys (k,k), (k,k-m),
+(k,k+m), (k,k-1), (k,k+1) in that order (FDLaplacian2D.py:13-21); the DOK ->
+COO -> CSR conversion is stable per row, so every CSR row is stored as
+[diag, -m, +m, -1, +1] with boundary neighbours omitted (indices NOT sorted).
+Values are ``-4.0/h/h`` and ``1.0/h/h`` with ``h = abs(b-a)/double(m+1)``
+(FDLaplacian2D.py:6,13,15).
+"""
+import numpy as np
+import scipy.sparse as sp
+
+
+def fd_laplacian_2d_arrays(a, b, m):
+    """Return (indptr int32, indices int32, data float64) of FDLaplacian2D(a,b,m)."""
+    m = int(m)
+    n = m * m
+    h = np.abs(b - a) / np.double(m + 1)          # FDLaplacian2D.py:6
+    diag = -4.0 / h / h                           # :13
+    off = 1.0 / h / h                             # :15-21
+    k = np.arange(n, dtype=np.int64)
+    ix = k % m
+    iy = k // m
+    # slot order per row: diag, -m, +m, -1, +1  (insertion order, :13-21)
+    cols = np.stack([k, k - m, k + m, k - 1, k + 1], axis=1)
+    present = np.stack([np.ones(n, bool), iy > 0, iy < m - 1, ix > 0, ix < m - 1], axis=1)
+    vals = np.empty((n, 5), dtype=np.float64)
+    vals[:, 0] = diag
+    vals[:, 1:] = off
+    counts = present.sum(axis=1)
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    indices = cols[present].astype(np.int32)
+    data = vals[present]
+    return indptr.astype(np.int32), indices, data
+
+
+def fd_laplacian_2d(a, b, m):
+    """scipy CSR identical (arrays and entry order) to examples/FDLaplacian2D.py."""
+    indptr, indices, data = fd_laplacian_2d_arrays(a, b, m)
+    n = int(m) * int(m)
+    A = sp.csr_matrix((data, indices, indptr), shape=(n, n))
+    A.has_sorted_indices = False
+    return A
+
+
+def fd_rowptr_closed_form(m, k):
+    """Closed-form rowptr[k] of the m x m 5-point stencil (used by the device generator).
+
+    rowptr[k] = 5k - #(iy==0) - #(iy==m-1) - #(ix==0) - #(ix==m-1) over rows < k.
+    """
+    k = np.asarray(k, dtype=np.int64)
+    return (5 * k - np.minimum(k, m) - np.maximum(0, k - m * (m - 1))
+            - (k + m - 1) // m - k // m)
+
+
+def manufactured_rhs(A, seed=12345):
+    """x_exact = default_rng(seed).random(n), b = A @ x_exact (DHTestProblem.py:53-57, seeded)."""
+    n = A.shape[0]
+    x = np.random.default_rng(seed).random(n)
+    b = A @ x
+    return b, x

@@ -1,0 +1,15 @@
+"""pysolvers_amd — MI355X-native Krylov engine behind the PySolvers.Linear solver API.
+
+Importing this package loads libpsk.so (hand-written gfx950 HIP kernels);
+there is no CPU fallback.
+"""
+from . import Linear
+from .IterativeSolver import CommonSolverArgs, IterativeSolver, NamedObject, SolveStatus
+from .Linear import (GMRES, PCG, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
+                     IdentityPreconditionerType, IterativeLinearSolver, Jacobi, JacobiPreconditioner,
+                     JacobiPreconditionerType, PCGSolver, mvmult)
+
+__all__ = ["Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
+           "GMRESSolver", "PCGSolver", "DeviceCSR", "DeviceVector", "IdentityPreconditioner",
+           "IdentityPreconditionerType", "IterativeLinearSolver", "Jacobi", "JacobiPreconditioner",
+           "JacobiPreconditionerType", "mvmult"]

@@ -1,0 +1,121 @@
+"""ctypes binding of libpsk.so (include/psk.h), the gfx950 Krylov engine.
+
+There is no CPU fallback: if the library is missing or cannot be loaded this
+module raises ImportError, and every solve goes through the HIP kernels.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"))
+
+PSK_OK = 0
+PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
+PSK_HOST, PSK_DEVICE = 0, 1
+PSK_PREC_IDENTITY, PSK_PREC_JACOBI = 0, 1
+PSK_UNIQUE_ID_BYTES = 128
+
+STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOWN: "breakdown",
+                PSK_TRUE_RESID_FAIL: "true residual above tolerance"}
+
+
+class PskCtl(ctypes.Structure):
+    _fields_ = [("maxiter", ctypes.c_int64), ("tau", ctypes.c_double),
+                ("fail_on_maxiter", ctypes.c_int32), ("restart", ctypes.c_int32),
+                ("check_every", ctypes.c_int32), ("time_kernels", ctypes.c_int32)]
+
+
+class PskResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int32), ("success", ctypes.c_int32), ("iters", ctypes.c_int64),
+                ("resid", ctypes.c_double), ("resid_recursive", ctypes.c_double),
+                ("norm_b", ctypes.c_double), ("loop_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double),
+                ("spmv_launches", ctypes.c_int64), ("hist_len", ctypes.c_int64), ("msg", ctypes.c_char * 256)]
+
+
+# name -> (restype, argtypes); this is the full list of symbols include/psk.h declares
+P = ctypes.c_void_p
+I32, I64, F64 = ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+PP = ctypes.POINTER(ctypes.c_void_p)
+SIGNATURES = {
+    "psk_abi_version": (ctypes.c_int, []),
+    "psk_last_error": (ctypes.c_char_p, []),
+    "psk_device_count": (ctypes.c_int, [ctypes.POINTER(I32)]),
+    "psk_set_device": (ctypes.c_int, [I32]),
+    "psk_synchronize": (ctypes.c_int, []),
+    "psk_dmalloc": (ctypes.c_int, [I64, PP]),
+    "psk_dfree": (ctypes.c_int, [P]),
+    "psk_h2d": (ctypes.c_int, [P, P, I64]),
+    "psk_d2h": (ctypes.c_int, [P, P, I64]),
+    "psk_dmemset0": (ctypes.c_int, [P, I64]),
+    "psk_csr_create": (ctypes.c_int, [I64, I64, P, P, P, I32, PP]),
+    "psk_csr_create_fd2d": (ctypes.c_int, [F64, F64, I64, PP]),
+    "psk_csr_info": (ctypes.c_int, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
+    "psk_csr_download": (ctypes.c_int, [P, P, P, P]),
+    "psk_csr_destroy": (ctypes.c_int, [P]),
+    "psk_spmv": (ctypes.c_int, [P, P, P, I32]),
+    "psk_dot": (ctypes.c_int, [I64, P, P, I32, ctypes.POINTER(F64)]),
+    "psk_nrm2": (ctypes.c_int, [I64, P, I32, ctypes.POINTER(F64)]),
+    "psk_axpy": (ctypes.c_int, [I64, F64, P, P, I32]),
+    "psk_prec_create": (ctypes.c_int, [P, I32, PP]),
+    "psk_prec_apply": (ctypes.c_int, [P, I64, P, P, I32]),
+    "psk_prec_destroy": (ctypes.c_int, [P]),
+    "psk_pcg": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
+    "psk_gmres": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
+    "psk_comm_unique_id": (ctypes.c_int, [P]),
+    "psk_comm_init": (ctypes.c_int, [I32, I32, P, PP]),
+    "psk_comm_destroy": (ctypes.c_int, [P]),
+    "psk_csr_create_fd2d_dist": (ctypes.c_int, [F64, F64, I64, P, PP, ctypes.POINTER(I64),
+                                                ctypes.POINTER(I64)]),
+    "psk_csr_create_dist": (ctypes.c_int, [I64, I64, I64, P, P, P, P, PP]),
+}
+
+
+class PskError(RuntimeError):
+    """A negative return code from libpsk (API/HIP/RCCL error, not a numerical failure)."""
+
+    def __init__(self, code, where, text):
+        super().__init__("%s failed (%d): %s" % (where, code, text))
+        self.code = code
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libpsk.so not found at %s — build it with `python -c 'import __graft_entry__ as "
+                          "g; g.build()'` (make -C pysolvers_amd/csrc)" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.psk_abi_version() != 1:
+        raise ImportError("libpsk ABI version mismatch")
+    return lib
+
+
+lib = _load()
+
+
+def check(rc, where):
+    if rc != PSK_OK:
+        raise PskError(rc, where, lib.psk_last_error().decode(errors="replace"))
+
+
+def ptr(a):
+    """Data pointer of a numpy array, a torch tensor or a raw int address."""
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return ctypes.c_void_p(a)
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data_as(ctypes.c_void_p)
+    if hasattr(a, "data_ptr"):
+        return ctypes.c_void_p(a.data_ptr())
+    raise TypeError("cannot take the address of %r" % type(a))
+
+
+def device_count():
+    n = I32(0)
+    check(lib.psk_device_count(ctypes.byref(n)), "psk_device_count")
+    return n.value

@@ -1,0 +1,395 @@
+// pcg.hip — device-resident preconditioned CG (PCGSolver.solve, PCGSolver.py:64-142).
+//
+// Per iteration k three launches, no host synchronisation:
+//   K1  Ap = A p  and per-workgroup partials of p.Ap              (spmv.hip, kSpmvDot)   :111,:113
+//   K2  alpha = uDotR/pTAp; x += alpha p; r -= alpha Ap; u = M^-1 r; partials of r.r and u.r
+//                                                                    :114-125,:134
+//   K3  ||r|| test (tau*||b||, or k==maxiter-1 when !failOnMaxiter); beta; p = u + beta p
+//                                                                    :125-138
+// Every consumer workgroup re-reduces the producer's <=2048 partials in the same fixed order, so
+// all workgroups (and all ranks) see bit-identical scalars and take identical branches; the
+// control state (done flag, iteration count, residual) lives in HBM and the host only polls it
+// every `check_every` iterations with a lag, keeping the launch queue full.
+// u is never stored: K2 and K3 both recompute u_i = DInv_i * r_i (one rounding, as np.multiply).
+// Elementwise updates use two roundings (-ffp-contract=off), exactly as numpy's x + alpha*p.
+#include "psk_internal.hpp"
+
+#include <cmath>
+#include <cstdio>
+
+namespace psk {
+
+struct PcgState {
+    int32_t done;      // 0 running, 1 converged, 2 breakdown
+    int32_t brk_kind;  // 1: dot(u,r)==0 at start, 2: dot(p,Ap)==0
+    int64_t iters;
+    double resid;
+    double normB;
+    double tauNormB;
+    double pad[3];
+};
+
+// ---- K0: r = b; p = M r; x = 0; partials [b.b, u.r] ----------------------------------------
+__global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const double *__restrict__ b,
+                                                          const double *__restrict__ dinv,
+                                                          double *__restrict__ x, double *__restrict__ r,
+                                                          double *__restrict__ p, double *__restrict__ part) {
+    __shared__ double sh[kWaves];
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    double bb = 0.0, ur = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
+        const double bi = b[i];
+        const double ui = dinv ? dinv[i] * bi : bi;   // p = precond.applyRight(r)  :98
+        r[i] = bi;                                     // r = np.copy(b)             :97
+        p[i] = ui;
+        x[i] = 0.0;                                    // x = np.zeros_like(b)       :100
+        bb = fma(bi, bi, bb);
+        ur = fma(ui, bi, ur);                          // uDotR = np.dot(u, r)       :102
+    }
+    const double s0 = block_sum(bb, sh);
+    const double s1 = block_sum(ur, sh);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s0;
+        part[2 * blockIdx.x + 1] = s1;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *part, int np, double tau,
+                                                                 PcgState *st, double *udr) {
+    __shared__ double sh[kWaves];
+    const double bb = reduce_partials(part, np, 2, sh);
+    const double ur = reduce_partials(part + 1, np, 2, sh);
+    if (threadIdx.x == 0) {
+        const double normB = sqrt(bb);                 // self.norm(b)   :86
+        st->normB = normB;
+        st->tauNormB = tau * normB;
+        st->iters = 0;
+        st->resid = 0.0;
+        st->brk_kind = 0;
+        udr[0] = ur;
+        if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
+            st->done = 1;
+            st->iters = 1;
+        } else if (ur == 0.0) {                        // :104-105
+            st->done = 2;
+            st->brk_kind = 1;
+            st->iters = 0;
+        } else {
+            st->done = 0;
+        }
+    }
+}
+
+// ---- K2: x, r update + partials [r.r, u.r] -------------------------------------------------
+__global__ __launch_bounds__(kBlock) void pcg_update_kernel(
+    int64_t n, double *__restrict__ x, double *__restrict__ r, const double *__restrict__ p,
+    const double *__restrict__ Ap, const double *__restrict__ dinv, const double *__restrict__ part1,
+    int np, double *__restrict__ part2, PcgState *st, const double *__restrict__ udr, int64_t k) {
+    if (st->done) return;
+    __shared__ double sh[kWaves];
+    const double pTAp = reduce_partials(part1, np, 1, sh);   // np.dot(p, Ap)  :113
+    if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->brk_kind = 2;
+            st->iters = k;
+            st->done = 2;
+        }
+        return;
+    }
+    const double alpha = udr[k] / pTAp;                      // :118
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    double rr = 0.0, ur = 0.0;
+    int64_t i = i0 + 2 * threadIdx.x;
+    for (; i + 1 < i1; i += kVecTile) {                      // 16 B per lane per array
+        const double2 xv = *reinterpret_cast<const double2 *>(x + i);
+        const double2 pv = *reinterpret_cast<const double2 *>(p + i);
+        const double2 rv = *reinterpret_cast<const double2 *>(r + i);
+        const double2 av = *reinterpret_cast<const double2 *>(Ap + i);
+        double2 xn, rn;
+        xn.x = xv.x + alpha * pv.x;                          // x = x + alpha*p   :121
+        xn.y = xv.y + alpha * pv.y;
+        rn.x = rv.x - alpha * av.x;                          // r = r - alpha*Ap  :122
+        rn.y = rv.y - alpha * av.y;
+        double u0 = rn.x, u1 = rn.y;
+        if (dinv) {
+            const double2 dv = *reinterpret_cast<const double2 *>(dinv + i);
+            u0 = dv.x * rn.x;                                // u = precond.applyRight(r)  :123
+            u1 = dv.y * rn.y;
+        }
+        *reinterpret_cast<double2 *>(x + i) = xn;
+        *reinterpret_cast<double2 *>(r + i) = rn;
+        rr = fma(rn.x, rn.x, rr);
+        rr = fma(rn.y, rn.y, rr);
+        ur = fma(u0, rn.x, ur);
+        ur = fma(u1, rn.y, ur);
+    }
+    if (i < i1) {   // odd tail element
+        const double xn = x[i] + alpha * p[i];
+        const double rn = r[i] - alpha * Ap[i];
+        const double u0 = dinv ? dinv[i] * rn : rn;
+        x[i] = xn;
+        r[i] = rn;
+        rr = fma(rn, rn, rr);
+        ur = fma(u0, rn, ur);
+    }
+    const double s0 = block_sum(rr, sh);
+    const double s1 = block_sum(ur, sh);
+    if (threadIdx.x == 0) {
+        part2[2 * blockIdx.x] = s0;
+        part2[2 * blockIdx.x + 1] = s1;
+    }
+}
+
+// ---- K3: convergence test, beta, p = u + beta p ------------------------------------------------
+__global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
+    int64_t n, const double *__restrict__ r, double *__restrict__ p, const double *__restrict__ dinv,
+    const double *__restrict__ part2, int np, PcgState *st, double *__restrict__ udr,
+    double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
+    if (st->done) return;
+    __shared__ double sh[kWaves];
+    const double rr = reduce_partials(part2, np, 2, sh);
+    const double ur = reduce_partials(part2 + 1, np, 2, sh);
+    const double normR = sqrt(rr);                           // self.norm(r)  :125
+    if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
+    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->iters = k + 1;                               // handleConvergence(k, ...)
+            st->resid = normR;
+            st->done = 1;
+        }
+        return;
+    }
+    const double beta = ur / udr[k];                         // :134-135
+    if (blockIdx.x == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    int64_t i = i0 + 2 * threadIdx.x;
+    for (; i + 1 < i1; i += kVecTile) {
+        const double2 rv = *reinterpret_cast<const double2 *>(r + i);
+        const double2 pv = *reinterpret_cast<const double2 *>(p + i);
+        double u0 = rv.x, u1 = rv.y;
+        if (dinv) {
+            const double2 dv = *reinterpret_cast<const double2 *>(dinv + i);
+            u0 = dv.x * rv.x;
+            u1 = dv.y * rv.y;
+        }
+        double2 pn;
+        pn.x = u0 + beta * pv.x;                             // p = u + beta*p  :138
+        pn.y = u1 + beta * pv.y;
+        *reinterpret_cast<double2 *>(p + i) = pn;
+    }
+    if (i < i1) {
+        const double u0 = dinv ? dinv[i] * r[i] : r[i];
+        p[i] = u0 + beta * p[i];
+    }
+}
+
+// -------------------------------------------------------------------------------------------------
+// host driver
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+struct PcgWork {
+    double *x, *r, *p, *Ap, *part1, *part2, *udr, *hist;
+    PcgState *st;
+};
+
+static int pcg_workspace(psk_csr *A, int64_t maxiter, PcgWork &w) {
+    const size_t vec = align_up((size_t)A->n * 8, 256), vecc = align_up((size_t)A->ncols * 8, 256);
+    const size_t big = 3 * vec + vecc;
+    PSK_TRY(A->ws.ensure(big > 0 ? big : 256));
+    char *b = A->ws.as<char>();
+    w.x = reinterpret_cast<double *>(b);
+    w.r = reinterpret_cast<double *>(b + vec);
+    w.Ap = reinterpret_cast<double *>(b + 2 * vec);
+    w.p = reinterpret_cast<double *>(b + 3 * vec);
+    const size_t small = align_up(sizeof(PcgState), 256) + align_up(kMaxGrid * 8, 256) +
+                         align_up(2 * kMaxGrid * 8, 256) + align_up((size_t)(maxiter + 2) * 8, 256) +
+                         align_up((size_t)(maxiter + 1) * 8, 256);
+    PSK_TRY(A->ws_small.ensure(small));
+    char *s = A->ws_small.as<char>();
+    w.st = reinterpret_cast<PcgState *>(s);
+    s += align_up(sizeof(PcgState), 256);
+    w.part1 = reinterpret_cast<double *>(s);
+    s += align_up(kMaxGrid * 8, 256);
+    w.part2 = reinterpret_cast<double *>(s);
+    s += align_up(2 * kMaxGrid * 8, 256);
+    w.udr = reinterpret_cast<double *>(s);
+    s += align_up((size_t)(maxiter + 2) * 8, 256);
+    w.hist = reinterpret_cast<double *>(s);
+    return PSK_OK;
+}
+
+static void set_msg(psk_result *res, const char *m) {
+    std::snprintf(res->msg, sizeof(res->msg), "%s", m);
+}
+
+}  // namespace psk
+
+using namespace psk;
+
+extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, double *xout,
+                       const psk_ctl *ctl, psk_result *res, double *hist, int32_t loc) {
+    if (!Ac || !b || !xout || !ctl || !res) return fail(PSK_ERR_ARG, "psk_pcg: NULL argument");
+    if (ctl->maxiter < 0) return fail(PSK_ERR_ARG, "psk_pcg: maxiter < 0");
+    if (M && M->n != Ac->n) return fail(PSK_ERR_ARG, "psk_pcg: preconditioner size mismatch");
+    psk_csr *A = const_cast<psk_csr *>(Ac);
+    Context *c;
+    PSK_TRY(ctx(&c));
+    hipStream_t s = c->stream;
+    std::memset(res, 0, sizeof(*res));
+    const int64_t n = A->n, maxiter = ctl->maxiter;
+    PcgWork w;
+    PSK_TRY(pcg_workspace(A, maxiter, w));
+    const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
+    const int gs = grid_for_rows(c, n, kTileRows);   // SpMV grid
+    const int gv = grid_for_rows(c, n, kVecTile);    // elementwise grid
+
+    hipEvent_t ev0, ev1;
+    PSK_HIP(hipEventCreate(&ev0));
+    PSK_HIP(hipEventCreate(&ev1));
+    // b staged in the Ap buffer (unused until the first SpMV)
+    PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
+    PSK_HIP(hipEventRecord(ev0, s));
+    hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
+    PSK_HIP(hipGetLastError());
+    if (A->comm) PSK_TRY(allreduce_sum(A, w.part2, 2 * gv, s));
+    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, gv, ctl->tau, w.st, w.udr);
+    PSK_HIP(hipGetLastError());
+
+    // polling ring: flag copies every C iterations, host waits on the copy L chunks back
+    int C = ctl->check_every > 0 ? ctl->check_every : (n >= (1 << 20) ? 2 : 16);
+    const int L = 2, NS = L + 2;
+    int32_t *hflag = nullptr;
+    PSK_HIP(hipHostMalloc(&hflag, NS * sizeof(int32_t), hipHostMallocDefault));
+    hipEvent_t fev[NS];
+    for (int i = 0; i < NS; ++i) PSK_HIP(hipEventCreateWithFlags(&fev[i], hipEventDisableTiming));
+    // optional SpMV timing ring
+    const int TP = 64;
+    hipEvent_t ta[TP], tb[TP];
+    int64_t tk[TP];
+    std::vector<float> spmv_ms;
+    if (ctl->time_kernels) {
+        for (int i = 0; i < TP; ++i) {
+            PSK_HIP(hipEventCreate(&ta[i]));
+            PSK_HIP(hipEventCreate(&tb[i]));
+            tk[i] = -1;
+        }
+        spmv_ms.assign((size_t)maxiter, 0.0f);
+    }
+    auto harvest = [&](int slot) -> int {
+        if (tk[slot] < 0) return PSK_OK;
+        float ms = 0.f;
+        PSK_HIP(hipEventSynchronize(tb[slot]));
+        PSK_HIP(hipEventElapsedTime(&ms, ta[slot], tb[slot]));
+        spmv_ms[(size_t)tk[slot]] = ms;
+        tk[slot] = -1;
+        return PSK_OK;
+    };
+
+    int64_t launched = 0;
+    int rc = PSK_OK;
+    for (int64_t k = 0; k < maxiter && rc == PSK_OK; ++k) {
+        if (k > 0 && k % C == 0) {
+            const int64_t chunk = k / C;   // chunks fully launched
+            const int slot = (int)((chunk - 1) % NS);
+            rc = hipMemcpyAsync(&hflag[slot], &w.st->done, 4, hipMemcpyDeviceToHost, s) == hipSuccess
+                     ? PSK_OK : fail(PSK_ERR_HIP, "flag copy");
+            if (rc == PSK_OK && hipEventRecord(fev[slot], s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
+            if (rc == PSK_OK && chunk - 1 - L >= 0) {
+                const int os = (int)((chunk - 1 - L) % NS);
+                if (hipEventSynchronize(fev[os]) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
+                else if (hflag[os] != 0) break;
+            }
+            if (rc != PSK_OK) break;
+        }
+        if (A->comm && (rc = halo_exchange(A, w.p, s)) != PSK_OK) break;
+        int slot = (int)(k % TP);
+        if (ctl->time_kernels) {
+            if ((rc = harvest(slot)) != PSK_OK) break;
+            tk[slot] = k;
+            if (hipEventRecord(ta[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
+        }
+        if ((rc = launch_spmv(A, kSpmvDot, w.p, w.Ap, nullptr, nullptr, w.part1, &w.st->done, gs, s)) != PSK_OK)
+            break;
+        if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
+        if (A->comm && (rc = allreduce_sum(A, w.part1, gs, s)) != PSK_OK) break;
+        hipLaunchKernelGGL(pcg_update_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap, dinv,
+                           w.part1, gs, w.part2, w.st, w.udr, k);
+        if (A->comm && (rc = allreduce_sum(A, w.part2, 2 * gv, s)) != PSK_OK) break;
+        hipLaunchKernelGGL(pcg_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv, w.part2,
+                           gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+        if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
+        launched = k + 1;
+    }
+    if (rc == PSK_OK && hipEventRecord(ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
+    PcgState hs{};
+    if (rc == PSK_OK && hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess)
+        rc = fail(PSK_ERR_HIP, "state copy");
+    if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg sync");
+    if (rc == PSK_OK && ctl->time_kernels)
+        for (int i = 0; i < TP && rc == PSK_OK; ++i) rc = harvest(i);
+    if (rc == PSK_OK) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, ev0, ev1);
+        res->loop_ms = ms;
+        res->norm_b = hs.normB;
+        int64_t nk = 0;   // iterations whose kernels did real work
+        if (hs.done == 1) {
+            res->status = PSK_CONVERGED;
+            res->success = 1;
+            res->iters = hs.iters;
+            res->resid = hs.resid;
+            nk = hs.normB == 0.0 ? 0 : hs.iters;
+        } else if (hs.done == 2) {
+            res->status = PSK_BREAKDOWN;
+            res->success = 0;
+            res->iters = hs.iters;
+            res->resid = NAN;
+            set_msg(res, hs.brk_kind == 1 ? "breakdown dot(u,r)==0" : "breakdown dot(p, Ap)==0");
+            nk = hs.brk_kind == 1 ? 0 : hs.iters + 1;
+        } else {
+            // handleMaxiter(k=maxiter-1, ...) (IterativeSolver.py:115-129); maxiter==0 -> k unset
+            res->status = PSK_MAXITER;
+            res->success = 0;
+            res->iters = maxiter > 0 ? maxiter - 1 : 0;
+            set_msg(res, "failure to converge");
+            nk = launched;
+        }
+        // residual history, the recursive residual and the solution
+        const int64_t nh = nk < maxiter ? nk : maxiter;
+        std::vector<double> hh((size_t)nh);
+        if (nh > 0 && hipMemcpy(hh.data(), w.hist, (size_t)nh * 8, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = fail(PSK_ERR_HIP, "hist copy");
+        if (rc == PSK_OK) {
+            if (hist) for (int64_t i = 0; i < nh; ++i) hist[i] = hh[(size_t)i];
+            res->hist_len = nh;
+            res->resid_recursive = nh > 0 ? hh[(size_t)nh - 1] : hs.normB;
+            if (res->status == PSK_MAXITER) res->resid = maxiter > 0 ? res->resid_recursive : hs.normB;
+            rc = from_device_vec(w.x, loc, n, xout, s);
+            if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x copy");
+        }
+        if (ctl->time_kernels) {
+            double tot = 0.0;
+            const int64_t cnt = nk < (int64_t)spmv_ms.size() ? nk : (int64_t)spmv_ms.size();
+            for (int64_t i = 0; i < cnt; ++i) tot += spmv_ms[(size_t)i];
+            res->spmv_launches = cnt;
+            res->spmv_ms = cnt > 0 ? tot / (double)cnt : 0.0;
+        }
+    }
+    if (ctl->time_kernels)
+        for (int i = 0; i < TP; ++i) {
+            (void)hipEventDestroy(ta[i]);
+            (void)hipEventDestroy(tb[i]);
+        }
+    for (int i = 0; i < NS; ++i) (void)hipEventDestroy(fev[i]);
+    (void)hipHostFree(hflag);
+    (void)hipEventDestroy(ev0);
+    (void)hipEventDestroy(ev1);
+    return rc;
+}

@@ -1,0 +1,180 @@
+// psk_internal.hpp — shared types, error plumbing and device helpers of libpsk.so (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/psk.h"
+
+namespace psk {
+
+// ---------------------------------------------------------------------------------------------
+// launch geometry (CDNA4: 64-wide waves, 256 CUs in 8 XCDs)
+constexpr int kBlock = 256;            // threads per workgroup = 4 waves
+constexpr int kWaves = kBlock / 64;
+constexpr int kTileRows = 256;         // SpMV rows per tile (one row per thread for the row sums)
+constexpr int kChunk = 2048;           // SpMV LDS-staged products per chunk (16 KiB of f64)
+constexpr int kMaxGrid = 2048;         // 256 CUs x 8 resident workgroups; partial arrays sized for it
+constexpr int kVecTile = 2 * kBlock;   // elementwise tile: 2 doubles (16 B) per lane
+
+// ---------------------------------------------------------------------------------------------
+// errors
+void set_error(int code, const std::string &msg);
+int fail(int code, const std::string &msg);
+const char *hip_err_str(hipError_t e);
+
+#define PSK_HIP(call)                                                                         \
+    do {                                                                                      \
+        hipError_t _e = (call);                                                               \
+        if (_e != hipSuccess)                                                                 \
+            return ::psk::fail(PSK_ERR_HIP, std::string(#call) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+#define PSK_RCCL(call)                                                                           \
+    do {                                                                                         \
+        ncclResult_t _r = (call);                                                                \
+        if (_r != ncclSuccess)                                                                   \
+            return ::psk::fail(PSK_ERR_RCCL, std::string(#call) + ": " + ncclGetErrorString(_r)); \
+    } while (0)
+
+#define PSK_TRY(call)              \
+    do {                           \
+        int _rc = (call);          \
+        if (_rc != PSK_OK) return _rc; \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------------
+// per-process device context: one non-blocking stream per device
+struct Context {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    int num_cus = 256;
+    int grid_cap = kMaxGrid;
+};
+int ctx(Context **out);   // current device's context (created lazily)
+
+// ---------------------------------------------------------------------------------------------
+// grow-only device buffer
+struct DevBuf {
+    void *p = nullptr;
+    size_t bytes = 0;
+    int ensure(size_t need);
+    void release();
+    template <class T> T *as() const { return static_cast<T *>(p); }
+};
+
+// halo exchange plan of a row-block sharded matrix: local vector layout [owned | halo]
+struct HaloPeer {
+    int rank;
+    int64_t send_count;   // owned entries we send to this peer
+    int64_t recv_count;   // halo entries we receive from it
+    int64_t recv_offset;  // offset inside the halo region
+    int32_t *send_idx;    // device: owned local indices to pack (nullptr when contiguous)
+    int64_t send_begin;   // contiguous owned range start when send_idx == nullptr
+};
+
+}  // namespace psk
+
+struct psk_comm {
+    int nranks = 1;
+    int rank = 0;
+    int device = 0;
+    ncclComm_t nccl = nullptr;
+};
+
+struct psk_csr {
+    int64_t n = 0;        // local (owned) rows
+    int64_t ncols = 0;    // local columns = n + halo
+    int64_t nnz = 0;
+    int32_t *rowptr = nullptr;
+    int32_t *colidx = nullptr;
+    double *vals = nullptr;
+    int device = 0;
+    // distributed
+    psk_comm *comm = nullptr;
+    int64_t n_global = 0, row_begin = 0, row_end = 0;
+    std::vector<psk::HaloPeer> peers;
+    psk::DevBuf sendbuf;  // packed halo sends
+    // per-matrix solver workspace (grow-only)
+    psk::DevBuf ws;
+    psk::DevBuf ws_small;
+};
+
+struct psk_prec {
+    int kind = PSK_PREC_IDENTITY;
+    int64_t n = 0;
+    double *dinv = nullptr;   // JACOBI
+};
+
+namespace psk {
+
+// ---------------------------------------------------------------------------------------------
+// device-side reduction helpers (deterministic: fixed order for a fixed grid)
+
+__device__ __forceinline__ double wave_sum(double v) {
+    // butterfly: every lane ends with the same bits (IEEE add is commutative)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Block-wide sum; all threads get the same value. `sh` must hold kWaves doubles.
+__device__ __forceinline__ double block_sum(double v, double *sh) {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[w] = v;
+    __syncthreads();
+    double r = sh[0];
+#pragma unroll
+    for (int i = 1; i < kWaves; ++i) r += sh[i];
+    return r;
+}
+
+// Sum of np partials laid out with `stride` (identical bits in every workgroup).
+__device__ __forceinline__ double reduce_partials(const double *part, int np, int stride, double *sh) {
+    double v = 0.0;
+    for (int i = threadIdx.x; i < np; i += kBlock) v += part[(int64_t)i * stride];
+    return block_sum(v, sh);
+}
+
+// contiguous share [b0,b1) of `ntiles` tiles for workgroup `b` of `g`
+__device__ __forceinline__ void block_range(int64_t ntiles, int64_t &t0, int64_t &t1) {
+    const int64_t g = gridDim.x, b = blockIdx.x;
+    t0 = ntiles * b / g;
+    t1 = ntiles * (b + 1) / g;
+}
+
+inline int grid_for_rows(const Context *c, int64_t rows, int per_tile) {
+    int64_t tiles = (rows + per_tile - 1) / per_tile;
+    if (tiles < 1) tiles = 1;
+    return (int)(tiles < c->grid_cap ? tiles : c->grid_cap);
+}
+
+// ---------------------------------------------------------------------------------------------
+// host helpers shared by the solver TUs
+int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
+int from_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
+int halo_exchange(psk_csr *A, double *x_local, hipStream_t s);
+int allreduce_sum(psk_csr *A, double *buf, int64_t count, hipStream_t s);
+
+// SpMV launch (defined in spmv.hip); modes below
+enum SpmvMode : int {
+    kSpmvPlain = 0,     // y = A x
+    kSpmvDot = 1,       // y = A x, partial[b] = sum_i x_i y_i        (PCG: p.Ap)
+    kSpmvJacobiDot = 2, // y = A (d .* x), partial[b] = sum_i q_i y_i (GMRES: A M^-1 q_k, q_0.u)
+    kSpmvPlainDot = 3,  // y = A x, partial[b] = sum_i q_i y_i        (GMRES identity)
+    kSpmvResid = 4,     // y = b - A x, partial[b] = sum_i y_i^2      (true residual)
+};
+int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int64_t row_end,
+              int64_t halo_lo_start, hipStream_t s);
+int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
+                const double *aux_q, double *partial, const int32_t *done_flag, int grid,
+                hipStream_t s);
+
+}  // namespace psk

@@ -1,0 +1,155 @@
+// runtime.hip — error plumbing, per-device context, device-memory entry points.
+#include "psk_internal.hpp"
+
+#include <mutex>
+
+namespace psk {
+
+static thread_local std::string g_last_error;
+
+void set_error(int code, const std::string &msg) {
+    g_last_error = "psk error " + std::to_string(code) + ": " + msg;
+}
+
+int fail(int code, const std::string &msg) {
+    set_error(code, msg);
+    return code;
+}
+
+static std::mutex g_ctx_mu;
+static Context g_ctx[64];
+
+int ctx(Context **out) {
+    int dev = 0;
+    PSK_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(PSK_ERR_ARG, "device index out of range");
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    Context &c = g_ctx[dev];
+    if (c.stream == nullptr) {
+        PSK_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        hipDeviceProp_t prop;
+        PSK_HIP(hipGetDeviceProperties(&prop, dev));
+        c.device = dev;
+        c.num_cus = prop.multiProcessorCount;
+        // 8 resident 256-thread workgroups per CU; partial arrays are sized for kMaxGrid
+        int cap = c.num_cus * 8;
+        c.grid_cap = cap < kMaxGrid ? cap : kMaxGrid;
+        // keep the grid a multiple of 8 (XCD-aware tile mapping) when it is capped
+        c.grid_cap -= c.grid_cap % 8;
+        if (c.grid_cap < 8) c.grid_cap = 8;
+    }
+    *out = &c;
+    return PSK_OK;
+}
+
+int DevBuf::ensure(size_t need) {
+    if (need <= bytes && p != nullptr) return PSK_OK;
+    if (p) {
+        hipError_t e = hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        if (e != hipSuccess) return fail(PSK_ERR_HIP, std::string("hipFree: ") + hipGetErrorString(e));
+    }
+    if (need == 0) return PSK_OK;
+    hipError_t e = hipMalloc(&p, need);
+    if (e != hipSuccess) {
+        p = nullptr;
+        return fail(PSK_ERR_ALLOC, "hipMalloc(" + std::to_string(need) + "): " + hipGetErrorString(e));
+    }
+    bytes = need;
+    return PSK_OK;
+}
+
+void DevBuf::release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+}
+
+int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s) {
+    if (n <= 0) return PSK_OK;
+    PSK_HIP(hipMemcpyAsync(dst, src, (size_t)n * sizeof(double),
+                           loc == PSK_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, s));
+    return PSK_OK;
+}
+
+int from_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s) {
+    if (n <= 0) return PSK_OK;
+    PSK_HIP(hipMemcpyAsync(dst, src, (size_t)n * sizeof(double),
+                           loc == PSK_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice, s));
+    return PSK_OK;
+}
+
+}  // namespace psk
+
+using namespace psk;
+
+extern "C" {
+
+int psk_abi_version(void) { return PSK_ABI_VERSION; }
+
+const char *psk_last_error(void) { return g_last_error.c_str(); }
+
+int psk_device_count(int32_t *n) {
+    if (!n) return fail(PSK_ERR_ARG, "n is NULL");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) c = 0;
+    *n = c;
+    return PSK_OK;
+}
+
+int psk_set_device(int32_t dev) {
+    PSK_HIP(hipSetDevice(dev));
+    return PSK_OK;
+}
+
+int psk_synchronize(void) {
+    Context *c;
+    PSK_TRY(ctx(&c));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+int psk_dmalloc(int64_t bytes, void **dptr) {
+    if (!dptr || bytes < 0) return fail(PSK_ERR_ARG, "psk_dmalloc: bad arguments");
+    *dptr = nullptr;
+    if (bytes == 0) return PSK_OK;
+    hipError_t e = hipMalloc(dptr, (size_t)bytes);
+    if (e != hipSuccess) return fail(PSK_ERR_ALLOC, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return PSK_OK;
+}
+
+int psk_dfree(void *dptr) {
+    if (dptr) PSK_HIP(hipFree(dptr));
+    return PSK_OK;
+}
+
+int psk_h2d(void *dst, const void *src, int64_t bytes) {
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (bytes <= 0) return PSK_OK;
+    PSK_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+int psk_d2h(void *dst, const void *src, int64_t bytes) {
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (bytes <= 0) return PSK_OK;
+    PSK_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+int psk_dmemset0(void *dst, int64_t bytes) {
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (bytes <= 0) return PSK_OK;
+    PSK_HIP(hipMemsetAsync(dst, 0, (size_t)bytes, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,534 @@
+// spmv.hip — CSR SpMV (the hot kernel), the CSR handle, the FD generator, Jacobi, BLAS-1 entry points.
+//
+// SpMV replaces mvmult(A, x) (IterativeLinearSolver.py:94-106) = scipy csr_matvec: for each row,
+// sum = 0; sum += vals[jj] * x[colidx[jj]] in STORED order, product rounded before the add.
+// We reproduce that bit for bit: the products are staged through LDS (so no FMA can form) and each
+// row is summed sequentially by one lane in stored order, starting from 0.0.
+//
+// Layout/schedule (gfx950): a workgroup of 256 threads (4 waves) walks a contiguous range of
+// 256-row tiles. Per tile, the tile's nnz range [rowptr[r0], rowptr[r1]) is streamed in
+// 2048-entry chunks with fully coalesced loads of colidx (4 B/lane) and vals (8 B/lane), the x
+// gather is issued branch-free for up to 8 entries per lane (ILP), products land in a 16 KiB LDS
+// slab, and each lane then sums its own row from LDS. Rows longer than a chunk keep their running
+// sum across chunks, so ANY row length is exact. Optional epilogues fuse the dot products the
+// Krylov loops need next (p.Ap for PCG, q_0.u for GMRES, ||b-Ax||^2 for the true residual), each
+// reduced deterministically per workgroup into partial[blockIdx.x].
+#include "psk_internal.hpp"
+
+#include <climits>
+#include <cmath>
+
+namespace psk {
+
+// logical workgroup id: give each XCD (blockIdx % 8 observed round-robin) a contiguous run of
+// tiles so that the x-gathers of neighbouring grid lines stay in one XCD's L2. Speed only.
+__device__ __forceinline__ int64_t logical_block() {
+    const int64_t g = gridDim.x, b = blockIdx.x;
+    if (g % 8 != 0) return b;
+    return (b % 8) * (g / 8) + b / 8;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void spmv_kernel(
+    int64_t n, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
+    const double *__restrict__ vals, const double *__restrict__ x, double *__restrict__ y,
+    const double *__restrict__ aux_d, const double *__restrict__ aux_q, double *__restrict__ partial,
+    const int32_t *__restrict__ done) {
+    if (done != nullptr && *done != 0) return;
+    __shared__ double prod[kChunk];
+    __shared__ double sh[kWaves];
+    const int tid = threadIdx.x;
+    const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+    const int64_t g = gridDim.x, lb = logical_block();
+    const int64_t t0 = ntiles * lb / g, t1 = ntiles * (lb + 1) / g;
+    double acc = 0.0;
+    constexpr int KU = kChunk / kBlock;   // 8 staged entries per lane per chunk
+
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t r0 = t * kTileRows;
+        const int64_t r1 = (r0 + kTileRows < n) ? r0 + kTileRows : n;
+        const int64_t row = r0 + tid;
+        const bool has = row < r1;
+        int32_t rs = 0, re = 0;
+        if (has) {
+            rs = rowptr[row];
+            re = rowptr[row + 1];
+        }
+        const int32_t e0 = rowptr[r0], e1 = rowptr[r1];
+        double sum = 0.0;
+        for (int32_t c0 = e0; c0 < e1; c0 += kChunk) {
+            const int32_t c1 = (e1 - c0 > kChunk) ? c0 + kChunk : e1;
+            const int nk = (c1 - c0 + kBlock - 1) / kBlock;   // wave-uniform
+            int32_t ci[KU];
+            double vv[KU], xv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                if (k < nk) {
+                    const int32_t e = c0 + k * kBlock + tid;
+                    const int32_t ee = e < c1 ? e : c0;   // branch-free: clamp to a valid entry
+                    ci[k] = colidx[ee];
+                    vv[k] = vals[ee];
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                if (k < nk) {
+                    double xx = x[ci[k]];
+                    if (MODE == kSpmvJacobiDot) xx = aux_d[ci[k]] * xx;   // (DInv*q)[c], rounded
+                    xv[k] = xx;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                if (k < nk) {
+                    const int32_t e = c0 + k * kBlock + tid;
+                    if (e < c1) prod[k * kBlock + tid] = vv[k] * xv[k];   // rounded product
+                }
+            }
+            __syncthreads();
+            const int32_t a = rs > c0 ? rs : c0;
+            const int32_t bnd = re < c1 ? re : c1;
+            for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
+            __syncthreads();
+        }
+        if (has) {
+            if (MODE == kSpmvResid) {
+                const double r = aux_q[row] - sum;   // b - A*x (GMRESSolver.py:163)
+                y[row] = r;
+                acc = fma(r, r, acc);
+            } else {
+                y[row] = sum;
+                if (MODE == kSpmvDot) acc = fma(x[row], sum, acc);
+                if (MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot) acc = fma(aux_q[row], sum, acc);
+            }
+        }
+    }
+    if (MODE != kSpmvPlain) {
+        const double s = block_sum(acc, sh);
+        if (tid == 0) partial[blockIdx.x] = s;
+    }
+}
+
+int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
+                const double *aux_q, double *partial, const int32_t *done_flag, int grid,
+                hipStream_t s) {
+    if (A->n == 0) return PSK_OK;
+    dim3 gd(grid), bd(kBlock);
+    switch (mode) {
+    case kSpmvPlain:
+        hipLaunchKernelGGL(spmv_kernel<kSpmvPlain>, gd, bd, 0, s, A->n, A->rowptr, A->colidx, A->vals,
+                           x, y, aux_d, aux_q, partial, done_flag);
+        break;
+    case kSpmvDot:
+        hipLaunchKernelGGL(spmv_kernel<kSpmvDot>, gd, bd, 0, s, A->n, A->rowptr, A->colidx, A->vals,
+                           x, y, aux_d, aux_q, partial, done_flag);
+        break;
+    case kSpmvJacobiDot:
+        hipLaunchKernelGGL(spmv_kernel<kSpmvJacobiDot>, gd, bd, 0, s, A->n, A->rowptr, A->colidx,
+                           A->vals, x, y, aux_d, aux_q, partial, done_flag);
+        break;
+    case kSpmvPlainDot:
+        hipLaunchKernelGGL(spmv_kernel<kSpmvPlainDot>, gd, bd, 0, s, A->n, A->rowptr, A->colidx,
+                           A->vals, x, y, aux_d, aux_q, partial, done_flag);
+        break;
+    case kSpmvResid:
+        hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, A->rowptr, A->colidx, A->vals,
+                           x, y, aux_d, aux_q, partial, done_flag);
+        break;
+    default:
+        return fail(PSK_ERR_ARG, "unknown spmv mode");
+    }
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// FDLaplacian2D on the device (examples/FDLaplacian2D.py:5-23). Row k = m*iy + ix stores
+// [diag, -m, +m, -1, +1] minus absent neighbours; rowptr in closed form
+//   rowptr[k] = 5k - min(k,m) - max(0,k-m(m-1)) - ceil(k/m) - floor(k/m).
+// Rows [row_begin, row_end) of the global matrix; column c is written as col_of(c) where
+// local = c - col_shift for owned columns and halo columns map after the owned block.
+__device__ __forceinline__ int64_t fd_rowptr(int64_t m, int64_t k) {
+    int64_t mk = k < m ? k : m;
+    int64_t top = k - m * (m - 1);
+    if (top < 0) top = 0;
+    return 5 * k - mk - top - (k + m - 1) / m - k / m;
+}
+
+__global__ void fd2d_kernel(int64_t m, int64_t row_begin, int64_t row_end, double dval, double oval,
+                            int32_t *rowptr, int32_t *colidx, double *vals, int64_t halo_lo_start,
+                            int64_t n_own) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t nloc = row_end - row_begin;
+    if (i > nloc) return;
+    const int64_t k = row_begin + i;
+    const int64_t base = fd_rowptr(m, row_begin);
+    const int64_t off = fd_rowptr(m, k) - base;
+    rowptr[i] = (int32_t)off;
+    if (i == nloc) return;
+    const int64_t ix = k % m, iy = k / m;
+    // local column of a global column c: owned -> c-row_begin; below -> halo_lo; above -> halo_hi
+    auto lc = [&](int64_t c) -> int32_t {
+        if (c >= row_begin && c < row_end) return (int32_t)(c - row_begin);
+        if (c < row_begin) return (int32_t)(n_own + (c - halo_lo_start));
+        return (int32_t)(n_own + (row_begin - halo_lo_start) + (c - row_end));
+    };
+    int64_t p = off;
+    colidx[p] = lc(k);
+    vals[p++] = dval;
+    if (iy > 0) { colidx[p] = lc(k - m); vals[p++] = oval; }
+    if (iy < m - 1) { colidx[p] = lc(k + m); vals[p++] = oval; }
+    if (ix > 0) { colidx[p] = lc(k - 1); vals[p++] = oval; }
+    if (ix < m - 1) { colidx[p] = lc(k + 1); vals[p++] = oval; }
+}
+
+int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int64_t row_end,
+              int64_t halo_lo_start, hipStream_t s) {
+    const double h = std::fabs(b - a) / (double)(m + 1);   // FDLaplacian2D.py:6
+    const double dval = -4.0 / h / h;                       // :13
+    const double oval = 1.0 / h / h;                        // :15-21
+    const int64_t nloc = row_end - row_begin;
+    const int64_t threads = nloc + 1;
+    const int64_t blocks = (threads + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(fd2d_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, m, row_begin, row_end,
+                       dval, oval, A->rowptr, A->colidx, A->vals, halo_lo_start, nloc);
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
+// diagonal (scipy csr_diagonal: sum of col==row entries in stored order) and its reciprocal
+__global__ void jacobi_dinv_kernel(int64_t n, const int32_t *rowptr, const int32_t *colidx,
+                                   const double *vals, double *dinv) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    double d = 0.0;
+    for (int32_t jj = rowptr[i]; jj < rowptr[i + 1]; ++jj)
+        if (colidx[jj] == (int32_t)i) d = d + vals[jj];
+    dinv[i] = 1.0 / d;   // np.reciprocal
+}
+
+// ---------------------------------------------------------------------------------------------
+// BLAS-1 (dot / nrm2 / axpy) for the standalone entry points
+__global__ __launch_bounds__(kBlock) void dot_partial_kernel(int64_t n, const double *__restrict__ x,
+                                                             const double *__restrict__ y,
+                                                             double *__restrict__ part) {
+    __shared__ double sh[kWaves];
+    int64_t t0, t1;
+    const int64_t ntiles = (n + kVecTile - 1) / kVecTile;
+    block_range(ntiles, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    double acc = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) acc = fma(x[i], y[i], acc);
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBlock) void reduce_final_kernel(const double *part, int np, double *out,
+                                                              int do_sqrt) {
+    __shared__ double sh[kWaves];
+    const double s = reduce_partials(part, np, 1, sh);
+    if (threadIdx.x == 0) out[0] = do_sqrt ? sqrt(s) : s;
+}
+
+__global__ void axpy_kernel(int64_t n, double alpha, const double *__restrict__ x, double *__restrict__ y) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = y[i] + alpha * x[i];   // compiled with -ffp-contract=off: two roundings
+}
+
+__global__ void scale_kernel(int64_t n, const double *__restrict__ d, const double *__restrict__ v,
+                             double *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = d[i] * v[i];
+}
+
+}  // namespace psk
+
+using namespace psk;
+
+static int csr_alloc(psk_csr *A, int64_t n, int64_t nnz) {
+    hipError_t e;
+    e = hipMalloc(&A->rowptr, (size_t)(n + 1) * sizeof(int32_t));
+    if (e != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc rowptr");
+    if (nnz > 0) {
+        e = hipMalloc(&A->colidx, (size_t)nnz * sizeof(int32_t));
+        if (e != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc colidx");
+        e = hipMalloc(&A->vals, (size_t)nnz * sizeof(double));
+        if (e != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc vals");
+    }
+    return PSK_OK;
+}
+
+static void csr_free(psk_csr *A) {
+    if (A->rowptr) (void)hipFree(A->rowptr);
+    if (A->colidx) (void)hipFree(A->colidx);
+    if (A->vals) (void)hipFree(A->vals);
+    A->rowptr = nullptr;
+    A->colidx = nullptr;
+    A->vals = nullptr;
+    A->ws.release();
+    A->ws_small.release();
+    A->sendbuf.release();
+    for (auto &p : A->peers)
+        if (p.send_idx) (void)hipFree(p.send_idx);
+    A->peers.clear();
+}
+
+extern "C" {
+
+int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
+                   const double *vals, int32_t loc, psk_csr **out) {
+    if (!out || n < 0 || nnz < 0 || !rowptr || (nnz > 0 && (!colidx || !vals)))
+        return fail(PSK_ERR_ARG, "psk_csr_create: bad arguments");
+    if (nnz > INT32_MAX || n >= INT32_MAX)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create: int32 CSR indices required (nnz < 2^31)");
+    if (loc == PSK_HOST) {
+        // a malformed CSR would make the gather fault on the device: validate it here, O(nnz)
+        if (rowptr[0] != 0 || rowptr[n] != nnz)
+            return fail(PSK_ERR_ARG, "psk_csr_create: rowptr[0] must be 0 and rowptr[n] == nnz");
+        for (int64_t i = 0; i < n; ++i)
+            if (rowptr[i + 1] < rowptr[i]) return fail(PSK_ERR_ARG, "psk_csr_create: rowptr not monotone");
+        for (int64_t j = 0; j < nnz; ++j)
+            if (colidx[j] < 0 || colidx[j] >= n) return fail(PSK_ERR_ARG, "psk_csr_create: column index out of range");
+    }
+    Context *c;
+    PSK_TRY(ctx(&c));
+    psk_csr *A = new psk_csr();
+    A->n = n;
+    A->ncols = n;
+    A->nnz = nnz;
+    A->n_global = n;
+    A->row_begin = 0;
+    A->row_end = n;
+    A->device = c->device;
+    int rc = csr_alloc(A, n, nnz);
+    if (rc != PSK_OK) {
+        csr_free(A);
+        delete A;
+        return rc;
+    }
+    const hipMemcpyKind k = loc == PSK_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    hipError_t e = hipMemcpyAsync(A->rowptr, rowptr, (size_t)(n + 1) * sizeof(int32_t), k, c->stream);
+    if (e == hipSuccess && nnz > 0)
+        e = hipMemcpyAsync(A->colidx, colidx, (size_t)nnz * sizeof(int32_t), k, c->stream);
+    if (e == hipSuccess && nnz > 0)
+        e = hipMemcpyAsync(A->vals, vals, (size_t)nnz * sizeof(double), k, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        csr_free(A);
+        delete A;
+        return fail(PSK_ERR_HIP, std::string("psk_csr_create copy: ") + hipGetErrorString(e));
+    }
+    *out = A;
+    return PSK_OK;
+}
+
+int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out) {
+    if (!out || m < 1) return fail(PSK_ERR_ARG, "psk_csr_create_fd2d: m must be >= 1");
+    const int64_t n = m * m;
+    const int64_t nnz = (m == 1) ? 1 : 5 * n - 4 * m;
+    if (nnz > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "FD2D: nnz exceeds int32 CSR");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    psk_csr *A = new psk_csr();
+    A->n = n;
+    A->ncols = n;
+    A->nnz = nnz;
+    A->n_global = n;
+    A->row_end = n;
+    A->device = c->device;
+    int rc = csr_alloc(A, n, nnz);
+    if (rc == PSK_OK) rc = fd2d_fill(A, m, a, b, 0, n, 0, c->stream);
+    if (rc == PSK_OK) {
+        hipError_t e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) rc = fail(PSK_ERR_HIP, std::string("fd2d: ") + hipGetErrorString(e));
+    }
+    if (rc != PSK_OK) {
+        csr_free(A);
+        delete A;
+        return rc;
+    }
+    *out = A;
+    return PSK_OK;
+}
+
+int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz) {
+    if (!A) return fail(PSK_ERR_ARG, "NULL matrix");
+    if (n) *n = A->n;
+    if (nnz) *nnz = A->nnz;
+    return PSK_OK;
+}
+
+int psk_csr_download(const psk_csr *A, int32_t *rowptr, int32_t *colidx, double *vals) {
+    if (!A) return fail(PSK_ERR_ARG, "NULL matrix");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (rowptr)
+        PSK_HIP(hipMemcpyAsync(rowptr, A->rowptr, (size_t)(A->n + 1) * 4, hipMemcpyDeviceToHost, c->stream));
+    if (colidx && A->nnz)
+        PSK_HIP(hipMemcpyAsync(colidx, A->colidx, (size_t)A->nnz * 4, hipMemcpyDeviceToHost, c->stream));
+    if (vals && A->nnz)
+        PSK_HIP(hipMemcpyAsync(vals, A->vals, (size_t)A->nnz * 8, hipMemcpyDeviceToHost, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+int psk_csr_destroy(psk_csr *A) {
+    if (!A) return PSK_OK;
+    csr_free(A);
+    delete A;
+    return PSK_OK;
+}
+
+int psk_spmv(const psk_csr *Ac, const double *x, double *y, int32_t loc) {
+    if (!Ac || !x || !y) return fail(PSK_ERR_ARG, "psk_spmv: NULL argument");
+    psk_csr *A = const_cast<psk_csr *>(Ac);
+    Context *c;
+    PSK_TRY(ctx(&c));
+    const double *dx = x;
+    double *dy = y;
+    DevBuf tmp;
+    if (loc == PSK_HOST || A->comm) {
+        // stage into [owned | halo] x and y
+        PSK_TRY(tmp.ensure((size_t)(A->ncols + A->n) * sizeof(double)));
+        double *tx = tmp.as<double>();
+        PSK_TRY(to_device_vec(x, loc, A->n, tx, c->stream));
+        if (A->comm) PSK_TRY(halo_exchange(A, tx, c->stream));
+        dx = tx;
+        dy = (loc == PSK_HOST) ? tx + A->ncols : y;
+    }
+    const int grid = grid_for_rows(c, A->n, kTileRows);
+    PSK_TRY(launch_spmv(A, kSpmvPlain, dx, dy, nullptr, nullptr, nullptr, nullptr, grid, c->stream));
+    if (loc == PSK_HOST) PSK_TRY(from_device_vec(dy, PSK_HOST, A->n, y, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    tmp.release();
+    return PSK_OK;
+}
+
+static int dot_impl(int64_t n, const double *x, const double *y, int32_t loc, double *out, bool nrm) {
+    if (!out || n < 0 || !x || (!nrm && !y)) return fail(PSK_ERR_ARG, "psk_dot: bad arguments");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    DevBuf tmp;
+    const int grid = grid_for_rows(c, n, kVecTile);
+    PSK_TRY(tmp.ensure((size_t)(2 * n + kMaxGrid + 1) * sizeof(double)));
+    double *dx = const_cast<double *>(x), *dy = const_cast<double *>(y);
+    double *base = tmp.as<double>();
+    if (loc == PSK_HOST) {
+        dx = base;
+        PSK_TRY(to_device_vec(x, loc, n, dx, c->stream));
+        if (!nrm) {
+            dy = base + n;
+            PSK_TRY(to_device_vec(y, loc, n, dy, c->stream));
+        }
+    }
+    if (nrm) dy = dx;
+    double *part = base + 2 * n;
+    double *res = part + kMaxGrid;
+    hipLaunchKernelGGL(dot_partial_kernel, dim3(grid), dim3(kBlock), 0, c->stream, n, dx, dy, part);
+    PSK_HIP(hipGetLastError());
+    hipLaunchKernelGGL(reduce_final_kernel, dim3(1), dim3(kBlock), 0, c->stream, part, grid, res, nrm ? 1 : 0);
+    PSK_HIP(hipGetLastError());
+    PSK_HIP(hipMemcpyAsync(out, res, sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    tmp.release();
+    return PSK_OK;
+}
+
+int psk_dot(int64_t n, const double *x, const double *y, int32_t loc, double *out) {
+    return dot_impl(n, x, y, loc, out, false);
+}
+
+int psk_nrm2(int64_t n, const double *x, int32_t loc, double *out) {
+    return dot_impl(n, x, nullptr, loc, out, true);
+}
+
+int psk_axpy(int64_t n, double alpha, const double *x, double *y, int32_t loc) {
+    if (n < 0 || !x || !y) return fail(PSK_ERR_ARG, "psk_axpy: bad arguments");
+    if (n == 0) return PSK_OK;
+    Context *c;
+    PSK_TRY(ctx(&c));
+    DevBuf tmp;
+    const double *dx = x;
+    double *dy = y;
+    if (loc == PSK_HOST) {
+        PSK_TRY(tmp.ensure((size_t)2 * n * sizeof(double)));
+        double *b = tmp.as<double>();
+        PSK_TRY(to_device_vec(x, loc, n, b, c->stream));
+        PSK_TRY(to_device_vec(y, loc, n, b + n, c->stream));
+        dx = b;
+        dy = b + n;
+    }
+    hipLaunchKernelGGL(axpy_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       c->stream, n, alpha, dx, dy);
+    PSK_HIP(hipGetLastError());
+    if (loc == PSK_HOST) PSK_TRY(from_device_vec(dy, PSK_HOST, n, y, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out) {
+    if (!A || !out) return fail(PSK_ERR_ARG, "psk_prec_create: NULL argument");
+    if (kind != PSK_PREC_IDENTITY && kind != PSK_PREC_JACOBI)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_create: unknown preconditioner kind");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    psk_prec *M = new psk_prec();
+    M->kind = kind;
+    M->n = A->n;
+    if (kind == PSK_PREC_JACOBI && A->n > 0) {
+        hipError_t e = hipMalloc(&M->dinv, (size_t)A->n * sizeof(double));
+        if (e != hipSuccess) {
+            delete M;
+            return fail(PSK_ERR_ALLOC, "hipMalloc dinv");
+        }
+        hipLaunchKernelGGL(jacobi_dinv_kernel, dim3((unsigned)((A->n + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, c->stream, A->n, A->rowptr, A->colidx, A->vals, M->dinv);
+        e = hipGetLastError();
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(M->dinv);
+            delete M;
+            return fail(PSK_ERR_HIP, std::string("jacobi: ") + hipGetErrorString(e));
+        }
+    }
+    *out = M;
+    return PSK_OK;
+}
+
+int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, int32_t loc) {
+    if (!M || !v || !outv || n != M->n) return fail(PSK_ERR_ARG, "psk_prec_apply: bad arguments");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (n == 0) return PSK_OK;
+    if (M->kind == PSK_PREC_IDENTITY) {
+        const hipMemcpyKind k = loc == PSK_HOST ? hipMemcpyHostToHost : hipMemcpyDeviceToDevice;
+        if (v != outv) PSK_HIP(hipMemcpyAsync(outv, v, (size_t)n * 8, k, c->stream));
+        PSK_HIP(hipStreamSynchronize(c->stream));
+        return PSK_OK;
+    }
+    DevBuf tmp;
+    const double *dv = v;
+    double *dout = outv;
+    if (loc == PSK_HOST) {
+        PSK_TRY(tmp.ensure((size_t)2 * n * sizeof(double)));
+        double *b = tmp.as<double>();
+        PSK_TRY(to_device_vec(v, loc, n, b, c->stream));
+        dv = b;
+        dout = b + n;
+    }
+    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       c->stream, n, M->dinv, dv, dout);
+    PSK_HIP(hipGetLastError());
+    if (loc == PSK_HOST) PSK_TRY(from_device_vec(dout, PSK_HOST, n, outv, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return PSK_OK;
+}
+
+int psk_prec_destroy(psk_prec *M) {
+    if (!M) return PSK_OK;
+    if (M->dinv) (void)hipFree(M->dinv);
+    delete M;
+    return PSK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,266 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures in tests/golden/ by running the REFERENCE itself.
+
+Run only in the build container, where the reference is mounted read-only at
+/root/reference:
+
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py
+
+What it does
+------------
+* imports the reference package (krlong014/PySolvers) from /root/reference.  Two
+  external modules the reference imports are absent from the image (PyTab,
+  PyTimer); they only print indentation / timing, so minimal
+  stand-ins are injected into ``sys.modules`` (nothing is written into the
+  reference tree; bytecode writing is disabled);
+* runs the reference solvers (PCG, patched GMRES), its FD generator, its mvmult
+  and its Givens helpers on seeded inputs;
+* runs the oracle restatement (oracle/) on the same inputs in the same process
+  and ASSERTS bit-identity (iteration counts, residual histories, solutions);
+* writes inputs + reference outputs as compressed .npz fixtures.  Fixtures are
+  data only (matrices, vectors, scalars); no reference source is stored.
+
+The GPU box never runs this file (it has no /root/reference).
+"""
+import contextlib
+import hashlib
+import io
+import json
+import os
+import sys
+import types
+
+import numpy as np
+import scipy.sparse as sp
+from scipy.io import mmread
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+sys.dont_write_bytecode = True
+sys.path.insert(0, REPO)
+
+
+def _install_standins():
+    tab = types.ModuleType("PyTab")
+
+    class Tab:                       # used only as an indentation prefix in prints
+        def __str__(self):
+            return ""
+    tab.Tab = Tab
+    sys.modules["PyTab"] = tab
+    tm = types.ModuleType("PyTimer")
+
+    class Timer:                     # used only by SA-AMG setup timing
+        def __init__(self, *a, **k):
+            pass
+
+        def start(self):
+            pass
+
+        def stop(self):
+            pass
+
+        @staticmethod
+        def report():
+            pass
+    tm.Timer = Timer
+    sys.modules["PyTimer"] = tm
+
+
+_install_standins()
+sys.path.insert(0, REF)
+sys.path.insert(0, os.path.join(REF, "examples"))
+
+from PySolvers import CommonSolverArgs                                   # noqa: E402
+from PySolvers.Linear import PCG, GMRES                                  # noqa: E402
+from PySolvers.Linear.PreconditionerType import PreconditionerType       # noqa: E402
+from PySolvers.Linear.Preconditioner import GenericPreconditioner        # noqa: E402
+from PySolvers.Linear.IterativeLinearSolver import mvmult as ref_mvmult  # noqa: E402
+from PySolvers.Linear import Givens as ref_givens                        # noqa: E402
+from FDLaplacian2D import FDLaplacian2D as ref_fd2d                      # noqa: E402
+
+from oracle import krylov, fdlap                                          # noqa: E402
+
+
+class _JacobiPrec(GenericPreconditioner):
+    """Jacobi through the reference's own plugin API (Preconditioner.py:20-36)."""
+
+    def __init__(self, A):
+        self.DInv = np.reciprocal(A.diagonal())
+
+    def apply(self, vec):
+        return np.multiply(self.DInv, vec)
+
+
+class _Jacobi(PreconditionerType):
+    def form(self, A):
+        return _JacobiPrec(A)
+
+
+def _run_ref(kind, A, b, maxiter, tau, fail_on_maxiter=True, jacobi=False):
+    ctl = CommonSolverArgs(maxiter=maxiter, tau=tau, failOnMaxiter=fail_on_maxiter,
+                           showIters=False, showFinal=False)
+    pt = _Jacobi() if jacobi else None
+    if kind == "pcg":
+        st = (PCG(control=ctl, precond=pt) if pt else PCG(control=ctl)).makeSolver()
+    else:
+        st = (GMRES(control=ctl, precond=pt) if pt else GMRES(control=ctl)).makeSolver()
+        st.precond = None          # GMRESSolver.py:71 reads an attribute it never sets
+    hist = []
+    st.reportIter = lambda it, nr, n0: hist.append(float(nr))
+    with contextlib.redirect_stdout(io.StringIO()):
+        res = st.solve(A, b)
+    return res, np.array(hist)
+
+
+def _check_same(tag, res, hist, orc):
+    assert res.iters() == orc["iters"], (tag, res.iters(), orc["iters"])
+    assert bool(res.success()) == bool(orc["success"]), tag
+    assert np.array_equal(hist, orc["hist"]), tag
+    if res.soln() is not None:
+        assert np.array_equal(res.soln(), orc["soln"]), tag
+    if res.resid() is not None:
+        assert float(res.resid()) == float(orc["resid"]), tag
+
+
+def _csr_arrays(A):
+    A = A.tocsr()
+    return dict(indptr=A.indptr.astype(np.int32), indices=A.indices.astype(np.int32),
+                data=A.data.astype(np.float64), n=np.int64(A.shape[0]))
+
+
+def _sha(*arrs):
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+def _dh(lev):
+    return mmread(os.path.join(REF, "TestMatrices", "DH-Matrix-%d.mtx" % lev)).tocsr()
+
+
+def main():
+    out = {}
+    manifest = {}
+
+    # --- FD generator: full arrays for small m, hashes for larger m -----------------
+    fd_small = {}
+    for m in (1, 2, 3, 5, 16):
+        A = ref_fd2d(-1.0, 1.0, m)
+        ip, ix, dt = fdlap.fd_laplacian_2d_arrays(-1.0, 1.0, m)
+        assert np.array_equal(A.indptr, ip) and np.array_equal(A.indices, ix) \
+            and np.array_equal(A.data, dt), m
+        fd_small["m%d_indptr" % m] = A.indptr.astype(np.int32)
+        fd_small["m%d_indices" % m] = A.indices.astype(np.int32)
+        fd_small["m%d_data" % m] = A.data
+    hashes = {}
+    for m in (64, 128, 300):
+        A = ref_fd2d(-1.0, 1.0, m)
+        ip, ix, dt = fdlap.fd_laplacian_2d_arrays(-1.0, 1.0, m)
+        assert np.array_equal(A.indptr, ip) and np.array_equal(A.indices, ix) \
+            and np.array_equal(A.data, dt), m
+        hashes[str(m)] = dict(sha256=_sha(A.indptr.astype(np.int32), A.indices.astype(np.int32),
+                                          A.data), nnz=int(A.nnz))
+    np.savez_compressed(os.path.join(HERE, "fd_generator.npz"), **fd_small)
+    manifest["fd_generator_sha256"] = hashes
+    print("fd generator: ok")
+
+    # --- SpMV golden (stored-order, non-sorted FD rows; and a DH matrix) -------------
+    A = ref_fd2d(-1.0, 1.0, 64)
+    x = np.random.default_rng(7).random(A.shape[0])
+    y = ref_mvmult(A, x)
+    A8 = _dh(8)
+    x8 = np.random.default_rng(8).random(A8.shape[0])
+    y8 = ref_mvmult(A8, x8)
+    np.savez_compressed(os.path.join(HERE, "spmv.npz"),
+                        fd64_x=x, fd64_y=y, dh8_x=x8, dh8_y=y8,
+                        **{"fd64_" + k: v for k, v in _csr_arrays(A).items()},
+                        **{"dh8_" + k: v for k, v in _csr_arrays(A8).items()})
+    print("spmv: ok")
+
+    # --- Givens self-test (Givens.py:36-120) ------------------------------------------
+    H, g = krylov.givens_selftest_matrix()
+    Hr, gr = H.copy(), g.copy()
+    n_, m_ = Hr.shape
+    CS = np.zeros([m_, 2])
+    for i in range(m_):
+        for j in range(i):
+            ref_givens.applyGivensInPlace(Hr[:, i], CS[j, 0], CS[j, 1], j)
+        CS[i, :] = ref_givens.findGivensCoefficients(Hr[:, i], i)
+        ref_givens.applyGivensInPlace(Hr[:, i], CS[i, 0], CS[i, 1], i)
+        ref_givens.applyGivensInPlace(gr, CS[i, 0], CS[i, 1], i)
+    yr = np.linalg.solve(Hr[0:m_, :], gr[0:m_])
+    Ho, go, CSo, yo = krylov.givens_triangularize(H, g)
+    assert np.array_equal(Hr, Ho) and np.array_equal(gr, go) and np.array_equal(yr, yo)
+    np.savez_compressed(os.path.join(HERE, "givens.npz"), H=H, g=g, H_rot=Hr, g_rot=gr, CS=CS, y=yr)
+    print("givens: ok")
+
+    # --- Solver cases ------------------------------------------------------------------
+    cases = []
+    for lev in (8, 10, 12, 15):
+        cases.append(("pcg", "dh%d" % lev, _dh(lev), 2000, 1e-8, True, False))
+    for lev in (8, 10):
+        cases.append(("pcg", "dh%d" % lev, _dh(lev), 2000, 1e-8, True, True))
+    for m in (16, 64, 128):
+        cases.append(("pcg", "fd%d" % m, ref_fd2d(-1.0, 1.0, m), 4000, 1e-8, True, True))
+    cases.append(("pcg", "fd32", ref_fd2d(-1.0, 1.0, 32), 4000, 1e-8, True, False))
+    # maxiter edge cases (IterativeSolver.py:115-129 / PCGSolver.py:129-131)
+    cases.append(("pcg", "dh8_maxiter10_fail", _dh(8), 10, 1e-8, True, False))
+    cases.append(("pcg", "dh8_maxiter10_nofail", _dh(8), 10, 1e-8, False, False))
+    cases.append(("pcg", "dh8_maxiter1_fail", _dh(8), 1, 1e-8, True, False))
+    cases.append(("pcg", "fd16_tau0_nofail", ref_fd2d(-1.0, 1.0, 16), 25, 0.0, False, True))
+    # GMRES (patched, non-restarted): maxiter large enough to converge (GMRESSolver.py:180)
+    for lev in (8, 10):
+        cases.append(("gmres", "dh%d" % lev, _dh(lev), 300, 1e-8, True, False))
+    cases.append(("gmres", "dh8", _dh(8), 300, 1e-8, True, True))
+    cases.append(("gmres", "fd16", ref_fd2d(-1.0, 1.0, 16), 300, 1e-8, True, False))
+    cases.append(("gmres", "fd16", ref_fd2d(-1.0, 1.0, 16), 300, 1e-8, True, True))
+    cases.append(("gmres", "fd32", ref_fd2d(-1.0, 1.0, 32), 300, 1e-10, True, True))
+
+    index = []
+    for kind, name, A, maxiter, tau, fom, jac in cases:
+        b, xex = fdlap.manufactured_rhs(A, 12345)
+        # b from the reference's own mvmult must equal the oracle's
+        assert np.array_equal(b, ref_mvmult(A, xex))
+        res, hist = _run_ref(kind, A, b, maxiter, tau, fom, jac)
+        prec = krylov.jacobi_form(A) if jac else krylov.identity_apply
+        fn = krylov.pcg if kind == "pcg" else krylov.gmres
+        orc = fn(A, b, maxiter=maxiter, tau=tau, fail_on_maxiter=fom, precond=prec)
+        tag = "%s_%s_%s" % (kind, name, "jacobi" if jac else "identity")
+        _check_same(tag, res, hist, orc)
+        fname = tag + ".npz"
+        payload = dict(b=b, x_exact=xex, hist=hist, maxiter=np.int64(maxiter), tau=np.float64(tau),
+                       fail_on_maxiter=np.int64(fom), jacobi=np.int64(jac),
+                       iters=np.int64(res.iters()), success=np.int64(bool(res.success())),
+                       resid=np.float64(res.resid() if res.resid() is not None else np.nan),
+                       soln=res.soln() if res.soln() is not None else np.zeros(0),
+                       **_csr_arrays(A))
+        np.savez_compressed(os.path.join(HERE, fname), **payload)
+        index.append(dict(file=fname, kind=kind, matrix=name, n=int(A.shape[0]), nnz=int(A.nnz),
+                          maxiter=maxiter, tau=tau, fail_on_maxiter=fom, jacobi=jac,
+                          iters=int(res.iters()), success=bool(res.success()),
+                          resid=None if res.resid() is None else float(res.resid()),
+                          final_ratio=float(hist[-1] / np.linalg.norm(b)) if len(hist) else None))
+        print("%-40s iters=%5d success=%s" % (tag, res.iters(), res.success()))
+
+    # b = 0 (PCGSolver.py:86-88, GMRESSolver.py:66-68): iters=1, x=0
+    A = _dh(8)
+    for kind in ("pcg", "gmres"):
+        res, hist = _run_ref(kind, A, np.zeros(A.shape[0]), 50, 1e-8)
+        assert res.iters() == 1 and res.success() and not np.any(res.soln())
+    manifest["zero_rhs"] = dict(iters=1, success=True, resid=0)
+
+    manifest["cases"] = index
+    manifest["generator"] = "tests/golden/make_golden.py"
+    manifest["numpy"] = np.__version__
+    import scipy
+    manifest["scipy"] = scipy.__version__
+    with open(os.path.join(HERE, "manifest.json"), "w") as f:
+        json.dump(manifest, f, indent=1)
+    print("wrote", len(index), "solver fixtures")
+
+
+if __name__ == "__main__":
+    main()

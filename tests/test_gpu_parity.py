@@ -1,0 +1,237 @@
+"""Parity of the HIP engine (through the C ABI) with the oracle and the reference's golden vectors.
+
+Bars (BASELINE.json north_star): SpMV, the FD generator, the Jacobi diagonal and
+the elementwise updates are bit-exact; solver iteration counts are identical and
+residuals agree to 1e-10 relative.
+"""
+import ctypes
+import hashlib
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import golden_matrix, load_golden, manifest, solver_cases
+
+pytestmark = pytest.mark.gpu
+
+RTOL_RESID = 1e-10        # north_star: residuals within 1e-10 relative
+
+
+@pytest.fixture(scope="module")
+def psk():
+    import pysolvers_amd
+    from pysolvers_amd import _native as N
+    assert N.device_count() >= 1, "no GPU visible to libpsk"
+    return pysolvers_amd
+
+
+def _ctl(**kw):
+    from pysolvers_amd import CommonSolverArgs
+    kw.setdefault("showIters", False)
+    kw.setdefault("showFinal", False)
+    return CommonSolverArgs(**kw)
+
+
+# ---------------------------------------------------------------------------------------------
+# bit-exact kernels
+
+@pytest.mark.parametrize("tag", ["fd64", "dh8"])
+def test_spmv_bitwise_golden(psk, tag):
+    d = load_golden("spmv.npz")
+    A = golden_matrix(d, tag + "_")
+    y = psk.mvmult(A, d[tag + "_x"])
+    assert np.array_equal(y, d[tag + "_y"])
+
+
+def _ragged_matrix(rng, n, long_rows=(), empty_rows=()):
+    rows, cols = [], []
+    for i in range(n):
+        if i in empty_rows:
+            continue
+        k = 3000 if i in long_rows else int(rng.integers(1, 9))
+        c = rng.choice(n, size=min(k, n), replace=False)
+        rows += [i] * len(c)
+        cols += list(c)
+    vals = rng.standard_normal(len(rows))
+    A = sp.coo_matrix((vals, (rows, cols)), shape=(n, n)).tocsr()
+    # shuffle each row's stored order: the kernel must follow stored order, not column order
+    for i in range(n):
+        s, e = A.indptr[i], A.indptr[i + 1]
+        p = rng.permutation(e - s)
+        A.indices[s:e] = A.indices[s:e][p]
+        A.data[s:e] = A.data[s:e][p]
+    A.has_sorted_indices = False
+    return A
+
+
+@pytest.mark.parametrize("n,long_rows,empty_rows", [
+    (1, (), ()), (7, (), (3,)), (257, (), (0, 256)), (5000, (17, 4096), (5, 6, 7)), (70001, (300,), (69999,)),
+])
+def test_spmv_bitwise_ragged(psk, n, long_rows, empty_rows):
+    rng = np.random.default_rng(n)
+    A = _ragged_matrix(rng, n, long_rows, empty_rows)
+    x = rng.standard_normal(n)
+    assert np.array_equal(psk.mvmult(A, x), A @ x)
+
+
+def test_spmv_empty_matrix(psk):
+    A = sp.csr_matrix((4, 4))
+    assert np.array_equal(psk.mvmult(A, np.ones(4)), np.zeros(4))
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 5, 16, 64, 300])
+def test_fd_generator_device_bitwise(psk, m):
+    from oracle import fdlap
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    A = dA.to_scipy()
+    ip, ix, dt = fdlap.fd_laplacian_2d_arrays(-1.0, 1.0, m)
+    assert np.array_equal(A.indptr, ip) and np.array_equal(A.indices, ix) and np.array_equal(A.data, dt)
+    if str(m) in manifest()["fd_generator_sha256"]:
+        h = hashlib.sha256()
+        for a in (A.indptr, A.indices, A.data):
+            h.update(np.ascontiguousarray(a).tobytes())
+        assert h.hexdigest() == manifest()["fd_generator_sha256"][str(m)]["sha256"]
+
+
+def test_jacobi_bitwise(psk):
+    d = load_golden("spmv.npz")
+    for tag in ("fd64", "dh8"):
+        A = golden_matrix(d, tag + "_")
+        M = psk.JacobiPreconditionerType().form(A)
+        v = d[tag + "_x"]
+        assert np.array_equal(M.applyRight(v), np.multiply(np.reciprocal(A.diagonal()), v))
+
+
+def test_blas1(psk):
+    from pysolvers_amd import _native as N
+    rng = np.random.default_rng(3)
+    for n in (1, 511, 512, 513, 100003):
+        x, y = rng.standard_normal(n), rng.standard_normal(n)
+        out = ctypes.c_double()
+        N.check(N.lib.psk_dot(n, N.ptr(x), N.ptr(y), N.PSK_HOST, ctypes.byref(out)), "dot")
+        assert abs(out.value - np.dot(x, y)) <= 1e-13 * np.abs(x) @ np.abs(y)
+        N.check(N.lib.psk_nrm2(n, N.ptr(x), N.PSK_HOST, ctypes.byref(out)), "nrm2")
+        assert abs(out.value - np.linalg.norm(x)) <= 1e-14 * np.linalg.norm(x)
+        yy = y.copy()
+        N.check(N.lib.psk_axpy(n, 0.37, N.ptr(x), N.ptr(yy), N.PSK_HOST), "axpy")
+        assert np.array_equal(yy, y + 0.37 * x)      # two roundings, as numpy
+
+
+# ---------------------------------------------------------------------------------------------
+# solvers vs the reference's golden runs
+
+def _check_against_golden(st, d, case):
+    assert st.iters() == case["iters"], (st.iters(), case["iters"])
+    assert bool(st.success()) == case["success"]
+    h_ref = d["hist"]
+    h = st.info["hist"]
+    assert len(h) == len(h_ref)
+    np.testing.assert_allclose(h, h_ref, rtol=RTOL_RESID, atol=0)
+    if case["resid"] is not None:
+        assert abs(st.resid() - case["resid"]) <= RTOL_RESID * abs(case["resid"])
+    if d["soln"].size:
+        err = np.linalg.norm(st.soln() - d["soln"]) / np.linalg.norm(d["soln"])
+        assert err <= 1e-8, err
+
+
+@pytest.mark.parametrize("case", solver_cases(), ids=lambda c: c["file"][:-4])
+def test_solver_matches_reference(psk, case):
+    d = load_golden(case["file"])
+    A = golden_matrix(d)
+    ctl = _ctl(maxiter=case["maxiter"], tau=case["tau"], failOnMaxiter=bool(case["fail_on_maxiter"]))
+    pt = psk.JacobiPreconditionerType() if case["jacobi"] else psk.IdentityPreconditionerType()
+    factory = psk.PCG if case["kind"] == "pcg" else psk.GMRES
+    st = factory(control=ctl, precond=pt).makeSolver().solve(A, d["b"])
+    _check_against_golden(st, d, case)
+
+
+@pytest.mark.parametrize("kind", ["pcg", "gmres"])
+def test_zero_rhs(psk, kind):
+    d = load_golden("pcg_dh8_identity.npz")
+    A = golden_matrix(d)
+    f = psk.PCG if kind == "pcg" else psk.GMRES
+    st = f(control=_ctl(maxiter=50)).makeSolver().solve(A, np.zeros(A.shape[0]))
+    assert st.success() and st.iters() == 1 and not np.any(st.soln())
+
+
+def test_pcg_breakdown_zero_matrix(psk):
+    # pTAp == 0 at k=0 -> handleBreakdown(0, ...) (PCGSolver.py:114-115): soln None, iters 0
+    A = sp.csr_matrix((5, 5))
+    st = psk.PCG(control=_ctl(maxiter=10)).makeSolver().solve(A, np.ones(5))
+    assert not st.success() and st.iters() == 0 and st.soln() is None and "p, Ap" in st.msg()
+
+
+def test_pcg_maxiter_zero(psk):
+    d = load_golden("pcg_dh8_identity.npz")
+    st = psk.PCG(control=_ctl(maxiter=0)).makeSolver().solve(golden_matrix(d), d["b"])
+    assert not st.success() and st.iters() == 0
+
+
+def test_device_resident_vectors(psk):
+    """b and x in HBM (DeviceVector): same answer as the host path."""
+    d = load_golden("pcg_fd64_jacobi.npz")
+    A = psk.DeviceCSR.from_scipy(golden_matrix(d))
+    s = psk.PCG(control=_ctl(maxiter=4000), precond=psk.Jacobi()).makeSolver()
+    st_h = s.solve(A, d["b"])
+    st_d = s.solve(A, psk.DeviceVector.from_numpy(d["b"]))
+    assert st_d.iters() == st_h.iters() == 177
+    assert np.array_equal(st_d.soln().numpy(), st_h.soln())
+
+
+def test_frozen_matrix_and_prec_reuse(psk):
+    d = load_golden("pcg_dh10_jacobi.npz")
+    A = golden_matrix(d)
+    s = psk.PCG(control=_ctl(maxiter=2000), precond=psk.Jacobi()).makeSolver()
+    s.freezeMatrix()
+    s.freezePrec()
+    a = s.solve(A, d["b"])
+    b = s.solve(A, d["b"])
+    assert a.iters() == b.iters() == 103 and np.array_equal(a.soln(), b.soln())
+
+
+def test_gmres_restarted_converges(psk):
+    d = load_golden("gmres_fd32_jacobi.npz")
+    A = golden_matrix(d)
+    st = psk.GMRES(control=_ctl(maxiter=2000, tau=1e-10), precond=psk.Jacobi(), restart=30).makeSolver().solve(
+        A, d["b"])
+    assert st.success()
+    r = d["b"] - A @ st.soln()
+    assert np.linalg.norm(r) <= 1e-10 * np.linalg.norm(d["b"])
+
+
+def test_gmres_maxiter_status(psk):
+    d = load_golden("gmres_dh8_identity.npz")
+    st = psk.GMRES(control=_ctl(maxiter=10)).makeSolver().solve(golden_matrix(d), d["b"])
+    assert not st.success() and st.iters() == 9 and st.msg() == "failure to converge"
+    np.testing.assert_allclose(st.info["hist"], d["hist"][:10], rtol=RTOL_RESID)
+
+
+# ---------------------------------------------------------------------------------------------
+# larger sizes: size-independent properties against the oracle
+
+def test_fd1024_pcg_jacobi_iterations(psk):
+    d = load_golden("large_fd1024.npz")
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, 1024)
+    b = psk.mvmult(dA, np.random.default_rng(12345).random(1024 * 1024))
+    assert np.array_equal(b[:4096], d["b_head"])
+    assert hashlib.sha256(b.tobytes()).hexdigest() == str(d["b_sha256"])
+    st = psk.PCG(control=_ctl(maxiter=4000), precond=psk.Jacobi()).makeSolver().solve(dA, b)
+    assert st.iters() == int(d["iters"])
+    np.testing.assert_allclose(st.info["hist"], d["hist"], rtol=RTOL_RESID)
+
+
+def test_fd4096_spmv_and_first_iterations(psk):
+    """configs[1] size (n = 16.7M): SpMV bit-exact vs the C oracle, 12 PCG+Jacobi steps vs the numpy oracle."""
+    from oracle import fdlap, krylov, native
+    m = 4096
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    x = np.random.default_rng(12345).random(m * m)
+    b = psk.mvmult(dA, x)
+    assert np.array_equal(b, native.csr_matvec(A, x))
+    ctl = _ctl(maxiter=12, tau=0.0, failOnMaxiter=False)
+    st = psk.PCG(control=ctl, precond=psk.Jacobi()).makeSolver().solve(dA, b)
+    ref = krylov.pcg(A, b, maxiter=12, tau=0.0, fail_on_maxiter=False, precond=krylov.jacobi_form(A))
+    assert st.iters() == ref["iters"] == 12
+    np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=RTOL_RESID)

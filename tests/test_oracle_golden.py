@@ -1,0 +1,91 @@
+"""The oracle (CPU restatement) against the golden vectors produced by the reference itself.
+
+tests/golden/make_golden.py ran the reference (krlong014/PySolvers) and asserted
+bit-identity with the oracle in the build container; these tests re-check the
+oracle against the committed vectors wherever the suite runs (another host's
+OpenBLAS may order its dot products differently, so solver outputs are compared
+with tight tolerances while SpMV / generator / Givens outputs must be exact).
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import golden_matrix, load_golden, manifest, solver_cases
+from oracle import fdlap, krylov, native
+
+
+def _sha(*arrs):
+    h = hashlib.sha256()
+    for a in arrs:
+        h.update(np.ascontiguousarray(a).tobytes())
+    return h.hexdigest()
+
+
+@pytest.mark.parametrize("m", [1, 2, 3, 5, 16])
+def test_fd_generator_arrays_exact(m):
+    d = load_golden("fd_generator.npz")
+    ip, ix, dt = fdlap.fd_laplacian_2d_arrays(-1.0, 1.0, m)
+    assert np.array_equal(ip, d["m%d_indptr" % m])
+    assert np.array_equal(ix, d["m%d_indices" % m])
+    assert np.array_equal(dt, d["m%d_data" % m])
+    assert np.array_equal(fdlap.fd_rowptr_closed_form(m, np.arange(m * m + 1)), ip)
+
+
+@pytest.mark.parametrize("m", ["64", "128", "300"])
+def test_fd_generator_hash(m):
+    ref = manifest()["fd_generator_sha256"][m]
+    ip, ix, dt = fdlap.fd_laplacian_2d_arrays(-1.0, 1.0, int(m))
+    assert len(dt) == ref["nnz"]
+    assert _sha(ip, ix, dt) == ref["sha256"]
+
+
+@pytest.mark.parametrize("tag", ["fd64", "dh8"])
+def test_spmv_exact(tag):
+    d = load_golden("spmv.npz")
+    A = golden_matrix(d, tag + "_")
+    y_ref = d[tag + "_y"]
+    assert np.array_equal(A @ d[tag + "_x"], y_ref)                       # scipy csr_matvec
+    assert np.array_equal(native.csr_matvec(A, d[tag + "_x"]), y_ref)     # plain-C restatement
+
+
+def test_csr_diagonal_exact():
+    d = load_golden("spmv.npz")
+    for tag in ("fd64", "dh8"):
+        A = golden_matrix(d, tag + "_")
+        assert np.array_equal(native.csr_diagonal(A), A.diagonal())
+
+
+def test_givens_selftest_exact():
+    d = load_golden("givens.npz")
+    H, g, CS, y = krylov.givens_triangularize(d["H"], d["g"])
+    assert np.array_equal(H, d["H_rot"]) and np.array_equal(g, d["g_rot"])
+    assert np.array_equal(CS, d["CS"]) and np.array_equal(y, d["y"])
+
+
+@pytest.mark.parametrize("case", solver_cases(), ids=lambda c: c["file"][:-4])
+def test_oracle_solvers_match_reference(case):
+    d = load_golden(case["file"])
+    A = golden_matrix(d)
+    b = d["b"]
+    assert np.array_equal(A @ d["x_exact"], b)
+    prec = krylov.jacobi_form(A) if case["jacobi"] else krylov.identity_apply
+    fn = krylov.pcg if case["kind"] == "pcg" else krylov.gmres
+    st = fn(A, b, maxiter=case["maxiter"], tau=case["tau"], fail_on_maxiter=bool(case["fail_on_maxiter"]),
+            precond=prec)
+    assert st["iters"] == case["iters"]
+    assert bool(st["success"]) == case["success"]
+    h = d["hist"]
+    assert len(st["hist"]) == len(h)
+    np.testing.assert_allclose(st["hist"], h, rtol=1e-10, atol=0)
+    if d["soln"].size:
+        np.testing.assert_allclose(st["soln"], d["soln"], rtol=1e-9, atol=1e-12 * np.abs(d["soln"]).max())
+
+
+def test_zero_rhs_convention():
+    d = load_golden("pcg_dh8_identity.npz")
+    A = golden_matrix(d)
+    for fn in (krylov.pcg, krylov.gmres):
+        st = fn(A, np.zeros(A.shape[0]))
+        assert st["iters"] == manifest()["zero_rhs"]["iters"] and st["success"]
+        assert not np.any(st["soln"])
