@@ -108,6 +108,7 @@ int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *cm, psk_cs
         return 5 * k - mk - top - (k + m - 1) / m - k / m;
     };
     A->nnz = fdrp(re) - fdrp(rb);
+    A->tile_rows = tile_rows_for(nloc, A->nnz);
     int rc = PSK_OK;
     if (hipMalloc(&A->rowptr, (size_t)(nloc + 1) * 4) != hipSuccess ||
         hipMalloc(&A->colidx, (size_t)A->nnz * 4) != hipSuccess ||

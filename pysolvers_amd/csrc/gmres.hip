@@ -239,7 +239,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     if (K < 1) K = 1;
     const int ld = (int)(K + 1);
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
-    const int gs = grid_for_rows(c, n, kTileRows);
+    const int gs = spmv_grid(c, A);
     const int gv = grid_for_rows(c, n, kVecTile);
     const size_t vec = aup((size_t)n * 8);
     const size_t qbytes = vec * (size_t)(K + 1);
@@ -282,7 +282,10 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     PSK_HIP(hipEventCreate(&ev0));
     PSK_HIP(hipEventCreate(&ev1));
     PSK_HIP(hipMemsetAsync(st, 0, sizeof(GmresState), s));
+    // Hessenberg and rotated copies start at zero: entries below the subdiagonal are never written
+    // and the least-squares solve reads them (HBar = np.zeros, GMRESSolver.py:80)
     PSK_HIP(hipMemsetAsync(H, 0, hb, s));
+    PSK_HIP(hipMemsetAsync(R, 0, hb, s));
     PSK_TRY(to_device_vec(b, loc, n, bv, s));
     PSK_HIP(hipMemsetAsync(x, 0, (size_t)n * 8, s));
     PSK_HIP(hipEventRecord(ev0, s));

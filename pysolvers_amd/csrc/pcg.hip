@@ -104,24 +104,26 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     double rr = 0.0, ur = 0.0;
     int64_t i = i0 + 2 * threadIdx.x;
+    // cache policy: x and Ap are dead after this kernel (non-temporal); r and p are re-read by K3
+#pragma unroll 2
     for (; i + 1 < i1; i += kVecTile) {                      // 16 B per lane per array
-        const double2 xv = *reinterpret_cast<const double2 *>(x + i);
-        const double2 pv = *reinterpret_cast<const double2 *>(p + i);
-        const double2 rv = *reinterpret_cast<const double2 *>(r + i);
-        const double2 av = *reinterpret_cast<const double2 *>(Ap + i);
-        double2 xn, rn;
+        const dv2 xv = ld2nt(x + i);
+        const dv2 pv = ld2(p + i);
+        const dv2 rv = ld2(r + i);
+        const dv2 av = ld2nt(Ap + i);
+        dv2 xn, rn;
         xn.x = xv.x + alpha * pv.x;                          // x = x + alpha*p   :121
         xn.y = xv.y + alpha * pv.y;
         rn.x = rv.x - alpha * av.x;                          // r = r - alpha*Ap  :122
         rn.y = rv.y - alpha * av.y;
         double u0 = rn.x, u1 = rn.y;
         if (dinv) {
-            const double2 dv = *reinterpret_cast<const double2 *>(dinv + i);
+            const dv2 dv = ld2(dinv + i);
             u0 = dv.x * rn.x;                                // u = precond.applyRight(r)  :123
             u1 = dv.y * rn.y;
         }
-        *reinterpret_cast<double2 *>(x + i) = xn;
-        *reinterpret_cast<double2 *>(r + i) = rn;
+        st2nt(x + i, xn);
+        st2(r + i, rn);
         rr = fma(rn.x, rn.x, rr);
         rr = fma(rn.y, rn.y, rr);
         ur = fma(u0, rn.x, ur);
@@ -169,19 +171,21 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     block_range((n + kVecTile - 1) / kVecTile, t0, t1);
     const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     int64_t i = i0 + 2 * threadIdx.x;
+    // r and dinv are not needed again this iteration (non-temporal); p is gathered by the next SpMV
+#pragma unroll 2
     for (; i + 1 < i1; i += kVecTile) {
-        const double2 rv = *reinterpret_cast<const double2 *>(r + i);
-        const double2 pv = *reinterpret_cast<const double2 *>(p + i);
+        const dv2 rv = ld2nt(r + i);
+        const dv2 pv = ld2(p + i);
         double u0 = rv.x, u1 = rv.y;
         if (dinv) {
-            const double2 dv = *reinterpret_cast<const double2 *>(dinv + i);
+            const dv2 dv = ld2nt(dinv + i);
             u0 = dv.x * rv.x;
             u1 = dv.y * rv.y;
         }
-        double2 pn;
+        dv2 pn;
         pn.x = u0 + beta * pv.x;                             // p = u + beta*p  :138
         pn.y = u1 + beta * pv.y;
-        *reinterpret_cast<double2 *>(p + i) = pn;
+        st2(p + i, pn);
     }
     if (i < i1) {
         const double u0 = dinv ? dinv[i] * r[i] : r[i];
@@ -247,7 +251,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     PcgWork w;
     PSK_TRY(pcg_workspace(A, maxiter, w));
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
-    const int gs = grid_for_rows(c, n, kTileRows);   // SpMV grid
+    const int gs = spmv_grid(c, A);   // SpMV grid
     const int gv = grid_for_rows(c, n, kVecTile);    // elementwise grid
 
     hipEvent_t ev0, ev1;

@@ -17,8 +17,7 @@ namespace psk {
 // launch geometry (CDNA4: 64-wide waves, 256 CUs in 8 XCDs)
 constexpr int kBlock = 256;            // threads per workgroup = 4 waves
 constexpr int kWaves = kBlock / 64;
-constexpr int kTileRows = 256;         // SpMV rows per tile (one row per thread for the row sums)
-constexpr int kChunk = 2048;           // SpMV LDS-staged products per chunk (16 KiB of f64)
+constexpr int kChunk = 1280;           // SpMV LDS-staged products per chunk (10 KiB of f64) = 256 FD rows
 constexpr int kMaxGrid = 2048;         // 256 CUs x 8 resident workgroups; partial arrays sized for it
 constexpr int kVecTile = 2 * kBlock;   // elementwise tile: 2 doubles (16 B) per lane
 
@@ -91,6 +90,7 @@ struct psk_csr {
     int64_t n = 0;        // local (owned) rows
     int64_t ncols = 0;    // local columns = n + halo
     int64_t nnz = 0;
+    int tile_rows = 256;  // SpMV rows per tile (psk::tile_rows_for)
     int32_t *rowptr = nullptr;
     int32_t *colidx = nullptr;
     double *vals = nullptr;
@@ -143,6 +143,15 @@ __device__ __forceinline__ double reduce_partials(const double *part, int np, in
     return block_sum(v, sh);
 }
 
+// 16-byte vector accesses; *_nt = non-temporal (streamed data that is not re-read soon)
+typedef double dv2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ dv2 ld2(const double *p) { return *reinterpret_cast<const dv2 *>(p); }
+__device__ __forceinline__ dv2 ld2nt(const double *p) {
+    return __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(p));
+}
+__device__ __forceinline__ void st2(double *p, dv2 v) { *reinterpret_cast<dv2 *>(p) = v; }
+__device__ __forceinline__ void st2nt(double *p, dv2 v) { __builtin_nontemporal_store(v, reinterpret_cast<dv2 *>(p)); }
+
 // contiguous share [b0,b1) of `ntiles` tiles for workgroup `b` of `g`
 __device__ __forceinline__ void block_range(int64_t ntiles, int64_t &t0, int64_t &t1) {
     const int64_t g = gridDim.x, b = blockIdx.x;
@@ -173,6 +182,8 @@ enum SpmvMode : int {
 };
 int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int64_t row_end,
               int64_t halo_lo_start, hipStream_t s);
+int tile_rows_for(int64_t n, int64_t nnz);
+int spmv_grid(const Context *c, const psk_csr *A);
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, int grid,
                 hipStream_t s);

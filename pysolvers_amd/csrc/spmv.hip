@@ -28,62 +28,99 @@ __device__ __forceinline__ int64_t logical_block() {
     return (b % 8) * (g / 8) + b / 8;
 }
 
+// Stream loads of colidx/vals (read once per SpMV) are non-temporal; the x gathers keep the default
+// policy so neighbouring grid lines are served from L2 / Infinity Cache (tools/spmv_lab.hip A/B:
+// nt on the stream +9-12% at n = 10M / 16.7M).
+__device__ __forceinline__ int32_t ld_stream(const int32_t *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ double ld_stream(const double *p) { return __builtin_nontemporal_load(p); }
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(
-    int64_t n, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
+    int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const double *__restrict__ vals, const double *__restrict__ x, double *__restrict__ y,
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, double *__restrict__ partial,
     const int32_t *__restrict__ done) {
     if (done != nullptr && *done != 0) return;
+    constexpr int KU = kChunk / kBlock;   // staged entries per lane per chunk
     __shared__ double prod[kChunk];
     __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
-    const int64_t ntiles = (n + kTileRows - 1) / kTileRows;
+    const int64_t ntiles = (n + trows - 1) / trows;
     const int64_t g = gridDim.x, lb = logical_block();
     const int64_t t0 = ntiles * lb / g, t1 = ntiles * (lb + 1) / g;
     double acc = 0.0;
-    constexpr int KU = kChunk / kBlock;   // 8 staged entries per lane per chunk
+
+    // issue the colidx/vals stream of the first chunk of tile t (branch-free, clamped to the tile)
+    int32_t cc[KU], ncc[KU];
+    double vv[KU], nvv[KU];
+    int32_t e0 = 0, e1 = 0;
+    auto issue = [&](int64_t t, int32_t &a, int32_t &b, int32_t *c_, double *v_) {
+        const int64_t r0 = t * trows, r1 = (r0 + trows < n) ? r0 + trows : n;
+        a = rowptr[r0];
+        b = rowptr[r1];
+        if (b > a) {   // wave-uniform; an empty tile issues nothing (and never reads past nnz)
+            const int32_t c1 = (b - a > kChunk) ? a + kChunk : b;
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                const int32_t e = a + k * kBlock + tid;
+                const int32_t ee = e < c1 ? e : a;
+                c_[k] = ld_stream(colidx + ee);
+                v_[k] = ld_stream(vals + ee);
+            }
+        }
+    };
+    if (t0 < t1) issue(t0, e0, e1, cc, vv);
 
     for (int64_t t = t0; t < t1; ++t) {
-        const int64_t r0 = t * kTileRows;
-        const int64_t r1 = (r0 + kTileRows < n) ? r0 + kTileRows : n;
+        const int64_t r0 = t * trows;
+        const int64_t r1 = (r0 + trows < n) ? r0 + trows : n;
         const int64_t row = r0 + tid;
-        const bool has = row < r1;
+        const bool has = tid < trows && row < r1;
         int32_t rs = 0, re = 0;
         if (has) {
             rs = rowptr[row];
             re = rowptr[row + 1];
         }
-        const int32_t e0 = rowptr[r0], e1 = rowptr[r1];
+        const int32_t ce0 = e0, ce1 = e1;
+        bool prefetched = false;
         double sum = 0.0;
-        for (int32_t c0 = e0; c0 < e1; c0 += kChunk) {
-            const int32_t c1 = (e1 - c0 > kChunk) ? c0 + kChunk : e1;
-            const int nk = (c1 - c0 + kBlock - 1) / kBlock;   // wave-uniform
-            int32_t ci[KU];
-            double vv[KU], xv[KU];
+        for (int32_t c0 = ce0; c0 < ce1; c0 += kChunk) {
+            const int32_t c1 = (ce1 - c0 > kChunk) ? c0 + kChunk : ce1;
+            if (c0 != ce0) {   // tile longer than one chunk: stream the next chunk now
+#pragma unroll
+                for (int k = 0; k < KU; ++k) {
+                    const int32_t e = c0 + k * kBlock + tid;
+                    const int32_t ee = e < c1 ? e : c0;
+                    cc[k] = ld_stream(colidx + ee);
+                    vv[k] = ld_stream(vals + ee);
+                }
+            }
+            double xv[KU], pv[KU];
 #pragma unroll
             for (int k = 0; k < KU; ++k) {
-                if (k < nk) {
-                    const int32_t e = c0 + k * kBlock + tid;
-                    const int32_t ee = e < c1 ? e : c0;   // branch-free: clamp to a valid entry
-                    ci[k] = colidx[ee];
-                    vv[k] = vals[ee];
+                double xx = x[cc[k]];
+                if (MODE == kSpmvJacobiDot) xx = aux_d[cc[k]] * xx;   // (DInv*q)[c], rounded
+                xv[k] = xx;
+            }
+            // software pipeline: the next tile's stream is in flight while this tile's gathers land
+            const bool pf = c1 == ce1 && t + 1 < t1;
+            if (pf) {
+                issue(t + 1, e0, e1, ncc, nvv);
+                prefetched = true;
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) pv[k] = vv[k] * xv[k];   // rounded product
+            if (pf) {
+#pragma unroll
+                for (int k = 0; k < KU; ++k) {
+                    cc[k] = ncc[k];
+                    vv[k] = nvv[k];
                 }
             }
 #pragma unroll
             for (int k = 0; k < KU; ++k) {
-                if (k < nk) {
-                    double xx = x[ci[k]];
-                    if (MODE == kSpmvJacobiDot) xx = aux_d[ci[k]] * xx;   // (DInv*q)[c], rounded
-                    xv[k] = xx;
-                }
-            }
-#pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                if (k < nk) {
-                    const int32_t e = c0 + k * kBlock + tid;
-                    if (e < c1) prod[k * kBlock + tid] = vv[k] * xv[k];   // rounded product
-                }
+                const int32_t e = c0 + k * kBlock + tid;
+                if (e < c1) prod[k * kBlock + tid] = pv[k];
             }
             __syncthreads();
             const int32_t a = rs > c0 ? rs : c0;
@@ -91,13 +128,14 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
             __syncthreads();
         }
+        if (!prefetched && t + 1 < t1) issue(t + 1, e0, e1, cc, vv);   // empty tile
         if (has) {
             if (MODE == kSpmvResid) {
                 const double r = aux_q[row] - sum;   // b - A*x (GMRESSolver.py:163)
                 y[row] = r;
                 acc = fma(r, r, acc);
             } else {
-                y[row] = sum;
+                __builtin_nontemporal_store(sum, y + row);
                 if (MODE == kSpmvDot) acc = fma(x[row], sum, acc);
                 if (MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot) acc = fma(aux_q[row], sum, acc);
             }
@@ -109,30 +147,48 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     }
 }
 
+int tile_rows_for(int64_t n, int64_t nnz) {
+    // rows per tile so that a typical tile's entries fit one LDS chunk
+    const double avg = n > 0 ? (double)nnz / (double)n : 1.0;
+    int r = kBlock;
+    while (r > 32 && avg * r > kChunk) r >>= 1;
+    return r;
+}
+
+int spmv_grid(const Context *c, const psk_csr *A) {
+    const int64_t tiles = (A->n + A->tile_rows - 1) / A->tile_rows;
+    int cap = c->num_cus * 4;   // 4 workgroups per CU streamed best (spmv_lab: g1024-1536)
+    cap -= cap % 8;
+    if (cap < 8) cap = 8;
+    if (cap > kMaxGrid) cap = kMaxGrid;
+    return (int)(tiles < cap ? (tiles < 1 ? 1 : tiles) : cap);
+}
+
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, int grid,
                 hipStream_t s) {
     if (A->n == 0) return PSK_OK;
     dim3 gd(grid), bd(kBlock);
+    const int tr = A->tile_rows;
     switch (mode) {
     case kSpmvPlain:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvPlain>, gd, bd, 0, s, A->n, A->rowptr, A->colidx, A->vals,
+        hipLaunchKernelGGL(spmv_kernel<kSpmvPlain>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
                            x, y, aux_d, aux_q, partial, done_flag);
         break;
     case kSpmvDot:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvDot>, gd, bd, 0, s, A->n, A->rowptr, A->colidx, A->vals,
+        hipLaunchKernelGGL(spmv_kernel<kSpmvDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
                            x, y, aux_d, aux_q, partial, done_flag);
         break;
     case kSpmvJacobiDot:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvJacobiDot>, gd, bd, 0, s, A->n, A->rowptr, A->colidx,
+        hipLaunchKernelGGL(spmv_kernel<kSpmvJacobiDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
                            A->vals, x, y, aux_d, aux_q, partial, done_flag);
         break;
     case kSpmvPlainDot:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvPlainDot>, gd, bd, 0, s, A->n, A->rowptr, A->colidx,
+        hipLaunchKernelGGL(spmv_kernel<kSpmvPlainDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
                            A->vals, x, y, aux_d, aux_q, partial, done_flag);
         break;
     case kSpmvResid:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, A->rowptr, A->colidx, A->vals,
+        hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
                            x, y, aux_d, aux_q, partial, done_flag);
         break;
     default:
@@ -296,6 +352,7 @@ int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t 
     A->n = n;
     A->ncols = n;
     A->nnz = nnz;
+    A->tile_rows = tile_rows_for(n, nnz);
     A->n_global = n;
     A->row_begin = 0;
     A->row_end = n;
@@ -333,6 +390,7 @@ int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out) {
     A->n = n;
     A->ncols = n;
     A->nnz = nnz;
+    A->tile_rows = tile_rows_for(n, nnz);
     A->n_global = n;
     A->row_end = n;
     A->device = c->device;
@@ -396,7 +454,7 @@ int psk_spmv(const psk_csr *Ac, const double *x, double *y, int32_t loc) {
         dx = tx;
         dy = (loc == PSK_HOST) ? tx + A->ncols : y;
     }
-    const int grid = grid_for_rows(c, A->n, kTileRows);
+    const int grid = spmv_grid(c, A);
     PSK_TRY(launch_spmv(A, kSpmvPlain, dx, dy, nullptr, nullptr, nullptr, nullptr, grid, c->stream));
     if (loc == PSK_HOST) PSK_TRY(from_device_vec(dy, PSK_HOST, A->n, y, c->stream));
     PSK_HIP(hipStreamSynchronize(c->stream));

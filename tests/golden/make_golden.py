@@ -124,6 +124,43 @@ def _check_same(tag, res, hist, orc):
         assert float(res.resid()) == float(orc["resid"]), tag
 
 
+def sensitivity(kind, A, b, maxiter, tau, fom, jac, hist_ref, soln_ref, seeds=8):
+    """How far the reference path itself moves when every dot/norm is perturbed by <= 1 ulp.
+
+    Runs the oracle (bit-identical to the reference) with np.dot / npla.norm results multiplied by
+    (1 + e), e in {-2^-52, 0, 2^-52}, for `seeds` random draws. Returns the max over seeds of
+    max_k |hist_k - hist_ref_k| / ||b|| and of ||x - x_ref|| / ||x_ref||, plus whether every
+    perturbed run kept the reference's iteration count. This is the floor any re-implementation
+    with a different (even exact) dot rounding can be held to.
+    """
+    import math
+    import numpy.linalg as npla_
+    od, on = krylov.np.dot, krylov.npla.norm
+    nb = np.linalg.norm(b)
+    dh, dx, same = 0.0, 0.0, True
+    for seed in range(seeds):
+        rng = np.random.default_rng(1000 + seed)
+
+        def pdot(a, c):
+            return od(a, c) * (1.0 + rng.choice([-1.0, 0.0, 1.0]) * 2.0 ** -52)
+        krylov.np.dot = pdot
+        krylov.npla.norm = lambda v: math.sqrt(pdot(v, v))
+        try:
+            prec = krylov.jacobi_form(A) if jac else krylov.identity_apply
+            fn = krylov.pcg if kind == "pcg" else krylov.gmres
+            st = fn(A, b, maxiter=maxiter, tau=tau, fail_on_maxiter=fom, precond=prec)
+        finally:
+            krylov.np.dot, krylov.npla.norm = od, on
+        h = st["hist"]
+        m = min(len(h), len(hist_ref))
+        same &= len(h) == len(hist_ref)
+        if m:
+            dh = max(dh, float(np.max(np.abs(h[:m] - hist_ref[:m])) / nb))
+        if soln_ref is not None and st["soln"] is not None and np.linalg.norm(soln_ref) > 0:
+            dx = max(dx, float(np.linalg.norm(st["soln"] - soln_ref) / np.linalg.norm(soln_ref)))
+    return dict(hist_over_normb=dh, x_rel=dx, iters_stable=bool(same))
+
+
 def _csr_arrays(A):
     A = A.tocsr()
     return dict(indptr=A.indptr.astype(np.int32), indices=A.indices.astype(np.int32),
@@ -242,8 +279,9 @@ def main():
                           maxiter=maxiter, tau=tau, fail_on_maxiter=fom, jacobi=jac,
                           iters=int(res.iters()), success=bool(res.success()),
                           resid=None if res.resid() is None else float(res.resid()),
-                          final_ratio=float(hist[-1] / np.linalg.norm(b)) if len(hist) else None))
-        print("%-40s iters=%5d success=%s" % (tag, res.iters(), res.success()))
+                          final_ratio=float(hist[-1] / np.linalg.norm(b)) if len(hist) else None,
+                          sensitivity=sensitivity(kind, A, b, maxiter, tau, fom, jac, hist, res.soln())))
+        print("%-40s iters=%5d success=%s sens=%s" % (tag, res.iters(), res.success(), index[-1]["sensitivity"]))
 
     # b = 0 (PCGSolver.py:86-88, GMRESSolver.py:66-68): iters=1, x=0
     A = _dh(8)

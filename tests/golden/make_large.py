@@ -33,9 +33,13 @@ def main(m=1024):
     orc = krylov.pcg(A, b, maxiter=4000, tau=1e-8, precond=krylov.jacobi_form(A))
     mg._check_same("fd%d" % m, res, hist, orc)
     print("reference PCG+Jacobi m=%d: iters=%d (%.0f s)" % (m, res.iters(), time.time() - t))
+    sens = mg.sensitivity("pcg", A, b, 4000, 1e-8, True, True, hist, res.soln(), seeds=3)
+    print("sensitivity", sens)
     np.savez_compressed(os.path.join(HERE, "large_fd%d.npz" % m), iters=np.int64(res.iters()), hist=hist,
                         b_head=b[:4096], b_sha256=np.array(hashlib.sha256(b.tobytes()).hexdigest()),
-                        resid=np.float64(res.resid()), m=np.int64(m))
+                        resid=np.float64(res.resid()), m=np.int64(m),
+                        sens_hist=np.float64(sens["hist_over_normb"]), sens_x=np.float64(sens["x_rel"]),
+                        soln_head=res.soln()[:4096], soln_norm=np.float64(np.linalg.norm(res.soln())))
 
 
 if __name__ == "__main__":

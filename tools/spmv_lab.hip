@@ -1,0 +1,461 @@
+// spmv_lab.hip — A/B harness for CSR SpMV schedules on gfx950 (development tool, not shipped).
+// Builds FDLaplacian2D(m) on the device, runs every variant, checks each is bit-identical to
+// variant A (scipy csr_matvec order), and times them in interleaved rounds in one process.
+//   hipcc -O3 --offload-arch=gfx950 -ffp-contract=off -o spmv_lab tools/spmv_lab.hip
+//   ./spmv_lab 3163 4096
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+constexpr int BS = 256;
+constexpr int PAD = 1024;   // padding entries after colidx/vals (vector loads may run past nnz)
+
+__device__ __forceinline__ int64_t lblock() {
+    const int64_t g = gridDim.x, b = blockIdx.x;
+    if (g % 8 != 0) return b;
+    return (b % 8) * (g / 8) + b / 8;
+}
+
+// ---------------- A: block tiles of 256 rows, 2048-entry LDS chunks (current libpsk) ---------------
+__global__ __launch_bounds__(BS) void spmv_A(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                             const double* __restrict__ va, const double* __restrict__ x,
+                                             double* __restrict__ y) {
+    constexpr int CH = 2048, KU = CH / BS;
+    __shared__ double prod[CH];
+    const int tid = threadIdx.x;
+    const int64_t nt = (n + 255) / 256, g = gridDim.x, lb = lblock();
+    const int64_t t0 = nt * lb / g, t1 = nt * (lb + 1) / g;
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n, row = r0 + tid;
+        const bool has = row < r1;
+        int rs = 0, re = 0;
+        if (has) { rs = rp[row]; re = rp[row + 1]; }
+        const int e0 = rp[r0], e1 = rp[r1];
+        double sum = 0.0;
+        for (int c0 = e0; c0 < e1; c0 += CH) {
+            const int c1 = e1 - c0 > CH ? c0 + CH : e1;
+            const int nk = (c1 - c0 + BS - 1) / BS;
+            int cc[KU]; double vv[KU], xv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) { int e = c0 + k * BS + tid; int ee = e < c1 ? e : c0; cc[k] = ci[ee]; vv[k] = va[ee]; }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) xv[k] = x[cc[k]];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) { int e = c0 + k * BS + tid; if (e < c1) prod[k * BS + tid] = vv[k] * xv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            __syncthreads();
+        }
+        if (has) y[row] = sum;
+    }
+}
+
+// ---------------- A2: A with the next tile's colidx/vals prefetched into registers --------------------
+template <int CH, bool NT>
+__global__ __launch_bounds__(BS) void spmv_A2(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                              const double* __restrict__ va, const double* __restrict__ x,
+                                              double* __restrict__ y) {
+    constexpr int KU = CH / BS;
+    __shared__ double prod[CH];
+    const int tid = threadIdx.x;
+    const int64_t nt = (n + 255) / 256, g = gridDim.x, lb = lblock();
+    const int64_t t0 = nt * lb / g, t1 = nt * (lb + 1) / g;
+    auto ld_i = [](const int* p) { return NT ? __builtin_nontemporal_load(p) : *p; };
+    auto ld_d = [](const double* p) { return NT ? __builtin_nontemporal_load(p) : *p; };
+    int cc[KU]; double vv[KU];
+    int ncc[KU]; double nvv[KU];
+    int e0 = 0, e1 = 0;
+    auto issue = [&](int64_t t, int& a, int& b, int* c_, double* v_) {
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n;
+        a = rp[r0]; b = rp[r1];
+        const int c1 = b - a > CH ? a + CH : b;
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { int e = a + k * BS + tid; int ee = e < c1 ? e : a; c_[k] = ld_i(ci + ee); v_[k] = ld_d(va + ee); }
+    };
+    if (t0 < t1) issue(t0, e0, e1, cc, vv);
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n, row = r0 + tid;
+        const bool has = row < r1;
+        int rs = 0, re = 0;
+        if (has) { rs = rp[row]; re = rp[row + 1]; }
+        double sum = 0.0;
+        const int ce0 = e0, ce1 = e1;
+        for (int c0 = ce0; c0 < ce1; c0 += CH) {
+            const int c1 = ce1 - c0 > CH ? c0 + CH : ce1;
+            if (c0 != ce0) {   // rare: tile longer than one chunk
+#pragma unroll
+                for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; int ee = e < c1 ? e : c0; cc[k] = ld_i(ci + ee); vv[k] = ld_d(va + ee); }
+            }
+            double xv[KU], pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) xv[k] = x[cc[k]];
+            const bool pf = c1 == ce1 && t + 1 < t1;
+            if (pf) issue(t + 1, e0, e1, ncc, nvv);       // next tile's stream issued before the gathers land
+#pragma unroll
+            for (int k = 0; k < KU; ++k) pv[k] = vv[k] * xv[k];
+            if (pf) {
+#pragma unroll
+                for (int k = 0; k < KU; ++k) { cc[k] = ncc[k]; vv[k] = nvv[k]; }
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; if (e < c1) prod[k * BS + tid] = pv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            __syncthreads();
+        }
+        if (has) { if (NT) __builtin_nontemporal_store(sum, y + row); else y[row] = sum; }
+    }
+}
+
+__global__ __launch_bounds__(BS) void copy4(int64_t n, const double* __restrict__ a, double* __restrict__ b) {
+    const int64_t nt = n / 2, stride = (int64_t)gridDim.x * BS;
+    const double2* s = reinterpret_cast<const double2*>(a);
+    double2* d = reinterpret_cast<double2*>(b);
+    int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
+    for (; i + 3 * stride < nt; i += 4 * stride) {
+        double2 v0 = s[i], v1 = s[i + stride], v2 = s[i + 2 * stride], v3 = s[i + 3 * stride];
+        d[i] = v0; d[i + stride] = v1; d[i + 2 * stride] = v2; d[i + 3 * stride] = v3;
+    }
+    for (; i < nt; i += stride) d[i] = s[i];
+}
+
+typedef double dv2 __attribute__((ext_vector_type(2)));
+
+template <int U, bool NT>
+__global__ __launch_bounds__(BS) void readU(int64_t n, const double* __restrict__ a, double* __restrict__ out) {
+    const int64_t nt = n / 2, stride = (int64_t)gridDim.x * BS;
+    const dv2* s = reinterpret_cast<const dv2*>(a);
+    double acc = 0.0;
+    int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
+    for (; i + (U - 1) * stride < nt; i += U * stride) {
+        dv2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(s + i + u * stride) : s[i + u * stride];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y;
+    }
+    if (acc == 12345.678) out[0] = acc;
+}
+
+// contiguous-range reader: each block streams its own contiguous slab (like the SpMV tiles)
+template <int U, bool NT>
+__global__ __launch_bounds__(BS) void readSlab(int64_t n, const double* __restrict__ a, double* __restrict__ out) {
+    const int64_t nt = n / 2, per = (nt + gridDim.x - 1) / gridDim.x;
+    const int64_t b0 = blockIdx.x * per, b1 = b0 + per < nt ? b0 + per : nt;
+    const dv2* s = reinterpret_cast<const dv2*>(a);
+    double acc = 0.0;
+    int64_t i = b0 + threadIdx.x;
+    for (; i + (U - 1) * BS < b1; i += U * BS) {
+        dv2 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(s + i + u * BS) : s[i + u * BS];
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += v[u].x + v[u].y;
+    }
+    for (; i < b1; i += BS) acc += s[i].x;
+    if (acc == 12345.678) out[0] = acc;
+}
+
+__global__ __launch_bounds__(BS) void read4(int64_t n, const double* __restrict__ a, double* __restrict__ out) {
+    const int64_t nt = n / 2, stride = (int64_t)gridDim.x * BS;
+    const double2* s = reinterpret_cast<const double2*>(a);
+    double acc = 0.0;
+    int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x;
+    for (; i + 3 * stride < nt; i += 4 * stride) {
+        double2 v0 = s[i], v1 = s[i + stride], v2 = s[i + 2 * stride], v3 = s[i + 3 * stride];
+        acc += v0.x + v1.y + v2.x + v3.y;
+    }
+    if (acc == 12345.678) out[0] = acc;
+}
+
+// ---------------- B: wave-local tiles (RPW rows per wave), no block barriers ------------------------
+template <int RPW, int CH>
+__global__ __launch_bounds__(BS) void spmv_B(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                             const double* __restrict__ va, const double* __restrict__ x,
+                                             double* __restrict__ y) {
+    constexpr int KU = CH / 64, RPL = RPW / 64;
+    __shared__ double slab[4][CH];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double* prod = slab[w];
+    const int64_t nt = (n + RPW - 1) / RPW, gw = (int64_t)gridDim.x * 4, wid = lblock() * 4 + w;
+    const int64_t t0 = nt * wid / gw, t1 = nt * (wid + 1) / gw;
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t r0 = t * RPW, r1 = r0 + RPW < n ? r0 + RPW : n;
+        int rs[RPL], re[RPL];
+        double sum[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int64_t row = r0 + q * 64 + lane;
+            rs[q] = 0; re[q] = 0; sum[q] = 0.0;
+            if (row < r1) { rs[q] = rp[row]; re[q] = rp[row + 1]; }
+        }
+        const int e0 = __builtin_amdgcn_readfirstlane(rp[r0]);
+        const int e1 = __builtin_amdgcn_readfirstlane(rp[r1]);
+        for (int c0 = e0; c0 < e1; c0 += CH) {
+            const int c1 = e1 - c0 > CH ? c0 + CH : e1;
+            const int nk = (c1 - c0 + 63) / 64;
+            int cc[KU]; double vv[KU], xv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) { int e = c0 + k * 64 + lane; int ee = e < c1 ? e : c0; cc[k] = ci[ee]; vv[k] = va[ee]; }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) xv[k] = x[cc[k]];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) { int e = c0 + k * 64 + lane; if (e < c1) prod[k * 64 + lane] = vv[k] * xv[k]; }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const int a = rs[q] > c0 ? rs[q] : c0, b = re[q] < c1 ? re[q] : c1;
+                for (int e = a; e < b; ++e) sum[q] = sum[q] + prod[e - c0];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int64_t row = r0 + q * 64 + lane;
+            if (row < r1) y[row] = sum[q];
+        }
+    }
+}
+
+// ---------------- C: wave-local tiles + 16-byte loads (4 entries per lane per step) -----------------
+template <int RPW, int CH>
+__global__ __launch_bounds__(BS) void spmv_C(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                             const double* __restrict__ va, const double* __restrict__ x,
+                                             double* __restrict__ y) {
+    constexpr int KU = CH / 256, RPL = RPW / 64;   // 4 entries per lane per k
+    __shared__ double slab[4][CH + 4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double* prod = slab[w];
+    const int64_t nt = (n + RPW - 1) / RPW, gw = (int64_t)gridDim.x * 4, wid = lblock() * 4 + w;
+    const int64_t t0 = nt * wid / gw, t1 = nt * (wid + 1) / gw;
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t r0 = t * RPW, r1 = r0 + RPW < n ? r0 + RPW : n;
+        int rs[RPL], re[RPL];
+        double sum[RPL];
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int64_t row = r0 + q * 64 + lane;
+            rs[q] = 0; re[q] = 0; sum[q] = 0.0;
+            if (row < r1) { rs[q] = rp[row]; re[q] = rp[row + 1]; }
+        }
+        const int e0 = __builtin_amdgcn_readfirstlane(rp[r0]);
+        const int e1 = __builtin_amdgcn_readfirstlane(rp[r1]);
+        for (int c0 = e0, c1 = 0; c0 < e1; c0 = c1) {
+            const int a0 = c0 & ~3;                       // 16-B aligned start (entries [a0,c0) ignored)
+            c1 = e1 - a0 > CH ? a0 + CH : e1;
+            const int nk = (c1 - a0 + 255) / 256;
+            int4 cc[KU]; double2 v0[KU], v1[KU]; double xv[KU][4];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) {
+                const int e = a0 + 4 * (k * 64 + lane);
+                cc[k] = *reinterpret_cast<const int4*>(ci + e);
+                v0[k] = *reinterpret_cast<const double2*>(va + e);
+                v1[k] = *reinterpret_cast<const double2*>(va + e + 2);
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) {
+                xv[k][0] = x[cc[k].x]; xv[k][1] = x[cc[k].y]; xv[k][2] = x[cc[k].z]; xv[k][3] = x[cc[k].w];
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) if (k < nk) {
+                const int e = a0 + 4 * (k * 64 + lane);
+                const double p0 = v0[k].x * xv[k][0], p1 = v0[k].y * xv[k][1];
+                const double p2 = v1[k].x * xv[k][2], p3 = v1[k].y * xv[k][3];
+                // slab index = e - a0 (+ alignment slack); entries outside [c0,c1) are never read
+                double* d = prod + (e - a0);
+                if (e < c1 + 0) { d[0] = p0; d[1] = p1; d[2] = p2; d[3] = p3; }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+            for (int q = 0; q < RPL; ++q) {
+                const int a = rs[q] > c0 ? rs[q] : c0, b = re[q] < c1 ? re[q] : c1;
+                for (int e = a; e < b; ++e) sum[q] = sum[q] + prod[e - a0];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int64_t row = r0 + q * 64 + lane;
+            if (row < r1) y[row] = sum[q];
+        }
+    }
+}
+
+// ---------------- E: thread per row, direct loads, up to 8 entries in registers ---------------------
+__global__ __launch_bounds__(BS) void spmv_E(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                             const double* __restrict__ va, const double* __restrict__ x,
+                                             double* __restrict__ y) {
+    const int64_t nt = (n + BS - 1) / BS, g = gridDim.x, lb = lblock();
+    const int64_t t0 = nt * lb / g, t1 = nt * (lb + 1) / g;
+    for (int64_t t = t0; t < t1; ++t) {
+        const int64_t row = t * BS + threadIdx.x;
+        if (row >= n) continue;
+        const int rs = rp[row], re = rp[row + 1];
+        double sum = 0.0;
+        for (int c = rs; c < re; c += 8) {
+            int cc[8]; double vv[8], xv[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { int e = c + j < re ? c + j : rs; cc[j] = ci[e]; vv[j] = va[e]; }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] = x[cc[j]];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) if (c + j < re) { const double pr = vv[j] * xv[j]; sum = sum + pr; }
+        }
+        y[row] = sum;
+    }
+}
+
+// ---------------- bandwidth references ------------------------------------------------------------------
+__global__ __launch_bounds__(BS) void copy2(int64_t n, const double* __restrict__ a, double* __restrict__ b) {
+    const int64_t nt = n / 2;
+    for (int64_t i = (int64_t)blockIdx.x * BS + threadIdx.x; i < nt; i += (int64_t)gridDim.x * BS)
+        reinterpret_cast<double2*>(b)[i] = reinterpret_cast<const double2*>(a)[i];
+}
+
+__global__ void fd2d(int64_t m, int* rp, int* ci, double* va, double dv, double ov) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, n = m * m;
+    if (k > n) return;
+    int64_t mk = k < m ? k : m, top = k - m * (m - 1); if (top < 0) top = 0;
+    const int64_t off = 5 * k - mk - top - (k + m - 1) / m - k / m;
+    rp[k] = (int)off;
+    if (k == n) return;
+    const int64_t ix = k % m, iy = k / m;
+    int64_t p = off;
+    ci[p] = (int)k; va[p++] = dv;
+    if (iy > 0) { ci[p] = (int)(k - m); va[p++] = ov; }
+    if (iy < m - 1) { ci[p] = (int)(k + m); va[p++] = ov; }
+    if (ix > 0) { ci[p] = (int)(k - 1); va[p++] = ov; }
+    if (ix < m - 1) { ci[p] = (int)(k + 1); va[p++] = ov; }
+}
+
+__global__ void fillx(int64_t n, double* x) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) { uint64_t h = (uint64_t)i * 0x9E3779B97F4A7C15ull; h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
+        x[i] = (double)(h >> 11) * (1.0 / 9007199254740992.0); }
+}
+
+typedef void (*Kern)(int64_t, const int*, const int*, const double*, const double*, double*);
+typedef void (*Kern2)(int64_t, const double*, double*);
+
+int main(int argc, char** argv) {
+    std::vector<int64_t> ms;
+    for (int i = 1; i < argc; ++i) ms.push_back(atoll(argv[i]));
+    if (ms.empty()) ms = {3163, 4096};
+    struct V { const char* name; Kern k; int grid; };
+    for (int64_t m : ms) {
+        const int64_t n = m * m, nnz = 5 * n - 4 * m;
+        int *rp, *ci; double *va, *x, *y, *yr;
+        CK(hipMalloc(&rp, (n + 1) * 4)); CK(hipMalloc(&ci, (nnz + PAD) * 4)); CK(hipMalloc(&va, (nnz + PAD) * 8));
+        CK(hipMalloc(&x, n * 8)); CK(hipMalloc(&y, n * 8)); CK(hipMalloc(&yr, n * 8));
+        CK(hipMemset(ci + nnz, 0, PAD * 4)); CK(hipMemset(va + nnz, 0, PAD * 8));
+        const double h = 2.0 / (double)(m + 1);
+        fd2d<<<(n + 256) / 256, 256>>>(m, rp, ci, va, -4.0 / h / h, 1.0 / h / h);
+        fillx<<<(n + 255) / 256, 256>>>(n, x);
+        CK(hipDeviceSynchronize());
+        const double bytes = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
+        std::vector<V> vs = {
+            {"A blk256/ch2048", spmv_A, 2048},
+            {"A2 pf ch1536 nt g512", spmv_A2<1536, true>, 512},
+            {"A2 pf ch1536 nt g768", spmv_A2<1536, true>, 768},
+            {"A2 pf ch1536 nt g1024", spmv_A2<1536, true>, 1024},
+            {"A2 pf ch1536 nt g1536", spmv_A2<1536, true>, 1536},
+            {"A2 pf ch1536 nt g2048", spmv_A2<1536, true>, 2048},
+            {"A2 pf ch2048 nt g1024", spmv_A2<2048, true>, 1024},
+            {"A2 pf ch1280 nt g1024", spmv_A2<1280, true>, 1024},
+        };
+        // reference result
+        spmv_A<<<2048, BS>>>(n, rp, ci, va, x, yr);
+        CK(hipDeviceSynchronize());
+        std::vector<double> hr(n), hy(n);
+        CK(hipMemcpy(hr.data(), yr, n * 8, hipMemcpyDeviceToHost));
+        for (auto& v : vs) {
+            CK(hipMemset(y, 0xff, n * 8));
+            v.k<<<v.grid, BS>>>(n, rp, ci, va, x, y);
+            CK(hipDeviceSynchronize());
+            CK(hipMemcpy(hy.data(), y, n * 8, hipMemcpyDeviceToHost));
+            const bool same = memcmp(hr.data(), hy.data(), n * 8) == 0;
+            printf("m=%ld %-24s bitwise=%s\n", (long)m, v.name, same ? "yes" : "NO");
+        }
+        hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+        std::vector<std::vector<float>> t(vs.size());
+        const int R = 7, L = 20;
+        for (int r = 0; r < R; ++r) {
+            for (size_t i = 0; i < vs.size(); ++i) {
+                CK(hipEventRecord(e0));
+                for (int l = 0; l < L; ++l) vs[i].k<<<vs[i].grid, BS>>>(n, rp, ci, va, x, y);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1)); t[i].push_back(ms / L);
+            }
+        }
+        for (size_t i = 0; i < vs.size(); ++i) {
+            std::sort(t[i].begin(), t[i].end());
+            printf("m=%ld %-24s min %.1f us med %.1f us  -> %.0f GB/s (%.1f%% of 8 TB/s)\n", (long)m, vs[i].name,
+                   t[i][0] * 1e3, t[i][R / 2] * 1e3, bytes / (t[i][0] * 1e-3) / 1e9, 100.0 * bytes / (t[i][0] * 1e-3) / 8e12);
+        }
+        // stream copy reference: 2 x 8n bytes... use a dedicated buffer pair of size nnz doubles
+        double *a2, *b2; const int64_t cn = nnz;
+        CK(hipMalloc(&a2, cn * 8)); CK(hipMalloc(&b2, cn * 8)); CK(hipMemset(a2, 0, cn * 8));
+        float best = 1e9;
+        for (int r = 0; r < R; ++r) {
+            CK(hipEventRecord(e0));
+            for (int l = 0; l < L; ++l) copy2<<<4096, BS>>>(cn, a2, b2);
+            CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = std::min(best, ms / L);
+        }
+        printf("m=%ld copy %ld doubles: %.1f us -> %.0f GB/s\n", (long)m, (long)cn, best * 1e3, 16.0 * cn / (best * 1e-3) / 1e9);
+        {
+            struct RV { const char* name; Kern2 k; int grid; };
+            std::vector<RV> rv = {
+                {"readU4", readU<4, false>, 2048}, {"readU4 nt", readU<4, true>, 2048},
+                {"readU8 nt", readU<8, true>, 2048}, {"readU8 nt g1024", readU<8, true>, 1024},
+                {"readU8 nt g4096", readU<8, true>, 4096}, {"readSlab4 nt g1024", readSlab<4, true>, 1024},
+                {"readSlab8 nt g1024", readSlab<8, true>, 1024}, {"readSlab8 g1024", readSlab<8, false>, 1024},
+                {"readSlab8 nt g2048", readSlab<8, true>, 2048},
+            };
+            for (auto& v : rv) {
+                float b = 1e9;
+                for (int r = 0; r < R; ++r) {
+                    CK(hipEventRecord(e0));
+                    for (int l = 0; l < L; ++l) v.k<<<v.grid, BS>>>(cn, a2, b2);
+                    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                    float ms; CK(hipEventElapsedTime(&ms, e0, e1)); b = std::min(b, ms / L);
+                }
+                printf("m=%ld %-22s %.0f GB/s\n", (long)m, v.name, 8.0 * cn / (b * 1e-3) / 1e9);
+            }
+        }
+        for (int grid : {1024, 8192}) {
+            float bc = 1e9, br = 1e9;
+            for (int r = 0; r < R; ++r) {
+                CK(hipEventRecord(e0));
+                for (int l = 0; l < L; ++l) copy4<<<grid, BS>>>(cn, a2, b2);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                float ms; CK(hipEventElapsedTime(&ms, e0, e1)); bc = std::min(bc, ms / L);
+                CK(hipEventRecord(e0));
+                for (int l = 0; l < L; ++l) read4<<<grid, BS>>>(cn, a2, b2);
+                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                CK(hipEventElapsedTime(&ms, e0, e1)); br = std::min(br, ms / L);
+            }
+            printf("m=%ld copy4 g%d: %.0f GB/s   read4: %.0f GB/s\n", (long)m, grid, 16.0 * cn / (bc * 1e-3) / 1e9,
+                   8.0 * cn / (br * 1e-3) / 1e9);
+        }
+        CK(hipFree(a2)); CK(hipFree(b2));
+        CK(hipFree(rp)); CK(hipFree(ci)); CK(hipFree(va)); CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(yr));
+    }
+    return 0;
+}
