@@ -22,20 +22,32 @@ def fd_laplacian_2d_arrays(a, b, m):
     h = np.abs(b - a) / np.double(m + 1)          # FDLaplacian2D.py:6
     diag = -4.0 / h / h                           # :13
     off = 1.0 / h / h                             # :15-21
-    k = np.arange(n, dtype=np.int64)
+    it = np.int32 if 5 * n < 2 ** 31 else np.int64
+    k = np.arange(n, dtype=it)
     ix = k % m
     iy = k // m
-    # slot order per row: diag, -m, +m, -1, +1  (insertion order, :13-21)
-    cols = np.stack([k, k - m, k + m, k - 1, k + 1], axis=1)
-    present = np.stack([np.ones(n, bool), iy > 0, iy < m - 1, ix > 0, ix < m - 1], axis=1)
-    vals = np.empty((n, 5), dtype=np.float64)
-    vals[:, 0] = diag
-    vals[:, 1:] = off
-    counts = present.sum(axis=1)
+    # slot order per row: diag, -m, +m, -1, +1  (insertion order, :13-21); filled slot by slot
+    # so that peak memory stays a few vectors (m = 16384 has 1.34e9 entries)
+    slots = [(None, None), (iy > 0, -m), (iy < m - 1, m), (ix > 0, -1), (ix < m - 1, 1)]
+    counts = np.ones(n, dtype=np.int8)
+    for mask, _ in slots[1:]:
+        counts += mask
     indptr = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(counts, out=indptr[1:])
-    indices = cols[present].astype(np.int32)
-    data = vals[present]
+    del counts
+    nnz = int(indptr[-1])
+    indices = np.empty(nnz, dtype=np.int32)
+    data = np.empty(nnz, dtype=np.float64)
+    pos = indptr[:-1].copy()
+    indices[pos] = k
+    data[pos] = diag
+    pos += 1
+    for mask, d in slots[1:]:
+        p = pos[mask]
+        indices[p] = k[mask] + d
+        data[p] = off
+        pos[mask] += 1
+        del p
     return indptr.astype(np.int32), indices, data
 
 

@@ -31,8 +31,9 @@ int ctx(Context **out) {
         PSK_HIP(hipGetDeviceProperties(&prop, dev));
         c.device = dev;
         c.num_cus = prop.multiProcessorCount;
-        // 8 resident 256-thread workgroups per CU; partial arrays are sized for kMaxGrid
-        int cap = c.num_cus * 8;
+        // 4 streaming 256-thread workgroups per CU (spmv_lab: 1024 workgroups beat 2048 for both the
+        // SpMV and the 16-B/lane vector streams); partial arrays are sized for kMaxGrid
+        int cap = c.num_cus * 4;
         c.grid_cap = cap < kMaxGrid ? cap : kMaxGrid;
         // keep the grid a multiple of 8 (XCD-aware tile mapping) when it is capped
         c.grid_cap -= c.grid_cap % 8;

@@ -20,14 +20,6 @@
 
 namespace psk {
 
-// logical workgroup id: give each XCD (blockIdx % 8 observed round-robin) a contiguous run of
-// tiles so that the x-gathers of neighbouring grid lines stay in one XCD's L2. Speed only.
-__device__ __forceinline__ int64_t logical_block() {
-    const int64_t g = gridDim.x, b = blockIdx.x;
-    if (g % 8 != 0) return b;
-    return (b % 8) * (g / 8) + b / 8;
-}
-
 // Stream loads of colidx/vals (read once per SpMV) are non-temporal; the x gathers keep the default
 // policy so neighbouring grid lines are served from L2 / Infinity Cache (tools/spmv_lab.hip A/B:
 // nt on the stream +9-12% at n = 10M / 16.7M).
@@ -45,9 +37,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     __shared__ double prod[kChunk];
     __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
+    // tiles are dealt round-robin (tile = block + k*grid): the whole grid sweeps one compact window
+    // of rows at a time, so x entries gathered by rows i-m, i and i+m are fetched once and re-served
+    // from L2 / Infinity Cache (spmv_lab A3: +22% over contiguous per-block ranges at n = 268M)
     const int64_t ntiles = (n + trows - 1) / trows;
-    const int64_t g = gridDim.x, lb = logical_block();
-    const int64_t t0 = ntiles * lb / g, t1 = ntiles * (lb + 1) / g;
+    const int64_t tstep = gridDim.x, t0 = blockIdx.x, t1 = ntiles;
     double acc = 0.0;
 
     // issue the colidx/vals stream of the first chunk of tile t (branch-free, clamped to the tile)
@@ -71,7 +65,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     };
     if (t0 < t1) issue(t0, e0, e1, cc, vv);
 
-    for (int64_t t = t0; t < t1; ++t) {
+    for (int64_t t = t0; t < t1; t += tstep) {
         const int64_t r0 = t * trows;
         const int64_t r1 = (r0 + trows < n) ? r0 + trows : n;
         const int64_t row = r0 + tid;
@@ -103,9 +97,9 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
                 xv[k] = xx;
             }
             // software pipeline: the next tile's stream is in flight while this tile's gathers land
-            const bool pf = c1 == ce1 && t + 1 < t1;
+            const bool pf = c1 == ce1 && t + tstep < t1;
             if (pf) {
-                issue(t + 1, e0, e1, ncc, nvv);
+                issue(t + tstep, e0, e1, ncc, nvv);
                 prefetched = true;
             }
 #pragma unroll
@@ -128,7 +122,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
             __syncthreads();
         }
-        if (!prefetched && t + 1 < t1) issue(t + 1, e0, e1, cc, vv);   // empty tile
+        if (!prefetched && t + tstep < t1) issue(t + tstep, e0, e1, cc, vv);   // empty tile
         if (has) {
             if (MODE == kSpmvResid) {
                 const double r = aux_q[row] - sum;   // b - A*x (GMRESSolver.py:163)

@@ -115,6 +115,94 @@ __global__ __launch_bounds__(BS) void spmv_A2(int64_t n, const int* __restrict__
     }
 }
 
+// ---------------- A3: A2 with a selectable tile order --------------------------------------------------
+// ORDER 0: contiguous tile range per block; 1: each XCD (blockIdx % 8) owns a contiguous slab of
+// tiles and its blocks interleave inside it; 2: global interleave (tile = block + k * grid).
+template <int CH, int ORDER>
+__global__ __launch_bounds__(BS) void spmv_A3(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                              const double* __restrict__ va, const double* __restrict__ x,
+                                              double* __restrict__ y) {
+    constexpr int KU = CH / BS;
+    __shared__ double prod[CH];
+    const int tid = threadIdx.x;
+    const int64_t nt = (n + 255) / 256, g = gridDim.x;
+    int64_t tbeg, tend, tstep;
+    if (ORDER == 0) { const int64_t lb = lblock(); tbeg = nt * lb / g; tend = nt * (lb + 1) / g; tstep = 1; }
+    else if (ORDER == 1) {
+        const int64_t xcd = blockIdx.x % 8, lb = blockIdx.x / 8, g8 = g / 8;
+        const int64_t s0 = nt * xcd / 8, s1 = nt * (xcd + 1) / 8;
+        tbeg = s0 + lb; tend = s1; tstep = g8;
+    } else { tbeg = blockIdx.x; tend = nt; tstep = g; }
+    int cc[KU], ncc[KU]; double vv[KU], nvv[KU];
+    int e0 = 0, e1 = 0;
+    auto issue = [&](int64_t t, int& a, int& b, int* c_, double* v_) {
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n;
+        a = rp[r0]; b = rp[r1];
+        const int c1 = b - a > CH ? a + CH : b;
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { int e = a + k * BS + tid; int ee = e < c1 ? e : a;
+            c_[k] = __builtin_nontemporal_load(ci + ee); v_[k] = __builtin_nontemporal_load(va + ee); }
+    };
+    if (tbeg < tend) issue(tbeg, e0, e1, cc, vv);
+    for (int64_t t = tbeg; t < tend; t += tstep) {
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n, row = r0 + tid;
+        const bool has = row < r1;
+        int rs = 0, re = 0;
+        if (has) { rs = rp[row]; re = rp[row + 1]; }
+        double sum = 0.0;
+        const int ce0 = e0, ce1 = e1;
+        for (int c0 = ce0; c0 < ce1; c0 += CH) {
+            const int c1 = ce1 - c0 > CH ? c0 + CH : ce1;
+            if (c0 != ce0) {
+#pragma unroll
+                for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; int ee = e < c1 ? e : c0;
+                    cc[k] = __builtin_nontemporal_load(ci + ee); vv[k] = __builtin_nontemporal_load(va + ee); }
+            }
+            double xv[KU], pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) xv[k] = x[cc[k]];
+            const bool pf = c1 == ce1 && t + tstep < tend;
+            if (pf) issue(t + tstep, e0, e1, ncc, nvv);
+#pragma unroll
+            for (int k = 0; k < KU; ++k) pv[k] = vv[k] * xv[k];
+            if (pf) {
+#pragma unroll
+                for (int k = 0; k < KU; ++k) { cc[k] = ncc[k]; vv[k] = nvv[k]; }
+            }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; if (e < c1) prod[k * BS + tid] = pv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            __syncthreads();
+        }
+        if (has) __builtin_nontemporal_store(sum, y + row);
+    }
+}
+
+// elementwise-style stream with the same three orders (8 B x 2 per lane, 512-element tiles)
+template <int ORDER>
+__global__ __launch_bounds__(BS) void readOrd(int64_t n, const double* __restrict__ a, double* __restrict__ out) {
+    const int64_t nt = n / 512, g = gridDim.x;
+    int64_t tbeg, tend, tstep;
+    if (ORDER == 0) { tbeg = nt * blockIdx.x / g; tend = nt * (blockIdx.x + 1) / g; tstep = 1; }
+    else if (ORDER == 1) {
+        const int64_t xcd = blockIdx.x % 8, lb = blockIdx.x / 8, g8 = g / 8;
+        tbeg = nt * xcd / 8 + lb; tend = nt * (xcd + 1) / 8; tstep = g8;
+    } else { tbeg = blockIdx.x; tend = nt; tstep = g; }
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    const d2* s = reinterpret_cast<const d2*>(a);
+    double acc = 0;
+    int64_t t = tbeg;
+    for (; t + tstep < tend; t += 2 * tstep) {
+        d2 v0 = __builtin_nontemporal_load(s + t * 256 + threadIdx.x);
+        d2 v1 = __builtin_nontemporal_load(s + (t + tstep) * 256 + threadIdx.x);
+        acc += v0.x + v1.y;
+    }
+    for (; t < tend; t += tstep) acc += __builtin_nontemporal_load(s + t * 256 + threadIdx.x).x;
+    if (acc == 12345.678) out[0] = acc;
+}
+
 __global__ __launch_bounds__(BS) void copy4(int64_t n, const double* __restrict__ a, double* __restrict__ b) {
     const int64_t nt = n / 2, stride = (int64_t)gridDim.x * BS;
     const double2* s = reinterpret_cast<const double2*>(a);
@@ -371,13 +459,13 @@ int main(int argc, char** argv) {
         const double bytes = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
         std::vector<V> vs = {
             {"A blk256/ch2048", spmv_A, 2048},
-            {"A2 pf ch1536 nt g512", spmv_A2<1536, true>, 512},
-            {"A2 pf ch1536 nt g768", spmv_A2<1536, true>, 768},
-            {"A2 pf ch1536 nt g1024", spmv_A2<1536, true>, 1024},
-            {"A2 pf ch1536 nt g1536", spmv_A2<1536, true>, 1536},
-            {"A2 pf ch1536 nt g2048", spmv_A2<1536, true>, 2048},
-            {"A2 pf ch2048 nt g1024", spmv_A2<2048, true>, 1024},
             {"A2 pf ch1280 nt g1024", spmv_A2<1280, true>, 1024},
+            {"A3 contig g1024", spmv_A3<1280, 0>, 1024},
+            {"A3 xcd-slab g1024", spmv_A3<1280, 1>, 1024},
+            {"A3 xcd-slab g2048", spmv_A3<1280, 1>, 2048},
+            {"A3 xcd-slab g1536", spmv_A3<1280, 1>, 1536},
+            {"A3 interleave g1024", spmv_A3<1280, 2>, 1024},
+            {"A3 interleave g2048", spmv_A3<1280, 2>, 2048},
         };
         // reference result
         spmv_A<<<2048, BS>>>(n, rp, ci, va, x, yr);
@@ -422,11 +510,10 @@ int main(int argc, char** argv) {
         {
             struct RV { const char* name; Kern2 k; int grid; };
             std::vector<RV> rv = {
-                {"readU4", readU<4, false>, 2048}, {"readU4 nt", readU<4, true>, 2048},
-                {"readU8 nt", readU<8, true>, 2048}, {"readU8 nt g1024", readU<8, true>, 1024},
-                {"readU8 nt g4096", readU<8, true>, 4096}, {"readSlab4 nt g1024", readSlab<4, true>, 1024},
-                {"readSlab8 nt g1024", readSlab<8, true>, 1024}, {"readSlab8 g1024", readSlab<8, false>, 1024},
-                {"readSlab8 nt g2048", readSlab<8, true>, 2048},
+                {"readSlab8 nt g1024", readSlab<8, true>, 1024},
+                {"readOrd contig g1024", readOrd<0>, 1024}, {"readOrd contig g2048", readOrd<0>, 2048},
+                {"readOrd xcd g1024", readOrd<1>, 1024}, {"readOrd xcd g2048", readOrd<1>, 2048},
+                {"readOrd inter g1024", readOrd<2>, 1024}, {"readOrd inter g2048", readOrd<2>, 2048},
             };
             for (auto& v : rv) {
                 float b = 1e9;
