@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark: PCG + Jacobi iterations/s on the 5-point FDLaplacian2D, CSR SpMV vs the HBM roofline.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--m M]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--side M]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -76,7 +76,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--m", type=int, default=16384, help="grid side (n = m^2 rows)")
+    ap.add_argument("--side", type=int, default=16384, help="grid side m of FDLaplacian2D (n = m^2 rows)")
     ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
     args = ap.parse_args()
@@ -88,7 +88,8 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
 
     from pysolvers_amd import _native as N
-    N.check(N.lib.psk_set_device(local_rank), "psk_set_device")
+    dev = int(os.environ.get("PSK_BENCH_DEVICE", local_rank))   # override only for rehearsals
+    N.check(N.lib.psk_set_device(dev), "psk_set_device")
 
     dist = None
     if world > 1:
@@ -99,7 +100,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    m = args.m
+    m = args.side
     n, nnz = fd_sizes(m)
     t_setup = time.time()
     # ---- operator, preconditioner, right-hand side (all resident in HBM before timing) -----------

@@ -140,11 +140,19 @@ int psk_gmres(const psk_csr *A, const psk_prec *M, const double *b, double *x, c
 #define PSK_UNIQUE_ID_BYTES 128
 int psk_comm_unique_id(uint8_t *id /* PSK_UNIQUE_ID_BYTES */);
 int psk_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, psk_comm **out);
+/* Validation only: a communicator of `nranks` with no RCCL behind it. Sharded matrices can be
+ * built on ONE GPU for any rank and psk_spmv then takes the full local [owned | halo] x from the
+ * caller; collectives (and hence sharded solves) return PSK_ERR_UNSUPPORTED. */
+int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out);
 int psk_comm_destroy(psk_comm *c);
 /* Rank `rank`'s row block of FDLaplacian2D(a,b,m): rows [row_begin,row_end) split on
  * whole grid lines; local columns are [owned | halo_lo | halo_hi]. */
 int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *c, psk_csr **out,
                              int64_t *row_begin, int64_t *row_end);
+/* Host-only: the row block and local column layout psk_csr_create_fd2d_dist uses for `rank`
+ * (callable without a GPU; the CPU tests check the sharding plan with it). */
+int psk_fd2d_dist_plan(int64_t m, int32_t nranks, int32_t rank, int64_t *row_begin, int64_t *row_end,
+                       int64_t *ncols, int64_t *halo_lo, int64_t *halo_hi);
 /* Row block [row_begin,row_end) of a global CSR given with GLOBAL column indices
  * (host arrays of the local rows only: rowptr[nloc+1] starting anywhere, colidx, vals). */
 int psk_csr_create_dist(int64_t n_global, int64_t row_begin, int64_t row_end,

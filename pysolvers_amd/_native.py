@@ -66,10 +66,19 @@ SIGNATURES = {
     "psk_comm_unique_id": (ctypes.c_int, [P]),
     "psk_comm_init": (ctypes.c_int, [I32, I32, P, PP]),
     "psk_comm_destroy": (ctypes.c_int, [P]),
+    "psk_comm_init_dry": (ctypes.c_int, [I32, I32, PP]),
     "psk_csr_create_fd2d_dist": (ctypes.c_int, [F64, F64, I64, P, PP, ctypes.POINTER(I64),
                                                 ctypes.POINTER(I64)]),
     "psk_csr_create_dist": (ctypes.c_int, [I64, I64, I64, P, P, P, P, PP]),
+    "psk_fd2d_dist_plan": (ctypes.c_int, [I64, I32, I32] + [ctypes.POINTER(I64)] * 5),
 }
+
+
+def fd2d_dist_plan(m, nranks, rank):
+    """(row_begin, row_end, ncols, halo_lo, halo_hi) of `rank` (host-only, no GPU needed)."""
+    v = [I64() for _ in range(5)]
+    check(lib.psk_fd2d_dist_plan(m, nranks, rank, *[ctypes.byref(x) for x in v]), "psk_fd2d_dist_plan")
+    return tuple(x.value for x in v)
 
 
 class PskError(RuntimeError):
@@ -80,10 +89,26 @@ class PskError(RuntimeError):
         self.code = code
 
 
+def _pin_runtime():
+    """Make sure the process ends up with ONE HIP/HSA/RCCL runtime.
+
+    PyTorch-ROCm wheels ship their own HIP/HSA/RCCL and load them by UNVERSIONED names; libpsk
+    asks by SONAME (libamdhip64.so.7, librccl.so.1). If libpsk were loaded first, a later
+    `import torch` would map a second HIP runtime into the process (measured here: duplicate
+    libamdhip64/libhsa-runtime64/librccl and a heap corruption at exit). So when torch is
+    installed it is imported FIRST and libpsk binds to the runtime torch loaded (same sonames);
+    without torch, the system ROCm runtime is used.
+    """
+    import importlib.util
+    if importlib.util.find_spec("torch") is not None:
+        import torch  # noqa: F401
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError("libpsk.so not found at %s — build it with `python -c 'import __graft_entry__ as "
                           "g; g.build()'` (make -C pysolvers_amd/csrc)" % LIB_PATH)
+    _pin_runtime()
     lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -16,6 +16,7 @@ namespace psk {
 
 int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
     if (!A->comm || A->peers.empty()) return PSK_OK;
+    if (A->comm->dry) return PSK_OK;   // the caller supplied the halo entries
     ncclComm_t nc = A->comm->nccl;
     PSK_RCCL(ncclGroupStart());
     for (const HaloPeer &p : A->peers) {
@@ -32,7 +33,27 @@ int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
 
 int allreduce_sum(psk_csr *A, double *buf, int64_t count, hipStream_t s) {
     if (!A->comm || A->comm->nranks == 1) return PSK_OK;
+    if (A->comm->dry) return fail(PSK_ERR_UNSUPPORTED, "collective on a dry (RCCL-less) communicator");
     PSK_RCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, A->comm->nccl, s));
+    return PSK_OK;
+}
+
+// Row-block plan of the m x m 5-point matrix over P ranks: whole grid lines per rank; local column
+// layout [owned | halo_lo (previous rank's last line) | halo_hi (next rank's first line)].
+struct FdPlan {
+    int64_t rb, re, nloc, ncols, halo_lo, halo_hi;
+};
+
+static int fd2d_plan(int64_t m, int P, int r, FdPlan &p) {
+    if (m < 1 || P < 1 || r < 0 || r >= P) return fail(PSK_ERR_ARG, "fd2d plan: bad arguments");
+    if (P > m) return fail(PSK_ERR_ARG, "fd2d_dist: more ranks than grid lines");
+    const int64_t l0 = m * r / P, l1 = m * (r + 1) / P;
+    p.rb = l0 * m;
+    p.re = l1 * m;
+    p.nloc = p.re - p.rb;
+    p.halo_lo = l0 > 0 ? m : 0;
+    p.halo_hi = l1 < m ? m : 0;
+    p.ncols = p.nloc + p.halo_lo + p.halo_hi;
     return PSK_OK;
 }
 
@@ -41,6 +62,18 @@ int allreduce_sum(psk_csr *A, double *buf, int64_t count, hipStream_t s) {
 using namespace psk;
 
 extern "C" {
+
+int psk_fd2d_dist_plan(int64_t m, int32_t nranks, int32_t rank, int64_t *row_begin, int64_t *row_end,
+                       int64_t *ncols, int64_t *halo_lo, int64_t *halo_hi) {
+    FdPlan p;
+    PSK_TRY(fd2d_plan(m, nranks, rank, p));
+    if (row_begin) *row_begin = p.rb;
+    if (row_end) *row_end = p.re;
+    if (ncols) *ncols = p.ncols;
+    if (halo_lo) *halo_lo = p.halo_lo;
+    if (halo_hi) *halo_hi = p.halo_hi;
+    return PSK_OK;
+}
 
 int psk_comm_unique_id(uint8_t *id) {
     if (!id) return fail(PSK_ERR_ARG, "NULL id");
@@ -74,6 +107,17 @@ int psk_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, psk_comm **ou
     return PSK_OK;
 }
 
+int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out) {
+    if (!out || nranks < 1 || rank < 0 || rank >= nranks) return fail(PSK_ERR_ARG, "psk_comm_init_dry: bad arguments");
+    psk_comm *c = new psk_comm();
+    c->nranks = nranks;
+    c->rank = rank;
+    c->dry = true;
+    if (hipGetDevice(&c->device) != hipSuccess) c->device = 0;
+    *out = c;
+    return PSK_OK;
+}
+
 int psk_comm_destroy(psk_comm *c) {
     if (!c) return PSK_OK;
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
@@ -84,18 +128,17 @@ int psk_comm_destroy(psk_comm *c) {
 int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *cm, psk_csr **out,
                              int64_t *row_begin, int64_t *row_end) {
     if (!cm || !out || m < 1) return fail(PSK_ERR_ARG, "psk_csr_create_fd2d_dist: bad arguments");
-    const int P = cm->nranks, r = cm->rank;
-    if (P > m) return fail(PSK_ERR_ARG, "fd2d_dist: more ranks than grid lines");
+    const int r = cm->rank;
     if ((m == 1 ? 1 : 5 * m * m - 4 * m) > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "nnz > int32");
+    FdPlan plan;
+    PSK_TRY(fd2d_plan(m, cm->nranks, r, plan));
     Context *c;
     PSK_TRY(ctx(&c));
-    // whole grid lines per rank
-    const int64_t l0 = m * r / P, l1 = m * (r + 1) / P;
-    const int64_t rb = l0 * m, re = l1 * m, nloc = re - rb;
-    const bool lo = l0 > 0, hi = l1 < m;
+    const int64_t rb = plan.rb, re = plan.re, nloc = plan.nloc;
+    const bool lo = plan.halo_lo > 0, hi = plan.halo_hi > 0;
     psk_csr *A = new psk_csr();
     A->n = nloc;
-    A->ncols = nloc + (lo ? m : 0) + (hi ? m : 0);
+    A->ncols = plan.ncols;
     A->n_global = m * m;
     A->row_begin = rb;
     A->row_end = re;

@@ -253,6 +253,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
     const int gs = spmv_grid(c, A);   // SpMV grid
     const int gv = grid_for_rows(c, n, kVecTile);    // elementwise grid
+    // Sharded: every rank all-reduces (and re-reduces) the same kMaxGrid-long, zero-padded partial
+    // arrays, whatever its own grid sizes are, so RCCL counts match across ranks.
+    const bool sharded = A->comm != nullptr;
+    const int np1 = sharded ? kMaxGrid : gs, np2 = sharded ? kMaxGrid : gv;
+    if (sharded) {
+        PSK_HIP(hipMemsetAsync(w.part1, 0, kMaxGrid * sizeof(double), s));
+        PSK_HIP(hipMemsetAsync(w.part2, 0, 2 * kMaxGrid * sizeof(double), s));
+    }
 
     hipEvent_t ev0, ev1;
     PSK_HIP(hipEventCreate(&ev0));
@@ -262,8 +270,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     PSK_HIP(hipEventRecord(ev0, s));
     hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
     PSK_HIP(hipGetLastError());
-    if (A->comm) PSK_TRY(allreduce_sum(A, w.part2, 2 * gv, s));
-    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, gv, ctl->tau, w.st, w.udr);
+    if (sharded) PSK_TRY(allreduce_sum(A, w.part2, 2 * np2, s));
+    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, np2, ctl->tau, w.st, w.udr);
     PSK_HIP(hipGetLastError());
 
     // polling ring: flag copies every C iterations, host waits on the copy L chunks back
@@ -322,12 +330,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if ((rc = launch_spmv(A, kSpmvDot, w.p, w.Ap, nullptr, nullptr, w.part1, &w.st->done, gs, s)) != PSK_OK)
             break;
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
-        if (A->comm && (rc = allreduce_sum(A, w.part1, gs, s)) != PSK_OK) break;
+        if (sharded && (rc = allreduce_sum(A, w.part1, np1, s)) != PSK_OK) break;
         hipLaunchKernelGGL(pcg_update_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap, dinv,
-                           w.part1, gs, w.part2, w.st, w.udr, k);
-        if (A->comm && (rc = allreduce_sum(A, w.part2, 2 * gv, s)) != PSK_OK) break;
+                           w.part1, np1, w.part2, w.st, w.udr, k);
+        if (sharded && (rc = allreduce_sum(A, w.part2, 2 * np2, s)) != PSK_OK) break;
         hipLaunchKernelGGL(pcg_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv, w.part2,
-                           gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+                           np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;
     }

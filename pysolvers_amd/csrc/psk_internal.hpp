@@ -84,6 +84,7 @@ struct psk_comm {
     int rank = 0;
     int device = 0;
     ncclComm_t nccl = nullptr;
+    bool dry = false;     // psk_comm_init_dry: builds shards, no collectives (single-GPU validation)
 };
 
 struct psk_csr {

@@ -443,7 +443,8 @@ int psk_spmv(const psk_csr *Ac, const double *x, double *y, int32_t loc) {
         // stage into [owned | halo] x and y
         PSK_TRY(tmp.ensure((size_t)(A->ncols + A->n) * sizeof(double)));
         double *tx = tmp.as<double>();
-        PSK_TRY(to_device_vec(x, loc, A->n, tx, c->stream));
+        const bool dry = A->comm && A->comm->dry;   // caller passes [owned | halo]
+        PSK_TRY(to_device_vec(x, loc, dry ? A->ncols : A->n, tx, c->stream));
         if (A->comm) PSK_TRY(halo_exchange(A, tx, c->stream));
         dx = tx;
         dy = (loc == PSK_HOST) ? tx + A->ncols : y;
