@@ -79,6 +79,8 @@ def main():
     ap.add_argument("--side", type=int, default=16384, help="grid side m of FDLaplacian2D (n = m^2 rows)")
     ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1_pmc_traffic_16384.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py) of the same kernel and side")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -195,7 +197,8 @@ def main():
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": "spmv_kernel<kSpmvDot> (rank 0)",
                          "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": (ach / HBM_PEAK_GBPS) if ach else None, "traffic": None,
+                         "frac": (ach / HBM_PEAK_GBPS) if ach else None,
+                         **pmc_traffic(args.traffic_json, m, world),
                          "algorithmic_bytes_per_launch": bspmv, "avg_launch_ms": res.spmv_ms,
                          "launches": res.spmv_launches},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter,
@@ -222,6 +225,24 @@ def main():
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
+
+
+def pmc_traffic(path, m, world):
+    """HBM bytes per SpMV launch measured by rocprofv3 PMC passes on the same kernel and matrix
+    (scripts/gpu_pmc.sh -> tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections
+    calibrated by tools/pmc_calib.hip). Counters cannot be read from inside the timed run."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return {"traffic": None}
+    if d.get("config", {}).get("side") != m or world != 1:
+        return {"traffic": None}
+    for k, v in d["kernels"].items():
+        if k.startswith("void psk::spmv_kernel<1>"):
+            return {"traffic": v["hbm_bytes_per_launch"],
+                    "traffic_source": os.path.relpath(path, REPO) + " (rocprofv3 PMC, same kernel/config)"}
+    return {"traffic": None}
 
 
 def spmv_10m(N, iters=30):

@@ -180,6 +180,117 @@ __global__ __launch_bounds__(BS) void spmv_A3(int64_t n, const int* __restrict__
     }
 }
 
+// ---------------- A4: 3-stage pipeline: stream(t+2) | gather(t+1) | sum(t), round-robin tiles -----------
+template <int CH>
+__global__ __launch_bounds__(BS) void spmv_A4(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                              const double* __restrict__ va, const double* __restrict__ x,
+                                              double* __restrict__ y) {
+    constexpr int KU = CH / BS;
+    __shared__ double prod[CH];
+    const int tid = threadIdx.x;
+    const int64_t nt = (n + 255) / 256, g = gridDim.x;
+    // assumes every tile fits one chunk (true for the 5-point matrix: <= 1280 entries / 256 rows)
+    int c0_[KU], c1_[KU]; double v0_[KU], v1_[KU];   // stream stage for tiles t+1, t+2
+    double xg[KU];                                     // gathered x for tile t+1
+    int a1 = 0, b1 = 0, a2 = 0, b2 = 0;
+    auto stream = [&](int64_t t, int& a, int& b, int* c_, double* v_) {
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n;
+        a = rp[r0]; b = rp[r1];
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { int e = a + k * BS + tid; int ee = e < b ? e : a;
+            c_[k] = __builtin_nontemporal_load(ci + ee); v_[k] = __builtin_nontemporal_load(va + ee); }
+    };
+    int64_t t = blockIdx.x;
+    if (t < nt) stream(t, a1, b1, c0_, v0_);
+    if (t < nt) {
+#pragma unroll
+        for (int k = 0; k < KU; ++k) xg[k] = x[c0_[k]];
+    }
+    if (t + g < nt) stream(t + g, a2, b2, c1_, v1_);
+    for (; t < nt; t += g) {
+        // products of tile t (its gathers were issued one stage earlier)
+        double pv[KU];
+#pragma unroll
+        for (int k = 0; k < KU; ++k) pv[k] = v0_[k] * xg[k];
+        const int ca = a1, cb = b1;
+        // advance the pipeline: tile t+g's stream landed -> issue its gathers; stream tile t+2g
+        if (t + g < nt) {
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { xg[k] = x[c1_[k]]; c0_[k] = c1_[k]; v0_[k] = v1_[k]; }
+            a1 = a2; b1 = b2;
+            if (t + 2 * g < nt) stream(t + 2 * g, a2, b2, c1_, v1_);
+        }
+        const int64_t r0 = t * 256, r1 = r0 + 256 < n ? r0 + 256 : n, row = r0 + tid;
+        const bool has = row < r1;
+        int rs = 0, re = 0;
+        if (has) { rs = rp[row]; re = rp[row + 1]; }
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { int e = ca + k * BS + tid; if (e < cb) prod[k * BS + tid] = pv[k]; }
+        __syncthreads();
+        double sum = 0.0;
+        for (int e = rs; e < re; ++e) sum = sum + prod[e - ca];
+        __syncthreads();
+        if (has) __builtin_nontemporal_store(sum, y + row);
+    }
+}
+
+// ---------------- PCG update-like kernels (K2: 5 reads + 2 writes; K3: 3 reads + 1 write) -------------
+typedef double ev2 __attribute__((ext_vector_type(2)));
+template <bool NT> __device__ __forceinline__ ev2 L2(const double* p) {
+    return NT ? __builtin_nontemporal_load(reinterpret_cast<const ev2*>(p)) : *reinterpret_cast<const ev2*>(p);
+}
+template <bool NT> __device__ __forceinline__ void S2(double* p, ev2 v) {
+    if (NT) __builtin_nontemporal_store(v, reinterpret_cast<ev2*>(p)); else *reinterpret_cast<ev2*>(p) = v;
+}
+// MODE 0: current policy (x,Ap nt loads, x nt store); 1: all nt; 2: none nt
+template <int ORDER, int MODE, int U>
+__global__ __launch_bounds__(BS) void k2like(int64_t n, double* __restrict__ x, double* __restrict__ r,
+                                             const double* __restrict__ p, const double* __restrict__ Ap,
+                                             const double* __restrict__ d, double alpha, double* __restrict__ out) {
+    constexpr bool NX = MODE != 2, NP = MODE == 1, NR = MODE == 1, NA = MODE != 2, ND = MODE == 1;
+    constexpr bool SX = MODE != 2, SR = MODE == 1;
+    double rr = 0, ur = 0;
+    auto body = [&](int64_t i) {
+        ev2 xv = L2<NX>(x + i), pv = L2<NP>(p + i), rv = L2<NR>(r + i), av = L2<NA>(Ap + i), dv = L2<ND>(d + i);
+        ev2 xn = xv + alpha * pv, rn = rv - alpha * av;
+        S2<SX>(x + i, xn); S2<SR>(r + i, rn);
+        rr += rn.x * rn.x + rn.y * rn.y; ur += dv.x * rn.x * rn.x + dv.y * rn.y * rn.y;
+    };
+    if (ORDER == 0) {
+        const int64_t nt = n / 512, t0 = nt * blockIdx.x / gridDim.x, t1 = nt * (blockIdx.x + 1) / gridDim.x;
+        const int64_t i1 = t1 * 512;
+        int64_t i = t0 * 512 + 2 * threadIdx.x;
+#pragma unroll U
+        for (; i < i1; i += 512) body(i);
+    } else {
+        const int64_t np = n / 2, gs = (int64_t)gridDim.x * BS;
+#pragma unroll U
+        for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < np; q += gs) body(2 * q);
+    }
+    if (rr == 1.2345 && ur == 1.2345) out[0] = rr;
+}
+
+template <int ORDER, int MODE, int U>
+__global__ __launch_bounds__(BS) void k3like(int64_t n, const double* __restrict__ r, double* __restrict__ p,
+                                             const double* __restrict__ d, double beta) {
+    constexpr bool NR = MODE != 2, NP = MODE == 1, ND = MODE != 2, SP = MODE == 1;
+    auto body = [&](int64_t i) {
+        ev2 rv = L2<NR>(r + i), pv = L2<NP>(p + i), dv = L2<ND>(d + i);
+        S2<SP>(p + i, dv * rv + beta * pv);
+    };
+    if (ORDER == 0) {
+        const int64_t nt = n / 512, t0 = nt * blockIdx.x / gridDim.x, t1 = nt * (blockIdx.x + 1) / gridDim.x;
+        const int64_t i1 = t1 * 512;
+        int64_t i = t0 * 512 + 2 * threadIdx.x;
+#pragma unroll U
+        for (; i < i1; i += 512) body(i);
+    } else {
+        const int64_t np = n / 2, gs = (int64_t)gridDim.x * BS;
+#pragma unroll U
+        for (int64_t q = (int64_t)blockIdx.x * BS + threadIdx.x; q < np; q += gs) body(2 * q);
+    }
+}
+
 // elementwise-style stream with the same three orders (8 B x 2 per lane, 512-element tiles)
 template <int ORDER>
 __global__ __launch_bounds__(BS) void readOrd(int64_t n, const double* __restrict__ a, double* __restrict__ out) {
@@ -459,13 +570,11 @@ int main(int argc, char** argv) {
         const double bytes = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
         std::vector<V> vs = {
             {"A blk256/ch2048", spmv_A, 2048},
-            {"A2 pf ch1280 nt g1024", spmv_A2<1280, true>, 1024},
-            {"A3 contig g1024", spmv_A3<1280, 0>, 1024},
-            {"A3 xcd-slab g1024", spmv_A3<1280, 1>, 1024},
-            {"A3 xcd-slab g2048", spmv_A3<1280, 1>, 2048},
-            {"A3 xcd-slab g1536", spmv_A3<1280, 1>, 1536},
             {"A3 interleave g1024", spmv_A3<1280, 2>, 1024},
-            {"A3 interleave g2048", spmv_A3<1280, 2>, 2048},
+            {"A4 3-stage g1024", spmv_A4<1280>, 1024},
+            {"A4 3-stage g768", spmv_A4<1280>, 768},
+            {"A4 3-stage g1536", spmv_A4<1280>, 1536},
+            {"A4 3-stage g2048", spmv_A4<1280>, 2048},
         };
         // reference result
         spmv_A<<<2048, BS>>>(n, rp, ci, va, x, yr);
@@ -496,52 +605,47 @@ int main(int argc, char** argv) {
             printf("m=%ld %-24s min %.1f us med %.1f us  -> %.0f GB/s (%.1f%% of 8 TB/s)\n", (long)m, vs[i].name,
                    t[i][0] * 1e3, t[i][R / 2] * 1e3, bytes / (t[i][0] * 1e-3) / 1e9, 100.0 * bytes / (t[i][0] * 1e-3) / 8e12);
         }
-        // stream copy reference: 2 x 8n bytes... use a dedicated buffer pair of size nnz doubles
-        double *a2, *b2; const int64_t cn = nnz;
-        CK(hipMalloc(&a2, cn * 8)); CK(hipMalloc(&b2, cn * 8)); CK(hipMemset(a2, 0, cn * 8));
-        float best = 1e9;
-        for (int r = 0; r < R; ++r) {
-            CK(hipEventRecord(e0));
-            for (int l = 0; l < L; ++l) copy2<<<4096, BS>>>(cn, a2, b2);
-            CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-            float ms; CK(hipEventElapsedTime(&ms, e0, e1)); best = std::min(best, ms / L);
-        }
-        printf("m=%ld copy %ld doubles: %.1f us -> %.0f GB/s\n", (long)m, (long)cn, best * 1e3, 16.0 * cn / (best * 1e-3) / 1e9);
+        // ---- PCG update-like kernels over 5 vectors of n doubles (K2: 5R+2W, K3: 3R+1W) ----
         {
-            struct RV { const char* name; Kern2 k; int grid; };
-            std::vector<RV> rv = {
-                {"readSlab8 nt g1024", readSlab<8, true>, 1024},
-                {"readOrd contig g1024", readOrd<0>, 1024}, {"readOrd contig g2048", readOrd<0>, 2048},
-                {"readOrd xcd g1024", readOrd<1>, 1024}, {"readOrd xcd g2048", readOrd<1>, 2048},
-                {"readOrd inter g1024", readOrd<2>, 1024}, {"readOrd inter g2048", readOrd<2>, 2048},
+            double* v5; CK(hipMalloc(&v5, 5 * n * 8)); CK(hipMemset(v5, 0, 5 * n * 8));
+            double *vx = v5, *vr = v5 + n, *vp = v5 + 2 * n, *va2 = v5 + 3 * n, *vd = v5 + 4 * n;
+            typedef void (*K2)(int64_t, double*, double*, const double*, const double*, const double*, double, double*);
+            typedef void (*K3)(int64_t, const double*, double*, const double*, double);
+            struct E2 { const char* name; K2 k; int grid; };
+            struct E3 { const char* name; K3 k; int grid; };
+            std::vector<E2> e2 = {
+                {"K2 contig cur u2 g1024", k2like<0, 0, 2>, 1024}, {"K2 contig cur u2 g2048", k2like<0, 0, 2>, 2048},
+                {"K2 contig allnt u2 g1024", k2like<0, 1, 2>, 1024}, {"K2 contig nont u2 g1024", k2like<0, 2, 2>, 1024},
+                {"K2 contig cur u1 g1024", k2like<0, 0, 1>, 1024}, {"K2 contig cur u4 g1024", k2like<0, 0, 4>, 1024},
+                {"K2 inter cur u2 g1024", k2like<1, 0, 2>, 1024}, {"K2 inter allnt u2 g1024", k2like<1, 1, 2>, 1024},
+                {"K2 contig cur u2 g512", k2like<0, 0, 2>, 512},
             };
-            for (auto& v : rv) {
-                float b = 1e9;
-                for (int r = 0; r < R; ++r) {
-                    CK(hipEventRecord(e0));
-                    for (int l = 0; l < L; ++l) v.k<<<v.grid, BS>>>(cn, a2, b2);
-                    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-                    float ms; CK(hipEventElapsedTime(&ms, e0, e1)); b = std::min(b, ms / L);
-                }
-                printf("m=%ld %-22s %.0f GB/s\n", (long)m, v.name, 8.0 * cn / (b * 1e-3) / 1e9);
-            }
-        }
-        for (int grid : {1024, 8192}) {
-            float bc = 1e9, br = 1e9;
+            std::vector<E3> e3 = {
+                {"K3 contig cur u2 g1024", k3like<0, 0, 2>, 1024}, {"K3 contig cur u2 g2048", k3like<0, 0, 2>, 2048},
+                {"K3 contig allnt u2 g1024", k3like<0, 1, 2>, 1024}, {"K3 contig nont u2 g1024", k3like<0, 2, 2>, 1024},
+                {"K3 contig cur u4 g1024", k3like<0, 0, 4>, 1024}, {"K3 inter cur u2 g1024", k3like<1, 0, 2>, 1024},
+            };
+            std::vector<float> b2(e2.size(), 1e9f), b3(e3.size(), 1e9f);
             for (int r = 0; r < R; ++r) {
-                CK(hipEventRecord(e0));
-                for (int l = 0; l < L; ++l) copy4<<<grid, BS>>>(cn, a2, b2);
-                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-                float ms; CK(hipEventElapsedTime(&ms, e0, e1)); bc = std::min(bc, ms / L);
-                CK(hipEventRecord(e0));
-                for (int l = 0; l < L; ++l) read4<<<grid, BS>>>(cn, a2, b2);
-                CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
-                CK(hipEventElapsedTime(&ms, e0, e1)); br = std::min(br, ms / L);
+                for (size_t i = 0; i < e2.size(); ++i) {
+                    CK(hipEventRecord(e0));
+                    for (int l = 0; l < L; ++l) e2[i].k<<<e2[i].grid, BS>>>(n, vx, vr, vp, va2, vd, 1e-3, y);
+                    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                    float ms; CK(hipEventElapsedTime(&ms, e0, e1)); b2[i] = std::min(b2[i], ms / L);
+                }
+                for (size_t i = 0; i < e3.size(); ++i) {
+                    CK(hipEventRecord(e0));
+                    for (int l = 0; l < L; ++l) e3[i].k<<<e3[i].grid, BS>>>(n, vr, vp, vd, 0.5);
+                    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+                    float ms; CK(hipEventElapsedTime(&ms, e0, e1)); b3[i] = std::min(b3[i], ms / L);
+                }
             }
-            printf("m=%ld copy4 g%d: %.0f GB/s   read4: %.0f GB/s\n", (long)m, grid, 16.0 * cn / (bc * 1e-3) / 1e9,
-                   8.0 * cn / (br * 1e-3) / 1e9);
+            for (size_t i = 0; i < e2.size(); ++i)
+                printf("m=%ld %-26s %.1f us -> %.0f GB/s\n", (long)m, e2[i].name, b2[i] * 1e3, 56.0 * n / (b2[i] * 1e-3) / 1e9);
+            for (size_t i = 0; i < e3.size(); ++i)
+                printf("m=%ld %-26s %.1f us -> %.0f GB/s\n", (long)m, e3[i].name, b3[i] * 1e3, 32.0 * n / (b3[i] * 1e-3) / 1e9);
+            CK(hipFree(v5));
         }
-        CK(hipFree(a2)); CK(hipFree(b2));
         CK(hipFree(rp)); CK(hipFree(ci)); CK(hipFree(va)); CK(hipFree(x)); CK(hipFree(y)); CK(hipFree(yr));
     }
     return 0;
