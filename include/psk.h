@@ -57,6 +57,7 @@ extern "C" {
 /* preconditioner kinds */
 #define PSK_PREC_IDENTITY 0      /* IdentityPreconditionerType   PreconditionerType.py:13-19 */
 #define PSK_PREC_JACOBI   1      /* DInv*v                        ClassicSmoothers.py:5-16 pattern */
+#define PSK_PREC_ILU      2      /* SuperLU ILU.solve             ILUTPreconditioner.py:70-78 */
 
 typedef struct psk_csr  psk_csr;    /* device CSR (int32 rowptr/colidx, f64 vals), library-owned */
 typedef struct psk_prec psk_prec;   /* formed preconditioner, library-owned */
@@ -123,6 +124,12 @@ int psk_axpy(int64_t n, double alpha, const double *x, double *y, int32_t loc);
 
 /* ---- preconditioners (PreconditionerType.form / applyRight) ---------------------------- */
 int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out);
+/* ILU from host factors of SuperLU spilu (RightILUTPreconditioner, ILUTPreconditioner.py:51-53):
+ * L (unit lower, diagonal optional) and U (upper with diagonal) as CSR, perm_r / perm_c as in
+ * scipy's SuperLU (Pr A Pc = L U). apply(v) = (U^-1 L^-1 (v scattered by perm_r))[perm_c]. */
+int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx, const double *l_vals,
+                        const int32_t *u_rowptr, const int32_t *u_colidx, const double *u_vals,
+                        const int32_t *perm_r, const int32_t *perm_c, psk_prec **out);
 int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *out, int32_t loc);
 int psk_prec_destroy(psk_prec *M);
 

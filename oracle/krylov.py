@@ -32,6 +32,14 @@ def jacobi_form(A):
     return lambda v: np.multiply(DInv, v)          # ClassicSmoothers.py:14
 
 
+def ilut_form(A, drop_tol=0.001, fill_factor=15):
+    """RightILUTPreconditioner: SuperLU spilu with the reference's arguments (ILUTPreconditioner.py:51-53);
+    applyRight = ILU.solve (:77-78)."""
+    import scipy.sparse.linalg as spla
+    ilu = spla.spilu(A.tocsc(), drop_tol=drop_tol, fill_factor=fill_factor, diag_pivot_thresh=0.0)
+    return ilu.solve
+
+
 def mvmult(A, x):
     """IterativeLinearSolver.py:94-106: ``A*x`` -> scipy csr_matvec for sparse A."""
     return A @ x

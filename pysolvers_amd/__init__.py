@@ -7,9 +7,9 @@ from . import Linear
 from .IterativeSolver import CommonSolverArgs, IterativeSolver, NamedObject, SolveStatus
 from .Linear import (GMRES, PCG, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
                      IdentityPreconditionerType, IterativeLinearSolver, Jacobi, JacobiPreconditioner,
-                     JacobiPreconditionerType, PCGSolver, mvmult)
+                     JacobiPreconditionerType, LeftILUT, PCGSolver, RightILUT, mvmult)
 
 __all__ = ["Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
            "GMRESSolver", "PCGSolver", "DeviceCSR", "DeviceVector", "IdentityPreconditioner",
            "IdentityPreconditionerType", "IterativeLinearSolver", "Jacobi", "JacobiPreconditioner",
-           "JacobiPreconditionerType", "mvmult"]
+           "JacobiPreconditionerType", "LeftILUT", "RightILUT", "mvmult"]

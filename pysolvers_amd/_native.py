@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"
 PSK_OK = 0
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_HOST, PSK_DEVICE = 0, 1
-PSK_PREC_IDENTITY, PSK_PREC_JACOBI = 0, 1
+PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU = 0, 1, 2
 PSK_UNIQUE_ID_BYTES = 128
 
 STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOWN: "breakdown",
@@ -60,6 +60,7 @@ SIGNATURES = {
     "psk_axpy": (ctypes.c_int, [I64, F64, P, P, I32]),
     "psk_prec_create": (ctypes.c_int, [P, I32, PP]),
     "psk_prec_apply": (ctypes.c_int, [P, I64, P, P, I32]),
+    "psk_prec_create_ilu": (ctypes.c_int, [I64, P, P, P, P, P, P, P, P, PP]),
     "psk_prec_destroy": (ctypes.c_int, [P]),
     "psk_pcg": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
     "psk_gmres": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),

@@ -174,6 +174,12 @@ __global__ __launch_bounds__(kBlock) void gm_update_x_kernel(int64_t n, const do
     x[i] = accumulate ? x[i] + v : v;
 }
 
+__global__ __launch_bounds__(kBlock) void gm_add_or_copy_kernel(int64_t n, const double *__restrict__ v,
+                                                                double *__restrict__ x, int accumulate) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) x[i] = accumulate ? x[i] + v[i] : v[i];
+}
+
 __global__ __launch_bounds__(kBlock) void gm_true_resid_kernel(const double *part, int np, GmresState *st) {
     __shared__ double sh[kWaves];
     const double rr = reduce_partials(part, np, 1, sh);
@@ -249,12 +255,16 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             return fail(PSK_ERR_ALLOC, "psk_gmres: Krylov basis of " + std::to_string(K + 1) +
                                            " vectors does not fit in HBM; use restart");
     }
-    PSK_TRY(A->ws.ensure(qbytes + 3 * vec));
+    // general (ILU) preconditioner: M^-1 q_k is materialised in w before the SpMV; t is scratch
+    const bool gen = M && M->kind == PSK_PREC_ILU;
+    PSK_TRY(A->ws.ensure(qbytes + (gen ? 5 : 3) * vec));
     char *wb = A->ws.as<char>();
     double *Q = reinterpret_cast<double *>(wb);
     double *u = reinterpret_cast<double *>(wb + qbytes);
     double *x = reinterpret_cast<double *>(wb + qbytes + vec);
     double *bv = reinterpret_cast<double *>(wb + qbytes + 2 * vec);
+    double *w = gen ? reinterpret_cast<double *>(wb + qbytes + 3 * vec) : nullptr;
+    double *tt = gen ? reinterpret_cast<double *>(wb + qbytes + 4 * vec) : nullptr;
     const size_t hb = aup((size_t)ld * K * 8);
     const size_t small = aup(sizeof(GmresState)) + 2 * hb + aup((size_t)2 * K * 8) + aup((size_t)ld * 8) +
                          2 * aup((size_t)kMaxGrid * 8) + aup((size_t)(maxiter + 1) * 8) + aup((size_t)ld * 8);
@@ -313,8 +323,19 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
         if (!small_solve(kc + 1, hR.data(), ld, hg.data(), y))
             return fail(PSK_ERR_ARG, "GMRES least-squares system is singular (LinAlgError in the reference)");
         PSK_HIP(hipMemcpyAsync(dy, y.data(), (size_t)(kc + 1) * 8, hipMemcpyHostToDevice, s));
-        hipLaunchKernelGGL(gm_update_x_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,
-                           Q, (int64_t)(vec / 8), dy, kc + 1, dinv, x, accumulate ? 1 : 0);
+        const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+        if (!gen) {
+            hipLaunchKernelGGL(gm_update_x_kernel, dim3(nb), dim3(kBlock), 0, s, n, Q, (int64_t)(vec / 8), dy,
+                               kc + 1, dinv, x, accumulate ? 1 : 0);
+            PSK_HIP(hipGetLastError());
+            return PSK_OK;
+        }
+        // x (+)= M^-1 (Q y): gemv into w, apply the preconditioner into tt, then add/copy
+        hipLaunchKernelGGL(gm_update_x_kernel, dim3(nb), dim3(kBlock), 0, s, n, Q, (int64_t)(vec / 8), dy, kc + 1,
+                           (const double *)nullptr, w, 0);
+        PSK_HIP(hipGetLastError());
+        PSK_TRY(prec_apply_dev(M, n, w, tt, s));
+        hipLaunchKernelGGL(gm_add_or_copy_kernel, dim3(nb), dim3(kBlock), 0, s, n, tt, x, accumulate ? 1 : 0);
         PSK_HIP(hipGetLastError());
         return PSK_OK;
     };
@@ -361,8 +382,11 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             }
             const double *qk = Q + (size_t)k * (vec / 8);
             const double *q0 = Q;
-            if ((rc = launch_spmv(A, dinv ? kSpmvJacobiDot : kSpmvPlainDot, qk, u, dinv, q0, pa, &st->done, gs,
-                                  s)) != PSK_OK)
+            if (gen) {   // u = A (M^-1 q_k): materialise M^-1 q_k (GMRESSolver.py:107)
+                if ((rc = prec_apply_dev(M, n, qk, w, s)) != PSK_OK) break;
+                if ((rc = launch_spmv(A, kSpmvPlainDot, w, u, nullptr, q0, pa, &st->done, gs, s)) != PSK_OK) break;
+            } else if ((rc = launch_spmv(A, dinv ? kSpmvJacobiDot : kSpmvPlainDot, qk, u, dinv, q0, pa, &st->done,
+                                         gs, s)) != PSK_OK)
                 break;
             ++spmv_count;
             double *pin = pa, *pout = pb;
@@ -430,6 +454,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     }
     if (rc == PSK_OK && hipEventRecord(ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "gmres sync");
+    if (rc == PSK_OK && gen) rc = ilu_check_error(M, s);
     if (rc == PSK_OK) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, ev0, ev1);

@@ -193,26 +193,101 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     }
 }
 
+// ---- general preconditioner (ILU, ...): u = M^-1 r is materialised by the preconditioner's own
+// kernels between K2 and K3, so u.r gets its own reduction and K3 reads u ----------------------
+__global__ __launch_bounds__(kBlock) void pcg_gen_init_kernel(int64_t n, const double *__restrict__ b,
+                                                              double *__restrict__ x, double *__restrict__ r) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) {
+        r[i] = b[i];   // r = np.copy(b)        :97
+        x[i] = 0.0;    // x = np.zeros_like(b)  :100
+    }
+}
+
+// p = u (copy of M^-1 r, :98-99); partials [b.b, u.r]
+__global__ __launch_bounds__(kBlock) void pcg_gen_init2_kernel(int64_t n, const double *__restrict__ r,
+                                                               const double *__restrict__ u, double *__restrict__ p,
+                                                               double *__restrict__ part) {
+    __shared__ double sh[kWaves];
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    double bb = 0.0, ur = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
+        const double ri = r[i], ui = u[i];
+        p[i] = ui;
+        bb = fma(ri, ri, bb);
+        ur = fma(ui, ri, ur);
+    }
+    const double s0 = block_sum(bb, sh);
+    const double s1 = block_sum(ur, sh);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = s0;
+        part[2 * blockIdx.x + 1] = s1;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void pcg_dot_kernel(int64_t n, const double *__restrict__ a,
+                                                         const double *__restrict__ c, double *__restrict__ part,
+                                                         const PcgState *st) {
+    if (st->done) return;
+    __shared__ double sh[kWaves];
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    double acc = 0.0;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) acc = fma(a[i], c[i], acc);   // np.dot(u, r) :134
+    const double s = block_sum(acc, sh);
+    if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+__global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
+    int64_t n, const double *__restrict__ u, double *__restrict__ p, const double *__restrict__ part2, int np2,
+    const double *__restrict__ part3, int np3, PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
+    int64_t k, int64_t maxiter, int fail_on_maxiter) {
+    if (st->done) return;
+    __shared__ double sh[kWaves];
+    const double rr = reduce_partials(part2, np2, 2, sh);
+    const double ur = reduce_partials(part3, np3, 1, sh);
+    const double normR = sqrt(rr);                           // :125
+    if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;
+    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            st->iters = k + 1;
+            st->resid = normR;
+            st->done = 1;
+        }
+        return;
+    }
+    const double beta = ur / udr[k];                         // :134-135
+    if (blockIdx.x == 0 && threadIdx.x == 0) udr[k + 1] = ur;
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) p[i] = u[i] + beta * p[i];   // :138
+}
+
 // -------------------------------------------------------------------------------------------------
 // host driver
 
 static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 struct PcgWork {
-    double *x, *r, *p, *Ap, *part1, *part2, *udr, *hist;
+    double *x, *r, *p, *Ap, *u, *part1, *part2, *part3, *udr, *hist;
     PcgState *st;
 };
 
-static int pcg_workspace(psk_csr *A, int64_t maxiter, PcgWork &w) {
+static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, PcgWork &w) {
     const size_t vec = align_up((size_t)A->n * 8, 256), vecc = align_up((size_t)A->ncols * 8, 256);
-    const size_t big = 3 * vec + vecc;
+    const size_t big = (gen ? 4 : 3) * vec + vecc;
     PSK_TRY(A->ws.ensure(big > 0 ? big : 256));
     char *b = A->ws.as<char>();
     w.x = reinterpret_cast<double *>(b);
     w.r = reinterpret_cast<double *>(b + vec);
     w.Ap = reinterpret_cast<double *>(b + 2 * vec);
     w.p = reinterpret_cast<double *>(b + 3 * vec);
-    const size_t small = align_up(sizeof(PcgState), 256) + align_up(kMaxGrid * 8, 256) +
+    w.u = gen ? reinterpret_cast<double *>(b + 3 * vec + vecc) : nullptr;
+    const size_t small = align_up(sizeof(PcgState), 256) + 2 * align_up(kMaxGrid * 8, 256) +
                          align_up(2 * kMaxGrid * 8, 256) + align_up((size_t)(maxiter + 2) * 8, 256) +
                          align_up((size_t)(maxiter + 1) * 8, 256);
     PSK_TRY(A->ws_small.ensure(small));
@@ -220,6 +295,8 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, PcgWork &w) {
     w.st = reinterpret_cast<PcgState *>(s);
     s += align_up(sizeof(PcgState), 256);
     w.part1 = reinterpret_cast<double *>(s);
+    s += align_up(kMaxGrid * 8, 256);
+    w.part3 = reinterpret_cast<double *>(s);
     s += align_up(kMaxGrid * 8, 256);
     w.part2 = reinterpret_cast<double *>(s);
     s += align_up(2 * kMaxGrid * 8, 256);
@@ -248,8 +325,11 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     hipStream_t s = c->stream;
     std::memset(res, 0, sizeof(*res));
     const int64_t n = A->n, maxiter = ctl->maxiter;
+    // general preconditioner (ILU): u = M^-1 r materialised between K2 and K3
+    const bool gen = M && M->kind == PSK_PREC_ILU;
+    if (gen && A->comm) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: ILU preconditioning of a sharded matrix");
     PcgWork w;
-    PSK_TRY(pcg_workspace(A, maxiter, w));
+    PSK_TRY(pcg_workspace(A, maxiter, gen, w));
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
     const int gs = spmv_grid(c, A);   // SpMV grid
     const int gv = grid_for_rows(c, n, kVecTile);    // elementwise grid
@@ -268,7 +348,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // b staged in the Ap buffer (unused until the first SpMV)
     PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
     PSK_HIP(hipEventRecord(ev0, s));
-    hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
+    if (gen) {
+        const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
+        if (n > 0) hipLaunchKernelGGL(pcg_gen_init_kernel, dim3(nb), dim3(kBlock), 0, s, n, w.Ap, w.x, w.r);
+        PSK_TRY(prec_apply_dev(M, n, w.r, w.u, s));                   // p = precond.applyRight(r)  :98
+        hipLaunchKernelGGL(pcg_gen_init2_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.u, w.p, w.part2);
+    } else {
+        hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
+    }
     PSK_HIP(hipGetLastError());
     if (sharded) PSK_TRY(allreduce_sum(A, w.part2, 2 * np2, s));
     hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, np2, ctl->tau, w.st, w.udr);
@@ -334,8 +421,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         hipLaunchKernelGGL(pcg_update_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap, dinv,
                            w.part1, np1, w.part2, w.st, w.udr, k);
         if (sharded && (rc = allreduce_sum(A, w.part2, 2 * np2, s)) != PSK_OK) break;
-        hipLaunchKernelGGL(pcg_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv, w.part2,
-                           np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+        if (gen) {
+            if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
+            hipLaunchKernelGGL(pcg_dot_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.u, w.r, w.part3, w.st);
+            hipLaunchKernelGGL(pcg_gen_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.u, w.p, w.part2, np2,
+                               w.part3, gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+        } else {
+            hipLaunchKernelGGL(pcg_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv, w.part2,
+                               np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+        }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;
     }
@@ -344,6 +438,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     if (rc == PSK_OK && hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = fail(PSK_ERR_HIP, "state copy");
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg sync");
+    if (rc == PSK_OK && gen) rc = ilu_check_error(M, s);
     if (rc == PSK_OK && ctl->time_kernels)
         for (int i = 0; i < TP && rc == PSK_OK; ++i) rc = harvest(i);
     if (rc == PSK_OK) {

@@ -110,6 +110,13 @@ struct psk_prec {
     int kind = PSK_PREC_IDENTITY;
     int64_t n = 0;
     double *dinv = nullptr;   // JACOBI
+    // ILU: L strictly lower (unit diag), U strictly upper + diag, CSR; permutations of SuperLU
+    int32_t *l_rowptr = nullptr, *l_colidx = nullptr, *u_rowptr = nullptr, *u_colidx = nullptr;
+    double *l_vals = nullptr, *u_vals = nullptr, *u_diag = nullptr;
+    int32_t *perm_r_inv = nullptr, *perm_c = nullptr;
+    double *work = nullptr;   // 2n: y, z
+    int32_t *err = nullptr;
+    int64_t nnz_l = 0, nnz_u = 0;
 };
 
 namespace psk {
@@ -183,6 +190,10 @@ enum SpmvMode : int {
 };
 int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int64_t row_end,
               int64_t halo_lo_start, hipStream_t s);
+// generic preconditioner apply (device pointers, out must not alias v): identity copy, Jacobi, ILU
+int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, hipStream_t s);
+int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
+int ilu_check_error(const psk_prec *M, hipStream_t s);
 int tile_rows_for(int64_t n, int64_t nnz);
 int spmv_grid(const Context *c, const psk_csr *A);
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,

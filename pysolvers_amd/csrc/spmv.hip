@@ -291,6 +291,22 @@ __global__ void scale_kernel(int64_t n, const double *__restrict__ d, const doub
     if (i < n) out[i] = d[i] * v[i];
 }
 
+int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, hipStream_t s) {
+    if (n == 0) return PSK_OK;
+    if (!M || M->kind == PSK_PREC_IDENTITY) {
+        PSK_HIP(hipMemcpyAsync(out, v, (size_t)n * 8, hipMemcpyDeviceToDevice, s));
+        return PSK_OK;
+    }
+    if (M->kind == PSK_PREC_JACOBI) {
+        hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,
+                           M->dinv, v, out);
+        PSK_HIP(hipGetLastError());
+        return PSK_OK;
+    }
+    if (M->kind == PSK_PREC_ILU) return ilu_apply(M, v, out, s);
+    return fail(PSK_ERR_UNSUPPORTED, "unknown preconditioner kind");
+}
+
 }  // namespace psk
 
 using namespace psk;
@@ -562,24 +578,26 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
     DevBuf tmp;
     const double *dv = v;
     double *dout = outv;
-    if (loc == PSK_HOST) {
+    if (loc == PSK_HOST || v == outv) {
         PSK_TRY(tmp.ensure((size_t)2 * n * sizeof(double)));
         double *b = tmp.as<double>();
         PSK_TRY(to_device_vec(v, loc, n, b, c->stream));
         dv = b;
         dout = b + n;
     }
-    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       c->stream, n, M->dinv, dv, dout);
-    PSK_HIP(hipGetLastError());
-    if (loc == PSK_HOST) PSK_TRY(from_device_vec(dout, PSK_HOST, n, outv, c->stream));
+    PSK_TRY(prec_apply_dev(M, n, dv, dout, c->stream));
+    if (M->kind == PSK_PREC_ILU) PSK_TRY(ilu_check_error(M, c->stream));
+    if (dout != outv) PSK_TRY(from_device_vec(dout, loc, n, outv, c->stream));
     PSK_HIP(hipStreamSynchronize(c->stream));
     return PSK_OK;
 }
 
 int psk_prec_destroy(psk_prec *M) {
     if (!M) return PSK_OK;
-    if (M->dinv) (void)hipFree(M->dinv);
+    void *ptrs[] = {M->dinv, M->l_rowptr, M->l_colidx, M->l_vals, M->u_rowptr, M->u_colidx, M->u_vals,
+                    M->u_diag, M->perm_r_inv, M->perm_c, M->work, M->err};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
     delete M;
     return PSK_OK;
 }

@@ -73,7 +73,7 @@ sys.path.insert(0, REF)
 sys.path.insert(0, os.path.join(REF, "examples"))
 
 from PySolvers import CommonSolverArgs                                   # noqa: E402
-from PySolvers.Linear import PCG, GMRES                                  # noqa: E402
+from PySolvers.Linear import PCG, GMRES, RightILUT                       # noqa: E402
 from PySolvers.Linear.PreconditionerType import PreconditionerType       # noqa: E402
 from PySolvers.Linear.Preconditioner import GenericPreconditioner        # noqa: E402
 from PySolvers.Linear.IterativeLinearSolver import mvmult as ref_mvmult  # noqa: E402
@@ -98,10 +98,20 @@ class _Jacobi(PreconditionerType):
         return _JacobiPrec(A)
 
 
+def _pname(jac):
+    """Case preconditioner flag -> name: False/True (identity/Jacobi) or a name such as "ilut"."""
+    return jac if isinstance(jac, str) else ("jacobi" if jac else "identity")
+
+
+def _oracle_prec(A, jac):
+    return {"identity": lambda: krylov.identity_apply, "jacobi": lambda: krylov.jacobi_form(A),
+            "ilut": lambda: krylov.ilut_form(A)}[_pname(jac)]()
+
+
 def _run_ref(kind, A, b, maxiter, tau, fail_on_maxiter=True, jacobi=False):
     ctl = CommonSolverArgs(maxiter=maxiter, tau=tau, failOnMaxiter=fail_on_maxiter,
                            showIters=False, showFinal=False)
-    pt = _Jacobi() if jacobi else None
+    pt = {"identity": None, "jacobi": _Jacobi(), "ilut": RightILUT()}[_pname(jacobi)]
     if kind == "pcg":
         st = (PCG(control=ctl, precond=pt) if pt else PCG(control=ctl)).makeSolver()
     else:
@@ -146,7 +156,7 @@ def sensitivity(kind, A, b, maxiter, tau, fom, jac, hist_ref, soln_ref, seeds=8)
         krylov.np.dot = pdot
         krylov.npla.norm = lambda v: math.sqrt(pdot(v, v))
         try:
-            prec = krylov.jacobi_form(A) if jac else krylov.identity_apply
+            prec = _oracle_prec(A, jac)
             fn = krylov.pcg if kind == "pcg" else krylov.gmres
             st = fn(A, b, maxiter=maxiter, tau=tau, fail_on_maxiter=fom, precond=prec)
         finally:
@@ -255,6 +265,12 @@ def main():
     cases.append(("gmres", "fd16", ref_fd2d(-1.0, 1.0, 16), 300, 1e-8, True, False))
     cases.append(("gmres", "fd16", ref_fd2d(-1.0, 1.0, 16), 300, 1e-8, True, True))
     cases.append(("gmres", "fd32", ref_fd2d(-1.0, 1.0, 32), 300, 1e-10, True, True))
+    # GMRES + RightILUT (examples/GMRESExample_ILUT.py plumbing, configs[2] at small sizes)
+    for lev in (8, 10):
+        cases.append(("gmres", "dh%d" % lev, _dh(lev), 100, 1e-8, True, "ilut"))
+    for m in (32, 64):
+        cases.append(("gmres", "fd%d" % m, ref_fd2d(-1.0, 1.0, m), 100, 1e-8, True, "ilut"))
+    cases.append(("pcg", "dh10", _dh(10), 300, 1e-8, True, "ilut"))
 
     index = []
     for kind, name, A, maxiter, tau, fom, jac in cases:
@@ -262,21 +278,23 @@ def main():
         # b from the reference's own mvmult must equal the oracle's
         assert np.array_equal(b, ref_mvmult(A, xex))
         res, hist = _run_ref(kind, A, b, maxiter, tau, fom, jac)
-        prec = krylov.jacobi_form(A) if jac else krylov.identity_apply
+        prec = _oracle_prec(A, jac)
         fn = krylov.pcg if kind == "pcg" else krylov.gmres
         orc = fn(A, b, maxiter=maxiter, tau=tau, fail_on_maxiter=fom, precond=prec)
-        tag = "%s_%s_%s" % (kind, name, "jacobi" if jac else "identity")
+        tag = "%s_%s_%s" % (kind, name, _pname(jac))
         _check_same(tag, res, hist, orc)
         fname = tag + ".npz"
         payload = dict(b=b, x_exact=xex, hist=hist, maxiter=np.int64(maxiter), tau=np.float64(tau),
-                       fail_on_maxiter=np.int64(fom), jacobi=np.int64(jac),
+                       fail_on_maxiter=np.int64(fom), jacobi=np.int64(_pname(jac) == "jacobi"),
+                       precond=np.array(_pname(jac)),
                        iters=np.int64(res.iters()), success=np.int64(bool(res.success())),
                        resid=np.float64(res.resid() if res.resid() is not None else np.nan),
                        soln=res.soln() if res.soln() is not None else np.zeros(0),
                        **_csr_arrays(A))
         np.savez_compressed(os.path.join(HERE, fname), **payload)
         index.append(dict(file=fname, kind=kind, matrix=name, n=int(A.shape[0]), nnz=int(A.nnz),
-                          maxiter=maxiter, tau=tau, fail_on_maxiter=fom, jacobi=jac,
+                          maxiter=maxiter, tau=tau, fail_on_maxiter=fom, jacobi=_pname(jac) == "jacobi",
+                          precond=_pname(jac),
                           iters=int(res.iters()), success=bool(res.success()),
                           resid=None if res.resid() is None else float(res.resid()),
                           final_ratio=float(hist[-1] / np.linalg.norm(b)) if len(hist) else None,

@@ -160,7 +160,9 @@ def test_solver_matches_reference(psk, case):
     d = load_golden(case["file"])
     A = golden_matrix(d)
     ctl = _ctl(maxiter=case["maxiter"], tau=case["tau"], failOnMaxiter=bool(case["fail_on_maxiter"]))
-    pt = psk.JacobiPreconditionerType() if case["jacobi"] else psk.IdentityPreconditionerType()
+    name = case.get("precond", "jacobi" if case["jacobi"] else "identity")
+    pt = {"identity": psk.IdentityPreconditionerType, "jacobi": psk.JacobiPreconditionerType,
+          "ilut": psk.RightILUT}[name]()
     factory = psk.PCG if case["kind"] == "pcg" else psk.GMRES
     st = factory(control=ctl, precond=pt).makeSolver().solve(A, d["b"])
     _check_against_golden(st, d, case)
@@ -262,3 +264,32 @@ def test_fd4096_spmv_and_first_iterations(psk):
     assert st.iters() == ref["iters"] == 12
     np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=RTOL_RESID)
     assert np.linalg.norm(st.soln() - ref["soln"]) <= 1e-12 * np.linalg.norm(ref["soln"])
+
+
+# ---------------------------------------------------------------------------------------------
+# ILUT apply (RightILUTPreconditioner.applyRight = SuperLU ILU.solve) on the device
+
+@pytest.mark.parametrize("tag", ["fd64", "dh8"])
+def test_ilut_apply_matches_superlu(psk, tag):
+    d = load_golden("spmv.npz")
+    A = golden_matrix(d, tag + "_")
+    M = psk.RightILUT().form(A)
+    v = d[tag + "_x"]
+    ref = M.ILU().solve(v)
+    out = M.applyRight(v)
+    assert np.linalg.norm(out - ref) <= 1e-13 * np.linalg.norm(ref)
+    assert np.array_equal(M.applyLeft(v), v)                  # right preconditioner: identity on the left
+    L = psk.LeftILUT().form(A)
+    assert np.array_equal(L.applyRight(v), v)                 # Preconditioner.py:44-45
+    assert np.linalg.norm(L.applyLeft(v) - ref) <= 1e-13 * np.linalg.norm(ref)
+
+
+def test_ilut_apply_large_fd():
+    """FD m=512 (262k rows, ~3.7k dependency levels): device sweep vs SuperLU ILU.solve."""
+    import pysolvers_amd as psk
+    from oracle import fdlap
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, 512)
+    M = psk.RightILUT().form(A)
+    v = np.random.default_rng(9).standard_normal(A.shape[0])
+    ref = M.ILU().solve(v)
+    assert np.linalg.norm(M.applyRight(v) - ref) <= 1e-12 * np.linalg.norm(ref)

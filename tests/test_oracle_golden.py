@@ -69,7 +69,9 @@ def test_oracle_solvers_match_reference(case):
     A = golden_matrix(d)
     b = d["b"]
     assert np.array_equal(A @ d["x_exact"], b)
-    prec = krylov.jacobi_form(A) if case["jacobi"] else krylov.identity_apply
+    name = case.get("precond", "jacobi" if case["jacobi"] else "identity")
+    prec = {"identity": lambda: krylov.identity_apply, "jacobi": lambda: krylov.jacobi_form(A),
+            "ilut": lambda: krylov.ilut_form(A)}[name]()
     fn = krylov.pcg if case["kind"] == "pcg" else krylov.gmres
     st = fn(A, b, maxiter=case["maxiter"], tau=case["tau"], fail_on_maxiter=bool(case["fail_on_maxiter"]),
             precond=prec)
