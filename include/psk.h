@@ -24,6 +24,14 @@
  *                    xGMI); no reference counterpart (the reference is single-process).
  *   psk_csr_create_fd2d: examples/FDLaplacian2D.py:5-23 generated on the device,
  *                    bit-identical arrays and entry order.
+ *   psk_prec_create_trisolve  RightIC applyRight (ICPreconditioner.py:58-63), Gauss-Seidel
+ *                    smoother U^-1 (ClassicSmoothers.py:28-36), coarse SuperLU solve
+ *                    (VCycleManager.py:34-37): one sync-free triangular-solve chain.
+ *   psk_prec_create_amg  AMGPreconditioner.apply (AMGPreconditioner.py:46-51) ->
+ *                    AMGVCycleSolver.solve (VCycleSolver.py:52-95) -> VCycleManager.runLevel
+ *                    (VCycleManager.py:31-62), hierarchy built on the host.
+ *   psk_sa_aggregate BuildAggregates + BuildFilteredMatrix (SmoothedAggregation.py:57-183),
+ *                    O(nnz) host code.
  */
 #ifndef PSK_H
 #define PSK_H
@@ -57,7 +65,9 @@ extern "C" {
 /* preconditioner kinds */
 #define PSK_PREC_IDENTITY 0      /* IdentityPreconditionerType   PreconditionerType.py:13-19 */
 #define PSK_PREC_JACOBI   1      /* DInv*v                        ClassicSmoothers.py:5-16 pattern */
-#define PSK_PREC_ILU      2      /* SuperLU ILU.solve             ILUTPreconditioner.py:70-78 */
+#define PSK_PREC_ILU      2      /* triangular-solve chain: SuperLU ILU.solve ILUTPreconditioner.py:70-78,
+                                    IC, Gauss-Seidel, coarse LU (psk_prec_create_trisolve) */
+#define PSK_PREC_AMG      3      /* smoothed-aggregation V-cycles  AMGPreconditioner.py:46-51 */
 
 typedef struct psk_csr  psk_csr;    /* device CSR (int32 rowptr/colidx, f64 vals), library-owned */
 typedef struct psk_prec psk_prec;   /* formed preconditioner, library-owned */
@@ -107,6 +117,9 @@ int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t 
                    const double *vals, int32_t loc, psk_csr **out);
 /* FDLaplacian2D(a, b, m) generated on the device (examples/FDLaplacian2D.py:5-23). */
 int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out);
+/* Rectangular nrows x ncols CSR (AMG prolongators / restrictions, MLHierarchy.py:283-292). */
+int psk_csr_create_rect(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
+                        const double *vals, int32_t loc, psk_csr **out);
 int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
 /* Copy the arrays back to host buffers (any pointer may be NULL). */
 int psk_csr_download(const psk_csr *A, int32_t *rowptr, int32_t *colidx, double *vals);
@@ -130,8 +143,43 @@ int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out);
 int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx, const double *l_vals,
                         const int32_t *u_rowptr, const int32_t *u_colidx, const double *u_vals,
                         const int32_t *perm_r, const int32_t *perm_c, psk_prec **out);
+/* General triangular-solve chain on the device (host CSR arrays, copied):
+ *   bb[j] = v[gather_in[j]]          (gather_in NULL: bb = v)
+ *   y = L^-1 bb                      (L lower; l_unit: unit diagonal, stored diagonal entries ignored;
+ *                                     else the stored diagonal divides; L NULL: y = bb)
+ *   z = U^-1 y                       (U upper; same rules with u_unit; U NULL: z = y)
+ *   out[i] = z[gather_out[i]]        (gather_out NULL: out = z)
+ * Row i's off-diagonal products are accumulated in stored order with FMA, then one wave sum. */
+int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx, const double *l_vals,
+                             int32_t l_unit, const int32_t *u_rowptr, const int32_t *u_colidx,
+                             const double *u_vals, int32_t u_unit, const int32_t *gather_in,
+                             const int32_t *gather_out, psk_prec **out);
+/* Smoothed-aggregation AMG preconditioner over a host-built hierarchy (levels 0 = coarsest ..
+ * num_levels-1 = finest, MLHierarchy.py:250-258). Arrays of num_levels handles, all BORROWED
+ * (they must outlive the preconditioner): A[k] level matrices (A[num_levels-1] = the fine A),
+ * P[k] (n_{k+1} x n_k) and R[k] (n_k x n_{k+1}) for k < num_levels-1, smoother[k] for k >= 1
+ * (any preconditioner S: one sweep is x <- x + S^-1 (f - A x): PSK_PREC_ILU upper solve with
+ * triu(A_k) = Gauss-Seidel, PSK_PREC_JACOBI = Jacobi; ClassicSmoothers.py:5-36), coarse = the
+ * level-0 direct solve. apply(v): x = v; num_iters V-cycles, stopping after the first cycle whose
+ * ||v - A x|| < tau ||v|| (VCycleSolver.py:119-146). */
+int psk_prec_create_amg(int32_t num_levels, psk_csr *const *A, psk_csr *const *P, psk_csr *const *R,
+                        psk_prec *const *smoother, psk_prec *coarse, int32_t num_iters, int32_t nu_pre,
+                        int32_t nu_post, double tau, psk_prec **out);
+/* kind, size and triangular-solve shape of a preconditioner (any out pointer may be NULL). */
+int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, int64_t *nnz_u,
+                  int64_t *levels_l, int64_t *levels_u);
 int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *out, int32_t loc);
 int psk_prec_destroy(psk_prec *M);
+
+/* ---- AMG setup (host only, no GPU needed) --------------------------------------------------- */
+/* Smoothed-aggregation coarsening of one level, SmoothedAggregation.py:41-183 in O(nnz):
+ * agg[i] = aggregate of node i (the reference's list order: isolated nodes, then phase-1
+ * aggregates; phase 2 by strongest |A[i,k]|), *count = number of aggregates, and af_vals =
+ * the values of the filtered matrix A_f (same structure as A; entries outside N_i lumped onto
+ * the diagonal in stored order, including the neighbourhood growth the reference's set aliasing
+ * causes). tol is the strength threshold (0.08 * 0.5^(lvl-1) by default). */
+int psk_sa_aggregate(int64_t n, const int32_t *rowptr, const int32_t *colidx, const double *vals, double tol,
+                     int32_t *agg, int64_t *count, double *af_vals);
 
 /* ---- solvers ------------------------------------------------------------------------------ */
 /* M == NULL means identity. b, x: length n (local length for a distributed A). hist: nullable

@@ -40,6 +40,25 @@ def ilut_form(A, drop_tol=0.001, fill_factor=15):
     return ilu.solve
 
 
+def ic_form(A, drop_tol=0.001, fill_factor=15):
+    """RightIC: ICRightPreconditioner setup (ICPreconditioner.py:45-56) and applyRight (:58-63),
+    the same scipy calls in the same order."""
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    ilu = spla.spilu(A.tocsc(), drop_tol=drop_tol, fill_factor=fill_factor, diag_pivot_thresh=0.0,
+                     options={'ColPerm': 'NATURAL'})
+    n = A.shape[0]
+    dinv = sp.dia_matrix((np.reciprocal(np.sqrt(ilu.U.diagonal())), [0]), shape=(n, n))
+    Lt = dinv * ilu.U
+    L = Lt.transpose().tocsr()
+    Lt = Lt.tocsr()
+
+    def apply(v):
+        u = spla.spsolve_triangular(L, v, lower=True)
+        return spla.spsolve_triangular(Lt, u, lower=False)
+    return apply
+
+
 def mvmult(A, x):
     """IterativeLinearSolver.py:94-106: ``A*x`` -> scipy csr_matvec for sparse A."""
     return A @ x

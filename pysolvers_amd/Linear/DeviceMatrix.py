@@ -66,9 +66,10 @@ def is_device_vector(v):
 class DeviceCSR:
     """CSR matrix (int32 rowptr/colidx, float64 vals) in HBM; stored entry order is preserved."""
 
-    def __init__(self, handle, n, nnz, comm=None, row_begin=0, row_end=None, n_global=None):
+    def __init__(self, handle, n, nnz, comm=None, row_begin=0, row_end=None, n_global=None, ncols=None):
         self._h = handle
         self.n = int(n)
+        self.ncols = int(n if ncols is None else ncols)
         self.nnz = int(nnz)
         self.comm = comm
         self.row_begin = int(row_begin)
@@ -77,12 +78,14 @@ class DeviceCSR:
 
     # --- constructors ---------------------------------------------------------------------
     @classmethod
-    def from_scipy(cls, A):
+    def from_scipy(cls, A, rectangular=False):
+        """Upload a scipy matrix (CSR kept in its stored entry order). rectangular=True allows
+        nrows != ncols (AMG transfer operators); solvers require square matrices."""
         if not sp.issparse(A):
             A = sp.csr_matrix(np.asarray(A, dtype=np.float64))
         A = A.tocsr()
         n, nc = A.shape
-        if n != nc:
+        if n != nc and not rectangular:
             raise AssertionError("matrix must be square")
         if A.nnz >= 2 ** 31:
             raise ValueError("int32 CSR required (nnz < 2^31)")
@@ -90,9 +93,9 @@ class DeviceCSR:
         indices = np.ascontiguousarray(A.indices, dtype=np.int32)
         data = np.ascontiguousarray(A.data, dtype=np.float64)
         h = ctypes.c_void_p()
-        N.check(N.lib.psk_csr_create(n, A.nnz, N.ptr(indptr), N.ptr(indices), N.ptr(data), N.PSK_HOST,
-                                     ctypes.byref(h)), "psk_csr_create")
-        return cls(h, n, A.nnz)
+        N.check(N.lib.psk_csr_create_rect(n, nc, A.nnz, N.ptr(indptr), N.ptr(indices), N.ptr(data), N.PSK_HOST,
+                                          ctypes.byref(h)), "psk_csr_create_rect")
+        return cls(h, n, A.nnz, ncols=nc)
 
     @classmethod
     def fd_laplacian_2d(cls, a, b, m):
@@ -106,7 +109,7 @@ class DeviceCSR:
     # --- accessors ------------------------------------------------------------------------
     @property
     def shape(self):
-        return (self.n, self.n) if self.comm is None else (self.n, self.n_global)
+        return (self.n, self.ncols) if self.comm is None else (self.n, self.n_global)
 
     @property
     def handle(self):
@@ -119,7 +122,7 @@ class DeviceCSR:
         N.check(N.lib.psk_csr_download(self._h, N.ptr(indptr), N.ptr(indices), N.ptr(data)), "psk_csr_download")
         if self.comm is not None:
             return indptr, indices, data
-        A = sp.csr_matrix((data, indices, indptr), shape=(self.n, self.n))
+        A = sp.csr_matrix((data, indices, indptr), shape=(self.n, self.ncols))
         A.has_sorted_indices = False
         return A
 
@@ -140,7 +143,7 @@ def as_device_matrix(A):
 
 def spmv(A, x):
     """y = A x on the device; bit-identical to scipy csr_matvec (stored-order row sums)."""
-    dA = as_device_matrix(A)
+    dA = A if isinstance(A, DeviceCSR) else DeviceCSR.from_scipy(A, rectangular=True)
     if isinstance(x, DeviceVector):
         y = DeviceVector(dA.n)
         N.check(N.lib.psk_spmv(dA.handle, x._p, y._p, N.PSK_DEVICE), "psk_spmv")
@@ -151,7 +154,7 @@ def spmv(A, x):
         N.check(N.lib.psk_spmv(dA.handle, N.ptr(x), N.ptr(y), N.PSK_DEVICE), "psk_spmv")
         return y
     x = np.ascontiguousarray(x, dtype=np.float64)
-    if x.shape[0] != dA.n:
+    if x.shape[0] != (dA.ncols if dA.comm is None else dA.n):
         raise ValueError("dimension mismatch")
     y = np.empty(dA.n, dtype=np.float64)
     N.check(N.lib.psk_spmv(dA.handle, N.ptr(x), N.ptr(y), N.PSK_HOST), "psk_spmv")

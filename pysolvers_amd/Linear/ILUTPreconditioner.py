@@ -14,8 +14,8 @@ import numpy as np
 import scipy.sparse.linalg as spla
 
 from .. import _native as N
-from .DeviceMatrix import DeviceCSR, DeviceVector, is_device_vector
-from .Preconditioner import LeftPreconditioner, Preconditioner, RightPreconditioner
+from .DeviceMatrix import DeviceCSR
+from .Preconditioner import DeviceOperator, LeftPreconditioner, Preconditioner, RightPreconditioner
 from .PreconditionerType import PreconditionerType
 
 
@@ -41,7 +41,7 @@ class RightILUT(PreconditionerType):
         return RightILUTPreconditioner(A, drop_tol=self.drop_tol, fill_factor=self.fill_factor)
 
 
-class ILUTPreconditioner(Preconditioner):
+class ILUTPreconditioner(DeviceOperator, Preconditioner):
     def __init__(self, A, drop_tol=0.001, fill_factor=15):
         Ah = _host_matrix(A)
         self._ILU = spla.spilu(Ah.tocsc(), drop_tol=drop_tol, fill_factor=fill_factor, diag_pivot_thresh=0.0)
@@ -59,29 +59,6 @@ class ILUTPreconditioner(Preconditioner):
     def ILU(self):
         return self._ILU
 
-    def _device_apply(self, vec):
-        if isinstance(vec, DeviceVector):
-            out = DeviceVector(self.n)
-            N.check(N.lib.psk_prec_apply(self._h, self.n, vec._p, out._p, N.PSK_DEVICE), "psk_prec_apply")
-            return out
-        if is_device_vector(vec):
-            import torch
-            out = torch.empty_like(vec)
-            N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(vec), N.ptr(out), N.PSK_DEVICE), "psk_prec_apply")
-            return out
-        v = np.ascontiguousarray(vec, dtype=np.float64)
-        out = np.empty_like(v)
-        N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(v), N.ptr(out), N.PSK_HOST), "psk_prec_apply")
-        return out
-
-    def __del__(self):
-        try:
-            if self._h:
-                N.lib.psk_prec_destroy(self._h)
-                self._h = ctypes.c_void_p()
-        except Exception:
-            pass
-
 
 class LeftILUTPreconditioner(ILUTPreconditioner, LeftPreconditioner):
     """applyRight is the identity (Preconditioner.py:44-45)."""
@@ -95,10 +72,6 @@ class LeftILUTPreconditioner(ILUTPreconditioner, LeftPreconditioner):
 
 class RightILUTPreconditioner(ILUTPreconditioner, RightPreconditioner):
     device_kind = N.PSK_PREC_ILU
-
-    @property
-    def device_handle(self):
-        return self._h
 
     def applyRight(self, vec):
         return self._device_apply(vec)

@@ -88,7 +88,7 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         kind = getattr(self.precond, "device_kind", None)
         if kind is None:
             raise TypeError("%s: preconditioner %r has no device implementation; available: "
-                            "IdentityPreconditionerType, JacobiPreconditionerType"
+                            "IdentityPreconditionerType, JacobiPreconditionerType, RightILUT, RightIC, AMG"
                             % (self.name(), type(self.precond).__name__))
         ph = None if kind == N.PSK_PREC_IDENTITY else self.precond.device_handle
 

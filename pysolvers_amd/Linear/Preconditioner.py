@@ -68,7 +68,49 @@ class IdentityPreconditioner:
         return vec
 
 
-class JacobiPreconditioner(GenericPreconditioner):
+class DeviceOperator:
+    """Mixin for preconditioners backed by a libpsk psk_prec handle (self._h, size self.n).
+
+    ``_device_apply`` takes a DeviceVector, a CUDA float64 tensor or a host array and returns the
+    same kind; the operator itself always runs on the GPU.
+    """
+
+    _h = None
+    device_kind = None
+
+    @property
+    def device_handle(self):
+        return self._h
+
+    def _device_apply(self, vec):
+        if isinstance(vec, DeviceVector):
+            out = DeviceVector(self.n)
+            N.check(N.lib.psk_prec_apply(self._h, self.n, vec._p, out._p, N.PSK_DEVICE), "psk_prec_apply")
+            return out
+        if is_device_vector(vec):
+            import torch
+            out = torch.empty_like(vec)
+            N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(vec), N.ptr(out), N.PSK_DEVICE), "psk_prec_apply")
+            return out
+        v = np.ascontiguousarray(vec, dtype=np.float64)
+        out = np.empty_like(v)
+        N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(v), N.ptr(out), N.PSK_HOST), "psk_prec_apply")
+        return out
+
+    def device_info(self):
+        """kind / size / triangular-solve nnz and dependency levels (psk_prec_info)."""
+        return N.prec_info(self._h)
+
+    def __del__(self):
+        try:
+            if self._h:
+                N.lib.psk_prec_destroy(self._h)
+                self._h = ctypes.c_void_p()
+        except Exception:
+            pass
+
+
+class JacobiPreconditioner(DeviceOperator, GenericPreconditioner):
     """M^-1 v = DInv * v with DInv = reciprocal(diag(A)) formed on the device.
 
     The reference has Jacobi only as a smoother (ClassicSmoothers.py:5-16:
@@ -86,29 +128,5 @@ class JacobiPreconditioner(GenericPreconditioner):
         self._h = h
         self.n = self._A.n
 
-    @property
-    def device_handle(self):
-        return self._h
-
     def apply(self, vec):
-        if isinstance(vec, DeviceVector):
-            out = DeviceVector(self.n)
-            N.check(N.lib.psk_prec_apply(self._h, self.n, vec._p, out._p, N.PSK_DEVICE), "psk_prec_apply")
-            return out
-        if is_device_vector(vec):
-            import torch
-            out = torch.empty_like(vec)
-            N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(vec), N.ptr(out), N.PSK_DEVICE), "psk_prec_apply")
-            return out
-        v = np.ascontiguousarray(vec, dtype=np.float64)
-        out = np.empty_like(v)
-        N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(v), N.ptr(out), N.PSK_HOST), "psk_prec_apply")
-        return out
-
-    def __del__(self):
-        try:
-            if self._h:
-                N.lib.psk_prec_destroy(self._h)
-                self._h = ctypes.c_void_p()
-        except Exception:
-            pass
+        return self._device_apply(vec)

@@ -5,11 +5,11 @@ there is no CPU fallback.
 """
 from . import Linear
 from .IterativeSolver import CommonSolverArgs, IterativeSolver, NamedObject, SolveStatus
-from .Linear import (GMRES, PCG, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
+from .Linear import (AMG, GMRES, PCG, RightIC, GaussSeidelSmoother, JacobiSmoother, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
                      IdentityPreconditionerType, IterativeLinearSolver, Jacobi, JacobiPreconditioner,
                      JacobiPreconditionerType, LeftILUT, PCGSolver, RightILUT, mvmult)
 
-__all__ = ["Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
+__all__ = ["AMG", "RightIC", "GaussSeidelSmoother", "JacobiSmoother", "Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
            "GMRESSolver", "PCGSolver", "DeviceCSR", "DeviceVector", "IdentityPreconditioner",
            "IdentityPreconditionerType", "IterativeLinearSolver", "Jacobi", "JacobiPreconditioner",
            "JacobiPreconditionerType", "LeftILUT", "RightILUT", "mvmult"]

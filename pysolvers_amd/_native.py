@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"
 PSK_OK = 0
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_HOST, PSK_DEVICE = 0, 1
-PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU = 0, 1, 2
+PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
 PSK_UNIQUE_ID_BYTES = 128
 
 STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOWN: "breakdown",
@@ -51,6 +51,7 @@ SIGNATURES = {
     "psk_dmemset0": (ctypes.c_int, [P, I64]),
     "psk_csr_create": (ctypes.c_int, [I64, I64, P, P, P, I32, PP]),
     "psk_csr_create_fd2d": (ctypes.c_int, [F64, F64, I64, PP]),
+    "psk_csr_create_rect": (ctypes.c_int, [I64, I64, I64, P, P, P, I32, PP]),
     "psk_csr_info": (ctypes.c_int, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
     "psk_csr_download": (ctypes.c_int, [P, P, P, P]),
     "psk_csr_destroy": (ctypes.c_int, [P]),
@@ -62,6 +63,10 @@ SIGNATURES = {
     "psk_prec_apply": (ctypes.c_int, [P, I64, P, P, I32]),
     "psk_prec_create_ilu": (ctypes.c_int, [I64, P, P, P, P, P, P, P, P, PP]),
     "psk_prec_destroy": (ctypes.c_int, [P]),
+    "psk_prec_create_trisolve": (ctypes.c_int, [I64, P, P, P, I32, P, P, P, I32, P, P, PP]),
+    "psk_prec_create_amg": (ctypes.c_int, [I32, PP, PP, PP, PP, P, I32, I32, I32, F64, PP]),
+    "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),
+    "psk_sa_aggregate": (ctypes.c_int, [I64, P, P, P, F64, P, ctypes.POINTER(I64), P]),
     "psk_pcg": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
     "psk_gmres": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
     "psk_comm_unique_id": (ctypes.c_int, [P]),
@@ -73,6 +78,23 @@ SIGNATURES = {
     "psk_csr_create_dist": (ctypes.c_int, [I64, I64, I64, P, P, P, P, PP]),
     "psk_fd2d_dist_plan": (ctypes.c_int, [I64, I32, I32] + [ctypes.POINTER(I64)] * 5),
 }
+
+
+def prec_info(h):
+    """dict(kind, n, nnz_l, nnz_u, levels_l, levels_u) of a psk_prec handle."""
+    k = I32()
+    v = [I64() for _ in range(5)]
+    check(lib.psk_prec_info(h, ctypes.byref(k), *[ctypes.byref(x) for x in v]), "psk_prec_info")
+    return dict(kind=k.value, n=v[0].value, nnz_l=v[1].value, nnz_u=v[2].value, levels_l=v[3].value,
+                levels_u=v[4].value)
+
+
+def handle_array(hs):
+    """ctypes void*[] of handles (None -> NULL)."""
+    arr = (ctypes.c_void_p * max(len(hs), 1))()
+    for i, h in enumerate(hs):
+        arr[i] = h.value if isinstance(h, ctypes.c_void_p) else h
+    return ctypes.cast(arr, PP), arr
 
 
 def fd2d_dist_plan(m, nranks, rank):

@@ -232,6 +232,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     if (!Ac || !b || !xout || !ctl || !res) return fail(PSK_ERR_ARG, "psk_gmres: NULL argument");
     if (ctl->maxiter < 0 || ctl->restart < 0) return fail(PSK_ERR_ARG, "psk_gmres: negative maxiter/restart");
     if (M && M->n != Ac->n) return fail(PSK_ERR_ARG, "psk_gmres: preconditioner size mismatch");
+    if (!Ac->comm && Ac->ncols != Ac->n) return fail(PSK_ERR_ARG, "psk_gmres: matrix must be square");
     psk_csr *A = const_cast<psk_csr *>(Ac);
     if (A->comm && A->comm->nranks > 1)
         return fail(PSK_ERR_UNSUPPORTED, "psk_gmres: sharded GMRES not built (replicas only)");
@@ -256,7 +257,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
                                            " vectors does not fit in HBM; use restart");
     }
     // general (ILU) preconditioner: M^-1 q_k is materialised in w before the SpMV; t is scratch
-    const bool gen = M && M->kind == PSK_PREC_ILU;
+    const bool gen = prec_is_general(M);
     PSK_TRY(A->ws.ensure(qbytes + (gen ? 5 : 3) * vec));
     char *wb = A->ws.as<char>();
     double *Q = reinterpret_cast<double *>(wb);
@@ -454,7 +455,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     }
     if (rc == PSK_OK && hipEventRecord(ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "gmres sync");
-    if (rc == PSK_OK && gen) rc = ilu_check_error(M, s);
+    if (rc == PSK_OK && gen) rc = prec_check_error(M, s);
     if (rc == PSK_OK) {
         float ms = 0.f;
         (void)hipEventElapsedTime(&ms, ev0, ev1);

@@ -1,4 +1,8 @@
-// ilu.hip — right-ILUT apply on the device (RightILUTPreconditioner.applyRight, ILUTPreconditioner.py:70-78).
+// ilu.hip — sparse triangular-solve chains on the device: right-ILUT apply
+// (RightILUTPreconditioner.applyRight, ILUTPreconditioner.py:70-78), RightIC apply
+// (ICPreconditioner.py:58-63), the Gauss-Seidel smoother's U^-1 (ClassicSmoothers.py:28-36) and the
+// AMG coarse-level SuperLU solve (VCycleManager.py:34-37) are all "gather, lower solve, upper solve,
+// gather" with some stages absent (psk_prec_create_trisolve).
 //
 // The reference calls SuperLU's ILU.solve(v) (scipy SuperLU, dgstrs): with Pr A Pc ~= L U,
 //     bb[perm_r[i]] = v[i];  y = L^-1 bb (unit lower);  z = U^-1 y;  out[i] = z[perm_c[i]].
@@ -46,12 +50,12 @@ __global__ void fill_sentinel_kernel(int64_t n, double *x) {
     if (i < n) reinterpret_cast<uint64_t *>(x)[i] = kSentinel;
 }
 
-// UPPER == false: x = L^-1 rhs[perm] (unit diagonal, strictly-lower entries only)
-// UPPER == true : x = U^-1 rhs       (strictly-upper entries + diag)
+// One triangular factor: x_i = (rhs_i - sum_j T_ij x_j) / diag_i  (diag == nullptr: unit), rhs_i =
+// rhs[rhs_idx[i]] when rhs_idx is given. T holds the off-diagonal entries only; lower or upper is
+// implied by the dependency order the host computed.
 // Rows are visited in `order`, a topological order sorted by dependency level (host-computed):
 // every wave walks order[wave], order[wave + W], ... so all waves work on the shallow levels first
 // and a row waiting on a deep level never blocks shallower rows queued behind it on its wave.
-template <bool UPPER>
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ rp,
                                                         const int32_t *__restrict__ ci, const double *__restrict__ va,
                                                         const double *__restrict__ diag, const double *__restrict__ rhs,
@@ -87,16 +91,17 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
         if (lane == 0) {
             const double bi = rhs_idx ? rhs[rhs_idx[i]] : rhs[i];
             double r = bi - sum;
-            if (UPPER) r = r / diag[i];
+            if (diag) r = r / diag[i];
             store_pub(x + i, r);
         }
     }
 }
 
+// out[i] = z[perm[i]] (perm == nullptr: copy)
 __global__ void gather_perm_kernel(int64_t n, const double *__restrict__ z, const int32_t *__restrict__ perm,
                                    double *__restrict__ out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = z[perm[i]];   // out = z[perm_c]
+    if (i < n) out[i] = perm ? z[perm[i]] : z[i];
 }
 
 static int sptrsv_grid(const Context *c, const void *kern) {
@@ -107,7 +112,19 @@ static int sptrsv_grid(const Context *c, const void *kern) {
     return c->num_cus * per_cu;
 }
 
-// out = M^-1 v for an ILU preconditioner (all device pointers; out may not alias v)
+static int launch_sptrsv(const Context *c, int64_t n, const int32_t *rp, const int32_t *ci, const double *va,
+                         const double *dg, const double *rhs, const int32_t *rhs_idx, double *x, int32_t *err,
+                         const int32_t *ord, hipStream_t s) {
+    const void *k = reinterpret_cast<const void *>(&sptrsv_kernel);
+    const int g = sptrsv_grid(c, k);
+    int64_t nn = n;
+    void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
+    PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, 0, s));
+    return PSK_OK;
+}
+
+// out = (U^-1 L^-1 v[gather_in])[gather_out] for a triangular-solve chain (device pointers; out may
+// not alias v)
 int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     const int64_t n = M->n;
     if (n == 0) return PSK_OK;
@@ -115,31 +132,33 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     PSK_TRY(ctx(&c));
     const unsigned fb = (unsigned)((n + kBlock - 1) / kBlock);
     double *y = M->work, *z = M->work + n;
-    int32_t *err = M->err;
-    hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((2 * n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s,
-                       2 * n, y);   // y and z are contiguous
-    PSK_HIP(hipGetLastError());
-    {
-        const void *kl = reinterpret_cast<const void *>(&sptrsv_kernel<false>);
-        const int g = sptrsv_grid(c, kl);
-        int64_t nn = n;
-        const int32_t *rp = M->l_rowptr, *ci = M->l_colidx, *pinv = M->perm_r_inv;
-        const double *va = M->l_vals, *dg = nullptr;
-        const int32_t *ord = M->l_order;
-        void *args[] = {&nn, &rp, &ci, &va, &dg, &v, &pinv, &y, &err, &ord};
-        PSK_HIP(hipLaunchCooperativeKernel(kl, dim3(g), dim3(kBlock), args, 0, s));
+    const int nbuf = (M->has_l ? 1 : 0) + (M->has_u ? 1 : 0);
+    if (nbuf > 0) {
+        hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((nbuf * n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           s, nbuf * n, y);   // y and z are contiguous
+        PSK_HIP(hipGetLastError());
     }
-    {
-        const void *ku = reinterpret_cast<const void *>(&sptrsv_kernel<true>);
-        const int g = sptrsv_grid(c, ku);
-        int64_t nn = n;
-        const int32_t *rp = M->u_rowptr, *ci = M->u_colidx, *none = nullptr;
-        const double *va = M->u_vals, *dg = M->u_diag, *yy = y;
-        const int32_t *ord = M->u_order;
-        void *args[] = {&nn, &rp, &ci, &va, &dg, &yy, &none, &z, &err, &ord};
-        PSK_HIP(hipLaunchCooperativeKernel(ku, dim3(g), dim3(kBlock), args, 0, s));
+    const double *cur = v;                // current right-hand side
+    const int32_t *cur_idx = M->gather_in;
+    if (M->has_l) {
+        PSK_TRY(launch_sptrsv(c, n, M->l_rowptr, M->l_colidx, M->l_vals, M->l_diag, cur, cur_idx, y, M->err,
+                              M->l_order, s));
+        cur = y;
+        cur_idx = nullptr;
     }
-    hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, z, M->perm_c, out);
+    if (M->has_u) {
+        double *dst = M->has_l ? z : y;
+        PSK_TRY(launch_sptrsv(c, n, M->u_rowptr, M->u_colidx, M->u_vals, M->u_diag, cur, cur_idx, dst, M->err,
+                              M->u_order, s));
+        cur = dst;
+        cur_idx = nullptr;
+    }
+    if (cur_idx) {   // no factor at all: out = v[gather_in][gather_out]
+        hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, cur, cur_idx, y);
+        PSK_HIP(hipGetLastError());
+        cur = y;
+    }
+    hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, cur, M->gather_out, out);
     PSK_HIP(hipGetLastError());
     return PSK_OK;
 }
@@ -148,7 +167,7 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
     int32_t h = 0;
     PSK_HIP(hipMemcpyAsync(&h, M->err, 4, hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
-    if (h) return fail(PSK_ERR_HIP, "ILU triangular solve: dependency wait exceeded its bound (not co-resident?)");
+    if (h) return fail(PSK_ERR_HIP, "triangular solve: dependency wait exceeded its bound (not co-resident?)");
     return PSK_OK;
 }
 
@@ -168,96 +187,119 @@ static int upload(T **d, const std::vector<T> &h) {
     return PSK_OK;
 }
 
-extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx, const double *l_vals,
-                                   const int32_t *u_rowptr, const int32_t *u_colidx, const double *u_vals,
-                                   const int32_t *perm_r, const int32_t *perm_c, psk_prec **out) {
-    if (!out || n < 0 || !l_rowptr || !u_rowptr || !perm_r || !perm_c)
-        return fail(PSK_ERR_ARG, "psk_prec_create_ilu: NULL argument");
-    // split: L strictly lower (unit diagonal implied), U strictly upper + diagonal
-    std::vector<int32_t> lrp(n + 1, 0), urp(n + 1, 0), lci, uci, pinv(n), pc(perm_c, perm_c + n);
-    std::vector<double> lva, uva, udg(n, 0.0);
+// Split one host CSR factor into off-diagonal entries + diagonal. lower: entries must have c <= i.
+static int split_factor(int64_t n, const int32_t *rp, const int32_t *ci, const double *va, bool lower, bool unit,
+                        std::vector<int32_t> &orp, std::vector<int32_t> &oci, std::vector<double> &ova,
+                        std::vector<double> &dg) {
+    orp.assign(n + 1, 0);
+    if (!unit) dg.assign(n, 0.0);
+    const char *what = lower ? "lower factor" : "upper factor";
+    if (rp[0] != 0) return fail(PSK_ERR_ARG, std::string(what) + ": rowptr[0] != 0");
     for (int64_t i = 0; i < n; ++i) {
-        for (int32_t j = l_rowptr[i]; j < l_rowptr[i + 1]; ++j) {
-            const int32_t c = l_colidx[j];
-            if (c < 0 || c > i) return fail(PSK_ERR_ARG, "ILU: L has an entry above the diagonal");
-            if (c == i) continue;
-            lci.push_back(c);
-            lva.push_back(l_vals[j]);
-        }
-        lrp[i + 1] = (int32_t)lci.size();
+        if (rp[i + 1] < rp[i]) return fail(PSK_ERR_ARG, std::string(what) + ": rowptr not monotone");
         bool has_diag = false;
-        for (int32_t j = u_rowptr[i]; j < u_rowptr[i + 1]; ++j) {
-            const int32_t c = u_colidx[j];
-            if (c < i || c >= n) return fail(PSK_ERR_ARG, "ILU: U has an entry below the diagonal");
+        for (int32_t j = rp[i]; j < rp[i + 1]; ++j) {
+            const int32_t c = ci[j];
+            if (c < 0 || c >= n || (lower ? c > i : c < i))
+                return fail(PSK_ERR_ARG, std::string(what) + ": entry on the wrong side of the diagonal");
             if (c == i) {
-                udg[i] += u_vals[j];
+                if (!unit) dg[i] += va[j];
                 has_diag = true;
                 continue;
             }
-            uci.push_back(c);
-            uva.push_back(u_vals[j]);
+            oci.push_back(c);
+            ova.push_back(va[j]);
         }
-        if (!has_diag) return fail(PSK_ERR_ARG, "ILU: U has a missing diagonal entry");
-        urp[i + 1] = (int32_t)uci.size();
+        if (!unit && !has_diag) return fail(PSK_ERR_ARG, std::string(what) + ": missing diagonal entry");
+        orp[i + 1] = (int32_t)oci.size();
     }
+    return PSK_OK;
+}
+
+// dependency levels -> counting-sort the rows by level (stable: solve order inside a level)
+static void level_order(int64_t n, const std::vector<int32_t> &rp, const std::vector<int32_t> &ci, bool upper,
+                        std::vector<int32_t> &order, int64_t &nlev) {
+    std::vector<int32_t> lev(n, 0);
+    int32_t maxl = -1;
+    for (int64_t t = 0; t < n; ++t) {
+        const int64_t i = upper ? n - 1 - t : t;
+        int32_t l = 0;
+        for (int32_t j = rp[i]; j < rp[i + 1]; ++j) l = std::max(l, lev[ci[j]] + 1);
+        lev[i] = l;
+        maxl = std::max(maxl, l);
+    }
+    nlev = maxl + 1;
+    std::vector<int64_t> cnt((size_t)nlev + 1, 0);
+    for (int64_t i = 0; i < n; ++i) cnt[lev[i] + 1]++;
+    for (int64_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
+    order.assign(n, 0);
+    for (int64_t t = 0; t < n; ++t) {
+        const int64_t i = upper ? n - 1 - t : t;
+        order[cnt[lev[i]]++] = (int32_t)i;
+    }
+}
+
+static int check_perm(int64_t n, const int32_t *p, const char *what) {
     std::vector<char> seen(n, 0);
     for (int64_t i = 0; i < n; ++i) {
-        const int32_t p = perm_r[i];
-        if (p < 0 || p >= n || seen[p] || perm_c[i] < 0 || perm_c[i] >= n)
-            return fail(PSK_ERR_ARG, "ILU: invalid permutation");
-        seen[p] = 1;
-        pinv[p] = (int32_t)i;   // bb[perm_r[i]] = v[i]  <=>  bb[j] = v[pinv[j]]
+        if (p[i] < 0 || p[i] >= n || seen[p[i]]) return fail(PSK_ERR_ARG, std::string(what) + ": not a permutation");
+        seen[p[i]] = 1;
     }
-    // dependency levels -> counting-sort the rows by level (stable: index order inside a level)
-    auto level_order = [n](const std::vector<int32_t> &rp, const std::vector<int32_t> &ci, bool upper,
-                           std::vector<int32_t> &order, int64_t &nlev) {
-        std::vector<int32_t> lev(n, 0);
-        int32_t maxl = -1;
-        for (int64_t t = 0; t < n; ++t) {
-            const int64_t i = upper ? n - 1 - t : t;
-            int32_t l = 0;
-            for (int32_t j = rp[i]; j < rp[i + 1]; ++j) l = std::max(l, lev[ci[j]] + 1);
-            lev[i] = l;
-            maxl = std::max(maxl, l);
-        }
-        nlev = maxl + 1;
-        std::vector<int64_t> cnt((size_t)nlev + 1, 0);
-        for (int64_t i = 0; i < n; ++i) cnt[lev[i] + 1]++;
-        for (int64_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
-        order.assign(n, 0);
-        for (int64_t t = 0; t < n; ++t) {
-            const int64_t i = upper ? n - 1 - t : t;
-            order[cnt[lev[i]]++] = (int32_t)i;
-        }
-    };
-    std::vector<int32_t> lord, uord;
+    return PSK_OK;
+}
+
+extern "C" int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx,
+                                        const double *l_vals, int32_t l_unit, const int32_t *u_rowptr,
+                                        const int32_t *u_colidx, const double *u_vals, int32_t u_unit,
+                                        const int32_t *gather_in, const int32_t *gather_out, psk_prec **out) {
+    if (!out || n < 0) return fail(PSK_ERR_ARG, "psk_prec_create_trisolve: bad arguments");
+    if (n >= INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_prec_create_trisolve: n must fit int32");
+    const bool has_l = l_rowptr != nullptr, has_u = u_rowptr != nullptr;
+    std::vector<int32_t> lrp, urp, lci, uci, lord, uord;
+    std::vector<double> lva, uva, ldg, udg;
     int64_t nlev_l = 0, nlev_u = 0;
-    level_order(lrp, lci, false, lord, nlev_l);
-    level_order(urp, uci, true, uord, nlev_u);
+    if (has_l) {
+        if (l_rowptr[n] > 0 && (!l_colidx || !l_vals)) return fail(PSK_ERR_ARG, "lower factor: NULL arrays");
+        PSK_TRY(split_factor(n, l_rowptr, l_colidx, l_vals, true, l_unit != 0, lrp, lci, lva, ldg));
+        level_order(n, lrp, lci, false, lord, nlev_l);
+    }
+    if (has_u) {
+        if (u_rowptr[n] > 0 && (!u_colidx || !u_vals)) return fail(PSK_ERR_ARG, "upper factor: NULL arrays");
+        PSK_TRY(split_factor(n, u_rowptr, u_colidx, u_vals, false, u_unit != 0, urp, uci, uva, udg));
+        level_order(n, urp, uci, true, uord, nlev_u);
+    }
+    if (gather_in) PSK_TRY(check_perm(n, gather_in, "gather_in"));
+    if (gather_out) PSK_TRY(check_perm(n, gather_out, "gather_out"));
+    std::vector<int32_t> gin, gout;
+    if (gather_in) gin.assign(gather_in, gather_in + n);
+    if (gather_out) gout.assign(gather_out, gather_out + n);
 
     Context *c;
     PSK_TRY(ctx(&c));
     psk_prec *M = new psk_prec();
     M->kind = PSK_PREC_ILU;
+    M->n = n;
+    M->has_l = has_l;
+    M->has_u = has_u;
     M->l_levels = nlev_l;
     M->u_levels = nlev_u;
-    M->n = n;
     int rc = PSK_OK;
     if (rc == PSK_OK) rc = upload(&M->l_rowptr, lrp);
     if (rc == PSK_OK) rc = upload(&M->l_colidx, lci);
     if (rc == PSK_OK) rc = upload(&M->l_vals, lva);
+    if (rc == PSK_OK) rc = upload(&M->l_diag, ldg);
     if (rc == PSK_OK) rc = upload(&M->u_rowptr, urp);
     if (rc == PSK_OK) rc = upload(&M->u_colidx, uci);
     if (rc == PSK_OK) rc = upload(&M->u_vals, uva);
     if (rc == PSK_OK) rc = upload(&M->u_diag, udg);
-    if (rc == PSK_OK) rc = upload(&M->perm_r_inv, pinv);
-    if (rc == PSK_OK) rc = upload(&M->perm_c, pc);
+    if (rc == PSK_OK) rc = upload(&M->gather_in, gin);
+    if (rc == PSK_OK) rc = upload(&M->gather_out, gout);
     if (rc == PSK_OK) rc = upload(&M->l_order, lord);
     if (rc == PSK_OK) rc = upload(&M->u_order, uord);
     if (rc == PSK_OK && n > 0 && hipMalloc(&M->work, (size_t)(2 * n) * sizeof(double)) != hipSuccess)
-        rc = fail(PSK_ERR_ALLOC, "ILU work");
-    if (rc == PSK_OK && hipMalloc(&M->err, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_ALLOC, "ILU err");
-    if (rc == PSK_OK && hipMemset(M->err, 0, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_HIP, "ILU err");
+        rc = fail(PSK_ERR_ALLOC, "trisolve work");
+    if (rc == PSK_OK && hipMalloc(&M->err, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_ALLOC, "trisolve err");
+    if (rc == PSK_OK && hipMemset(M->err, 0, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_HIP, "trisolve err");
     if (rc != PSK_OK) {
         psk_prec_destroy(M);
         return rc;
@@ -266,4 +308,17 @@ extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int
     M->nnz_u = (int64_t)uci.size();
     *out = M;
     return PSK_OK;
+}
+
+// SuperLU ILU.solve: bb[perm_r[i]] = v[i]  <=>  bb[j] = v[pinv[j]];  out[i] = z[perm_c[i]]
+extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx, const double *l_vals,
+                                   const int32_t *u_rowptr, const int32_t *u_colidx, const double *u_vals,
+                                   const int32_t *perm_r, const int32_t *perm_c, psk_prec **out) {
+    if (!out || n < 0 || !l_rowptr || !u_rowptr || !perm_r || !perm_c)
+        return fail(PSK_ERR_ARG, "psk_prec_create_ilu: NULL argument");
+    PSK_TRY(check_perm(n, perm_r, "ILU perm_r"));
+    std::vector<int32_t> pinv(n);
+    for (int64_t i = 0; i < n; ++i) pinv[perm_r[i]] = (int32_t)i;
+    return psk_prec_create_trisolve(n, l_rowptr, l_colidx, l_vals, 1, u_rowptr, u_colidx, u_vals, 0, pinv.data(),
+                                    perm_c, out);
 }

@@ -319,6 +319,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     if (!Ac || !b || !xout || !ctl || !res) return fail(PSK_ERR_ARG, "psk_pcg: NULL argument");
     if (ctl->maxiter < 0) return fail(PSK_ERR_ARG, "psk_pcg: maxiter < 0");
     if (M && M->n != Ac->n) return fail(PSK_ERR_ARG, "psk_pcg: preconditioner size mismatch");
+    if (!Ac->comm && Ac->ncols != Ac->n) return fail(PSK_ERR_ARG, "psk_pcg: matrix must be square");
     psk_csr *A = const_cast<psk_csr *>(Ac);
     Context *c;
     PSK_TRY(ctx(&c));
@@ -326,7 +327,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     std::memset(res, 0, sizeof(*res));
     const int64_t n = A->n, maxiter = ctl->maxiter;
     // general preconditioner (ILU): u = M^-1 r materialised between K2 and K3
-    const bool gen = M && M->kind == PSK_PREC_ILU;
+    const bool gen = prec_is_general(M);
     if (gen && A->comm) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: ILU preconditioning of a sharded matrix");
     PcgWork w;
     PSK_TRY(pcg_workspace(A, maxiter, gen, w));
@@ -438,7 +439,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     if (rc == PSK_OK && hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = fail(PSK_ERR_HIP, "state copy");
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg sync");
-    if (rc == PSK_OK && gen) rc = ilu_check_error(M, s);
+    if (rc == PSK_OK && gen) rc = prec_check_error(M, s);
     if (rc == PSK_OK && ctl->time_kernels)
         for (int i = 0; i < TP && rc == PSK_OK; ++i) rc = harvest(i);
     if (rc == PSK_OK) {

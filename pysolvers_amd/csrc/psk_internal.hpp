@@ -106,19 +106,25 @@ struct psk_csr {
     psk::DevBuf ws_small;
 };
 
+namespace psk { struct AmgHierarchy; }
+
 struct psk_prec {
     int kind = PSK_PREC_IDENTITY;
     int64_t n = 0;
     double *dinv = nullptr;   // JACOBI
-    // ILU: L strictly lower (unit diag), U strictly upper + diag, CSR; permutations of SuperLU
+    // PSK_PREC_ILU = triangular-solve chain: out = (U^-1 L^-1 v[gather_in])[gather_out].
+    // L strictly lower, U strictly upper (off-diagonal entries, stored order); l_diag / u_diag
+    // nullptr = unit diagonal. has_l / has_u: factor present.
+    bool has_l = false, has_u = false;
     int32_t *l_rowptr = nullptr, *l_colidx = nullptr, *u_rowptr = nullptr, *u_colidx = nullptr;
-    double *l_vals = nullptr, *u_vals = nullptr, *u_diag = nullptr;
-    int32_t *perm_r_inv = nullptr, *perm_c = nullptr;
+    double *l_vals = nullptr, *u_vals = nullptr, *l_diag = nullptr, *u_diag = nullptr;
+    int32_t *gather_in = nullptr, *gather_out = nullptr;
     int32_t *l_order = nullptr, *u_order = nullptr;   // rows sorted by dependency level
     int64_t l_levels = 0, u_levels = 0;
     double *work = nullptr;   // 2n: y, z
     int32_t *err = nullptr;
     int64_t nnz_l = 0, nnz_u = 0;
+    psk::AmgHierarchy *amg = nullptr;   // PSK_PREC_AMG
 };
 
 namespace psk {
@@ -188,7 +194,8 @@ enum SpmvMode : int {
     kSpmvDot = 1,       // y = A x, partial[b] = sum_i x_i y_i        (PCG: p.Ap)
     kSpmvJacobiDot = 2, // y = A (d .* x), partial[b] = sum_i q_i y_i (GMRES: A M^-1 q_k, q_0.u)
     kSpmvPlainDot = 3,  // y = A x, partial[b] = sum_i q_i y_i        (GMRES identity)
-    kSpmvResid = 4,     // y = b - A x, partial[b] = sum_i y_i^2      (true residual)
+    kSpmvResid = 4,     // y = b - A x, partial[b] = sum_i y_i^2      (true residual; partial nullable)
+    kSpmvAdd = 5,       // y = q + A x                                (AMG prolongation x + P x2)
 };
 int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int64_t row_end,
               int64_t halo_lo_start, hipStream_t s);
@@ -196,6 +203,15 @@ int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int6
 int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, hipStream_t s);
 int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
 int ilu_check_error(const psk_prec *M, hipStream_t s);
+int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
+void amg_free(AmgHierarchy *h);
+// preconditioners whose apply is not a single elementwise op (triangular solves, AMG): the
+// Krylov drivers take their general path for these
+inline bool prec_is_general(const psk_prec *M) {
+    return M && (M->kind == PSK_PREC_ILU || M->kind == PSK_PREC_AMG);
+}
+// reports a bounded-spin timeout of any triangular solve inside M (syncs the stream)
+int prec_check_error(const psk_prec *M, hipStream_t s);
 int tile_rows_for(int64_t n, int64_t nnz);
 int spmv_grid(const Context *c, const psk_csr *A);
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,

@@ -128,6 +128,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
                 const double r = aux_q[row] - sum;   // b - A*x (GMRESSolver.py:163)
                 y[row] = r;
                 acc = fma(r, r, acc);
+            } else if (MODE == kSpmvAdd) {
+                y[row] = aux_q[row] + sum;           // x + P*x2 (VCycleManager.py:55)
             } else {
                 __builtin_nontemporal_store(sum, y + row);
                 if (MODE == kSpmvDot) acc = fma(x[row], sum, acc);
@@ -135,7 +137,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             }
         }
     }
-    if (MODE != kSpmvPlain) {
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && partial != nullptr) {   // partial: kernel-uniform
         const double s = block_sum(acc, sh);
         if (tid == 0) partial[blockIdx.x] = s;
     }
@@ -183,6 +185,10 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         break;
     case kSpmvResid:
         hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
+                           x, y, aux_d, aux_q, partial, done_flag);
+        break;
+    case kSpmvAdd:
+        hipLaunchKernelGGL(spmv_kernel<kSpmvAdd>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
                            x, y, aux_d, aux_q, partial, done_flag);
         break;
     default:
@@ -304,6 +310,7 @@ int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, h
         return PSK_OK;
     }
     if (M->kind == PSK_PREC_ILU) return ilu_apply(M, v, out, s);
+    if (M->kind == PSK_PREC_AMG) return amg_apply(M, v, out, s);
     return fail(PSK_ERR_UNSUPPORTED, "unknown preconditioner kind");
 }
 
@@ -343,9 +350,14 @@ extern "C" {
 
 int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
                    const double *vals, int32_t loc, psk_csr **out) {
-    if (!out || n < 0 || nnz < 0 || !rowptr || (nnz > 0 && (!colidx || !vals)))
+    return psk_csr_create_rect(n, n, nnz, rowptr, colidx, vals, loc, out);
+}
+
+int psk_csr_create_rect(int64_t n, int64_t ncols, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
+                        const double *vals, int32_t loc, psk_csr **out) {
+    if (!out || n < 0 || ncols < 0 || nnz < 0 || !rowptr || (nnz > 0 && (!colidx || !vals)))
         return fail(PSK_ERR_ARG, "psk_csr_create: bad arguments");
-    if (nnz > INT32_MAX || n >= INT32_MAX)
+    if (nnz > INT32_MAX || n >= INT32_MAX || ncols >= INT32_MAX)
         return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create: int32 CSR indices required (nnz < 2^31)");
     if (loc == PSK_HOST) {
         // a malformed CSR would make the gather fault on the device: validate it here, O(nnz)
@@ -354,13 +366,13 @@ int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t 
         for (int64_t i = 0; i < n; ++i)
             if (rowptr[i + 1] < rowptr[i]) return fail(PSK_ERR_ARG, "psk_csr_create: rowptr not monotone");
         for (int64_t j = 0; j < nnz; ++j)
-            if (colidx[j] < 0 || colidx[j] >= n) return fail(PSK_ERR_ARG, "psk_csr_create: column index out of range");
+            if (colidx[j] < 0 || colidx[j] >= ncols) return fail(PSK_ERR_ARG, "psk_csr_create: column index out of range");
     }
     Context *c;
     PSK_TRY(ctx(&c));
     psk_csr *A = new psk_csr();
     A->n = n;
-    A->ncols = n;
+    A->ncols = ncols;
     A->nnz = nnz;
     A->tile_rows = tile_rows_for(n, nnz);
     A->n_global = n;
@@ -460,7 +472,8 @@ int psk_spmv(const psk_csr *Ac, const double *x, double *y, int32_t loc) {
         PSK_TRY(tmp.ensure((size_t)(A->ncols + A->n) * sizeof(double)));
         double *tx = tmp.as<double>();
         const bool dry = A->comm && A->comm->dry;   // caller passes [owned | halo]
-        PSK_TRY(to_device_vec(x, loc, dry ? A->ncols : A->n, tx, c->stream));
+        const int64_t nx = (A->comm && !dry) ? A->n : A->ncols;   // rectangular: x has ncols entries
+        PSK_TRY(to_device_vec(x, loc, nx, tx, c->stream));
         if (A->comm) PSK_TRY(halo_exchange(A, tx, c->stream));
         dx = tx;
         dy = (loc == PSK_HOST) ? tx + A->ncols : y;
@@ -586,7 +599,7 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
         dout = b + n;
     }
     PSK_TRY(prec_apply_dev(M, n, dv, dout, c->stream));
-    if (M->kind == PSK_PREC_ILU) PSK_TRY(ilu_check_error(M, c->stream));
+    if (prec_is_general(M)) PSK_TRY(prec_check_error(M, c->stream));
     if (dout != outv) PSK_TRY(from_device_vec(dout, loc, n, outv, c->stream));
     PSK_HIP(hipStreamSynchronize(c->stream));
     return PSK_OK;
@@ -594,11 +607,25 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
 
 int psk_prec_destroy(psk_prec *M) {
     if (!M) return PSK_OK;
-    void *ptrs[] = {M->dinv, M->l_rowptr, M->l_colidx, M->l_vals, M->u_rowptr, M->u_colidx, M->u_vals,
-                    M->u_diag, M->perm_r_inv, M->perm_c, M->work, M->err, M->l_order, M->u_order};
+    void *ptrs[] = {M->dinv,   M->l_rowptr,  M->l_colidx,   M->l_vals, M->l_diag, M->u_rowptr,
+                    M->u_colidx, M->u_vals,  M->u_diag,     M->gather_in, M->gather_out, M->work,
+                    M->err,    M->l_order,   M->u_order};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    if (M->amg) amg_free(M->amg);
     delete M;
+    return PSK_OK;
+}
+
+int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, int64_t *nnz_u, int64_t *levels_l,
+                  int64_t *levels_u) {
+    if (!M) return fail(PSK_ERR_ARG, "psk_prec_info: NULL preconditioner");
+    if (kind) *kind = M->kind;
+    if (n) *n = M->n;
+    if (nnz_l) *nnz_l = M->nnz_l;
+    if (nnz_u) *nnz_u = M->nnz_u;
+    if (levels_l) *levels_l = M->l_levels;
+    if (levels_u) *levels_u = M->u_levels;
     return PSK_OK;
 }
 

@@ -35,3 +35,32 @@ def manifest():
 
 def solver_cases(kind=None):
     return [c for c in manifest()["cases"] if kind is None or c["kind"] == kind]
+
+
+# AMG preconditioner variants of the golden cases (tests/golden/make_golden.py AMG_VARIANTS):
+# name -> (numIters, numLevels, smoother)
+AMG_VARIANTS = {"amg": (2, 2, "gs"), "amg_jacobi": (2, 2, "jacobi"), "amg3": (2, 3, "gs")}
+
+
+def case_precond(case):
+    return case.get("precond", "jacobi" if case["jacobi"] else "identity")
+
+
+def oracle_prec(A, name):
+    """The oracle's preconditioner apply for a golden-case preconditioner name."""
+    from oracle import amg, krylov
+    if name in AMG_VARIANTS:
+        it, lv, sm = AMG_VARIANTS[name]
+        return amg.AMGApply(A, num_iters=it, num_levels=lv, smoother=sm)
+    return {"identity": lambda: krylov.identity_apply, "jacobi": lambda: krylov.jacobi_form(A),
+            "ilut": lambda: krylov.ilut_form(A), "ic": lambda: krylov.ic_form(A)}[name]()
+
+
+def product_prec_type(psk, name):
+    """pysolvers_amd PreconditionerType for a golden-case preconditioner name."""
+    if name in AMG_VARIANTS:
+        it, lv, sm = AMG_VARIANTS[name]
+        kw = {"smoother": psk.JacobiSmoother} if sm == "jacobi" else {}
+        return psk.AMG(numIters=it, numLevels=lv, **kw)
+    return {"identity": psk.IdentityPreconditionerType, "jacobi": psk.JacobiPreconditionerType,
+            "ilut": psk.RightILUT, "ic": psk.RightIC}[name]()

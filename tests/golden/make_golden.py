@@ -73,14 +73,19 @@ sys.path.insert(0, REF)
 sys.path.insert(0, os.path.join(REF, "examples"))
 
 from PySolvers import CommonSolverArgs                                   # noqa: E402
-from PySolvers.Linear import PCG, GMRES, RightILUT                       # noqa: E402
+from PySolvers.Linear import PCG, GMRES, RightILUT, RightIC, AMG         # noqa: E402
+from PySolvers.Linear.ClassicSmoothers import JacobiSmoother as RefJacobiSmoother   # noqa: E402
+from PySolvers.Linear.SmoothedAggregation import SmoothedAggregationMLHierarchy     # noqa: E402
 from PySolvers.Linear.PreconditionerType import PreconditionerType       # noqa: E402
 from PySolvers.Linear.Preconditioner import GenericPreconditioner        # noqa: E402
 from PySolvers.Linear.IterativeLinearSolver import mvmult as ref_mvmult  # noqa: E402
 from PySolvers.Linear import Givens as ref_givens                        # noqa: E402
 from FDLaplacian2D import FDLaplacian2D as ref_fd2d                      # noqa: E402
 
-from oracle import krylov, fdlap                                          # noqa: E402
+from oracle import amg, krylov, fdlap                                     # noqa: E402
+
+# AMG preconditioner variants of the golden cases: name -> (numIters, numLevels, smoother)
+AMG_VARIANTS = {"amg": (2, 2, "gs"), "amg_jacobi": (2, 2, "jacobi"), "amg3": (2, 3, "gs")}
 
 
 class _JacobiPrec(GenericPreconditioner):
@@ -104,14 +109,25 @@ def _pname(jac):
 
 
 def _oracle_prec(A, jac):
+    name = _pname(jac)
+    if name in AMG_VARIANTS:
+        it, lv, sm = AMG_VARIANTS[name]
+        return amg.AMGApply(sp.csr_matrix(A), num_iters=it, num_levels=lv, smoother=sm)
     return {"identity": lambda: krylov.identity_apply, "jacobi": lambda: krylov.jacobi_form(A),
-            "ilut": lambda: krylov.ilut_form(A)}[_pname(jac)]()
+            "ilut": lambda: krylov.ilut_form(A), "ic": lambda: krylov.ic_form(A)}[name]()
+
+
+def _ref_prec_type(name):
+    if name in AMG_VARIANTS:
+        it, lv, sm = AMG_VARIANTS[name]
+        return AMG(numIters=it, numLevels=lv, **({"smoother": RefJacobiSmoother} if sm == "jacobi" else {}))
+    return {"identity": None, "jacobi": _Jacobi(), "ilut": RightILUT(), "ic": RightIC()}[name]
 
 
 def _run_ref(kind, A, b, maxiter, tau, fail_on_maxiter=True, jacobi=False):
     ctl = CommonSolverArgs(maxiter=maxiter, tau=tau, failOnMaxiter=fail_on_maxiter,
                            showIters=False, showFinal=False)
-    pt = {"identity": None, "jacobi": _Jacobi(), "ilut": RightILUT()}[_pname(jacobi)]
+    pt = _ref_prec_type(_pname(jacobi))
     if kind == "pcg":
         st = (PCG(control=ctl, precond=pt) if pt else PCG(control=ctl)).makeSolver()
     else:
@@ -244,6 +260,45 @@ def main():
     np.savez_compressed(os.path.join(HERE, "givens.npz"), H=H, g=g, H_rot=Hr, g_rot=gr, CS=CS, y=yr)
     print("givens: ok")
 
+    # --- AMG hierarchies and one apply each (SmoothedAggregation.py, VCycleManager.py) -----
+    amg_fix = {}
+    amg_index = []
+    for name, A in (("dh8", _dh(8)), ("dh10", _dh(10)), ("negfd16", -ref_fd2d(-1.0, 1.0, 16)),
+                    ("fd16", ref_fd2d(-1.0, 1.0, 16)), ("negfd32", -ref_fd2d(-1.0, 1.0, 32))):
+        A = sp.csr_matrix(A)
+        for L in (2, 3):
+            with contextlib.redirect_stdout(io.StringIO()):
+                h = SmoothedAggregationMLHierarchy(A, numLevels=L)
+            ops, Ps, Rs = amg.hierarchy(A, L)
+            key = "%s_L%d" % (name, L)
+            for k in range(L):
+                Mr, Mo = h.matrix(k).tocsr(), ops[k]
+                assert np.array_equal(Mr.indptr, Mo.indptr) and np.array_equal(Mr.indices, Mo.indices) \
+                    and np.array_equal(Mr.data, Mo.data), (key, k)
+                for tag, M in (("A%d" % k, Mr),) + ((("P%d" % k, h.update(k).tocsr()), ("R%d" % k, h.downdate(k).tocsr()))
+                                                       if k < L - 1 else ()):
+                    amg_fix["%s_%s_indptr" % (key, tag)] = M.indptr.astype(np.int32)
+                    amg_fix["%s_%s_indices" % (key, tag)] = M.indices.astype(np.int32)
+                    amg_fix["%s_%s_data" % (key, tag)] = M.data
+                    amg_fix["%s_%s_shape" % (key, tag)] = np.array(M.shape, dtype=np.int64)
+                if k < L - 1:
+                    for Mr_, Mo_ in ((h.update(k).tocsr(), Ps[k]), (h.downdate(k).tocsr(), Rs[k])):
+                        assert np.array_equal(Mr_.indptr, Mo_.indptr) and np.array_equal(Mr_.indices, Mo_.indices) \
+                            and np.array_equal(Mr_.data, Mo_.data), (key, k)
+            v = np.random.default_rng(7).standard_normal(A.shape[0])
+            amg_fix[key + "_v"] = v
+            for sm, cls in (("gs", None), ("jacobi", RefJacobiSmoother)):
+                with contextlib.redirect_stdout(io.StringIO()):
+                    M = (AMG(numIters=2, numLevels=L, smoother=cls) if cls else AMG(numIters=2, numLevels=L)).form(A)
+                    y = M.apply(v)
+                yo = amg.AMGApply(A, num_iters=2, num_levels=L, smoother=sm)(v)
+                assert np.array_equal(y, yo), (key, sm)
+                amg_fix["%s_apply_%s" % (key, sm)] = y
+            amg_index.append(dict(key=key, levels=[int(o.shape[0]) for o in ops]))
+    np.savez_compressed(os.path.join(HERE, "amg_hierarchy.npz"), **amg_fix)
+    manifest["amg_hierarchy"] = amg_index
+    print("amg hierarchy: ok", [d["key"] for d in amg_index])
+
     # --- Solver cases ------------------------------------------------------------------
     cases = []
     for lev in (8, 10, 12, 15):
@@ -271,6 +326,18 @@ def main():
     for m in (32, 64):
         cases.append(("gmres", "fd%d" % m, ref_fd2d(-1.0, 1.0, m), 100, 1e-8, True, "ilut"))
     cases.append(("pcg", "dh10", _dh(10), 300, 1e-8, True, "ilut"))
+    # PCG + RightIC (examples/PCGExample_IC.py plumbing)
+    for lev in (8, 10, 12):
+        cases.append(("pcg", "dh%d" % lev, _dh(lev), 300, 1e-8, True, "ic"))
+    cases.append(("pcg", "negfd32", -ref_fd2d(-1.0, 1.0, 32), 300, 1e-8, True, "ic"))   # IC needs SPD
+    # PCG/GMRES + AMG (examples/PCGExample_AMG.py: AMG(numIters=2); config 5 at small sizes)
+    for lev in (8, 10, 12):
+        cases.append(("pcg", "dh%d" % lev, _dh(lev), 100, 1e-8, True, "amg"))
+    cases.append(("pcg", "dh10", _dh(10), 100, 1e-8, True, "amg_jacobi"))
+    cases.append(("pcg", "dh10", _dh(10), 100, 1e-8, True, "amg3"))
+    cases.append(("gmres", "dh8", _dh(8), 100, 1e-8, True, "amg"))
+    # -FD2D (FDBratu2D.py:15 sign): PCG+AMG does not converge: 10 iterations, no fail
+    cases.append(("pcg", "negfd32_maxiter10_nofail", -ref_fd2d(-1.0, 1.0, 32), 10, 1e-8, False, "amg"))
 
     index = []
     for kind, name, A, maxiter, tau, fom, jac in cases:

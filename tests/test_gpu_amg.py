@@ -1,0 +1,155 @@
+"""GPU parity of the triangular-solve chains (IC, Gauss-Seidel, coarse LU) and the AMG V-cycle.
+
+Bars (written here, not inferred):
+* AMG apply vs the reference's own outputs (amg_hierarchy.npz): ||y - y_ref|| <= 1e-10 ||y_ref||.
+  Not bitwise: the triangular solves sum each row with FMA in stored order where SuperLU uses its
+  supernodal column order; SpMV, restriction, prolongation and Jacobi sweeps are bitwise.
+* RightIC apply vs the reference's spsolve_triangular pair: 1e-12 relative.
+* generic chains vs scipy on random factors with permutations: 1e-12 relative.
+Solver-level parity of PCG/GMRES + AMG / RightIC runs in test_gpu_parity.test_solver_matches_reference
+(the golden manifest carries those cases).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import scipy.sparse.linalg as spla
+
+from conftest import load_golden, manifest
+
+pytestmark = pytest.mark.gpu
+
+KEYS = [d["key"] for d in manifest()["amg_hierarchy"]]
+
+
+@pytest.fixture(scope="module")
+def psk():
+    import pysolvers_amd
+    return pysolvers_amd
+
+
+@pytest.fixture(scope="module")
+def fix():
+    return load_golden("amg_hierarchy.npz")
+
+
+def _fix_matrix(d, key, tag):
+    shape = tuple(int(s) for s in d["%s_%s_shape" % (key, tag)])
+    return sp.csr_matrix((d["%s_%s_data" % (key, tag)], d["%s_%s_indices" % (key, tag)],
+                          d["%s_%s_indptr" % (key, tag)]), shape=shape)
+
+
+def _rel(a, b):
+    return np.linalg.norm(a - b) / np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("key", KEYS)
+@pytest.mark.parametrize("sm", ["gs", "jacobi"])
+def test_amg_apply_matches_reference(psk, fix, key, sm):
+    L = int(key.split("_L")[1])
+    A = _fix_matrix(fix, key, "A%d" % (L - 1))
+    kw = {"smoother": psk.JacobiSmoother} if sm == "jacobi" else {}
+    M = psk.AMG(numIters=2, numLevels=L, **kw).form(A)
+    assert M.levels() == [int(_fix_matrix(fix, key, "A%d" % k).shape[0]) for k in range(L)]
+    y_ref = fix["%s_apply_%s" % (key, sm)]
+    v = fix[key + "_v"]
+    y = M.applyRight(v)
+    assert _rel(y, y_ref) <= 1e-10, _rel(y, y_ref)
+    assert np.array_equal(M.applyLeft(v), y)                 # GenericPreconditioner: same both sides
+    yd = M.apply(psk.DeviceVector.from_numpy(v)).numpy()     # device-resident vectors
+    assert np.array_equal(yd, y)
+
+
+def test_amg_early_exit_matches_oracle(psk):
+    """numIters large enough that the 1e-8 test stops the cycles early (VCycleSolver.py:141-142)."""
+    from oracle import amg
+    d = load_golden("pcg_dh8_amg.npz")
+    from conftest import golden_matrix
+    A = golden_matrix(d)
+    v = np.random.default_rng(3).standard_normal(A.shape[0])
+    ref = amg.AMGApply(A, num_iters=40, num_levels=2)
+    # how many cycles the oracle runs before the test holds
+    x = v.copy()
+    ncyc = None
+    for k in range(40):
+        x = amg.vcycle(ref.ops, ref.P, ref.R, ref.aux, "gs", v, x, 1)
+        if np.linalg.norm(v - A @ x) < 1e-8 * np.linalg.norm(v):
+            ncyc = k + 1
+            break
+    assert ncyc is not None and ncyc < 40
+    y = psk.AMG(numIters=40).form(A).applyRight(v)
+    assert _rel(y, ref(v)) <= 1e-10
+    assert _rel(y, x) <= 1e-10          # the snapshot after cycle ncyc, not the 40-cycle iterate
+
+
+def test_amg_zero_rhs(psk, fix):
+    A = _fix_matrix(fix, "dh8_L2", "A1")
+    M = psk.AMG(numIters=2).form(A)
+    y = M.applyRight(np.zeros(A.shape[0]))
+    assert not np.any(y)
+
+
+@pytest.mark.parametrize("m", [128, 384])
+def test_amg_apply_negfd_vs_oracle(psk, m):
+    """-FD2D (FDBratu2D.py:15), 2 and 3 levels, against the oracle (pinned bitwise to the reference
+    on the fixtures; the reference's own setup is quadratic, 253 s at m=512)."""
+    from oracle import amg, fdlap
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    v = np.random.default_rng(11).standard_normal(A.shape[0])
+    for L in (2, 3):
+        M = psk.AMG(numIters=2, numLevels=L).form(A)
+        ref = amg.AMGApply(A, num_iters=2, num_levels=L)
+        assert M.levels() == [o.shape[0] for o in ref.ops]
+        assert _rel(M.applyRight(v), ref(v)) <= 1e-10
+
+
+@pytest.mark.parametrize("case", ["pcg_dh10_ic.npz", "pcg_negfd32_ic.npz"])
+def test_ic_apply_matches_reference_ops(psk, case):
+    from conftest import golden_matrix
+    from oracle import krylov
+    A = golden_matrix(load_golden(case))
+    v = np.random.default_rng(2).standard_normal(A.shape[0])
+    M = psk.RightIC().form(A)
+    assert _rel(M.applyRight(v), krylov.ic_form(A)(v)) <= 1e-12
+    assert np.array_equal(M.applyLeft(v), v)
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (37, 1), (2000, 2), (20000, 3)])
+def test_trisolve_chain_random(psk, n, seed):
+    """out = (U^-1 L^-1 v[gin])[gout] for random unit/non-unit factors (rows of 0..40 entries)."""
+    from pysolvers_amd.Linear import TriangularSolveChain
+    rng = np.random.default_rng(seed)
+    dens = min(1.0, 8.0 / max(n, 1))
+    Lo = sp.tril(sp.random(n, n, density=dens, random_state=rng), k=-1).tocsr() * 0.1
+    Up = sp.triu(sp.random(n, n, density=dens, random_state=rng), k=1).tocsr() * 0.1
+    dl, du = 1.0 + rng.random(n), 1.0 + rng.random(n)
+    gin, gout = rng.permutation(n), rng.permutation(n)
+    v = rng.standard_normal(n)
+    for l_unit, u_unit in ((True, False), (False, True), (False, False)):
+        L = (Lo + sp.diags(dl)).tocsr()
+        U = (Up + sp.diags(du)).tocsr()
+        Ld = (Lo + sp.eye(n)).tocsr() if l_unit else L
+        Ud = (Up + sp.eye(n)).tocsr() if u_unit else U
+        ref = spla.spsolve_triangular(Ud, spla.spsolve_triangular(Ld, v[gin], lower=True), lower=False)[gout]
+        M = TriangularSolveChain(n, L=L, l_unit=l_unit, U=U, u_unit=u_unit, gather_in=gin, gather_out=gout)
+        assert _rel(M.apply(v), ref) <= 1e-12
+    # single factors, no permutations
+    M = TriangularSolveChain(n, U=U)
+    assert _rel(M.apply(v), spla.spsolve_triangular(U, v, lower=False)) <= 1e-12
+    M = TriangularSolveChain(n, L=L)
+    assert _rel(M.apply(v), spla.spsolve_triangular(L, v, lower=True)) <= 1e-12
+    info = M.device_info()
+    assert info["n"] == n and info["nnz_u"] == 0 and info["levels_l"] >= 1
+
+
+def test_trisolve_rejects_bad_factors(psk):
+    from pysolvers_amd import _native as N
+    from pysolvers_amd.Linear import TriangularSolveChain
+    U = sp.csr_matrix(np.array([[1.0, 0.0], [2.0, 1.0]]))       # entry below the diagonal
+    with pytest.raises(N.PskError):
+        TriangularSolveChain(2, U=U)
+    L = sp.csr_matrix(np.array([[0.0, 0.0], [2.0, 1.0]]))       # missing diagonal, non-unit
+    L.eliminate_zeros()
+    with pytest.raises(N.PskError):
+        TriangularSolveChain(2, L=L)
+    with pytest.raises(N.PskError):
+        TriangularSolveChain(2, L=L, l_unit=True, gather_in=np.array([0, 0]))   # not a permutation

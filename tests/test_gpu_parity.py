@@ -20,7 +20,7 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from conftest import golden_matrix, load_golden, manifest, solver_cases
+from conftest import case_precond, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type, solver_cases
 
 pytestmark = pytest.mark.gpu
 
@@ -160,9 +160,7 @@ def test_solver_matches_reference(psk, case):
     d = load_golden(case["file"])
     A = golden_matrix(d)
     ctl = _ctl(maxiter=case["maxiter"], tau=case["tau"], failOnMaxiter=bool(case["fail_on_maxiter"]))
-    name = case.get("precond", "jacobi" if case["jacobi"] else "identity")
-    pt = {"identity": psk.IdentityPreconditionerType, "jacobi": psk.JacobiPreconditionerType,
-          "ilut": psk.RightILUT}[name]()
+    pt = product_prec_type(psk, case_precond(case))
     factory = psk.PCG if case["kind"] == "pcg" else psk.GMRES
     st = factory(control=ctl, precond=pt).makeSolver().solve(A, d["b"])
     _check_against_golden(st, d, case)

@@ -11,7 +11,7 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import golden_matrix, load_golden, manifest, solver_cases
+from conftest import case_precond, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type, solver_cases
 from oracle import fdlap, krylov, native
 
 
@@ -69,9 +69,7 @@ def test_oracle_solvers_match_reference(case):
     A = golden_matrix(d)
     b = d["b"]
     assert np.array_equal(A @ d["x_exact"], b)
-    name = case.get("precond", "jacobi" if case["jacobi"] else "identity")
-    prec = {"identity": lambda: krylov.identity_apply, "jacobi": lambda: krylov.jacobi_form(A),
-            "ilut": lambda: krylov.ilut_form(A)}[name]()
+    prec = oracle_prec(A, case_precond(case))
     fn = krylov.pcg if case["kind"] == "pcg" else krylov.gmres
     st = fn(A, b, maxiter=case["maxiter"], tau=case["tau"], fail_on_maxiter=bool(case["fail_on_maxiter"]),
             precond=prec)
