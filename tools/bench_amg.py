@@ -1,0 +1,98 @@
+#!/usr/bin/env python3
+"""configs[4]: PCG + AMG V-cycle preconditioner on -FDLaplacian2D(m), one GPU — PCG iterations/s.
+
+    python tools/bench_amg.py --side 8192 --levels 5 --iters 10 [--smoother gs|jacobi] [--cycles 2]
+
+-A is the sign FDBratu2D.py:15 uses (A = -FDLaplacian2D is SPD). The hierarchy is built on the
+host (O(nnz) SA setup, timed separately); the timed region is ONE PCG solve of exactly `iters`
+iterations (tau = 0, failOnMaxiter = False; PCG+AMG does not converge on this matrix, SURVEY.md §6,
+so iterations/s is the protocol), operands resident in HBM. Also reports one AMG apply and one
+fine-level Gauss-Seidel sweep (triu(A)^-1) alone.
+
+numLevels: the reference's default (2) leaves a coarse level of ~n/6 unknowns that its per-call
+SuperLU factorisation cannot handle at this size (SuperLU fails at FD 4096^2 already, see
+tools/bench_gmres.py); 5 levels leave a ~10^5-unknown coarse problem at m = 8192.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--side", type=int, default=1024)
+    ap.add_argument("--levels", type=int, default=5)
+    ap.add_argument("--cycles", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--smoother", default="gs", choices=["gs", "jacobi"])
+    args = ap.parse_args()
+    import pysolvers_amd as psk
+    from pysolvers_amd import _native as N
+
+    m = args.side
+    n = m * m
+    t = time.time()
+    A = -psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m).to_scipy()
+    dA = psk.DeviceCSR.from_scipy(A)
+    x = psk.DeviceVector.from_numpy(np.random.default_rng(12345).random(n))
+    b = psk.Linear.spmv(dA, x)
+    del x
+    out = dict(side=m, n=n, levels=args.levels, cycles=args.cycles, smoother=args.smoother, iters=args.iters)
+    t1 = time.time()
+    sm = psk.JacobiSmoother if args.smoother == "jacobi" else psk.GaussSeidelSmoother
+    M = psk.AMG(numIters=args.cycles, numLevels=args.levels, smoother=sm).form(dA)
+    del A
+    out["amg_setup_s"] = time.time() - t1
+    out["level_sizes"] = M.levels()
+    if args.smoother == "gs":
+        info = M._S[-1].operator.device_info()
+        out["fine_gs_levels"] = info["levels_u"]
+    v = psk.DeviceVector.from_numpy(np.random.default_rng(1).standard_normal(n))
+    M.apply(v)
+    N.check(N.lib.psk_synchronize(), "sync")
+    reps = 3
+    t2 = time.perf_counter()
+    for _ in range(reps):
+        M.apply(v)
+    N.check(N.lib.psk_synchronize(), "sync")
+    out["amg_apply_ms"] = (time.perf_counter() - t2) * 1e3 / reps
+    if args.smoother == "gs":
+        S = M._S[-1].operator
+        S.apply(v)
+        N.check(N.lib.psk_synchronize(), "sync")
+        t3 = time.perf_counter()
+        for _ in range(reps):
+            S.apply(v)
+        N.check(N.lib.psk_synchronize(), "sync")
+        out["fine_gs_sweep_ms"] = (time.perf_counter() - t3) * 1e3 / reps
+    out["setup_s"] = time.time() - t
+    sol = psk.DeviceVector(n)
+
+    def run(k):
+        ctl = N.PskCtl(maxiter=k, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=0)
+        res = N.PskResult()
+        N.check(N.lib.psk_pcg(dA.handle, M.device_handle, b._p, sol._p, ctypes.byref(ctl), ctypes.byref(res), None,
+                              N.PSK_DEVICE), "psk_pcg")
+        return res
+
+    run(1)
+    N.check(N.lib.psk_synchronize(), "sync")
+    t0 = time.perf_counter()
+    res = run(args.iters)
+    N.check(N.lib.psk_synchronize(), "sync")
+    dt = time.perf_counter() - t0
+    out.update(pcg_it_per_s=args.iters / dt, ms_per_it=dt * 1e3 / args.iters, status=int(res.status),
+               iters_done=int(res.iters), rec_resid_ratio=res.resid_recursive / res.norm_b)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
