@@ -79,6 +79,7 @@ def main():
     ap.add_argument("--side", type=int, default=16384, help="grid side m of FDLaplacian2D (n = m^2 rows)")
     ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
+    ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1_pmc_traffic_16384.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same kernel and side")
     args = ap.parse_args()
@@ -208,6 +209,8 @@ def main():
         }
         if world == 1 and args.spmv10m and m != 3163:
             out["spmv_N10M"] = spmv_10m(N)
+        if world == 1 and args.config1 and m != 4096:
+            out["configs1_pcg_jacobi_4096"] = pcg_4096(N)
         if world == 1 and args.cpu_iters > 0:
             cb = cpu_baseline(m, args.cpu_iters)
             cb["threads_note"] = "scipy csr_matvec and numpy ufuncs are single-threaded; BLAS limited to 1"
@@ -262,9 +265,52 @@ def spmv_10m(N, iters=30):
     N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
     b = spmv_bytes(n, nnz)
     gbps = b / (res.spmv_ms * 1e-3) / 1e9
+    # back-to-back launches between two events (no per-launch event in between)
+    bms = ctypes.c_double()
+    N.check(N.lib.psk_spmv_timed(A, dx, db, 50, ctypes.byref(bms)), "psk_spmv_timed")
+    bb = b / (bms.value * 1e-3) / 1e9
     out = {"n": n, "nnz": nnz, "avg_launch_ms": res.spmv_ms, "achieved_GBps": gbps,
            "frac": gbps / HBM_PEAK_GBPS, "pcg_it_per_s": iters / (res.loop_ms * 1e-3),
-           "algorithmic_bytes_per_launch": b}
+           "algorithmic_bytes_per_launch": b,
+           "batch50": {"kernel": "spmv_kernel<kSpmvPlain>", "avg_launch_ms": bms.value, "achieved_GBps": bb,
+                       "frac": bb / HBM_PEAK_GBPS,
+                       "how": "50 back-to-back launches between two HIP events on the library stream"}}
+    for p in (db, dx):
+        N.lib.psk_dfree(p)
+    N.lib.psk_prec_destroy(M)
+    N.lib.psk_csr_destroy(A)
+    return out
+
+
+def pcg_4096(N, iters=300):
+    """configs[1]: PCG+Jacobi on FDLaplacian2D 4096^2, one GPU, `iters` fixed iterations."""
+    m = 4096
+    n, nnz = fd_sizes(m)
+    A, M, db, dx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    N.check(N.lib.psk_csr_create_fd2d(-1.0, 1.0, m, ctypes.byref(A)), "fd2d")
+    N.check(N.lib.psk_prec_create(A, N.PSK_PREC_JACOBI, ctypes.byref(M)), "prec")
+    N.check(N.lib.psk_dmalloc(n * 8, ctypes.byref(db)), "alloc")
+    N.check(N.lib.psk_dmalloc(n * 8, ctypes.byref(dx)), "alloc")
+    xe = np.random.default_rng(12345).random(n)
+    N.check(N.lib.psk_h2d(dx, N.ptr(xe), n * 8), "h2d")
+    N.check(N.lib.psk_spmv(A, dx, db, N.PSK_DEVICE), "spmv")
+
+    def run(k, tk):
+        ctl = N.PskCtl(maxiter=k, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=tk)
+        res = N.PskResult()
+        N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
+        return res
+    run(20, 0)
+    N.check(N.lib.psk_synchronize(), "sync")
+    t0 = time.perf_counter()
+    run(iters, 0)
+    N.check(N.lib.psk_synchronize(), "sync")
+    dt = time.perf_counter() - t0
+    res = run(50, 1)
+    b = spmv_bytes(n, nnz)
+    out = {"n": n, "nnz": nnz, "iters": iters, "pcg_it_per_s": iters / dt,
+           "pcg_iteration_frac_of_peak": pcg_iter_bytes(n, nnz) * iters / dt / 1e9 / HBM_PEAK_GBPS,
+           "spmv_avg_launch_ms": res.spmv_ms, "spmv_frac": b / (res.spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     for p in (db, dx):
         N.lib.psk_dfree(p)
     N.lib.psk_prec_destroy(M)

@@ -130,6 +130,9 @@ int psk_csr_destroy(psk_csr *A);
  * bit-identical to scipy csr_matvec. For a distributed matrix x is the local
  * [owned | halo] vector and the halo is refreshed first (collective). */
 int psk_spmv(const psk_csr *A, const double *x, double *y, int32_t loc);
+/* Measurement: `reps` back-to-back y = A x launches (device pointers) between two HIP events on
+ * the library stream; *avg_ms = elapsed / reps (one untimed warm-up launch first). */
+int psk_spmv_timed(const psk_csr *A, const double *x, double *y, int32_t reps, double *avg_ms);
 int psk_dot(int64_t n, const double *x, const double *y, int32_t loc, double *out);
 int psk_nrm2(int64_t n, const double *x, int32_t loc, double *out);
 /* y = y + alpha*x (two roundings, as numpy's y + alpha*x) */

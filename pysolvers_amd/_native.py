@@ -56,6 +56,7 @@ SIGNATURES = {
     "psk_csr_download": (ctypes.c_int, [P, P, P, P]),
     "psk_csr_destroy": (ctypes.c_int, [P]),
     "psk_spmv": (ctypes.c_int, [P, P, P, I32]),
+    "psk_spmv_timed": (ctypes.c_int, [P, P, P, I32, ctypes.POINTER(F64)]),
     "psk_dot": (ctypes.c_int, [I64, P, P, I32, ctypes.POINTER(F64)]),
     "psk_nrm2": (ctypes.c_int, [I64, P, I32, ctypes.POINTER(F64)]),
     "psk_axpy": (ctypes.c_int, [I64, F64, P, P, I32]),

@@ -486,6 +486,29 @@ int psk_spmv(const psk_csr *Ac, const double *x, double *y, int32_t loc) {
     return PSK_OK;
 }
 
+int psk_spmv_timed(const psk_csr *A, const double *x, double *y, int32_t reps, double *avg_ms) {
+    if (!A || !x || !y || reps < 1 || !avg_ms) return fail(PSK_ERR_ARG, "psk_spmv_timed: bad arguments");
+    if (A->comm) return fail(PSK_ERR_UNSUPPORTED, "psk_spmv_timed: sharded matrix");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    const int grid = spmv_grid(c, A);
+    hipEvent_t e0, e1;
+    PSK_HIP(hipEventCreate(&e0));
+    PSK_HIP(hipEventCreate(&e1));
+    int rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, grid, c->stream);   // warm
+    if (rc == PSK_OK && hipEventRecord(e0, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
+    for (int r = 0; r < reps && rc == PSK_OK; ++r)
+        rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, grid, c->stream);
+    if (rc == PSK_OK && hipEventRecord(e1, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
+    float ms = 0.f;
+    if (rc == PSK_OK && hipEventSynchronize(e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
+    if (rc == PSK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event time");
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (rc == PSK_OK) *avg_ms = (double)ms / reps;
+    return rc;
+}
+
 static int dot_impl(int64_t n, const double *x, const double *y, int32_t loc, double *out, bool nrm) {
     if (!out || n < 0 || !x || (!nrm && !y)) return fail(PSK_ERR_ARG, "psk_dot: bad arguments");
     Context *c;

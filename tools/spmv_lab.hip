@@ -117,7 +117,10 @@ __global__ __launch_bounds__(BS) void spmv_A2(int64_t n, const int* __restrict__
 
 // ---------------- A3: A2 with a selectable tile order --------------------------------------------------
 // ORDER 0: contiguous tile range per block; 1: each XCD (blockIdx % 8) owns a contiguous slab of
-// tiles and its blocks interleave inside it; 2: global interleave (tile = block + k * grid).
+// tiles and its blocks interleave inside it; 2: global interleave (tile = block + k * grid);
+// 3: strips: with S = m/256 tiles per grid line, block g walks tile column c = g % S over a
+// contiguous range of tile rows (tile = r*S + c), so the x[i-m] it needs was its own x[i] one
+// tile earlier (same CU -> L2), needs grid % S == 0.
 template <int CH, int ORDER>
 __global__ __launch_bounds__(BS) void spmv_A3(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
                                               const double* __restrict__ va, const double* __restrict__ x,
@@ -132,7 +135,12 @@ __global__ __launch_bounds__(BS) void spmv_A3(int64_t n, const int* __restrict__
         const int64_t xcd = blockIdx.x % 8, lb = blockIdx.x / 8, g8 = g / 8;
         const int64_t s0 = nt * xcd / 8, s1 = nt * (xcd + 1) / 8;
         tbeg = s0 + lb; tend = s1; tstep = g8;
-    } else { tbeg = blockIdx.x; tend = nt; tstep = g; }
+    } else if (ORDER == 2) { tbeg = blockIdx.x; tend = nt; tstep = g; }
+    else {
+        const int64_t m = (int64_t)sqrt((double)n), S = m / 256 > 0 ? m / 256 : 1;
+        const int64_t c = blockIdx.x % S, q = blockIdx.x / S, Q = g / S, R = (nt + S - 1) / S;
+        tbeg = (R * q / Q) * S + c; tend = (R * (q + 1) / Q) * S + c; if (tend > nt) tend = nt; tstep = S;
+    }
     int cc[KU], ncc[KU]; double vv[KU], nvv[KU];
     int e0 = 0, e1 = 0;
     auto issue = [&](int64_t t, int& a, int& b, int* c_, double* v_) {
@@ -568,13 +576,15 @@ int main(int argc, char** argv) {
         fillx<<<(n + 255) / 256, 256>>>(n, x);
         CK(hipDeviceSynchronize());
         const double bytes = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
+        const int S = m / 256 > 0 ? (int)(m / 256) : 1;
         std::vector<V> vs = {
             {"A blk256/ch2048", spmv_A, 2048},
             {"A3 interleave g1024", spmv_A3<1280, 2>, 1024},
+            {"A3 interleave g2048", spmv_A3<1280, 2>, 2048},
+            {"A3 strip g~512", spmv_A3<1280, 3>, S * (512 / S > 0 ? 512 / S : 1)},
+            {"A3 strip g~1024", spmv_A3<1280, 3>, S * (1024 / S > 0 ? 1024 / S : 1)},
+            {"A3 strip g~2048", spmv_A3<1280, 3>, S * (2048 / S > 0 ? 2048 / S : 1)},
             {"A4 3-stage g1024", spmv_A4<1280>, 1024},
-            {"A4 3-stage g768", spmv_A4<1280>, 768},
-            {"A4 3-stage g1536", spmv_A4<1280>, 1536},
-            {"A4 3-stage g2048", spmv_A4<1280>, 2048},
         };
         // reference result
         spmv_A<<<2048, BS>>>(n, rp, ci, va, x, yr);
@@ -587,7 +597,7 @@ int main(int argc, char** argv) {
             CK(hipDeviceSynchronize());
             CK(hipMemcpy(hy.data(), y, n * 8, hipMemcpyDeviceToHost));
             const bool same = memcmp(hr.data(), hy.data(), n * 8) == 0;
-            printf("m=%ld %-24s bitwise=%s\n", (long)m, v.name, same ? "yes" : "NO");
+            printf("m=%ld %-24s grid %d bitwise=%s\n", (long)m, v.name, v.grid, same ? "yes" : "NO");
         }
         hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
         std::vector<std::vector<float>> t(vs.size());
