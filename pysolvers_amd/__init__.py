@@ -3,13 +3,13 @@
 Importing this package loads libpsk.so (hand-written gfx950 HIP kernels);
 there is no CPU fallback.
 """
-from . import Linear
+from . import Linear, Nonlinear
 from .IterativeSolver import CommonSolverArgs, IterativeSolver, NamedObject, SolveStatus
 from .Linear import (AMG, GMRES, PCG, RightIC, GaussSeidelSmoother, JacobiSmoother, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
                      IdentityPreconditionerType, IterativeLinearSolver, Jacobi, JacobiPreconditioner,
                      JacobiPreconditionerType, LeftILUT, PCGSolver, RightILUT, mvmult)
 
-__all__ = ["AMG", "RightIC", "GaussSeidelSmoother", "JacobiSmoother", "Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
+__all__ = ["Nonlinear", "AMG", "RightIC", "GaussSeidelSmoother", "JacobiSmoother", "Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
            "GMRESSolver", "PCGSolver", "DeviceCSR", "DeviceVector", "IdentityPreconditioner",
            "IdentityPreconditionerType", "IterativeLinearSolver", "Jacobi", "JacobiPreconditioner",
            "JacobiPreconditionerType", "LeftILUT", "RightILUT", "mvmult"]

@@ -137,7 +137,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             }
         }
     }
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && partial != nullptr) {   // partial: kernel-uniform
+    // only the residual mode may be called without partials (AMG smoothing); kernel-uniform test
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || partial != nullptr)) {
         const double s = block_sum(acc, sh);
         if (tid == 0) partial[blockIdx.x] = s;
     }

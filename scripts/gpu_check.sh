@@ -29,7 +29,7 @@ if [ "${PROFILE:-1}" = "1" ]; then
   echo "== rocprofv3 kernel trace"
   export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- \
-      python bench.py ${PROF_ARGS:---cpu-iters 0 --spmv10m 0} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
+      python bench.py ${PROF_ARGS:---cpu-iters 0 --spmv10m 0 --config1 0} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
   rc=$?; tail -3 $OUT/prof_$TAG.err; stop_if_crashed $rc
   find $OUT/prof_$TAG -name '*kernel_stats.csv' -exec head -20 {} \;
 fi

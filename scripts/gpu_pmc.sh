@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; TAG=${TAG:-r1}
 mkdir -p $OUT
 export TMPDIR=/tmp
-ARGS=${PMC_ARGS:---steps 20 --warmup 2 --cpu-iters 0 --spmv10m 0}
+ARGS=${PMC_ARGS:---steps 20 --warmup 2 --cpu-iters 0 --spmv10m 0 --config1 0}
 for C in FETCH_SIZE WRITE_SIZE; do
   echo "== pmc $C"
   timeout -k 10 600 rocprofv3 --pmc $C --kernel-trace -d $OUT/pmc_${TAG}_$C -o run --output-format csv -- \

@@ -47,6 +47,12 @@ def _install_standins():
     class Tab:                       # used only as an indentation prefix in prints
         def __str__(self):
             return ""
+
+        def indent(self):
+            pass
+
+        def unindent(self):
+            pass
     tab.Tab = Tab
     sys.modules["PyTab"] = tab
     tm = types.ModuleType("PyTimer")
@@ -82,7 +88,9 @@ from PySolvers.Linear.IterativeLinearSolver import mvmult as ref_mvmult  # noqa:
 from PySolvers.Linear import Givens as ref_givens                        # noqa: E402
 from FDLaplacian2D import FDLaplacian2D as ref_fd2d                      # noqa: E402
 
-from oracle import amg, krylov, fdlap                                     # noqa: E402
+from oracle import amg, krylov, fdlap, newton                             # noqa: E402
+from PySolvers.Nonlinear import NewtonSolver                             # noqa: E402
+from FDBratu2D import FDBratu2D as RefBratu                              # noqa: E402
 
 # AMG preconditioner variants of the golden cases: name -> (numIters, numLevels, smoother)
 AMG_VARIANTS = {"amg": (2, 2, "gs"), "amg_jacobi": (2, 2, "jacobi"), "amg3": (2, 3, "gs")}
@@ -367,6 +375,40 @@ def main():
                           final_ratio=float(hist[-1] / np.linalg.norm(b)) if len(hist) else None,
                           sensitivity=sensitivity(kind, A, b, maxiter, tau, fom, jac, hist, res.soln())))
         print("%-40s iters=%5d success=%s sens=%s" % (tag, res.iters(), res.success(), index[-1]["sensitivity"]))
+
+    # --- Newton + PCG on FD-Bratu (examples/FDBratu2D.py:33-48), the caller of the hot path ------
+    newton_index = []
+    for m, pname in ((32, "ic"), (32, "amg5"), (64, "ic")):
+        func = RefBratu(m=m)
+        pt = RightIC() if pname == "ic" else AMG(numIters=5)
+        ctl = CommonSolverArgs(tau=1.0e-12, maxiter=10, showIters=False, showFinal=False)
+        lin_ctl = CommonSolverArgs(showIters=False, showFinal=False)
+        ns = NewtonSolver(control=ctl, solver=PCG(control=lin_ctl, precond=pt), fixLinTol=False, minLinTol=1.0e-6,
+                          freezePrec=True)
+        hist, lin = [], []
+        ns.reportIter = lambda it, nr, n0: hist.append(float(nr))
+        inner = ns.solver.solve
+
+        def counting_solve(A_, b_, inner=inner, lin=lin):
+            st_ = inner(A_, b_)
+            lin.append(st_.iters())
+            return st_
+        ns.solver.solve = counting_solve
+        with contextlib.redirect_stdout(io.StringIO()):
+            res = ns.solve(func, func.initialU())
+        fp = (lambda J: krylov.ic_form(J)) if pname == "ic" else (lambda J: amg.AMGApply(J, num_iters=5))
+        orc = newton.newton(newton.Bratu2D(m=m), np.ones(m * m), fp, maxiter=10, tau=1e-12, min_lin_tol=1e-6)
+        assert orc["iters"] == res.iters() and bool(orc["success"]) == bool(res.success()), (m, pname)
+        assert np.array_equal(orc["hist"], np.array(hist)) and orc["linear_iters"] == lin, (m, pname)
+        if res.soln() is not None:
+            assert np.array_equal(orc["soln"], res.soln())
+        tag = "newton_bratu%d_%s" % (m, pname)
+        np.savez_compressed(os.path.join(HERE, tag + ".npz"), hist=np.array(hist), linear_iters=np.array(lin),
+                            soln=res.soln() if res.soln() is not None else np.zeros(0))
+        newton_index.append(dict(file=tag + ".npz", m=m, precond=pname, iters=int(res.iters()),
+                                 success=bool(res.success()), msg=res.msg(), linear_iters=[int(v) for v in lin]))
+        print("%-28s iters=%d success=%s linear=%s msg=%s" % (tag, res.iters(), res.success(), lin, res.msg()))
+    manifest["newton"] = newton_index
 
     # b = 0 (PCGSolver.py:86-88, GMRESSolver.py:66-68): iters=1, x=0
     A = _dh(8)

@@ -1,0 +1,38 @@
+"""Newton's method (Nonlinear/Newton.py) with device PCG steps on FD-Bratu (examples/FDBratu2D.py).
+
+Bars: identical Newton iteration count, success flag and per-step PCG iteration counts;
+Newton residual history |h_k - h_ref_k| <= 1e-8 ||F_0||; solution within 1e-8 relative.
+(Each step's linear solve stops at a tolerance >= 1e-6, so device-vs-OpenBLAS rounding in the PCG
+moves the Newton iterates far below these bars; the counts are what must not change.)
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden, manifest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("case", manifest().get("newton", []), ids=lambda c: c["file"][:-4])
+def test_newton_bratu_matches_reference(case):
+    import pysolvers_amd as psk
+    from pysolvers_amd.Nonlinear import NewtonSolver
+    from oracle import newton
+    d = load_golden(case["file"])
+    m = case["m"]
+    func = newton.Bratu2D(m=m)
+    pt = psk.RightIC() if case["precond"] == "ic" else psk.AMG(numIters=5)
+    lin_ctl = psk.CommonSolverArgs(showIters=False, showFinal=False)
+    ns = NewtonSolver(control=psk.CommonSolverArgs(tau=1.0e-12, maxiter=10, showIters=False, showFinal=False),
+                      solver=psk.PCG(control=lin_ctl, precond=pt), fixLinTol=False, minLinTol=1.0e-6,
+                      freezePrec=True)
+    hist = []
+    ns.reportIter = lambda it, nr, n0: hist.append(float(nr))
+    st = ns.solve(func, func.initialU())
+    assert st.iters() == case["iters"] and bool(st.success()) == case["success"]
+    assert ns.linear_iters == case["linear_iters"]
+    h = np.array(hist)
+    assert len(h) == len(d["hist"]) and h[0] == d["hist"][0]
+    assert np.max(np.abs(h - d["hist"])) <= 1e-8 * d["hist"][0]
+    if d["soln"].size:
+        assert np.linalg.norm(st.soln() - d["soln"]) <= 1e-8 * np.linalg.norm(d["soln"])

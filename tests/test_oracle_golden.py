@@ -89,3 +89,19 @@ def test_zero_rhs_convention():
         st = fn(A, np.zeros(A.shape[0]))
         assert st["iters"] == manifest()["zero_rhs"]["iters"] and st["success"]
         assert not np.any(st["soln"])
+
+
+@pytest.mark.parametrize("case", manifest().get("newton", []), ids=lambda c: c["file"][:-4])
+def test_oracle_newton_matches_reference(case):
+    """NewtonSolver + PCG on FD-Bratu (examples/FDBratu2D.py): the oracle restatement reproduces the
+    reference's Newton residual history, per-step PCG iteration counts and solution bit for bit."""
+    from oracle import amg, newton
+    d = load_golden(case["file"])
+    m = case["m"]
+    fp = (lambda J: krylov.ic_form(J)) if case["precond"] == "ic" else (lambda J: amg.AMGApply(J, num_iters=5))
+    st = newton.newton(newton.Bratu2D(m=m), np.ones(m * m), fp, maxiter=10, tau=1e-12, min_lin_tol=1e-6)
+    assert st["iters"] == case["iters"] and bool(st["success"]) == case["success"]
+    assert st["linear_iters"] == case["linear_iters"]
+    assert np.array_equal(st["hist"], d["hist"])
+    if d["soln"].size:
+        assert np.array_equal(st["soln"], d["soln"])

@@ -6,7 +6,7 @@ corrections of MI355X_MICROARCH.md §HBM, verified by tools/pmc_calib.hip:
   write bytes = WRITE_SIZE[KB] * 1024 * (calibrated write factor; 1.0)
 
     python tools/pmc_summary.py gpurun_out/pmc_TAG_FETCH_SIZE gpurun_out/pmc_TAG_WRITE_SIZE \
-        gpurun_out/pmc_TAG_calib_FETCH_SIZE gpurun_out/pmc_TAG_calib_WRITE_SIZE > profiles/x.json
+        gpurun_out/pmc_TAG_calib_FETCH_SIZE gpurun_out/pmc_TAG_calib_WRITE_SIZE [SIDE "BENCH ARGS"] > profiles/x.json
 """
 import collections
 import csv
@@ -26,7 +26,7 @@ def per_kernel(d):
     return agg
 
 
-def main(fetch_dir, write_dir, cal_fetch, cal_write):
+def main(fetch_dir, write_dir, cal_fetch, cal_write, side=None, bench_args=None):
     cf, cw = per_kernel(cal_fetch), per_kernel(cal_write)
     rfac = {k.split("(")[0]: CALIB_BYTES / (sum(v) / len(v)) for k, v in cf.items() if k.startswith(("void rd", "rd16"))}
     wfac = {k.split("(")[0]: CALIB_BYTES / (sum(v) / len(v)) for k, v in cw.items() if k.startswith("wr8")}
@@ -41,9 +41,13 @@ def main(fetch_dir, write_dir, cal_fetch, cal_write):
         out["kernels"][k] = {"launches": len(fe[k]), "read_bytes_per_launch": rb,
                              "write_bytes_per_launch": wb,
                              "hbm_bytes_per_launch": rb + (wb or 0.0)}
+    if side is not None:
+        out["config"] = {"side": int(side), "bench_args": bench_args,
+                         "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/gpu_pmc.sh), corrected "
+                                 "with tools/pmc_calib.hip factors"}
     json.dump(out, sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:5])
+    main(*sys.argv[1:7])
