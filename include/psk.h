@@ -30,6 +30,7 @@
  *   psk_prec_create_amg  AMGPreconditioner.apply (AMGPreconditioner.py:46-51) ->
  *                    AMGVCycleSolver.solve (VCycleSolver.py:52-95) -> VCycleManager.runLevel
  *                    (VCycleManager.py:31-62), hierarchy built on the host.
+ *   psk_mm_*         scipy.io.mmread(path).tocsr() (examples/DHTestProblem.py:27-28).
  *   psk_sa_aggregate BuildAggregates + BuildFilteredMatrix (SmoothedAggregation.py:57-183),
  *                    O(nnz) host code.
  */
@@ -173,6 +174,16 @@ int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, 
                   int64_t *levels_l, int64_t *levels_u);
 int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *out, int32_t loc);
 int psk_prec_destroy(psk_prec *M);
+
+/* ---- MatrixMarket input (host only, except psk_csr_create_mm) --------------------------------- */
+/* scipy.io.mmread(path).tocsr() (examples/DHTestProblem.py:27-28) for coordinate files:
+ * real/integer/pattern, general/symmetric/skew-symmetric; symmetric files expanded, rows sorted by
+ * column, duplicates summed, explicit zeros kept. psk_mm_info gives the sizes (nnz_max = entries,
+ * doubled for symmetric files) so the caller can allocate rowptr[nrows+1], colidx/vals[nnz_max];
+ * psk_mm_read fills them and returns the actual nnz. */
+int psk_mm_info(const char *path, int64_t *nrows, int64_t *ncols, int64_t *nnz_max);
+int psk_mm_read(const char *path, int32_t *rowptr, int32_t *colidx, double *vals, int64_t *nnz);
+int psk_csr_create_mm(const char *path, psk_csr **out);
 
 /* ---- AMG setup (host only, no GPU needed) --------------------------------------------------- */
 /* Smoothed-aggregation coarsening of one level, SmoothedAggregation.py:41-183 in O(nnz):

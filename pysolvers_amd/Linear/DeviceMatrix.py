@@ -106,6 +106,17 @@ class DeviceCSR:
         nnz = 1 if m == 1 else 5 * n - 4 * int(m)
         return cls(h, n, nnz)
 
+    @classmethod
+    def from_mtx(cls, path):
+        """scipy.io.mmread(path).tocsr() read by the native MatrixMarket reader straight into HBM."""
+        import os
+        h = ctypes.c_void_p()
+        N.check(N.lib.psk_csr_create_mm(os.fsencode(os.fspath(path)), ctypes.byref(h)), "psk_csr_create_mm")
+        n, nnz = N.I64(), N.I64()
+        N.check(N.lib.psk_csr_info(h, ctypes.byref(n), ctypes.byref(nnz)), "psk_csr_info")
+        nr, nc, _ = __import__("pysolvers_amd.io", fromlist=["mm_info"]).mm_info(path)
+        return cls(h, n.value, nnz.value, ncols=nc)
+
     # --- accessors ------------------------------------------------------------------------
     @property
     def shape(self):

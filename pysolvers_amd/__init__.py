@@ -3,7 +3,7 @@
 Importing this package loads libpsk.so (hand-written gfx950 HIP kernels);
 there is no CPU fallback.
 """
-from . import Linear, Nonlinear
+from . import Linear, Nonlinear, io
 from .IterativeSolver import CommonSolverArgs, IterativeSolver, NamedObject, SolveStatus
 from .Linear import (AMG, GMRES, PCG, RightIC, GaussSeidelSmoother, JacobiSmoother, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
                      IdentityPreconditionerType, IterativeLinearSolver, Jacobi, JacobiPreconditioner,

@@ -67,6 +67,9 @@ SIGNATURES = {
     "psk_prec_create_trisolve": (ctypes.c_int, [I64, P, P, P, I32, P, P, P, I32, P, P, PP]),
     "psk_prec_create_amg": (ctypes.c_int, [I32, PP, PP, PP, PP, P, I32, I32, I32, F64, PP]),
     "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),
+    "psk_mm_info": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.POINTER(I64)] * 3),
+    "psk_mm_read": (ctypes.c_int, [ctypes.c_char_p, P, P, P, ctypes.POINTER(I64)]),
+    "psk_csr_create_mm": (ctypes.c_int, [ctypes.c_char_p, PP]),
     "psk_sa_aggregate": (ctypes.c_int, [I64, P, P, P, F64, P, ctypes.POINTER(I64), P]),
     "psk_pcg": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
     "psk_gmres": (ctypes.c_int, [P, P, P, P, ctypes.POINTER(PskCtl), ctypes.POINTER(PskResult), P, I32]),
