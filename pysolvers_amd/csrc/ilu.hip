@@ -10,27 +10,35 @@
 // reference's call, ILUTPreconditioner.py:51-53): they are uploaded once per form() and the two
 // triangular solves run on the GPU.
 //
-// Sparse triangular solve, "sync-free": one wave per row, rows dealt to a co-resident grid in a
-// level-sorted topological order computed on the host once per form() (k-th row of that order ->
-// wave k mod W, each wave walks its rows in order; every row depends only on rows earlier in the
-// order, so the first unsolved row can always proceed). Level order instead of index order cut the
-// apply at FD m=1024 from 255 ms to 17 ms (a wave stuck on a deep row no longer blocks shallow rows
-// queued behind it). A row's lanes load its entries
-// (coalesced), wait for each dependency x[c] to be PUBLISHED, then one deterministic wave reduction
-// and lane 0 publishes x[i]. Publication is the value itself: the output is pre-filled with a
-// signalling-NaN sentinel that arithmetic never produces, each x[i] is written by ONE 8-byte
-// agent-scope store (sc1) and read by agent-scope relaxed loads that bypass the non-coherent L1
-// (MI355X_MICROARCH.md, hand-off granule R2: "the data IS the flag"). Every spin is bounded and
-// reports PSK_ERR instead of hanging.
+// Publication protocol (both schedules): the output is pre-filled with a signalling-NaN sentinel that
+// arithmetic never produces; each x[i] is written by ONE 8-byte agent-scope store (sc1) and read by
+// agent-scope relaxed loads that bypass the non-coherent L1 (MI355X_MICROARCH.md, hand-off granule
+// R2: "the data IS the flag"). Every spin is bounded and reports PSK_ERR instead of hanging.
+//
+// Schedule 1, sync-free (sptrsv_kernel): one wave per row, rows dealt to a co-resident grid in a
+// level-sorted topological order computed on the host (k-th row of that order -> wave k mod W; every
+// row depends only on rows earlier in the order, so the first unsolved row can always proceed).
+// Level order instead of index order cut the apply at FD m=1024 from 255 ms to 17 ms. Each
+// dependency level costs about one cross-CU hand-off (~1 us, MI355X_MICROARCH.md "handoff-1to1").
+//
+// Schedule 2, band (sptrsv_band_kernel): the solve order is cut into contiguous blocks, one
+// workgroup per block; the workgroup walks the block's LOCAL dependency levels with a barrier
+// between levels, so a dependency inside the block costs a barrier and an LDS-ring read instead of
+// a hand-off; only dependencies on earlier blocks go through the published values. For the
+// Gauss-Seidel factor triu(A) of a 5-point grid (2m-1 levels, each up to m rows wide) this is what
+// makes the smoother usable at m = 8192. The host simulates both schedules with measured per-level
+// costs and keeps the faster (TriFactor::schedule).
 #include "psk_internal.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 namespace psk {
 
 constexpr uint64_t kSentinel = 0x7FF4DEAD0000BEEFull;   // sNaN payload: never an arithmetic result
 constexpr int64_t kMaxSpins = 1ll << 24;
+constexpr int kRingMaxWords = 16384;                     // 128 KiB LDS ring (then 1 workgroup / CU)
 
 __device__ __forceinline__ double load_pub(const double *p) {
     const uint64_t b = __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
@@ -45,17 +53,27 @@ __device__ __forceinline__ void store_pub(double *p, double v) {
 
 __device__ __forceinline__ bool is_sentinel(double v) { return (uint64_t)__double_as_longlong(v) == kSentinel; }
 
+__device__ __forceinline__ double wait_pub(const double *p, int32_t *err) {
+    double xv = load_pub(p);
+    int64_t spins = 0;
+    while (is_sentinel(xv)) {
+        if (++spins > kMaxSpins) {
+            atomicExch(err, 1);
+            return 0.0;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        xv = load_pub(p);
+    }
+    return xv;
+}
+
 __global__ void fill_sentinel_kernel(int64_t n, double *x) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) reinterpret_cast<uint64_t *>(x)[i] = kSentinel;
 }
 
-// One triangular factor: x_i = (rhs_i - sum_j T_ij x_j) / diag_i  (diag == nullptr: unit), rhs_i =
-// rhs[rhs_idx[i]] when rhs_idx is given. T holds the off-diagonal entries only; lower or upper is
-// implied by the dependency order the host computed.
-// Rows are visited in `order`, a topological order sorted by dependency level (host-computed):
-// every wave walks order[wave], order[wave + W], ... so all waves work on the shallow levels first
-// and a row waiting on a deep level never blocks shallower rows queued behind it on its wave.
+// Sync-free: x_i = (rhs_i - sum_j T_ij x_j) / diag_i  (diag == nullptr: unit), rhs_i = rhs[rhs_idx[i]]
+// when rhs_idx is given. Rows are visited in `order`; every wave walks order[wave], order[wave + W], ...
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ rp,
                                                         const int32_t *__restrict__ ci, const double *__restrict__ va,
                                                         const double *__restrict__ diag, const double *__restrict__ rhs,
@@ -70,22 +88,7 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
         double acc = 0.0;
         for (int32_t base = s; base < e; base += 64) {
             const int32_t idx = base + lane;
-            if (idx < e) {
-                const int32_t c = ci[idx];
-                const double v = va[idx];
-                double xv = load_pub(x + c);
-                int64_t spins = 0;
-                while (is_sentinel(xv)) {
-                    if (++spins > kMaxSpins) {
-                        atomicExch(err, 1);
-                        xv = 0.0;
-                        break;
-                    }
-                    __builtin_amdgcn_s_sleep(1);
-                    xv = load_pub(x + c);
-                }
-                acc = fma(v, xv, acc);
-            }
+            if (idx < e) acc = fma(va[idx], wait_pub(x + ci[idx], err), acc);
         }
         const double sum = wave_sum(acc);
         if (lane == 0) {
@@ -97,6 +100,128 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
     }
 }
 
+// Band: workgroup g takes blocks g, g+G, ... in solve order. Position of row i in solve order: i
+// (lower) or n-1-i (upper); block b = positions [b*B, (b+1)*B). The block's rows come as a RECORD
+// stream in local-level order (SoA, host-built): row, end of its level (relative to the block),
+// K off-diagonal (column, value) pairs (column -1 = padding), diagonal. Records are staged into LDS in
+// chunks of kBandChunk (one per thread), double-buffered, the next chunk's global loads issued a
+// whole chunk ahead, so a level costs LDS reads + barrier instead of dependent global loads. One
+// thread per record of a level (levels are at most kBandChunk wide, host-checked). In-block results
+// go to an LDS ring (position & ring_mask, host-verified reuse distance) as well as to x; dependencies
+// on earlier blocks are waited on through x.
+constexpr int kBandChunk = kBlock;   // records per staged chunk = widest level = threads
+
+template <int K>
+struct BandChunkRegs {
+    int32_t row = 0, end = 0, c[K];
+    double v[K], e[K], d = 1.0, b = 0.0;   // e: snapshot of external dependencies (sentinel = not yet)
+};
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
+    int64_t n, int upper, const double *__restrict__ rhs, const int32_t *__restrict__ rhs_idx, double *x,
+    int32_t *err, const int32_t *__restrict__ rec_row, const int32_t *__restrict__ rec_end,
+    const int32_t *__restrict__ rec_c, const double *__restrict__ rec_v, const double *__restrict__ rec_d,
+    int64_t nblocks, int64_t B, int ring_mask) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int ring_words = ring_mask + 1;
+    double *ring = reinterpret_cast<double *>(smem);
+    // two chunk buffers, SoA: v[K][C], d[C], b[C], e[K][C] (doubles) then row[C], end[C], c[K][C] (ints)
+    constexpr int kD = 2 * K + 2;
+    double *dbuf = ring + ring_words;
+    int32_t *ibuf = reinterpret_cast<int32_t *>(dbuf + 2 * kD * kBandChunk);
+    const int tid = threadIdx.x;
+    const double sentinel = __longlong_as_double((long long)kSentinel);
+    // global -> registers, a chunk ahead of use; dependencies on earlier blocks are loaded too (their
+    // producers usually finished them long before this block reaches them; if not, the snapshot is the
+    // sentinel and the consumer waits at use time)
+    auto stage_load = [&](int64_t q, int64_t q_end, int64_t p_lo, BandChunkRegs<K> &r) {
+        if (q < q_end) {
+            r.row = rec_row[q];
+            r.end = rec_end[q];
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                r.c[k] = rec_c[(int64_t)k * n + q];
+                r.v[k] = rec_v[(int64_t)k * n + q];
+                const int32_t c = r.c[k];
+                r.e[k] = (c >= 0 && (upper ? (n - 1 - c) : c) < p_lo) ? load_pub(x + c) : sentinel;
+            }
+            r.d = rec_d ? rec_d[q] : 1.0;
+            r.b = rhs_idx ? rhs[rhs_idx[r.row]] : rhs[r.row];
+        }
+    };
+    auto stage_store = [&](int buf, const BandChunkRegs<K> &r) {             // registers -> LDS
+        double *db = dbuf + buf * kD * kBandChunk;
+        int32_t *ib = ibuf + buf * (K + 2) * kBandChunk;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            db[k * kBandChunk + tid] = r.v[k];
+            db[(K + 2 + k) * kBandChunk + tid] = r.e[k];
+            ib[(2 + k) * kBandChunk + tid] = r.c[k];
+        }
+        db[K * kBandChunk + tid] = r.d;
+        db[(K + 1) * kBandChunk + tid] = r.b;
+        ib[tid] = r.row;
+        ib[kBandChunk + tid] = r.end;
+    };
+    for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+        const int64_t p_lo = blk * B, p_hi = (p_lo + B < n) ? p_lo + B : n, nrec = p_hi - p_lo;
+        const int64_t nchunks = (nrec + kBandChunk - 1) / kBandChunk;
+        BandChunkRegs<K> next;
+        stage_load(p_lo + tid, p_hi, p_lo, next);
+        stage_store(0, next);
+        if (nchunks > 1) stage_load(p_lo + kBandChunk + tid, p_hi, p_lo, next);   // chunk 1 in flight
+        int64_t have = 1;   // chunks [0, have) staged; chunk c lives in buffer c & 1
+        __syncthreads();
+        int64_t a = 0;
+        auto advance = [&]() {   // stage chunk `have` (loads issued a chunk ago), issue the next one
+            stage_store((int)(have & 1), next);
+            if (have + 1 < nchunks) stage_load(p_lo + (have + 1) * kBandChunk + tid, p_hi, p_lo, next);
+            ++have;
+            __syncthreads();
+        };
+        while (a < nrec) {
+            if (a / kBandChunk >= have) advance();                      // level starts in the next chunk
+            const int64_t ca = a / kBandChunk;
+            const int32_t *iba = ibuf + (ca & 1) * (K + 2) * kBandChunk;
+            const int64_t bnd = iba[kBandChunk + (a % kBandChunk)];   // end of this level (relative)
+            if ((bnd - 1) / kBandChunk >= have) advance();              // level reaches into the next chunk
+            const int64_t r = a + tid;
+            if (r < bnd) {
+                const int cb = (int)((r / kBandChunk) & 1), sl = (int)(r % kBandChunk);
+                const double *db = dbuf + cb * kD * kBandChunk;
+                const int32_t *ib = ibuf + cb * (K + 2) * kBandChunk;
+                const int32_t row = ib[sl];
+                double acc = 0.0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int32_t c = ib[(2 + k) * kBandChunk + sl];
+                    if (c >= 0) {
+                        const int64_t pc = upper ? (n - 1 - c) : c;
+                        double xv;
+                        if (pc < p_lo) {   // earlier block: the staged snapshot, else wait for it
+                            xv = db[(K + 2 + k) * kBandChunk + sl];
+                            if (is_sentinel(xv)) xv = wait_pub(x + c, err);
+                        } else {
+                            xv = ring_mask >= 0 ? ring[pc & ring_mask] : wait_pub(x + c, err);
+                        }
+                        acc = fma(db[k * kBandChunk + sl], xv, acc);
+                    }
+                }
+                double res = db[(K + 1) * kBandChunk + sl] - acc;
+                if (rec_d) res = res / db[K * kBandChunk + sl];
+                if (ring_mask >= 0) ring[(upper ? (n - 1 - row) : row) & ring_mask] = res;
+                store_pub(x + row, res);
+            }
+            // LDS results of this level visible to the next; x stores may still be in flight
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+            a = bnd;
+        }
+        __syncthreads();   // ring and buffers reused by the next block of this workgroup
+    }
+}
+
 // out[i] = z[perm[i]] (perm == nullptr: copy)
 __global__ void gather_perm_kernel(int64_t n, const double *__restrict__ z, const int32_t *__restrict__ perm,
                                    double *__restrict__ out) {
@@ -104,20 +229,49 @@ __global__ void gather_perm_kernel(int64_t n, const double *__restrict__ z, cons
     if (i < n) out[i] = perm ? z[perm[i]] : z[i];
 }
 
-static int sptrsv_grid(const Context *c, const void *kern) {
+static size_t band_lds_bytes(int ring_words, int K) {
+    return (size_t)ring_words * sizeof(double) +
+           2 * (size_t)kBandChunk * ((2 * K + 2) * sizeof(double) + (K + 2) * sizeof(int32_t));
+}
+
+static int coop_grid(const Context *c, const void *kern, size_t lds) {
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, 0) != hipSuccess) per_cu = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlock, lds) != hipSuccess) per_cu = 1;
     if (per_cu > 2) per_cu = 2;   // margin below the occupancy answer (MI355X_MICROARCH.md residency)
     if (per_cu < 1) per_cu = 1;
     return c->num_cus * per_cu;
 }
 
-static int launch_sptrsv(const Context *c, int64_t n, const int32_t *rp, const int32_t *ci, const double *va,
-                         const double *dg, const double *rhs, const int32_t *rhs_idx, double *x, int32_t *err,
-                         const int32_t *ord, hipStream_t s) {
-    const void *k = reinterpret_cast<const void *>(&sptrsv_kernel);
-    const int g = sptrsv_grid(c, k);
+// x = T^-1 rhs[rhs_idx] for one factor, with the factor's schedule
+static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const double *rhs, const int32_t *rhs_idx,
+                         double *x, int32_t *err, hipStream_t s) {
     int64_t nn = n;
+    const int32_t *rp = T.rowptr, *ci = T.colidx;
+    const double *va = T.vals, *dg = T.diag;
+    (void)rp;
+    if (T.schedule == kSchedBand) {
+        const void *k = nullptr;
+        switch (T.band_K) {
+        case 1: k = reinterpret_cast<const void *>(&sptrsv_band_kernel<1>); break;
+        case 2: k = reinterpret_cast<const void *>(&sptrsv_band_kernel<2>); break;
+        case 4: k = reinterpret_cast<const void *>(&sptrsv_band_kernel<4>); break;
+        case 8: k = reinterpret_cast<const void *>(&sptrsv_band_kernel<8>); break;
+        default: return fail(PSK_ERR_ARG, "band schedule: bad record width");
+        }
+        const size_t lds = band_lds_bytes(T.ring_words, T.band_K);
+        const int g = coop_grid(c, k, lds);
+        int upper = T.upper ? 1 : 0;
+        const int32_t *rr = T.rec_row, *re = T.rec_end, *rc = T.rec_c;
+        const double *rv = T.rec_v, *rd = T.diag ? T.rec_d : nullptr;
+        int64_t nb = T.band_nblocks, B = T.band_B;
+        int mask = T.ring_words > 0 ? T.ring_words - 1 : -1;
+        void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask};
+        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
+        return PSK_OK;
+    }
+    const void *k = reinterpret_cast<const void *>(&sptrsv_kernel);
+    const int g = coop_grid(c, k, 0);
+    const int32_t *ord = T.order;
     void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
     PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, 0, s));
     return PSK_OK;
@@ -132,7 +286,7 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     PSK_TRY(ctx(&c));
     const unsigned fb = (unsigned)((n + kBlock - 1) / kBlock);
     double *y = M->work, *z = M->work + n;
-    const int nbuf = (M->has_l ? 1 : 0) + (M->has_u ? 1 : 0);
+    const int nbuf = (M->lo.present ? 1 : 0) + (M->up.present ? 1 : 0);
     if (nbuf > 0) {
         hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((nbuf * n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            s, nbuf * n, y);   // y and z are contiguous
@@ -140,16 +294,14 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     }
     const double *cur = v;                // current right-hand side
     const int32_t *cur_idx = M->gather_in;
-    if (M->has_l) {
-        PSK_TRY(launch_sptrsv(c, n, M->l_rowptr, M->l_colidx, M->l_vals, M->l_diag, cur, cur_idx, y, M->err,
-                              M->l_order, s));
+    if (M->lo.present) {
+        PSK_TRY(launch_factor(c, n, M->lo, cur, cur_idx, y, M->err, s));
         cur = y;
         cur_idx = nullptr;
     }
-    if (M->has_u) {
-        double *dst = M->has_l ? z : y;
-        PSK_TRY(launch_sptrsv(c, n, M->u_rowptr, M->u_colidx, M->u_vals, M->u_diag, cur, cur_idx, dst, M->err,
-                              M->u_order, s));
+    if (M->up.present) {
+        double *dst = M->lo.present ? z : y;
+        PSK_TRY(launch_factor(c, n, M->up, cur, cur_idx, dst, M->err, s));
         cur = dst;
         cur_idx = nullptr;
     }
@@ -171,6 +323,176 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
     return PSK_OK;
 }
 
+void TriFactor::release() {
+    void *ptrs[] = {rowptr, colidx, vals, diag, order, rec_row, rec_end, rec_c, rec_v, rec_d};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
+    *this = TriFactor();
+}
+
+// ---------------------------------------------------------------------------------------------
+// host: schedules and their cost model
+namespace {
+
+// Cost model (us), fitted to measurements on MI355X (tools/bench_amg.py, tools/bench_gmres.py):
+// sync-free: a row costs one agent-scope load round trip (~0.85) on its wave, plus a hand-off (~0.5)
+// after its last dependency was published (FD m=1024 ILU: 1.34 us per level); band: a local level
+// costs ~0.9 us with the ring (it is paced by the one external load of the block's boundary row;
+// FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~1.3 us without.
+constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 1.3;
+
+struct HostFactor {
+    int64_t n = 0;
+    bool upper = false;
+    std::vector<int32_t> rp, ci;   // off-diagonal entries
+    int64_t pos(int64_t i) const { return upper ? n - 1 - i : i; }
+    int64_t row(int64_t p) const { return upper ? n - 1 - p : p; }
+};
+
+// global dependency levels -> counting-sort the rows by level (stable: solve order inside a level)
+void level_order(const HostFactor &F, std::vector<int32_t> &order, std::vector<int32_t> &lev, int64_t &nlev) {
+    const int64_t n = F.n;
+    lev.assign(n, 0);
+    int32_t maxl = -1;
+    for (int64_t p = 0; p < n; ++p) {
+        const int64_t i = F.row(p);
+        int32_t l = 0;
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) l = std::max(l, lev[F.ci[j]] + 1);
+        lev[i] = l;
+        maxl = std::max(maxl, l);
+    }
+    nlev = maxl + 1;
+    std::vector<int64_t> cnt((size_t)nlev + 1, 0);
+    for (int64_t i = 0; i < n; ++i) cnt[lev[i] + 1]++;
+    for (int64_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
+    order.assign(n, 0);
+    for (int64_t p = 0; p < n; ++p) {
+        const int64_t i = F.row(p);
+        order[cnt[lev[i]]++] = (int32_t)i;
+    }
+}
+
+// simulated time of the sync-free schedule: wave w processes order[w], order[w+W], ...
+double simulate_syncfree(const HostFactor &F, const std::vector<int32_t> &order, int64_t waves) {
+    std::vector<double> fin(F.n, 0.0), wave_free((size_t)std::max<int64_t>(waves, 1), 0.0);
+    double tmax = 0.0;
+    for (int64_t k = 0; k < F.n; ++k) {
+        const int64_t i = order[k];
+        double t = wave_free[k % waves];
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) t = std::max(t, fin[F.ci[j]] + kHopUs);
+        t += kRowUs;
+        fin[i] = t;
+        wave_free[k % waves] = t;
+        tmax = std::max(tmax, t);
+    }
+    return tmax;
+}
+
+struct Band {
+    int64_t B = 0, nblocks = 0, G = 0;
+    std::vector<int32_t> rows;
+    std::vector<int64_t> lvl_ptr, blk_lvl;
+    int32_t ring_words = 0;
+    double est = 0.0;
+};
+
+// band schedule with block size B: local levels, ring check, simulated time with the workgroups that
+// fit (per_cu_max per CU, fewer when the LDS ring + chunk buffers of record width K need it)
+void build_band(const HostFactor &F, int64_t B, int num_cus, int per_cu_max, int K, Band &bd) {
+    const int64_t n = F.n;
+    bd.B = B;
+    bd.nblocks = (n + B - 1) / B;
+    std::vector<int32_t> llev(n, 0);   // local level by row
+    int64_t max_dist = 0;
+    for (int64_t p = 0; p < n; ++p) {
+        const int64_t i = F.row(p), p_lo = (p / B) * B;
+        int32_t l = 0;
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+            const int64_t pj = F.pos(F.ci[j]);
+            if (pj >= p_lo) {
+                l = std::max(l, llev[F.ci[j]] + 1);
+                max_dist = std::max(max_dist, p - pj);
+            }
+        }
+        llev[i] = l;
+    }
+    // rows of each block sorted by (local level, position)
+    bd.rows.assign(n, 0);
+    bd.blk_lvl.assign(bd.nblocks + 1, 0);
+    bd.lvl_ptr.clear();
+    std::vector<int64_t> cnt;
+    for (int64_t b = 0; b < bd.nblocks; ++b) {
+        const int64_t p_lo = b * B, p_hi = std::min(n, p_lo + B);
+        int32_t maxl = 0;
+        for (int64_t p = p_lo; p < p_hi; ++p) maxl = std::max(maxl, llev[F.row(p)]);
+        cnt.assign((size_t)maxl + 2, 0);
+        for (int64_t p = p_lo; p < p_hi; ++p) cnt[llev[F.row(p)] + 1]++;
+        for (int32_t l = 0; l <= maxl; ++l) cnt[l + 1] += cnt[l];
+        bd.blk_lvl[b] = (int64_t)bd.lvl_ptr.size();
+        for (int32_t l = 0; l <= maxl; ++l) bd.lvl_ptr.push_back(p_lo + cnt[l]);
+        std::vector<int64_t> fillp(cnt.begin(), cnt.end() - 1);
+        for (int64_t p = p_lo; p < p_hi; ++p) {
+            const int64_t i = F.row(p);
+            bd.rows[p_lo + fillp[llev[i]]++] = (int32_t)i;
+        }
+    }
+    bd.blk_lvl[bd.nblocks] = (int64_t)bd.lvl_ptr.size();
+    bd.lvl_ptr.push_back(n);
+    // LDS ring: W = pow2 >= max in-block dependency distance + 1; the slot of position p is next
+    // written by position p+W, which must come at a later local level than p itself and than every
+    // in-block reader of p
+    bd.ring_words = 0;
+    int64_t W = 1;
+    while (W < max_dist + 1) W <<= 1;
+    if (W <= kRingMaxWords) {
+        std::vector<int32_t> maxcons(n, -1);   // by position
+        for (int64_t p = 0; p < n; ++p) {
+            const int64_t i = F.row(p), p_lo = (p / B) * B;
+            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+                const int64_t pj = F.pos(F.ci[j]);
+                if (pj >= p_lo) maxcons[pj] = std::max(maxcons[pj], llev[i]);
+            }
+        }
+        bool safe = true;
+        for (int64_t p = 0; p < n && safe; ++p) {
+            const int64_t q = p + W;
+            if (q >= n || q / B != p / B) continue;
+            const int32_t lq = llev[F.row(q)];
+            if (lq <= llev[F.row(p)] || lq <= maxcons[p]) safe = false;
+        }
+        if (safe) bd.ring_words = (int32_t)W;
+    }
+    // simulated time: G resident workgroups take blocks round-robin, in order
+    const size_t lds = band_lds_bytes(bd.ring_words, K);
+    const int64_t per_cu = std::max<int64_t>(1, std::min<int64_t>(per_cu_max, (int64_t)(160 * 1024 / std::max<size_t>(lds, 1))));
+    const int64_t G = (int64_t)num_cus * per_cu;
+    bd.G = G;
+    const double cl = bd.ring_words ? kBandLevelRingUs : kBandLevelMemUs;
+    std::vector<double> fin(n, 0.0), wg_free((size_t)std::max<int64_t>(G, 1), 0.0);
+    double tmax = 0.0;
+    for (int64_t b = 0; b < bd.nblocks; ++b) {
+        const int64_t p_lo = b * B;
+        double t = wg_free[b % G];
+        for (int64_t L = bd.blk_lvl[b]; L < bd.blk_lvl[b + 1]; ++L) {
+            double tl = t;
+            for (int64_t q = bd.lvl_ptr[L]; q < bd.lvl_ptr[L + 1]; ++q) {
+                const int64_t i = bd.rows[q];
+                for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j)
+                    if (F.pos(F.ci[j]) < p_lo) tl = std::max(tl, fin[F.ci[j]] + kHopUs);
+            }
+            const int64_t width = bd.lvl_ptr[L + 1] - bd.lvl_ptr[L];
+            tl += cl * (double)((width + kBlock - 1) / kBlock);
+            for (int64_t q = bd.lvl_ptr[L]; q < bd.lvl_ptr[L + 1]; ++q) fin[bd.rows[q]] = tl;
+            t = tl;
+        }
+        wg_free[b % G] = t;
+        tmax = std::max(tmax, t);
+    }
+    bd.est = tmax;
+}
+
+}  // namespace
+
 }  // namespace psk
 
 using namespace psk;
@@ -181,9 +503,9 @@ static int upload(T **d, const std::vector<T> &h) {
         *d = nullptr;
         return PSK_OK;
     }
-    if (hipMalloc(d, h.size() * sizeof(T)) != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc ILU");
+    if (hipMalloc(d, h.size() * sizeof(T)) != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc trisolve");
     if (hipMemcpy(*d, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) != hipSuccess)
-        return fail(PSK_ERR_HIP, "hipMemcpy ILU");
+        return fail(PSK_ERR_HIP, "hipMemcpy trisolve");
     return PSK_OK;
 }
 
@@ -216,29 +538,6 @@ static int split_factor(int64_t n, const int32_t *rp, const int32_t *ci, const d
     return PSK_OK;
 }
 
-// dependency levels -> counting-sort the rows by level (stable: solve order inside a level)
-static void level_order(int64_t n, const std::vector<int32_t> &rp, const std::vector<int32_t> &ci, bool upper,
-                        std::vector<int32_t> &order, int64_t &nlev) {
-    std::vector<int32_t> lev(n, 0);
-    int32_t maxl = -1;
-    for (int64_t t = 0; t < n; ++t) {
-        const int64_t i = upper ? n - 1 - t : t;
-        int32_t l = 0;
-        for (int32_t j = rp[i]; j < rp[i + 1]; ++j) l = std::max(l, lev[ci[j]] + 1);
-        lev[i] = l;
-        maxl = std::max(maxl, l);
-    }
-    nlev = maxl + 1;
-    std::vector<int64_t> cnt((size_t)nlev + 1, 0);
-    for (int64_t i = 0; i < n; ++i) cnt[lev[i] + 1]++;
-    for (int64_t l = 0; l < nlev; ++l) cnt[l + 1] += cnt[l];
-    order.assign(n, 0);
-    for (int64_t t = 0; t < n; ++t) {
-        const int64_t i = upper ? n - 1 - t : t;
-        order[cnt[lev[i]]++] = (int32_t)i;
-    }
-}
-
 static int check_perm(int64_t n, const int32_t *p, const char *what) {
     std::vector<char> seen(n, 0);
     for (int64_t i = 0; i < n; ++i) {
@@ -248,54 +547,116 @@ static int check_perm(int64_t n, const int32_t *p, const char *what) {
     return PSK_OK;
 }
 
+// Build, schedule and upload one factor.
+static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int32_t *ci, const double *va, bool upper,
+                       bool unit, TriFactor &T) {
+    HostFactor F;
+    F.n = n;
+    F.upper = upper;
+    std::vector<double> ova, dg;
+    PSK_TRY(split_factor(n, rp, ci, va, !upper, unit, F.rp, F.ci, ova, dg));
+    std::vector<int32_t> order, lev;
+    int64_t nlev = 0;
+    level_order(F, order, lev, nlev);
+    const int64_t G = (int64_t)c->num_cus * 2, waves = G * kWaves;
+    T.est_syncfree_us = simulate_syncfree(F, order, waves);
+    // band candidates: one block per workgroup, and 2x / 4x / 8x more blocks. Eligible: at most 8
+    // off-diagonal entries per row (record width K), levels at most one chunk wide, LDS fits a CU.
+    int32_t kmax = 0;
+    for (int64_t i = 0; i < n; ++i) kmax = std::max(kmax, F.rp[i + 1] - F.rp[i]);
+    int K = 1;
+    while (K < kmax) K <<= 1;
+    Band best;
+    best.est = -1.0;
+    bool band_ok = false;
+    std::vector<int64_t> cands = {(int64_t)c->num_cus, 2 * (int64_t)c->num_cus, 4 * (int64_t)c->num_cus,
+                                  8 * (int64_t)c->num_cus};
+    if (const char *e = std::getenv("PSK_BAND_BLOCKS")) cands = {std::max<int64_t>(1, std::atoll(e))};   // experiments
+    for (int64_t nb : cands) {
+        if (n == 0 || kmax > 8) break;
+        const int64_t B = std::max<int64_t>(64, (n + nb - 1) / nb);
+        Band bd;
+        build_band(F, B, c->num_cus, 2, K, bd);
+        int64_t wmax = 0;
+        for (size_t L = 0; L + 1 < bd.lvl_ptr.size(); ++L) wmax = std::max(wmax, bd.lvl_ptr[L + 1] - bd.lvl_ptr[L]);
+        const bool ok = wmax <= kBandChunk && band_lds_bytes(bd.ring_words, K) <= 160 * 1024;
+        if (ok && (!band_ok || bd.est < best.est)) {
+            best = std::move(bd);
+            band_ok = true;
+        }
+        if (B == 64) break;
+    }
+    T.est_band_us = band_ok ? best.est : -1.0;
+    T.schedule = (band_ok && best.est < T.est_syncfree_us) ? kSchedBand : kSchedSyncFree;
+    T.present = true;
+    T.upper = upper;
+    T.nnz = (int64_t)F.ci.size();
+    T.levels = nlev;
+    T.band_B = best.B;
+    T.band_nblocks = best.nblocks;
+    T.band_levels = best.lvl_ptr.empty() ? 0 : (int64_t)best.lvl_ptr.size() - 1;
+    T.ring_words = best.ring_words;
+    std::vector<int32_t> rrow, rend, rc_;
+    std::vector<double> rv, rd;
+    if (band_ok) {
+        T.band_K = K;
+        rrow.assign(n, 0);
+        rend.assign(n, 0);
+        rc_.assign((size_t)K * n, -1);
+        rv.assign((size_t)K * n, 0.0);
+        if (!dg.empty()) rd.assign(n, 1.0);
+        for (int64_t b = 0; b < best.nblocks; ++b) {
+            const int64_t p_lo = b * best.B;
+            for (int64_t L = best.blk_lvl[b]; L < best.blk_lvl[b + 1]; ++L)
+                for (int64_t q = best.lvl_ptr[L]; q < best.lvl_ptr[L + 1]; ++q) {
+                    const int32_t i = best.rows[q];
+                    rrow[q] = i;
+                    rend[q] = (int32_t)(best.lvl_ptr[L + 1] - p_lo);
+                    int k = 0;
+                    for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j, ++k) {
+                        rc_[(size_t)k * n + q] = F.ci[j];
+                        rv[(size_t)k * n + q] = ova[j];
+                    }
+                    if (!dg.empty()) rd[q] = dg[i];
+                }
+        }
+    }
+    int rc = upload(&T.rowptr, F.rp);
+    if (rc == PSK_OK) rc = upload(&T.colidx, F.ci);
+    if (rc == PSK_OK) rc = upload(&T.vals, ova);
+    if (rc == PSK_OK) rc = upload(&T.diag, dg);
+    if (rc == PSK_OK) rc = upload(&T.order, order);
+    if (rc == PSK_OK) rc = upload(&T.rec_row, rrow);
+    if (rc == PSK_OK) rc = upload(&T.rec_end, rend);
+    if (rc == PSK_OK) rc = upload(&T.rec_c, rc_);
+    if (rc == PSK_OK) rc = upload(&T.rec_v, rv);
+    if (rc == PSK_OK) rc = upload(&T.rec_d, rd);
+    return rc;
+}
+
 extern "C" int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, const int32_t *l_colidx,
                                         const double *l_vals, int32_t l_unit, const int32_t *u_rowptr,
                                         const int32_t *u_colidx, const double *u_vals, int32_t u_unit,
                                         const int32_t *gather_in, const int32_t *gather_out, psk_prec **out) {
     if (!out || n < 0) return fail(PSK_ERR_ARG, "psk_prec_create_trisolve: bad arguments");
     if (n >= INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_prec_create_trisolve: n must fit int32");
-    const bool has_l = l_rowptr != nullptr, has_u = u_rowptr != nullptr;
-    std::vector<int32_t> lrp, urp, lci, uci, lord, uord;
-    std::vector<double> lva, uva, ldg, udg;
-    int64_t nlev_l = 0, nlev_u = 0;
-    if (has_l) {
-        if (l_rowptr[n] > 0 && (!l_colidx || !l_vals)) return fail(PSK_ERR_ARG, "lower factor: NULL arrays");
-        PSK_TRY(split_factor(n, l_rowptr, l_colidx, l_vals, true, l_unit != 0, lrp, lci, lva, ldg));
-        level_order(n, lrp, lci, false, lord, nlev_l);
-    }
-    if (has_u) {
-        if (u_rowptr[n] > 0 && (!u_colidx || !u_vals)) return fail(PSK_ERR_ARG, "upper factor: NULL arrays");
-        PSK_TRY(split_factor(n, u_rowptr, u_colidx, u_vals, false, u_unit != 0, urp, uci, uva, udg));
-        level_order(n, urp, uci, true, uord, nlev_u);
-    }
+    if (l_rowptr && l_rowptr[n] > 0 && (!l_colidx || !l_vals)) return fail(PSK_ERR_ARG, "lower factor: NULL arrays");
+    if (u_rowptr && u_rowptr[n] > 0 && (!u_colidx || !u_vals)) return fail(PSK_ERR_ARG, "upper factor: NULL arrays");
     if (gather_in) PSK_TRY(check_perm(n, gather_in, "gather_in"));
     if (gather_out) PSK_TRY(check_perm(n, gather_out, "gather_out"));
-    std::vector<int32_t> gin, gout;
-    if (gather_in) gin.assign(gather_in, gather_in + n);
-    if (gather_out) gout.assign(gather_out, gather_out + n);
-
     Context *c;
     PSK_TRY(ctx(&c));
     psk_prec *M = new psk_prec();
     M->kind = PSK_PREC_ILU;
     M->n = n;
-    M->has_l = has_l;
-    M->has_u = has_u;
-    M->l_levels = nlev_l;
-    M->u_levels = nlev_u;
     int rc = PSK_OK;
-    if (rc == PSK_OK) rc = upload(&M->l_rowptr, lrp);
-    if (rc == PSK_OK) rc = upload(&M->l_colidx, lci);
-    if (rc == PSK_OK) rc = upload(&M->l_vals, lva);
-    if (rc == PSK_OK) rc = upload(&M->l_diag, ldg);
-    if (rc == PSK_OK) rc = upload(&M->u_rowptr, urp);
-    if (rc == PSK_OK) rc = upload(&M->u_colidx, uci);
-    if (rc == PSK_OK) rc = upload(&M->u_vals, uva);
-    if (rc == PSK_OK) rc = upload(&M->u_diag, udg);
+    if (l_rowptr) rc = make_factor(c, n, l_rowptr, l_colidx, l_vals, false, l_unit != 0, M->lo);
+    if (rc == PSK_OK && u_rowptr) rc = make_factor(c, n, u_rowptr, u_colidx, u_vals, true, u_unit != 0, M->up);
+    std::vector<int32_t> gin, gout;
+    if (gather_in) gin.assign(gather_in, gather_in + n);
+    if (gather_out) gout.assign(gather_out, gather_out + n);
     if (rc == PSK_OK) rc = upload(&M->gather_in, gin);
     if (rc == PSK_OK) rc = upload(&M->gather_out, gout);
-    if (rc == PSK_OK) rc = upload(&M->l_order, lord);
-    if (rc == PSK_OK) rc = upload(&M->u_order, uord);
     if (rc == PSK_OK && n > 0 && hipMalloc(&M->work, (size_t)(2 * n) * sizeof(double)) != hipSuccess)
         rc = fail(PSK_ERR_ALLOC, "trisolve work");
     if (rc == PSK_OK && hipMalloc(&M->err, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_ALLOC, "trisolve err");
@@ -304,8 +665,6 @@ extern "C" int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, cons
         psk_prec_destroy(M);
         return rc;
     }
-    M->nnz_l = (int64_t)lci.size();
-    M->nnz_u = (int64_t)uci.size();
     *out = M;
     return PSK_OK;
 }
@@ -321,4 +680,24 @@ extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int
     for (int64_t i = 0; i < n; ++i) pinv[perm_r[i]] = (int32_t)i;
     return psk_prec_create_trisolve(n, l_rowptr, l_colidx, l_vals, 1, u_rowptr, u_colidx, u_vals, 0, pinv.data(),
                                     perm_c, out);
+}
+
+extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t *schedule,
+                                          int64_t *blocks, int32_t *ring_words, double *est_syncfree_us,
+                                          double *est_band_us) {
+    if (!M || M->kind != PSK_PREC_ILU || (which != 0 && which != 1))
+        return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: not a triangular-solve chain / bad factor");
+    TriFactor &T = which == 0 ? M->lo : M->up;
+    if (!T.present) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: factor absent");
+    if (set == kSchedBand && T.band_K == 0)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor not eligible for the band schedule "
+                                         "(more than 8 entries in a row or a level wider than a chunk)");
+    if (set == kSchedSyncFree || set == kSchedBand) T.schedule = set;
+    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0 or 1");
+    if (schedule) *schedule = T.schedule;
+    if (blocks) *blocks = T.band_nblocks;
+    if (ring_words) *ring_words = T.ring_words;
+    if (est_syncfree_us) *est_syncfree_us = T.est_syncfree_us;
+    if (est_band_us) *est_band_us = T.est_band_us;
+    return PSK_OK;
 }

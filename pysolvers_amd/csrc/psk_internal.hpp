@@ -106,24 +106,47 @@ struct psk_csr {
     psk::DevBuf ws_small;
 };
 
-namespace psk { struct AmgHierarchy; }
+namespace psk {
+struct AmgHierarchy;
+
+// One sparse triangular factor on the device: off-diagonal entries in stored order (lower or
+// upper implied by the solve direction), diagonal (nullptr = unit), and two schedules built on
+// the host at creation (ilu.hip):
+//  * sync-free: rows dealt to waves in dependency-level order (`order`, `levels` global levels);
+//  * band: solve order cut into `band_nblocks` contiguous blocks of `band_B` rows, one workgroup
+//    per block walking the block's LOCAL levels (dependencies inside the block) with a barrier
+//    between levels; dependencies on earlier blocks are waited on through the published values;
+//    an LDS ring of `ring_words` doubles (0 = none) serves the in-block dependencies.
+// `schedule` picks one (kSchedSyncFree / kSchedBand), chosen by a host simulation of both.
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1 };
+struct TriFactor {
+    bool present = false, upper = false;
+    int64_t nnz = 0;
+    int32_t *rowptr = nullptr, *colidx = nullptr;
+    double *vals = nullptr, *diag = nullptr;
+    int32_t *order = nullptr;
+    int64_t levels = 0;
+    int schedule = kSchedSyncFree;
+    // band record stream (n records, block by block in local-level order; SoA, K entries each)
+    int32_t *rec_row = nullptr, *rec_end = nullptr, *rec_c = nullptr;
+    double *rec_v = nullptr, *rec_d = nullptr;
+    int band_K = 0;
+    int64_t band_B = 0, band_nblocks = 0, band_levels = 0;
+    int32_t ring_words = 0;
+    double est_syncfree_us = 0.0, est_band_us = 0.0;
+    void release();
+};
+}  // namespace psk
 
 struct psk_prec {
     int kind = PSK_PREC_IDENTITY;
     int64_t n = 0;
     double *dinv = nullptr;   // JACOBI
-    // PSK_PREC_ILU = triangular-solve chain: out = (U^-1 L^-1 v[gather_in])[gather_out].
-    // L strictly lower, U strictly upper (off-diagonal entries, stored order); l_diag / u_diag
-    // nullptr = unit diagonal. has_l / has_u: factor present.
-    bool has_l = false, has_u = false;
-    int32_t *l_rowptr = nullptr, *l_colidx = nullptr, *u_rowptr = nullptr, *u_colidx = nullptr;
-    double *l_vals = nullptr, *u_vals = nullptr, *l_diag = nullptr, *u_diag = nullptr;
+    // PSK_PREC_ILU = triangular-solve chain: out = (U^-1 L^-1 v[gather_in])[gather_out]
+    psk::TriFactor lo, up;
     int32_t *gather_in = nullptr, *gather_out = nullptr;
-    int32_t *l_order = nullptr, *u_order = nullptr;   // rows sorted by dependency level
-    int64_t l_levels = 0, u_levels = 0;
     double *work = nullptr;   // 2n: y, z
     int32_t *err = nullptr;
-    int64_t nnz_l = 0, nnz_u = 0;
     psk::AmgHierarchy *amg = nullptr;   // PSK_PREC_AMG
 };
 

@@ -631,11 +631,11 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
 
 int psk_prec_destroy(psk_prec *M) {
     if (!M) return PSK_OK;
-    void *ptrs[] = {M->dinv,   M->l_rowptr,  M->l_colidx,   M->l_vals, M->l_diag, M->u_rowptr,
-                    M->u_colidx, M->u_vals,  M->u_diag,     M->gather_in, M->gather_out, M->work,
-                    M->err,    M->l_order,   M->u_order};
+    void *ptrs[] = {M->dinv, M->gather_in, M->gather_out, M->work, M->err};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
+    M->lo.release();
+    M->up.release();
     if (M->amg) amg_free(M->amg);
     delete M;
     return PSK_OK;
@@ -646,10 +646,10 @@ int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, 
     if (!M) return fail(PSK_ERR_ARG, "psk_prec_info: NULL preconditioner");
     if (kind) *kind = M->kind;
     if (n) *n = M->n;
-    if (nnz_l) *nnz_l = M->nnz_l;
-    if (nnz_u) *nnz_u = M->nnz_u;
-    if (levels_l) *levels_l = M->l_levels;
-    if (levels_u) *levels_u = M->u_levels;
+    if (nnz_l) *nnz_l = M->lo.nnz;
+    if (nnz_u) *nnz_u = M->up.nnz;
+    if (levels_l) *levels_l = M->lo.levels;
+    if (levels_u) *levels_u = M->up.levels;
     return PSK_OK;
 }
 

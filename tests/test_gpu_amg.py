@@ -113,12 +113,12 @@ def test_ic_apply_matches_reference_ops(psk, case):
     assert np.array_equal(M.applyLeft(v), v)
 
 
-@pytest.mark.parametrize("n,seed", [(1, 0), (37, 1), (2000, 2), (20000, 3)])
+@pytest.mark.parametrize("n,seed", [(1, 0), (37, 1), (2000, 2), (20000, 3), (50000, 4)])
 def test_trisolve_chain_random(psk, n, seed):
     """out = (U^-1 L^-1 v[gin])[gout] for random unit/non-unit factors (rows of 0..40 entries)."""
     from pysolvers_amd.Linear import TriangularSolveChain
     rng = np.random.default_rng(seed)
-    dens = min(1.0, 8.0 / max(n, 1))
+    dens = min(1.0, (8.0 if seed < 4 else 3.0) / max(n, 1))   # seed 4: short rows -> band-eligible
     Lo = sp.tril(sp.random(n, n, density=dens, random_state=rng), k=-1).tocsr() * 0.1
     Up = sp.triu(sp.random(n, n, density=dens, random_state=rng), k=1).tocsr() * 0.1
     dl, du = 1.0 + rng.random(n), 1.0 + rng.random(n)
@@ -132,6 +132,11 @@ def test_trisolve_chain_random(psk, n, seed):
         ref = spla.spsolve_triangular(Ud, spla.spsolve_triangular(Ld, v[gin], lower=True), lower=False)[gout]
         M = TriangularSolveChain(n, L=L, l_unit=l_unit, U=U, u_unit=u_unit, gather_in=gin, gather_out=gout)
         assert _rel(M.apply(v), ref) <= 1e-12
+        for sched in ("syncfree", "band"):                   # both schedules, forced where eligible
+            for f in ("L", "U"):
+                if sched == "syncfree" or M.schedule(f)["est_band_us"] >= 0:
+                    M.schedule(f, set=sched)
+            assert _rel(M.apply(v), ref) <= 1e-12, sched
     # single factors, no permutations
     M = TriangularSolveChain(n, U=U)
     assert _rel(M.apply(v), spla.spsolve_triangular(U, v, lower=False)) <= 1e-12
@@ -153,3 +158,22 @@ def test_trisolve_rejects_bad_factors(psk):
         TriangularSolveChain(2, L=L)
     with pytest.raises(N.PskError):
         TriangularSolveChain(2, L=L, l_unit=True, gather_in=np.array([0, 0]))   # not a permutation
+
+
+@pytest.mark.parametrize("m", [64, 300])
+def test_gauss_seidel_factor_schedules(psk, m):
+    """triu(-FD2D) (the GS smoother's factor, ClassicSmoothers.py:33): band and sync-free schedules
+    both solve it; the band schedule must have an LDS ring (in-block distance m) at these sizes."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    U = sp.triu(A).tocsr()
+    v = np.random.default_rng(m).standard_normal(A.shape[0])
+    ref = spla.spsolve_triangular(U, v, lower=False)
+    M = TriangularSolveChain(A.shape[0], U=U)
+    info = M.schedule("U")
+    assert info["est_band_us"] > 0 and info["est_syncfree_us"] > 0
+    for sched in ("band", "syncfree"):
+        M.schedule("U", set=sched)
+        assert _rel(M.apply(v), ref) <= 1e-12, sched
+        assert _rel(M.apply(v), ref) <= 1e-12, sched          # re-apply (sentinel refill)

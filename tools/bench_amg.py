@@ -66,13 +66,20 @@ def main():
     out["amg_apply_ms"] = (time.perf_counter() - t2) * 1e3 / reps
     if args.smoother == "gs":
         S = M._S[-1].operator
-        S.apply(v)
-        N.check(N.lib.psk_synchronize(), "sync")
-        t3 = time.perf_counter()
-        for _ in range(reps):
+        info = S.schedule("U")
+        out["fine_gs_schedule"] = info
+        chosen = info["schedule"]
+        for sched in ("syncfree", "band"):
+            S.schedule("U", set=sched)
             S.apply(v)
-        N.check(N.lib.psk_synchronize(), "sync")
-        out["fine_gs_sweep_ms"] = (time.perf_counter() - t3) * 1e3 / reps
+            N.check(N.lib.psk_synchronize(), "sync")
+            t3 = time.perf_counter()
+            for _ in range(reps):
+                S.apply(v)
+            N.check(N.lib.psk_synchronize(), "sync")
+            out["fine_gs_sweep_ms_" + sched] = (time.perf_counter() - t3) * 1e3 / reps
+        S.schedule("U", set=chosen)
+        out["coarse_levels_schedules"] = [M._S[k].operator.schedule("U")["schedule"] for k in range(1, args.levels)]
     out["setup_s"] = time.time() - t
     sol = psk.DeviceVector(n)
 
