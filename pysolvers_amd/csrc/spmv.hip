@@ -16,6 +16,7 @@
 #include "psk_internal.hpp"
 
 #include <climits>
+#include <cstdlib>
 #include <cmath>
 
 namespace psk {
@@ -31,20 +32,32 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const double *__restrict__ vals, const double *__restrict__ x, double *__restrict__ y,
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, double *__restrict__ partial,
-    const int32_t *__restrict__ done) {
+    const int32_t *__restrict__ done, int32_t nnz, int32_t strip) {
     if (done != nullptr && *done != 0) return;
     constexpr int KU = kChunk / kBlock;   // staged entries per lane per chunk
-    __shared__ double prod[kChunk];
+    __shared__ double prod[kChunk + kBlock];   // + a dump row for lanes past the chunk's end
     __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
     // tiles are dealt round-robin (tile = block + k*grid): the whole grid sweeps one compact window
     // of rows at a time, so x entries gathered by rows i-m, i and i+m are fetched once and re-served
     // from L2 / Infinity Cache (spmv_lab A3: +22% over contiguous per-block ranges at n = 268M)
     const int64_t ntiles = (n + trows - 1) / trows;
-    const int64_t tstep = gridDim.x, t0 = blockIdx.x, t1 = ntiles;
+    int64_t tstep = gridDim.x, t0 = blockIdx.x, t1 = ntiles;
+    if (strip > 0 && gridDim.x % strip == 0) {
+        // strip order (experiment): with S = tiles per grid line, workgroup g walks tile column
+        // g % S over a contiguous range of tile rows, so x[i-m] was its own x[i] one tile earlier
+        const int64_t S = strip, c = blockIdx.x % S, q = blockIdx.x / S, Q = gridDim.x / S;
+        const int64_t R = (ntiles + S - 1) / S, rb = R * q / Q, re_ = R * (q + 1) / Q;
+        t0 = rb * S + c;
+        t1 = re_ * S + c < ntiles ? re_ * S + c : ntiles;
+        tstep = S;
+    }
+    const int32_t last = nnz > 0 ? nnz - 1 : 0;   // colidx/vals hold at least one (dummy) entry
     double acc = 0.0;
 
-    // issue the colidx/vals stream of the first chunk of tile t (branch-free, clamped to the tile)
+    // The colidx/vals stream of the first chunk of tile t, clamped to valid indices. ALWAYS the same
+    // number of loads (an empty tile re-reads one valid entry): the compiler can then wait for this
+    // tile's gathers with a static vmcnt while the next tile's stream is still in flight.
     int32_t cc[KU], ncc[KU];
     double vv[KU], nvv[KU];
     int32_t e0 = 0, e1 = 0;
@@ -52,15 +65,14 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
         const int64_t r0 = t * trows, r1 = (r0 + trows < n) ? r0 + trows : n;
         a = rowptr[r0];
         b = rowptr[r1];
-        if (b > a) {   // wave-uniform; an empty tile issues nothing (and never reads past nnz)
-            const int32_t c1 = (b - a > kChunk) ? a + kChunk : b;
+        const int32_t c1 = (b - a > kChunk) ? a + kChunk : b;
+        const int32_t base = a < last ? a : last;
 #pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                const int32_t e = a + k * kBlock + tid;
-                const int32_t ee = e < c1 ? e : a;
-                c_[k] = ld_stream(colidx + ee);
-                v_[k] = ld_stream(vals + ee);
-            }
+        for (int k = 0; k < KU; ++k) {
+            const int32_t e = a + k * kBlock + tid;
+            const int32_t ee = e < c1 ? e : base;
+            c_[k] = ld_stream(colidx + ee);
+            v_[k] = ld_stream(vals + ee);
         }
     };
     if (t0 < t1) issue(t0, e0, e1, cc, vv);
@@ -70,25 +82,19 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
         const int64_t r1 = (r0 + trows < n) ? r0 + trows : n;
         const int64_t row = r0 + tid;
         const bool has = tid < trows && row < r1;
-        int32_t rs = 0, re = 0;
-        if (has) {
-            rs = rowptr[row];
-            re = rowptr[row + 1];
-        }
+        const int64_t rowc = has ? row : r0;   // a valid row for the unconditional epilogue loads
+        // row bounds and the epilogue operands, loaded BEFORE the prefetch so that waiting for them
+        // never waits for the next tile's stream
+        const int32_t rs = rowptr[rowc], re = rowptr[rowc + 1];
+        double eq = 0.0;
+        if (MODE == kSpmvDot) eq = x[rowc];
+        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+            eq = aux_q[rowc];
         const int32_t ce0 = e0, ce1 = e1;
-        bool prefetched = false;
         double sum = 0.0;
-        for (int32_t c0 = ce0; c0 < ce1; c0 += kChunk) {
-            const int32_t c1 = (ce1 - c0 > kChunk) ? c0 + kChunk : ce1;
-            if (c0 != ce0) {   // tile longer than one chunk: stream the next chunk now
-#pragma unroll
-                for (int k = 0; k < KU; ++k) {
-                    const int32_t e = c0 + k * kBlock + tid;
-                    const int32_t ee = e < c1 ? e : c0;
-                    cc[k] = ld_stream(colidx + ee);
-                    vv[k] = ld_stream(vals + ee);
-                }
-            }
+        // chunk 0 (its stream was issued one tile ago)
+        {
+            const int32_t c0 = ce0, c1 = (ce1 - c0 > kChunk) ? c0 + kChunk : ce1;
             double xv[KU], pv[KU];
 #pragma unroll
             for (int k = 0; k < KU; ++k) {
@@ -97,19 +103,36 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
                 xv[k] = xx;
             }
             // software pipeline: the next tile's stream is in flight while this tile's gathers land
-            const bool pf = c1 == ce1 && t + tstep < t1;
-            if (pf) {
-                issue(t + tstep, e0, e1, ncc, nvv);
-                prefetched = true;
-            }
+            const int64_t tn = (t + tstep < t1) ? t + tstep : t;
+            issue(tn, e0, e1, ncc, nvv);
 #pragma unroll
             for (int k = 0; k < KU; ++k) pv[k] = vv[k] * xv[k];   // rounded product
-            if (pf) {
+            // unconditional stores (lanes past the chunk write the dump row): a conditional store
+            // would let the compiler sink that lane's gather behind the prefetch and wait for both
 #pragma unroll
-                for (int k = 0; k < KU; ++k) {
-                    cc[k] = ncc[k];
-                    vv[k] = nvv[k];
-                }
+            for (int k = 0; k < KU; ++k) {
+                const int32_t e = c0 + k * kBlock + tid;
+                prod[(e < c1 ? k * kBlock : kChunk) + tid] = pv[k];
+            }
+            __syncthreads();
+            const int32_t a = rs > c0 ? rs : c0;
+            const int32_t bnd = re < c1 ? re : c1;
+            if (has)
+                for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
+            __syncthreads();
+        }
+        // rare: tile longer than one chunk
+        for (int32_t c0 = ce0 + kChunk; c0 < ce1; c0 += kChunk) {
+            const int32_t c1 = (ce1 - c0 > kChunk) ? c0 + kChunk : ce1;
+            double pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) {
+                const int32_t e = c0 + k * kBlock + tid;
+                const int32_t ee = e < c1 ? e : c0;
+                const int32_t c = ld_stream(colidx + ee);
+                double xx = x[c];
+                if (MODE == kSpmvJacobiDot) xx = aux_d[c] * xx;
+                pv[k] = ld_stream(vals + ee) * xx;
             }
 #pragma unroll
             for (int k = 0; k < KU; ++k) {
@@ -119,21 +142,25 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             __syncthreads();
             const int32_t a = rs > c0 ? rs : c0;
             const int32_t bnd = re < c1 ? re : c1;
-            for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
+            if (has)
+                for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];
             __syncthreads();
         }
-        if (!prefetched && t + tstep < t1) issue(t + tstep, e0, e1, cc, vv);   // empty tile
+#pragma unroll
+        for (int k = 0; k < KU; ++k) {
+            cc[k] = ncc[k];
+            vv[k] = nvv[k];
+        }
         if (has) {
             if (MODE == kSpmvResid) {
-                const double r = aux_q[row] - sum;   // b - A*x (GMRESSolver.py:163)
+                const double r = eq - sum;   // b - A*x (GMRESSolver.py:163)
                 y[row] = r;
                 acc = fma(r, r, acc);
             } else if (MODE == kSpmvAdd) {
-                y[row] = aux_q[row] + sum;           // x + P*x2 (VCycleManager.py:55)
+                y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
             } else {
                 __builtin_nontemporal_store(sum, y + row);
-                if (MODE == kSpmvDot) acc = fma(x[row], sum, acc);
-                if (MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot) acc = fma(aux_q[row], sum, acc);
+                if (MODE != kSpmvPlain) acc = fma(eq, sum, acc);   // x.(Ax) or q.(Ax)
             }
         }
     }
@@ -154,7 +181,12 @@ int tile_rows_for(int64_t n, int64_t nnz) {
 
 int spmv_grid(const Context *c, const psk_csr *A) {
     const int64_t tiles = (A->n + A->tile_rows - 1) / A->tile_rows;
-    int cap = c->num_cus * 4;   // 4 workgroups per CU streamed best (spmv_lab: g1024-1536)
+    static const int per_cu = [] {   // 3 workgroups per CU streamed best (bench sweep 2..8, r1)
+        const char *e = std::getenv("PSK_SPMV_WG_PER_CU");   // experiments only
+        const int v = e ? std::atoi(e) : 3;
+        return v >= 1 && v <= 8 ? v : 3;
+    }();
+    int cap = c->num_cus * per_cu;
     cap -= cap % 8;
     if (cap < 8) cap = 8;
     if (cap > kMaxGrid) cap = kMaxGrid;
@@ -167,30 +199,32 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     if (A->n == 0) return PSK_OK;
     dim3 gd(grid), bd(kBlock);
     const int tr = A->tile_rows;
+    static const bool strip_on = std::getenv("PSK_SPMV_STRIP") != nullptr;   // experiments only
+    const int32_t strip = strip_on ? A->strip_tiles : 0;
     switch (mode) {
     case kSpmvPlain:
         hipLaunchKernelGGL(spmv_kernel<kSpmvPlain>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
         break;
     case kSpmvDot:
         hipLaunchKernelGGL(spmv_kernel<kSpmvDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
         break;
     case kSpmvJacobiDot:
         hipLaunchKernelGGL(spmv_kernel<kSpmvJacobiDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
-                           A->vals, x, y, aux_d, aux_q, partial, done_flag);
+                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
         break;
     case kSpmvPlainDot:
         hipLaunchKernelGGL(spmv_kernel<kSpmvPlainDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
-                           A->vals, x, y, aux_d, aux_q, partial, done_flag);
+                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
         break;
     case kSpmvResid:
         hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
         break;
     case kSpmvAdd:
         hipLaunchKernelGGL(spmv_kernel<kSpmvAdd>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
         break;
     default:
         return fail(PSK_ERR_ARG, "unknown spmv mode");
@@ -323,11 +357,17 @@ static int csr_alloc(psk_csr *A, int64_t n, int64_t nnz) {
     hipError_t e;
     e = hipMalloc(&A->rowptr, (size_t)(n + 1) * sizeof(int32_t));
     if (e != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc rowptr");
-    if (nnz > 0) {
-        e = hipMalloc(&A->colidx, (size_t)nnz * sizeof(int32_t));
+    {   // at least one entry: the SpMV's clamped stream loads always read a valid address
+        const size_t m = nnz > 0 ? (size_t)nnz : 1;
+        e = hipMalloc(&A->colidx, m * sizeof(int32_t));
         if (e != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc colidx");
-        e = hipMalloc(&A->vals, (size_t)nnz * sizeof(double));
+        e = hipMalloc(&A->vals, m * sizeof(double));
         if (e != hipSuccess) return fail(PSK_ERR_ALLOC, "hipMalloc vals");
+        if (nnz == 0) {
+            e = hipMemset(A->colidx, 0, sizeof(int32_t));
+            if (e == hipSuccess) e = hipMemset(A->vals, 0, sizeof(double));
+            if (e != hipSuccess) return fail(PSK_ERR_HIP, "hipMemset dummy entry");
+        }
     }
     return PSK_OK;
 }
@@ -414,6 +454,7 @@ int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out) {
     A->ncols = n;
     A->nnz = nnz;
     A->tile_rows = tile_rows_for(n, nnz);
+    A->strip_tiles = (int)(m / A->tile_rows);
     A->n_global = n;
     A->row_end = n;
     A->device = c->device;
