@@ -83,6 +83,9 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
 }
 
 // ---- K2: x, r update + partials [r.r, u.r] -------------------------------------------------
+// JAC: Jacobi preconditioner fused (dinv != nullptr). A template, not a runtime test: a branch in the
+// loop body makes the compiler drain vmcnt (stores included) at every join.
+template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ x, double *__restrict__ r, const double *__restrict__ p,
     const double *__restrict__ Ap, const double *__restrict__ dinv, const double *__restrict__ part1,
@@ -104,35 +107,57 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     double rr = 0.0, ur = 0.0;
     int64_t i = i0 + 2 * threadIdx.x;
-    // cache policy: x and Ap are dead after this kernel (non-temporal); r and p are re-read by K3
-#pragma unroll 2
-    for (; i + 1 < i1; i += kVecTile) {                      // 16 B per lane per array
-        const dv2 xv = ld2nt(x + i);
-        const dv2 pv = ld2(p + i);
-        const dv2 rv = ld2(r + i);
-        const dv2 av = ld2nt(Ap + i);
+    // cache policy: x and Ap are dead after this kernel (non-temporal); r and p are re-read by K3.
+    // Software pipeline: the next tile's five loads are issued before this tile's two stores, so the
+    // wait for this tile's operands is a static vmcnt that never includes a store acknowledgement.
+    struct Ops {
+        dv2 x, p, r, a, d;
+    } A{}, B{};
+    auto load = [&](Ops &o, int64_t j) {
+        o.x = ld2nt(x + j);
+        o.p = ld2(p + j);
+        o.r = ld2(r + j);
+        o.a = ld2nt(Ap + j);
+        if (JAC) o.d = ld2(dinv + j);
+    };
+    auto step = [&](const Ops &o, int64_t j) {
         dv2 xn, rn;
-        xn.x = xv.x + alpha * pv.x;                          // x = x + alpha*p   :121
-        xn.y = xv.y + alpha * pv.y;
-        rn.x = rv.x - alpha * av.x;                          // r = r - alpha*Ap  :122
-        rn.y = rv.y - alpha * av.y;
+        xn.x = o.x.x + alpha * o.p.x;                        // x = x + alpha*p   :121
+        xn.y = o.x.y + alpha * o.p.y;
+        rn.x = o.r.x - alpha * o.a.x;                        // r = r - alpha*Ap  :122
+        rn.y = o.r.y - alpha * o.a.y;
         double u0 = rn.x, u1 = rn.y;
-        if (dinv) {
-            const dv2 dv = ld2(dinv + i);
-            u0 = dv.x * rn.x;                                // u = precond.applyRight(r)  :123
-            u1 = dv.y * rn.y;
+        if (JAC) {
+            u0 = o.d.x * rn.x;                               // u = precond.applyRight(r)  :123
+            u1 = o.d.y * rn.y;
         }
-        st2nt(x + i, xn);
-        st2(r + i, rn);
+        st2nt(x + j, xn);
+        st2(r + j, rn);
         rr = fma(rn.x, rn.x, rr);
         rr = fma(rn.y, rn.y, rr);
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
+    };
+    // ping-pong register sets (no copies between them): the next tile's loads are in flight while
+    // this tile is computed and stored; clamped indices keep the load count static
+    auto nxt = [&](int64_t j) { return (j + kVecTile + 1 < i1) ? j + kVecTile : j; };
+    if (i + 1 < i1) {
+        load(A, i);
+        while (true) {
+            load(B, nxt(i));
+            step(A, i);
+            i += kVecTile;
+            if (!(i + 1 < i1)) break;
+            load(A, nxt(i));
+            step(B, i);
+            i += kVecTile;
+            if (!(i + 1 < i1)) break;
+        }
     }
     if (i < i1) {   // odd tail element
         const double xn = x[i] + alpha * p[i];
         const double rn = r[i] - alpha * Ap[i];
-        const double u0 = dinv ? dinv[i] * rn : rn;
+        const double u0 = JAC ? dinv[i] * rn : rn;
         x[i] = xn;
         r[i] = rn;
         rr = fma(rn, rn, rr);
@@ -147,6 +172,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
 }
 
 // ---- K3: convergence test, beta, p = u + beta p ------------------------------------------------
+template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, const double *__restrict__ r, double *__restrict__ p, const double *__restrict__ dinv,
     const double *__restrict__ part2, int np, PcgState *st, double *__restrict__ udr,
@@ -171,24 +197,43 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     block_range((n + kVecTile - 1) / kVecTile, t0, t1);
     const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     int64_t i = i0 + 2 * threadIdx.x;
-    // r and dinv are not needed again this iteration (non-temporal); p is gathered by the next SpMV
-#pragma unroll 2
-    for (; i + 1 < i1; i += kVecTile) {
-        const dv2 rv = ld2nt(r + i);
-        const dv2 pv = ld2(p + i);
-        double u0 = rv.x, u1 = rv.y;
-        if (dinv) {
-            const dv2 dv = ld2nt(dinv + i);
-            u0 = dv.x * rv.x;
-            u1 = dv.y * rv.y;
+    // r and dinv are not needed again this iteration (non-temporal); p is gathered by the next SpMV.
+    // Same software pipeline as pcg_update_kernel (next loads issued before this store).
+    struct Ops {
+        dv2 r, p, d;
+    } A{}, B{};
+    auto load = [&](Ops &o, int64_t j) {
+        o.r = ld2nt(r + j);
+        o.p = ld2(p + j);
+        if (JAC) o.d = ld2nt(dinv + j);
+    };
+    auto step = [&](const Ops &o, int64_t j) {
+        double u0 = o.r.x, u1 = o.r.y;
+        if (JAC) {
+            u0 = o.d.x * o.r.x;
+            u1 = o.d.y * o.r.y;
         }
         dv2 pn;
-        pn.x = u0 + beta * pv.x;                             // p = u + beta*p  :138
-        pn.y = u1 + beta * pv.y;
-        st2(p + i, pn);
+        pn.x = u0 + beta * o.p.x;                            // p = u + beta*p  :138
+        pn.y = u1 + beta * o.p.y;
+        st2(p + j, pn);
+    };
+    auto nxt = [&](int64_t j) { return (j + kVecTile + 1 < i1) ? j + kVecTile : j; };
+    if (i + 1 < i1) {
+        load(A, i);
+        while (true) {
+            load(B, nxt(i));
+            step(A, i);
+            i += kVecTile;
+            if (!(i + 1 < i1)) break;
+            load(A, nxt(i));
+            step(B, i);
+            i += kVecTile;
+            if (!(i + 1 < i1)) break;
+        }
     }
     if (i < i1) {
-        const double u0 = dinv ? dinv[i] * r[i] : r[i];
+        const double u0 = JAC ? dinv[i] * r[i] : r[i];
         p[i] = u0 + beta * p[i];
     }
 }
@@ -419,8 +464,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             break;
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         if (sharded && (rc = allreduce_sum(A, w.part1, np1, s)) != PSK_OK) break;
-        hipLaunchKernelGGL(pcg_update_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap, dinv,
-                           w.part1, np1, w.part2, w.st, w.udr, k);
+        if (dinv)
+            hipLaunchKernelGGL(pcg_update_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap, dinv,
+                               w.part1, np1, w.part2, w.st, w.udr, k);
+        else
+            hipLaunchKernelGGL(pcg_update_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap,
+                               dinv, w.part1, np1, w.part2, w.st, w.udr, k);
         if (sharded && (rc = allreduce_sum(A, w.part2, 2 * np2, s)) != PSK_OK) break;
         if (gen) {
             if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
@@ -428,8 +477,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             hipLaunchKernelGGL(pcg_gen_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.u, w.p, w.part2, np2,
                                w.part3, gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         } else {
-            hipLaunchKernelGGL(pcg_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv, w.part2,
-                               np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+            if (dinv)
+                hipLaunchKernelGGL(pcg_direction_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv,
+                                   w.part2, np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+            else
+                hipLaunchKernelGGL(pcg_direction_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv,
+                                   w.part2, np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;

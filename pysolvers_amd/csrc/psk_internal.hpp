@@ -92,7 +92,6 @@ struct psk_csr {
     int64_t ncols = 0;    // local columns = n + halo
     int64_t nnz = 0;
     int tile_rows = 256;  // SpMV rows per tile (psk::tile_rows_for)
-    int strip_tiles = 0;  // tiles per grid line when known (FD generator), for the strip tile order
     int32_t *rowptr = nullptr;
     int32_t *colidx = nullptr;
     double *vals = nullptr;

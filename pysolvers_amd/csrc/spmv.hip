@@ -32,7 +32,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const double *__restrict__ vals, const double *__restrict__ x, double *__restrict__ y,
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, double *__restrict__ partial,
-    const int32_t *__restrict__ done, int32_t nnz, int32_t strip) {
+    const int32_t *__restrict__ done, int32_t nnz) {
     if (done != nullptr && *done != 0) return;
     constexpr int KU = kChunk / kBlock;   // staged entries per lane per chunk
     __shared__ double prod[kChunk + kBlock];   // + a dump row for lanes past the chunk's end
@@ -42,16 +42,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     // of rows at a time, so x entries gathered by rows i-m, i and i+m are fetched once and re-served
     // from L2 / Infinity Cache (spmv_lab A3: +22% over contiguous per-block ranges at n = 268M)
     const int64_t ntiles = (n + trows - 1) / trows;
-    int64_t tstep = gridDim.x, t0 = blockIdx.x, t1 = ntiles;
-    if (strip > 0 && gridDim.x % strip == 0) {
-        // strip order (experiment): with S = tiles per grid line, workgroup g walks tile column
-        // g % S over a contiguous range of tile rows, so x[i-m] was its own x[i] one tile earlier
-        const int64_t S = strip, c = blockIdx.x % S, q = blockIdx.x / S, Q = gridDim.x / S;
-        const int64_t R = (ntiles + S - 1) / S, rb = R * q / Q, re_ = R * (q + 1) / Q;
-        t0 = rb * S + c;
-        t1 = re_ * S + c < ntiles ? re_ * S + c : ntiles;
-        tstep = S;
-    }
+    const int64_t tstep = gridDim.x, t0 = blockIdx.x, t1 = ntiles;
     const int32_t last = nnz > 0 ? nnz - 1 : 0;   // colidx/vals hold at least one (dummy) entry
     double acc = 0.0;
 
@@ -199,32 +190,30 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     if (A->n == 0) return PSK_OK;
     dim3 gd(grid), bd(kBlock);
     const int tr = A->tile_rows;
-    static const bool strip_on = std::getenv("PSK_SPMV_STRIP") != nullptr;   // experiments only
-    const int32_t strip = strip_on ? A->strip_tiles : 0;
     switch (mode) {
     case kSpmvPlain:
         hipLaunchKernelGGL(spmv_kernel<kSpmvPlain>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
         break;
     case kSpmvDot:
         hipLaunchKernelGGL(spmv_kernel<kSpmvDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
         break;
     case kSpmvJacobiDot:
         hipLaunchKernelGGL(spmv_kernel<kSpmvJacobiDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
-                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
+                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
         break;
     case kSpmvPlainDot:
         hipLaunchKernelGGL(spmv_kernel<kSpmvPlainDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
-                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
+                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
         break;
     case kSpmvResid:
         hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
         break;
     case kSpmvAdd:
         hipLaunchKernelGGL(spmv_kernel<kSpmvAdd>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz, strip);
+                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
         break;
     default:
         return fail(PSK_ERR_ARG, "unknown spmv mode");
@@ -454,7 +443,6 @@ int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out) {
     A->ncols = n;
     A->nnz = nnz;
     A->tile_rows = tile_rows_for(n, nnz);
-    A->strip_tiles = (int)(m / A->tile_rows);
     A->n_global = n;
     A->row_end = n;
     A->device = c->device;

@@ -188,6 +188,83 @@ __global__ __launch_bounds__(BS) void spmv_A3(int64_t n, const int* __restrict__
     }
 }
 
+// ---------------- A5: A3 interleave with an UNCONDITIONAL next-tile prefetch and unconditional LDS
+// stores (static vmcnt: the gathers are waited for while the prefetch stays in flight) = libpsk r1
+template <int CH, int TR = 256>
+__global__ __launch_bounds__(BS) void spmv_A5(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                              const double* __restrict__ va, const double* __restrict__ x,
+                                              double* __restrict__ y) {
+    constexpr int KU = CH / BS;
+    __shared__ double prod[CH + BS];
+    const int tid = threadIdx.x;
+    const int64_t nt = (n + TR - 1) / TR, g = gridDim.x;
+    const int last = rp[n] - 1;
+    int cc[KU], ncc[KU]; double vv[KU], nvv[KU];
+    int e0 = 0, e1 = 0;
+    auto issue = [&](int64_t t, int& a, int& b, int* c_, double* v_) {
+        const int64_t r0 = t * TR, r1 = r0 + TR < n ? r0 + TR : n;
+        a = rp[r0]; b = rp[r1];
+        const int c1 = b - a > CH ? a + CH : b;
+        const int base = a < last ? a : last;
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { int e = a + k * BS + tid; int ee = e < c1 ? e : base;
+            c_[k] = __builtin_nontemporal_load(ci + ee); v_[k] = __builtin_nontemporal_load(va + ee); }
+    };
+    if ((int64_t)blockIdx.x < nt) issue(blockIdx.x, e0, e1, cc, vv);
+    for (int64_t t = blockIdx.x; t < nt; t += g) {
+        const int64_t r0 = t * TR, r1 = r0 + TR < n ? r0 + TR : n;
+        double sum = 0.0, sum2 = 0.0;
+        const int64_t row = r0 + tid, row2 = r0 + BS + tid;
+        const bool has = tid < TR && row < r1, has2 = TR > BS && row2 < r1;
+        const int64_t rowc2 = has2 ? row2 : r0;
+        const int rs2 = rp[rowc2], re2 = rp[rowc2 + 1];
+        const int64_t rowc = has ? row : r0;
+        const int rs = rp[rowc], re = rp[rowc + 1];
+        const int ce0 = e0, ce1 = e1;
+        {
+            const int c0 = ce0, c1 = ce1 - c0 > CH ? c0 + CH : ce1;
+            double xv[KU], pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) xv[k] = x[cc[k]];
+            const int64_t tn = t + g < nt ? t + g : t;
+            issue(tn, e0, e1, ncc, nvv);
+#pragma unroll
+            for (int k = 0; k < KU; ++k) pv[k] = vv[k] * xv[k];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; prod[(e < c1 ? k * BS : CH) + tid] = pv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            if (has) for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            if (TR > BS) {
+                const int a2 = rs2 > c0 ? rs2 : c0, b2 = re2 < c1 ? re2 : c1;
+                if (has2) for (int e = a2; e < b2; ++e) sum2 = sum2 + prod[e - c0];
+            }
+            __syncthreads();
+        }
+        for (int c0 = ce0 + CH; c0 < ce1; c0 += CH) {
+            const int c1 = ce1 - c0 > CH ? c0 + CH : ce1;
+            double pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; int ee = e < c1 ? e : c0;
+                pv[k] = __builtin_nontemporal_load(va + ee) * x[__builtin_nontemporal_load(ci + ee)]; }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; prod[(e < c1 ? k * BS : CH) + tid] = pv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            if (has) for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            if (TR > BS) {
+                const int a2 = rs2 > c0 ? rs2 : c0, b2 = re2 < c1 ? re2 : c1;
+                if (has2) for (int e = a2; e < b2; ++e) sum2 = sum2 + prod[e - c0];
+            }
+            __syncthreads();
+        }
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { cc[k] = ncc[k]; vv[k] = nvv[k]; }
+        if (has) __builtin_nontemporal_store(sum, y + row);
+        if (has2) __builtin_nontemporal_store(sum2, y + row2);
+    }
+}
+
 // ---------------- A4: 3-stage pipeline: stream(t+2) | gather(t+1) | sum(t), round-robin tiles -----------
 template <int CH>
 __global__ __launch_bounds__(BS) void spmv_A4(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
@@ -576,15 +653,16 @@ int main(int argc, char** argv) {
         fillx<<<(n + 255) / 256, 256>>>(n, x);
         CK(hipDeviceSynchronize());
         const double bytes = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n;
-        const int S = m / 256 > 0 ? (int)(m / 256) : 1;
         std::vector<V> vs = {
             {"A blk256/ch2048", spmv_A, 2048},
             {"A3 interleave g1024", spmv_A3<1280, 2>, 1024},
-            {"A3 interleave g2048", spmv_A3<1280, 2>, 2048},
-            {"A3 strip g~512", spmv_A3<1280, 3>, S * (512 / S > 0 ? 512 / S : 1)},
-            {"A3 strip g~1024", spmv_A3<1280, 3>, S * (1024 / S > 0 ? 1024 / S : 1)},
-            {"A3 strip g~2048", spmv_A3<1280, 3>, S * (2048 / S > 0 ? 2048 / S : 1)},
-            {"A4 3-stage g1024", spmv_A4<1280>, 1024},
+            {"A5 g512", spmv_A5<1280>, 512},
+            {"A5 g640", spmv_A5<1280>, 640},
+            {"A5 g768", spmv_A5<1280>, 768},
+            {"A5 g896", spmv_A5<1280>, 896},
+            {"A5 tr512 g512", spmv_A5<2560, 512>, 512},
+            {"A5 tr512 g768", spmv_A5<2560, 512>, 768},
+            {"A5 tr512 g1024", spmv_A5<2560, 512>, 1024},
         };
         // reference result
         spmv_A<<<2048, BS>>>(n, rp, ci, va, x, yr);
@@ -616,7 +694,7 @@ int main(int argc, char** argv) {
                    t[i][0] * 1e3, t[i][R / 2] * 1e3, bytes / (t[i][0] * 1e-3) / 1e9, 100.0 * bytes / (t[i][0] * 1e-3) / 8e12);
         }
         // ---- PCG update-like kernels over 5 vectors of n doubles (K2: 5R+2W, K3: 3R+1W) ----
-        {
+        if (getenv("LAB_ELEMENTWISE")) {
             double* v5; CK(hipMalloc(&v5, 5 * n * 8)); CK(hipMemset(v5, 0, 5 * n * 8));
             double *vx = v5, *vr = v5 + n, *vp = v5 + 2 * n, *va2 = v5 + 3 * n, *vd = v5 + 4 * n;
             typedef void (*K2)(int64_t, double*, double*, const double*, const double*, const double*, double, double*);
