@@ -338,8 +338,8 @@ namespace {
 // sync-free: a row costs one agent-scope load round trip (~0.85) on its wave, plus a hand-off (~0.5)
 // after its last dependency was published (FD m=1024 ILU: 1.34 us per level); band: a local level
 // costs ~0.9 us with the ring (it is paced by the one external load of the block's boundary row;
-// FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~1.3 us without.
-constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 1.3;
+// FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
+constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
 
 struct HostFactor {
     int64_t n = 0;

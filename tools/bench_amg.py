@@ -80,6 +80,31 @@ def main():
             out["fine_gs_sweep_ms_" + sched] = (time.perf_counter() - t3) * 1e3 / reps
         S.schedule("U", set=chosen)
         out["coarse_levels_schedules"] = [M._S[k].operator.schedule("U")["schedule"] for k in range(1, args.levels)]
+
+    def timed(op, vec, reps=3):
+        op.apply(vec)
+        N.check(N.lib.psk_synchronize(), "sync")
+        t4 = time.perf_counter()
+        for _ in range(reps):
+            op.apply(vec)
+        N.check(N.lib.psk_synchronize(), "sync")
+        return (time.perf_counter() - t4) * 1e3 / reps
+
+    # per level: smoother sweep operator (S^-1) time and schedule; coarse solve time
+    per = []
+    for k in range(1, args.levels):
+        op = M._S[k].operator
+        vk = psk.DeviceVector.from_numpy(np.random.default_rng(k).standard_normal(M.levels()[k]))
+        e = dict(level=k, n=M.levels()[k], op_ms=timed(op, vk))
+        if args.smoother == "gs":
+            e.update(op.schedule("U"), dep_levels=op.device_info()["levels_u"])
+        per.append(e)
+    v0 = psk.DeviceVector.from_numpy(np.random.default_rng(0).standard_normal(M.levels()[0]))
+    co = M._coarse
+    per.append(dict(level=0, n=M.levels()[0], coarse_solve_ms=timed(co, v0), L=co.schedule("L"), U=co.schedule("U"),
+                    dep_levels=[co.device_info()["levels_l"], co.device_info()["levels_u"]],
+                    nnz=[co.device_info()["nnz_l"], co.device_info()["nnz_u"]]))
+    out["per_level"] = per
     out["setup_s"] = time.time() - t
     sol = psk.DeviceVector(n)
 
