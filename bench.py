@@ -46,7 +46,7 @@ def spmv_bytes(n, nnz):
 
 def pcg_iter_bytes(n, nnz, jacobi=True):
     """Compulsory bytes of one PCG iteration in libpsk's 3-launch schedule."""
-    return spmv_bytes(n, nnz) + (88 if jacobi else 72) * n
+    return spmv_bytes(n, nnz) + (80 if jacobi else 64) * n
 
 
 def cpu_baseline(m, iters):

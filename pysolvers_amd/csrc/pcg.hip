@@ -2,10 +2,12 @@
 //
 // Per iteration k three launches, no host synchronisation:
 //   K1  Ap = A p  and per-workgroup partials of p.Ap              (spmv.hip, kSpmvDot)   :111,:113
-//   K2  alpha = uDotR/pTAp; x += alpha p; r -= alpha Ap; u = M^-1 r; partials of r.r and u.r
+//   K2  alpha = uDotR/pTAp; r -= alpha Ap; u = M^-1 r; partials of r.r and u.r
 //                                                                    :114-125,:134
-//   K3  ||r|| test (tau*||b||, or k==maxiter-1 when !failOnMaxiter); beta; p = u + beta p
-//                                                                    :125-138
+//   K3  x += alpha p (alpha recomputed from K1's partials); ||r|| test (tau*||b||, or
+//       k==maxiter-1 when !failOnMaxiter); beta; p = u + beta p       :121,:125-138
+// x is updated in K3 rather than K2 because K3 streams p anyway: that saves one read of p (8n
+// bytes per iteration). x depends on nothing else in the iteration, so the order is invisible.
 // Every consumer workgroup re-reduces the producer's <=2048 partials in the same fixed order, so
 // all workgroups (and all ranks) see bit-identical scalars and take identical branches; the
 // control state (done flag, iteration count, residual) lives in HBM and the host only polls it
@@ -26,7 +28,8 @@ struct PcgState {
     double resid;
     double normB;
     double tauNormB;
-    double pad[3];
+    int64_t live;      // k of the last K2 that ran to completion (no breakdown); -1 before the loop
+    double pad[2];
 };
 
 // ---- K0: r = b; p = M r; x = 0; partials [b.b, u.r] ----------------------------------------
@@ -68,6 +71,7 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
         st->iters = 0;
         st->resid = 0.0;
         st->brk_kind = 0;
+        st->live = -1;
         udr[0] = ur;
         if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
             st->done = 1;
@@ -82,14 +86,14 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
     }
 }
 
-// ---- K2: x, r update + partials [r.r, u.r] -------------------------------------------------
+// ---- K2: r update + partials [r.r, u.r] ---------------------------------------------------
 // JAC: Jacobi preconditioner fused (dinv != nullptr). A template, not a runtime test: a branch in the
 // loop body makes the compiler drain vmcnt (stores included) at every join.
 template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
-    int64_t n, double *__restrict__ x, double *__restrict__ r, const double *__restrict__ p,
-    const double *__restrict__ Ap, const double *__restrict__ dinv, const double *__restrict__ part1,
-    int np, double *__restrict__ part2, PcgState *st, const double *__restrict__ udr, int64_t k) {
+    int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv,
+    const double *__restrict__ part1, int np, double *__restrict__ part2, PcgState *st,
+    const double *__restrict__ udr, int64_t k) {
     if (st->done) return;
     __shared__ double sh[kWaves];
     const double pTAp = reduce_partials(part1, np, 1, sh);   // np.dot(p, Ap)  :113
@@ -102,28 +106,27 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         return;
     }
     const double alpha = udr[k] / pTAp;                      // :118
+    // K3 (x update) runs iff this K2 did: it tests `live`, written by the previous kernel, never its
+    // own done flag, which its first workgroup may set while later ones are still starting
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
     int64_t t0, t1;
     block_range((n + kVecTile - 1) / kVecTile, t0, t1);
     const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     double rr = 0.0, ur = 0.0;
     int64_t i = i0 + 2 * threadIdx.x;
-    // cache policy: x and Ap are dead after this kernel (non-temporal); r and p are re-read by K3.
-    // Software pipeline: the next tile's five loads are issued before this tile's two stores, so the
-    // wait for this tile's operands is a static vmcnt that never includes a store acknowledgement.
+    // cache policy: Ap is dead after this kernel (non-temporal); r is re-read by K3.
+    // Software pipeline: the next tile's loads are issued before this tile's store, so the wait for
+    // this tile's operands is a static vmcnt that never includes a store acknowledgement.
     struct Ops {
-        dv2 x, p, r, a, d;
+        dv2 r, a, d;
     } A{}, B{};
     auto load = [&](Ops &o, int64_t j) {
-        o.x = ld2nt(x + j);
-        o.p = ld2(p + j);
         o.r = ld2(r + j);
         o.a = ld2nt(Ap + j);
         if (JAC) o.d = ld2(dinv + j);
     };
     auto step = [&](const Ops &o, int64_t j) {
-        dv2 xn, rn;
-        xn.x = o.x.x + alpha * o.p.x;                        // x = x + alpha*p   :121
-        xn.y = o.x.y + alpha * o.p.y;
+        dv2 rn;
         rn.x = o.r.x - alpha * o.a.x;                        // r = r - alpha*Ap  :122
         rn.y = o.r.y - alpha * o.a.y;
         double u0 = rn.x, u1 = rn.y;
@@ -131,7 +134,6 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
             u0 = o.d.x * rn.x;                               // u = precond.applyRight(r)  :123
             u1 = o.d.y * rn.y;
         }
-        st2nt(x + j, xn);
         st2(r + j, rn);
         rr = fma(rn.x, rn.x, rr);
         rr = fma(rn.y, rn.y, rr);
@@ -155,10 +157,8 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         }
     }
     if (i < i1) {   // odd tail element
-        const double xn = x[i] + alpha * p[i];
         const double rn = r[i] - alpha * Ap[i];
         const double u0 = JAC ? dinv[i] * rn : rn;
-        x[i] = xn;
         r[i] = rn;
         rr = fma(rn, rn, rr);
         ur = fma(u0, rn, ur);
@@ -171,40 +171,61 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     }
 }
 
-// ---- K3: convergence test, beta, p = u + beta p ------------------------------------------------
-template <bool JAC>
-__global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
-    int64_t n, const double *__restrict__ r, double *__restrict__ p, const double *__restrict__ dinv,
-    const double *__restrict__ part2, int np, PcgState *st, double *__restrict__ udr,
-    double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
-    if (st->done) return;
-    __shared__ double sh[kWaves];
-    const double rr = reduce_partials(part2, np, 2, sh);
-    const double ur = reduce_partials(part2 + 1, np, 2, sh);
+// K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
+// (K2's expression on the same partials), the convergence test, beta. Returns false when the
+// solve stopped at this iteration; x (which K3 owns) is then still advanced over [i0, i1).
+__device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
+                                             const double *__restrict__ part1, int np1, double rr, double ur,
+                                             PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
+                                             int64_t k, int64_t maxiter, int fail_on_maxiter, double *sh,
+                                             double &alpha, double &beta, int64_t &i0, int64_t &i1) {
+    alpha = udr[k] / reduce_partials(part1, np1, 1, sh);     // :118
+    int64_t t0, t1;
+    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
+    i0 = t0 * kVecTile;
+    i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
     if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+        for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) x[i] = x[i] + alpha * p[i];   // :121
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
             st->resid = normR;
             st->done = 1;
         }
-        return;
+        return false;
     }
-    const double beta = ur / udr[k];                         // :134-135
+    beta = ur / udr[k];                                      // :134-135
     if (blockIdx.x == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    return true;
+}
+
+// ---- K3: x += alpha p, convergence test, beta, p = u + beta p ---------------------------------
+template <bool JAC>
+__global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
+    int64_t n, double *__restrict__ x, const double *__restrict__ r, double *__restrict__ p,
+    const double *__restrict__ dinv, const double *__restrict__ part1, int np1, const double *__restrict__ part2,
+    int np, PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter,
+    int fail_on_maxiter) {
+    if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
+    __shared__ double sh[kWaves];
+    const double rr = reduce_partials(part2, np, 2, sh);
+    const double ur = reduce_partials(part2 + 1, np, 2, sh);
+    double alpha, beta;
+    int64_t i0, i1;
+    if (!pcg_direction_scalars(n, x, p, part1, np1, rr, ur, st, udr, hist, k, maxiter, fail_on_maxiter, sh, alpha,
+                               beta, i0, i1))
+        return;
     int64_t i = i0 + 2 * threadIdx.x;
-    // r and dinv are not needed again this iteration (non-temporal); p is gathered by the next SpMV.
-    // Same software pipeline as pcg_update_kernel (next loads issued before this store).
+    // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next
+    // SpMV. Same software pipeline as pcg_update_kernel (next loads issued before these stores).
     struct Ops {
-        dv2 r, p, d;
+        dv2 r, p, d, x;
     } A{}, B{};
     auto load = [&](Ops &o, int64_t j) {
         o.r = ld2nt(r + j);
         o.p = ld2(p + j);
+        o.x = ld2nt(x + j);
         if (JAC) o.d = ld2nt(dinv + j);
     };
     auto step = [&](const Ops &o, int64_t j) {
@@ -213,9 +234,12 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
             u0 = o.d.x * o.r.x;
             u1 = o.d.y * o.r.y;
         }
-        dv2 pn;
+        dv2 pn, xn;
+        xn.x = o.x.x + alpha * o.p.x;                        // x = x + alpha*p  :121
+        xn.y = o.x.y + alpha * o.p.y;
         pn.x = u0 + beta * o.p.x;                            // p = u + beta*p  :138
         pn.y = u1 + beta * o.p.y;
+        st2nt(x + j, xn);
         st2(p + j, pn);
     };
     auto nxt = [&](int64_t j) { return (j + kVecTile + 1 < i1) ? j + kVecTile : j; };
@@ -234,7 +258,9 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     }
     if (i < i1) {
         const double u0 = JAC ? dinv[i] * r[i] : r[i];
-        p[i] = u0 + beta * p[i];
+        const double pi = p[i];
+        x[i] = x[i] + alpha * pi;
+        p[i] = u0 + beta * pi;
     }
 }
 
@@ -287,29 +313,24 @@ __global__ __launch_bounds__(kBlock) void pcg_dot_kernel(int64_t n, const double
 }
 
 __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
-    int64_t n, const double *__restrict__ u, double *__restrict__ p, const double *__restrict__ part2, int np2,
+    int64_t n, double *__restrict__ x, const double *__restrict__ u, double *__restrict__ p,
+    const double *__restrict__ part1, int np1, const double *__restrict__ part2, int np2,
     const double *__restrict__ part3, int np3, PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
     int64_t k, int64_t maxiter, int fail_on_maxiter) {
-    if (st->done) return;
+    if (st->live != k) return;
     __shared__ double sh[kWaves];
     const double rr = reduce_partials(part2, np2, 2, sh);
     const double ur = reduce_partials(part3, np3, 1, sh);
-    const double normR = sqrt(rr);                           // :125
-    if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;
-    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
-            st->iters = k + 1;
-            st->resid = normR;
-            st->done = 1;
-        }
+    double alpha, beta;
+    int64_t i0, i1;
+    if (!pcg_direction_scalars(n, x, p, part1, np1, rr, ur, st, udr, hist, k, maxiter, fail_on_maxiter, sh, alpha,
+                               beta, i0, i1))
         return;
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
+        const double pi = p[i];
+        x[i] = x[i] + alpha * pi;                            // :121
+        p[i] = u[i] + beta * pi;                             // :138
     }
-    const double beta = ur / udr[k];                         // :134-135
-    if (blockIdx.x == 0 && threadIdx.x == 0) udr[k + 1] = ur;
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) p[i] = u[i] + beta * p[i];   // :138
 }
 
 // -------------------------------------------------------------------------------------------------
@@ -465,24 +486,26 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         if (sharded && (rc = allreduce_sum(A, w.part1, np1, s)) != PSK_OK) break;
         if (dinv)
-            hipLaunchKernelGGL(pcg_update_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap, dinv,
-                               w.part1, np1, w.part2, w.st, w.udr, k);
+            hipLaunchKernelGGL(pcg_update_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1,
+                               np1, w.part2, w.st, w.udr, k);
         else
-            hipLaunchKernelGGL(pcg_update_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, w.Ap,
-                               dinv, w.part1, np1, w.part2, w.st, w.udr, k);
+            hipLaunchKernelGGL(pcg_update_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1,
+                               np1, w.part2, w.st, w.udr, k);
         if (sharded && (rc = allreduce_sum(A, w.part2, 2 * np2, s)) != PSK_OK) break;
         if (gen) {
             if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
             hipLaunchKernelGGL(pcg_dot_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.u, w.r, w.part3, w.st);
-            hipLaunchKernelGGL(pcg_gen_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.u, w.p, w.part2, np2,
-                               w.part3, gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+            hipLaunchKernelGGL(pcg_gen_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, np1,
+                               w.part2, np2, w.part3, gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         } else {
             if (dinv)
-                hipLaunchKernelGGL(pcg_direction_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv,
-                                   w.part2, np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+                hipLaunchKernelGGL(pcg_direction_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
+                                   w.part1, np1, w.part2, np2, w.st, w.udr, w.hist, k, maxiter,
+                                   ctl->fail_on_maxiter);
             else
-                hipLaunchKernelGGL(pcg_direction_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.p, dinv,
-                                   w.part2, np2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+                hipLaunchKernelGGL(pcg_direction_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
+                                   w.part1, np1, w.part2, np2, w.st, w.udr, w.hist, k, maxiter,
+                                   ctl->fail_on_maxiter);
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;
