@@ -102,9 +102,8 @@ static int amg_smooth(const AmgHierarchy *h, const Context *c, int lev, const do
     psk_csr *A = h->A[lev];
     const int64_t n = A->n;
     double *r = h->r[lev].as<double>(), *t = h->t[lev].as<double>();
-    const int g = spmv_grid(c, A);
     for (int it = 0; it < nu; ++it) {
-        PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, g, s));
+        PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, s));
         PSK_TRY(prec_apply_dev(h->S[lev], n, r, t, s));
         hipLaunchKernelGGL(amg_add_kernel, vgrid(n), dim3(kBlock), 0, s, n, x, t);
         PSK_HIP(hipGetLastError());
@@ -119,14 +118,14 @@ static int amg_level(const AmgHierarchy *h, const Context *c, int lev, const dou
     psk_csr *A = h->A[lev];
     PSK_TRY(amg_smooth(h, c, lev, f, x, h->nu_pre, s));                         // :41
     double *r = h->r[lev].as<double>();
-    PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, spmv_grid(c, A), s));   // :44
+    PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, s));   // :44
     double *f2 = h->f[lev - 1].as<double>(), *x2 = h->x[lev - 1].as<double>();
     psk_csr *R = h->R[lev - 1], *P = h->P[lev - 1];
-    PSK_TRY(launch_spmv(R, kSpmvPlain, r, f2, nullptr, nullptr, nullptr, nullptr, spmv_grid(c, R), s));   // :47
+    PSK_TRY(launch_spmv(R, kSpmvPlain, r, f2, nullptr, nullptr, nullptr, nullptr, s));   // :47
     if (lev - 1 > 0 && h->A[lev - 1]->n > 0)
         PSK_HIP(hipMemsetAsync(x2, 0, (size_t)h->A[lev - 1]->n * sizeof(double), s));   // zeros_like (:50)
     PSK_TRY(amg_level(h, c, lev - 1, f2, x2, s));                                  // :51
-    PSK_TRY(launch_spmv(P, kSpmvAdd, x2, x, nullptr, x, nullptr, nullptr, spmv_grid(c, P), s));   // :54
+    PSK_TRY(launch_spmv(P, kSpmvAdd, x2, x, nullptr, x, nullptr, nullptr, s));   // :54
     return amg_smooth(h, c, lev, f, x, h->nu_post, s);                            // :59
 }
 
@@ -142,7 +141,7 @@ int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     double *scal = h->scal.as<double>();
     int64_t *flag = reinterpret_cast<int64_t *>(scal + 1);
     double *part = scal + 2;
-    const int gv = grid_for_rows(c, n, kVecTile), ga = spmv_grid(c, A);
+    const int gv = grid_for_rows(c, n, kVecTile), ga = 1;   // the residual SpMV's sum: in-launch
     hipLaunchKernelGGL(amg_sqnorm_partial_kernel, dim3(gv), dim3(kBlock), 0, s, n, v, part);
     PSK_HIP(hipGetLastError());
     hipLaunchKernelGGL(amg_init_kernel, dim3(1), dim3(kBlock), 0, s, part, gv, scal, flag);
@@ -151,7 +150,7 @@ int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     for (int k = 0; k < h->num_iters; ++k) {
         PSK_TRY(amg_level(h, c, top, v, x, s));                                            // runCycle (:79)
         if (k + 1 < h->num_iters) {
-            PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, v, part, nullptr, ga, s));   // r = b - A x (:82)
+            PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, v, part, nullptr, s));   // r = b - A x (:82)
             hipLaunchKernelGGL(amg_check_kernel, dim3(1), dim3(kBlock), 0, s, part, ga, scal, h->tau, flag);
             PSK_HIP(hipGetLastError());
             hipLaunchKernelGGL(amg_copy_if_kernel, vgrid(n), dim3(kBlock), 0, s, n, flag, (int64_t)1, x, out);

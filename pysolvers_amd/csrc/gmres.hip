@@ -246,7 +246,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     if (K < 1) K = 1;
     const int ld = (int)(K + 1);
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
-    const int gs = spmv_grid(c, A);
+    const int gs = 1;   // partials of a dot-mode SpMV: it finishes its sum in-launch (gridsum)
     const int gv = grid_for_rows(c, n, kVecTile);
     const size_t vec = aup((size_t)n * 8);
     const size_t qbytes = vec * (size_t)(K + 1);
@@ -348,7 +348,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             hipLaunchKernelGGL(gm_start_kernel, dim3(gv), dim3(kBlock), 0, s, n, bv, Q, pa, gv, g, ld, st,
                                ctl->tau, 1);
         } else {
-            if ((rc = launch_spmv(A, kSpmvResid, x, u, nullptr, bv, pa, nullptr, gs, s)) != PSK_OK) break;
+            if ((rc = launch_spmv(A, kSpmvResid, x, u, nullptr, bv, pa, nullptr, s)) != PSK_OK) break;
             ++spmv_count;
             hipLaunchKernelGGL(gm_start_kernel, dim3(gv), dim3(kBlock), 0, s, n, u, Q, pa, gs, g, ld, st,
                                ctl->tau, 0);
@@ -385,9 +385,9 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             const double *q0 = Q;
             if (gen) {   // u = A (M^-1 q_k): materialise M^-1 q_k (GMRESSolver.py:107)
                 if ((rc = prec_apply_dev(M, n, qk, w, s)) != PSK_OK) break;
-                if ((rc = launch_spmv(A, kSpmvPlainDot, w, u, nullptr, q0, pa, &st->done, gs, s)) != PSK_OK) break;
+                if ((rc = launch_spmv(A, kSpmvPlainDot, w, u, nullptr, q0, pa, &st->done, s)) != PSK_OK) break;
             } else if ((rc = launch_spmv(A, dinv ? kSpmvJacobiDot : kSpmvPlainDot, qk, u, dinv, q0, pa, &st->done,
-                                         gs, s)) != PSK_OK)
+                                         s)) != PSK_OK)
                 break;
             ++spmv_count;
             double *pin = pa, *pout = pb;
@@ -413,7 +413,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             // converged at step kc: x = M^-1 Q y, true residual (:159-174)
             const int kc = hs.kconv;
             if ((rc = run_finalize(kc, it > 0)) != PSK_OK) break;
-            if ((rc = launch_spmv(A, kSpmvResid, x, u, nullptr, bv, pa, nullptr, gs, s)) != PSK_OK) break;
+            if ((rc = launch_spmv(A, kSpmvResid, x, u, nullptr, bv, pa, nullptr, s)) != PSK_OK) break;
             ++spmv_count;
             hipLaunchKernelGGL(gm_true_resid_kernel, dim3(1), dim3(kBlock), 0, s, pa, gs, st);
             if (hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess ||

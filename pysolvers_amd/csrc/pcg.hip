@@ -1,21 +1,22 @@
 // pcg.hip — device-resident preconditioned CG (PCGSolver.solve, PCGSolver.py:64-142).
 //
 // Per iteration k three launches, no host synchronisation:
-//   K1  Ap = A p  and per-workgroup partials of p.Ap              (spmv.hip, kSpmvDot)   :111,:113
-//   K2  alpha = uDotR/pTAp; r -= alpha Ap; u = M^-1 r; partials of r.r and u.r
-//                                                                    :114-125,:134
-//   K3  x += alpha p (alpha recomputed from K1's partials); ||r|| test (tau*||b||, or
+//   K1  Ap = A p  and p.Ap                                         (spmv.hip, kSpmvDot)   :111,:113
+//   K2  alpha = uDotR/pTAp; r -= alpha Ap; u = M^-1 r; r.r and u.r   :114-125,:134
+//   K3  x += alpha p (alpha recomputed from K1's sum); ||r|| test (tau*||b||, or
 //       k==maxiter-1 when !failOnMaxiter); beta; p = u + beta p       :121,:125-138
 // x is updated in K3 rather than K2 because K3 streams p anyway: that saves one read of p (8n
 // bytes per iteration). x depends on nothing else in the iteration, so the order is invisible.
-// Every consumer workgroup re-reduces the producer's <=2048 partials in the same fixed order, so
-// all workgroups (and all ranks) see bit-identical scalars and take identical branches; the
+// All three are one-shot launches (one tile per workgroup); K1 and K2 finish their dot products in
+// the same launch with a fixed reduction order (gridsum, psk_internal.hpp), so every workgroup
+// (and every rank, after the RCCL sum) reads bit-identical scalars and takes identical branches; the
 // control state (done flag, iteration count, residual) lives in HBM and the host only polls it
 // every `check_every` iterations with a lag, keeping the launch queue full.
 // u is never stored: K2 and K3 both recompute u_i = DInv_i * r_i (one rounding, as np.multiply).
 // Elementwise updates use two roundings (-ffp-contract=off), exactly as numpy's x + alpha*p.
 #include "psk_internal.hpp"
 
+#include <climits>
 #include <cmath>
 #include <cstdio>
 
@@ -86,17 +87,16 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
     }
 }
 
-// ---- K2: r update + partials [r.r, u.r] ---------------------------------------------------
-// JAC: Jacobi preconditioner fused (dinv != nullptr). A template, not a runtime test: a branch in the
-// loop body makes the compiler drain vmcnt (stores included) at every join.
+// ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
+// One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses). JAC: Jacobi
+// preconditioner fused (dinv != nullptr).
 template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv,
-    const double *__restrict__ part1, int np, double *__restrict__ part2, PcgState *st,
-    const double *__restrict__ udr, int64_t k) {
+    const double *__restrict__ pap, GridSum gs, PcgState *st, const double *__restrict__ udr, int64_t k) {
     if (st->done) return;
     __shared__ double sh[kWaves];
-    const double pTAp = reduce_partials(part1, np, 1, sh);   // np.dot(p, Ap)  :113
+    const double pTAp = *pap;                                // np.dot(p, Ap)  :113 (K1's grid sum)
     if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
@@ -109,85 +109,50 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     // K3 (x update) runs iff this K2 did: it tests `live`, written by the previous kernel, never its
     // own done flag, which its first workgroup may set while later ones are still starting
     if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
     double rr = 0.0, ur = 0.0;
-    int64_t i = i0 + 2 * threadIdx.x;
-    // cache policy: Ap is dead after this kernel (non-temporal); r is re-read by K3.
-    // Software pipeline: the next tile's loads are issued before this tile's store, so the wait for
-    // this tile's operands is a static vmcnt that never includes a store acknowledgement.
-    struct Ops {
-        dv2 r, a, d;
-    } A{}, B{};
-    auto load = [&](Ops &o, int64_t j) {
-        o.r = ld2(r + j);
-        o.a = ld2nt(Ap + j);
-        if (JAC) o.d = ld2(dinv + j);
-    };
-    auto step = [&](const Ops &o, int64_t j) {
+    // cache policy: Ap is dead after this kernel (non-temporal); r and dinv are re-read by K3
+    if (i + 1 < n) {
+        const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
+        dv2 d{};
+        if (JAC) d = ld2(dinv + i);
         dv2 rn;
-        rn.x = o.r.x - alpha * o.a.x;                        // r = r - alpha*Ap  :122
-        rn.y = o.r.y - alpha * o.a.y;
+        rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
+        rn.y = ro.y - alpha * a.y;
         double u0 = rn.x, u1 = rn.y;
         if (JAC) {
-            u0 = o.d.x * rn.x;                               // u = precond.applyRight(r)  :123
-            u1 = o.d.y * rn.y;
+            u0 = d.x * rn.x;                                 // u = precond.applyRight(r)  :123
+            u1 = d.y * rn.y;
         }
-        st2(r + j, rn);
+        st2(r + i, rn);
         rr = fma(rn.x, rn.x, rr);
         rr = fma(rn.y, rn.y, rr);
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
-    };
-    // ping-pong register sets (no copies between them): the next tile's loads are in flight while
-    // this tile is computed and stored; clamped indices keep the load count static
-    auto nxt = [&](int64_t j) { return (j + kVecTile + 1 < i1) ? j + kVecTile : j; };
-    if (i + 1 < i1) {
-        load(A, i);
-        while (true) {
-            load(B, nxt(i));
-            step(A, i);
-            i += kVecTile;
-            if (!(i + 1 < i1)) break;
-            load(A, nxt(i));
-            step(B, i);
-            i += kVecTile;
-            if (!(i + 1 < i1)) break;
-        }
-    }
-    if (i < i1) {   // odd tail element
+    } else if (i < n) {   // odd tail element
         const double rn = r[i] - alpha * Ap[i];
         const double u0 = JAC ? dinv[i] * rn : rn;
         r[i] = rn;
-        rr = fma(rn, rn, rr);
-        ur = fma(u0, rn, ur);
+        rr = rn * rn;
+        ur = u0 * rn;
     }
-    const double s0 = block_sum(rr, sh);
-    const double s1 = block_sum(ur, sh);
-    if (threadIdx.x == 0) {
-        part2[2 * blockIdx.x] = s0;
-        part2[2 * blockIdx.x + 1] = s1;
-    }
+    const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
+    gridsum_publish<2>(gs, v, sh);
 }
 
 // K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
 // (K2's expression on the same partials), the convergence test, beta. Returns false when the
 // solve stopped at this iteration; x (which K3 owns) is then still advanced over [i0, i1).
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
-                                             const double *__restrict__ part1, int np1, double rr, double ur,
-                                             PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
-                                             int64_t k, int64_t maxiter, int fail_on_maxiter, double *sh,
-                                             double &alpha, double &beta, int64_t &i0, int64_t &i1) {
-    alpha = udr[k] / reduce_partials(part1, np1, 1, sh);     // :118
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    i0 = t0 * kVecTile;
-    i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+                                             const double *__restrict__ pap, double rr, double ur, PcgState *st,
+                                             double *__restrict__ udr, double *__restrict__ hist, int64_t k,
+                                             int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta) {
+    alpha = udr[k] / *pap;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
     if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
-        for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) x[i] = x[i] + alpha * p[i];   // :121
+        const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+        for (int64_t j = i; j < i + 2 && j < n; ++j) x[j] = x[j] + alpha * p[j];   // :121
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
             st->resid = normR;
@@ -200,63 +165,36 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
     return true;
 }
 
-// ---- K3: x += alpha p, convergence test, beta, p = u + beta p ---------------------------------
+// ---- K3: x += alpha p, convergence test, beta, p = u + beta p (one-shot, as K2) -------------
 template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ r, double *__restrict__ p,
-    const double *__restrict__ dinv, const double *__restrict__ part1, int np1, const double *__restrict__ part2,
-    int np, PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter,
-    int fail_on_maxiter) {
+    const double *__restrict__ dinv, const double *__restrict__ pap, const double *__restrict__ rrur, PcgState *st,
+    double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
-    __shared__ double sh[kWaves];
-    const double rr = reduce_partials(part2, np, 2, sh);
-    const double ur = reduce_partials(part2 + 1, np, 2, sh);
     double alpha, beta;
-    int64_t i0, i1;
-    if (!pcg_direction_scalars(n, x, p, part1, np1, rr, ur, st, udr, hist, k, maxiter, fail_on_maxiter, sh, alpha,
-                               beta, i0, i1))
+    if (!pcg_direction_scalars(n, x, p, pap, rrur[0], rrur[1], st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+                               beta))
         return;
-    int64_t i = i0 + 2 * threadIdx.x;
-    // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next
-    // SpMV. Same software pipeline as pcg_update_kernel (next loads issued before these stores).
-    struct Ops {
-        dv2 r, p, d, x;
-    } A{}, B{};
-    auto load = [&](Ops &o, int64_t j) {
-        o.r = ld2nt(r + j);
-        o.p = ld2(p + j);
-        o.x = ld2nt(x + j);
-        if (JAC) o.d = ld2nt(dinv + j);
-    };
-    auto step = [&](const Ops &o, int64_t j) {
-        double u0 = o.r.x, u1 = o.r.y;
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
+    if (i + 1 < n) {
+        const dv2 ro = ld2nt(r + i), po = ld2(p + i), xo = ld2nt(x + i);
+        dv2 d{};
+        if (JAC) d = ld2nt(dinv + i);
+        double u0 = ro.x, u1 = ro.y;
         if (JAC) {
-            u0 = o.d.x * o.r.x;
-            u1 = o.d.y * o.r.y;
+            u0 = d.x * ro.x;
+            u1 = d.y * ro.y;
         }
         dv2 pn, xn;
-        xn.x = o.x.x + alpha * o.p.x;                        // x = x + alpha*p  :121
-        xn.y = o.x.y + alpha * o.p.y;
-        pn.x = u0 + beta * o.p.x;                            // p = u + beta*p  :138
-        pn.y = u1 + beta * o.p.y;
-        st2nt(x + j, xn);
-        st2(p + j, pn);
-    };
-    auto nxt = [&](int64_t j) { return (j + kVecTile + 1 < i1) ? j + kVecTile : j; };
-    if (i + 1 < i1) {
-        load(A, i);
-        while (true) {
-            load(B, nxt(i));
-            step(A, i);
-            i += kVecTile;
-            if (!(i + 1 < i1)) break;
-            load(A, nxt(i));
-            step(B, i);
-            i += kVecTile;
-            if (!(i + 1 < i1)) break;
-        }
-    }
-    if (i < i1) {
+        xn.x = xo.x + alpha * po.x;                          // x = x + alpha*p  :121
+        xn.y = xo.y + alpha * po.y;
+        pn.x = u0 + beta * po.x;                             // p = u + beta*p  :138
+        pn.y = u1 + beta * po.y;
+        st2nt(x + i, xn);
+        st2(p + i, pn);
+    } else if (i < n) {
         const double u0 = JAC ? dinv[i] * r[i] : r[i];
         const double pi = p[i];
         x[i] = x[i] + alpha * pi;
@@ -299,37 +237,32 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_init2_kernel(int64_t n, const 
 }
 
 __global__ __launch_bounds__(kBlock) void pcg_dot_kernel(int64_t n, const double *__restrict__ a,
-                                                         const double *__restrict__ c, double *__restrict__ part,
+                                                         const double *__restrict__ c, GridSum gs,
                                                          const PcgState *st) {
     if (st->done) return;
     __shared__ double sh[kWaves];
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + threadIdx.x;
     double acc = 0.0;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) acc = fma(a[i], c[i], acc);   // np.dot(u, r) :134
-    const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) part[blockIdx.x] = s;
+    if (i < n) acc = a[i] * c[i];                                               // np.dot(u, r) :134
+    if (i + kBlock < n) acc = fma(a[i + kBlock], c[i + kBlock], acc);
+    const double v = block_sum(acc, sh);
+    gridsum_publish<1>(gs, &v, sh);
 }
 
 __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ u, double *__restrict__ p,
-    const double *__restrict__ part1, int np1, const double *__restrict__ part2, int np2,
-    const double *__restrict__ part3, int np3, PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
-    int64_t k, int64_t maxiter, int fail_on_maxiter) {
+    const double *__restrict__ pap, const double *__restrict__ rrur, const double *__restrict__ ur_gen, PcgState *st,
+    double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
     if (st->live != k) return;
-    __shared__ double sh[kWaves];
-    const double rr = reduce_partials(part2, np2, 2, sh);
-    const double ur = reduce_partials(part3, np3, 1, sh);
     double alpha, beta;
-    int64_t i0, i1;
-    if (!pcg_direction_scalars(n, x, p, part1, np1, rr, ur, st, udr, hist, k, maxiter, fail_on_maxiter, sh, alpha,
-                               beta, i0, i1))
+    if (!pcg_direction_scalars(n, x, p, pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+                               beta))
         return;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
-        const double pi = p[i];
-        x[i] = x[i] + alpha * pi;                            // :121
-        p[i] = u[i] + beta * pi;                             // :138
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    for (int64_t j = i; j < i + 2 && j < n; ++j) {
+        const double pj = p[j];
+        x[j] = x[j] + alpha * pj;                            // :121
+        p[j] = u[j] + beta * pj;                             // :138
     }
 }
 
@@ -398,16 +331,19 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     PcgWork w;
     PSK_TRY(pcg_workspace(A, maxiter, gen, w));
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
-    const int gs = spmv_grid(c, A);   // SpMV grid
-    const int gv = grid_for_rows(c, n, kVecTile);    // elementwise grid
-    // Sharded: every rank all-reduces (and re-reduces) the same kMaxGrid-long, zero-padded partial
-    // arrays, whatever its own grid sizes are, so RCCL counts match across ranks.
+    const int gv = grid_for_rows(c, n, kVecTile);    // persistent grid of the init kernels
+    // one-shot grid of K2/K3 (one 512-element tile per workgroup); K1/K2 finish their dot products
+    // in-launch (gridsum), so the loop's scalars are part1[0] = p.Ap and part2[0..1] = (r.r, u.r)
+    const int64_t nv = n > 0 ? (n + kVecTile - 1) / kVecTile : 1;
+    if (nv > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: vector too long for a one-shot grid");
+    GridSum gs2, gs3;
+    PSK_TRY(gridsum_prepare(c, nv, 2, w.part2, &gs2));
+    PSK_TRY(gridsum_prepare(c, nv, 1, w.part3, &gs3));
+    // Sharded: the init partials are all-reduced as zero-padded kMaxGrid-long arrays (same RCCL
+    // count on every rank whatever its grid); the loop's grid sums as 1 and 2 values.
     const bool sharded = A->comm != nullptr;
-    const int np1 = sharded ? kMaxGrid : gs, np2 = sharded ? kMaxGrid : gv;
-    if (sharded) {
-        PSK_HIP(hipMemsetAsync(w.part1, 0, kMaxGrid * sizeof(double), s));
-        PSK_HIP(hipMemsetAsync(w.part2, 0, 2 * kMaxGrid * sizeof(double), s));
-    }
+    const int npi = sharded ? kMaxGrid : gv;
+    if (sharded) PSK_HIP(hipMemsetAsync(w.part2, 0, 2 * kMaxGrid * sizeof(double), s));
 
     hipEvent_t ev0, ev1;
     PSK_HIP(hipEventCreate(&ev0));
@@ -424,8 +360,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
     }
     PSK_HIP(hipGetLastError());
-    if (sharded) PSK_TRY(allreduce_sum(A, w.part2, 2 * np2, s));
-    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, np2, ctl->tau, w.st, w.udr);
+    if (sharded) PSK_TRY(allreduce_sum(A, w.part2, 2 * npi, s));
+    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, npi, ctl->tau, w.st, w.udr);
     PSK_HIP(hipGetLastError());
 
     // polling ring: flag copies every C iterations, host waits on the copy L chunks back
@@ -481,31 +417,30 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
             if (hipEventRecord(ta[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         }
-        if ((rc = launch_spmv(A, kSpmvDot, w.p, w.Ap, nullptr, nullptr, w.part1, &w.st->done, gs, s)) != PSK_OK)
+        if ((rc = launch_spmv(A, kSpmvDot, w.p, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s)) != PSK_OK)
             break;
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
-        if (sharded && (rc = allreduce_sum(A, w.part1, np1, s)) != PSK_OK) break;
+        if (sharded && (rc = allreduce_sum(A, w.part1, 1, s)) != PSK_OK) break;
+        const dim3 gk((unsigned)nv);
         if (dinv)
-            hipLaunchKernelGGL(pcg_update_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1,
-                               np1, w.part2, w.st, w.udr, k);
+            hipLaunchKernelGGL(pcg_update_kernel<true>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1, gs2,
+                               w.st, w.udr, k);
         else
-            hipLaunchKernelGGL(pcg_update_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1,
-                               np1, w.part2, w.st, w.udr, k);
-        if (sharded && (rc = allreduce_sum(A, w.part2, 2 * np2, s)) != PSK_OK) break;
+            hipLaunchKernelGGL(pcg_update_kernel<false>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1, gs2,
+                               w.st, w.udr, k);
+        if (sharded && (rc = allreduce_sum(A, w.part2, 2, s)) != PSK_OK) break;
         if (gen) {
             if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
-            hipLaunchKernelGGL(pcg_dot_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.u, w.r, w.part3, w.st);
-            hipLaunchKernelGGL(pcg_gen_direction_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, np1,
-                               w.part2, np2, w.part3, gv, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+            hipLaunchKernelGGL(pcg_dot_kernel, gk, dim3(kBlock), 0, s, n, w.u, w.r, gs3, w.st);
+            hipLaunchKernelGGL(pcg_gen_direction_kernel, gk, dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, w.part2,
+                               w.part3, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         } else {
             if (dinv)
-                hipLaunchKernelGGL(pcg_direction_kernel<true>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
-                                   w.part1, np1, w.part2, np2, w.st, w.udr, w.hist, k, maxiter,
-                                   ctl->fail_on_maxiter);
+                hipLaunchKernelGGL(pcg_direction_kernel<true>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
+                                   w.part1, w.part2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
             else
-                hipLaunchKernelGGL(pcg_direction_kernel<false>, dim3(gv), dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
-                                   w.part1, np1, w.part2, np2, w.st, w.udr, w.hist, k, maxiter,
-                                   ctl->fail_on_maxiter);
+                hipLaunchKernelGGL(pcg_direction_kernel<false>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
+                                   w.part1, w.part2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;
@@ -516,6 +451,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         rc = fail(PSK_ERR_HIP, "state copy");
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg sync");
     if (rc == PSK_OK && gen) rc = prec_check_error(M, s);
+    if (rc == PSK_OK) rc = gridsum_check(c);
     if (rc == PSK_OK && ctl->time_kernels)
         for (int i = 0; i < TP && rc == PSK_OK; ++i) rc = harvest(i);
     if (rc == PSK_OK) {

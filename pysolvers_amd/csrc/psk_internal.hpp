@@ -54,6 +54,13 @@ struct Context {
     hipStream_t stream = nullptr;
     int num_cus = 256;
     int grid_cap = kMaxGrid;
+    // gridsum slots (below): one armed array per stream, grow-only; outgrown arrays are kept until
+    // exit because queued launches may still use them
+    uint64_t *gs_slots = nullptr;
+    int64_t gs_cap = 0;
+    uint64_t *gs_gslots = nullptr;   // kMaxGrid * kGridSumMaxW
+    std::vector<uint64_t *> gs_retired;
+    int32_t *gs_err = nullptr;
 };
 int ctx(Context **out);   // current device's context (created lazily)
 
@@ -182,6 +189,140 @@ __device__ __forceinline__ double reduce_partials(const double *part, int np, in
     return block_sum(v, sh);
 }
 
+// ---------------------------------------------------------------------------------------------
+// One-shot launches and their deterministic grid reduction ("gridsum").
+//
+// The streaming kernels (SpMV, PCG K2/K3) run ONE TILE PER WORKGROUP, grid = tiles: workgroups are
+// dispatched in id order, so the chip sweeps a compact window of every stream and no workgroup
+// carries loop state (tools/spmv_lab.hip / tools/stream_lab.hip at n = 268M: SpMV +5%, the K2
+// access shape +7% over persistent grids; SpMV +7-10% at n = 10-17M).
+// Their dot products are finished inside the same launch, deterministically, without data atomics
+// and without making the consumers re-reduce per-workgroup partials (at 5*10^5 workgroups that
+// re-reduction alone would cost more than the stream):
+//  1. workgroup b publishes its W partials with agent-scope 8-byte stores into slots armed with a
+//     signalling-NaN sentinel (value-is-flag);
+//  2. the partials of group g (grp ~ sqrt(nwg) consecutive workgroups) are summed in a
+//     fixed order by ONE reducer workgroup — the one kGridSumLag ids after the group's last member,
+//     or that last member itself when the lagged id is past the grid — and published the same way;
+//  3. the grid's last workgroup sums the group sums in a fixed order into out[0..W).
+// Every reader re-arms what it read. A workgroup only waits for LOWER ids, which were dispatched
+// before it and only wait for lower ids themselves, so every wait ends; with the lag above the
+// resident capacity (2048 workgroups) step 2 almost never waits. grp == 1 skips step 2.
+constexpr int64_t kGridSumLag = 4096;
+constexpr uint64_t kGridSumSentinel = 0x7FF0000000000001ull;   // sNaN: arithmetic never produces it
+constexpr int kGridSumMaxW = 4;
+
+struct GridSum {
+    uint64_t *slots;    // nwg*W workgroup partials (grp > 1)
+    uint64_t *gslots;   // ngroups*W group sums
+    double *out;        // the W grid sums
+    int64_t grp;        // workgroups per group
+    int32_t *err;       // set when a bounded wait expires (reported by gridsum_check)
+};
+
+// grp ~ sqrt(nwg): the launch's tail waits for one group reduction (grp/256 loads per lane) and
+// the final one (ngroups/256), so both are kept short; ngroups <= kMaxGrid
+inline int64_t gridsum_grp(int64_t nwg) {
+    if (nwg <= kBlock) return 1;
+    int64_t g = 1;
+    while (g * g < nwg) ++g;
+    const int64_t gmin = (nwg + kMaxGrid - 1) / kMaxGrid;
+    return g > gmin ? g : gmin;
+}
+
+__device__ __forceinline__ void gridsum_put(uint64_t *sl, double v) {
+    __hip_atomic_store(sl, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// waits for a published value (bounded: ~10 ms, never expected; reported by gridsum_check, result
+// poisoned; once the flag is up no later wait spins, so a broken launch still drains quickly)
+__device__ __forceinline__ uint64_t gridsum_wait(const uint64_t *sl, int32_t *err) {
+    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return 0x7FF8000000000000ull;
+    uint64_t bits;
+    int spins = 0;
+    while ((bits = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kGridSumSentinel) {
+        if (++spins > (1 << 18)) {
+            atomicOr(err, 1);
+            return 0x7FF8000000000000ull;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return bits;
+}
+
+// sum of src[j*W + c] for j in [j0, j1): lane-strided (lane t sums j0+t, j0+t+256, ... in order),
+// then block_sum — a fixed order for fixed bounds. The loads of a lane are issued together and
+// only the (rare) ones still holding the sentinel are waited on; every slot is re-armed.
+template <int W>
+__device__ __forceinline__ void gridsum_take_range(uint64_t *src, int64_t j0, int64_t j1, int32_t *err,
+                                                   double *sh, double *res) {
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+        // optimistic pass: independent loads (the compiler overlaps them), summed in order; a
+        // sentinel seen anywhere (rare) redoes the lane's sum in the same order with waits
+        double a = 0.0;
+        bool ok = true;
+#pragma unroll 4
+        for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
+            const uint64_t v = __hip_atomic_load(src + j * W + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && v != kGridSumSentinel;
+            a += __longlong_as_double((long long)v);
+        }
+        if (!ok) {
+            a = 0.0;
+            for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock)
+                a += __longlong_as_double((long long)gridsum_wait(src + j * W + c, err));
+        }
+        for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock)
+            src[j * W + c] = kGridSumSentinel;   // re-arm; ordered before the next launch by the boundary
+        res[c] = block_sum(a, sh);
+    }
+}
+
+// Called by every thread of every workgroup of a one-shot launch with the workgroup's W sums
+// (identical in all threads, e.g. from block_sum). Kernel-uniform control flow (barriers inside).
+template <int W>
+__device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double *v, double *sh) {
+    const int64_t b = blockIdx.x, nwg = gridDim.x, grp = gs.grp;
+    const int64_t ngroups = (nwg + grp - 1) / grp;
+    double r[W];
+    if (grp == 1) {
+        if (threadIdx.x == 0)
+#pragma unroll
+            for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + b * W + c, v[c]);
+    } else {
+        if (threadIdx.x == 0)
+#pragma unroll
+            for (int c = 0; c < W; ++c) gridsum_put(gs.slots + b * W + c, v[c]);
+        const int64_t t = b - (grp - 1) - kGridSumLag;   // lagged role: group t/grp
+        if (t >= 0 && t % grp == 0) {
+            const int64_t g = t / grp;
+            gridsum_take_range<W>(gs.slots, g * grp, g * grp + grp, gs.err, sh, r);
+            if (threadIdx.x == 0)
+#pragma unroll
+                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
+        }
+        const int64_t g = b / grp, lastm = (g * grp + grp - 1 < nwg) ? g * grp + grp - 1 : nwg - 1;
+        if (b == lastm && g * grp + grp - 1 + kGridSumLag >= nwg) {   // own-group role
+            gridsum_take_range<W>(gs.slots, g * grp, lastm + 1, gs.err, sh, r);
+            if (threadIdx.x == 0)
+#pragma unroll
+                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
+        }
+    }
+    if (b == nwg - 1) {   // final role
+        gridsum_take_range<W>(gs.gslots, 0, ngroups, gs.err, sh, r);
+        if (threadIdx.x == 0)
+#pragma unroll
+            for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+    }
+}
+
+// host: a GridSum for a one-shot launch of nwg workgroups with W (<= kGridSumMaxW) sums, written
+// to out[0..W)
+int gridsum_prepare(Context *c, int64_t nwg, int W, double *out, GridSum *gs);
+// reports (and clears) an expired gridsum wait; syncs the stream
+int gridsum_check(Context *c);
+
 // 16-byte vector accesses; *_nt = non-temporal (streamed data that is not re-read soon)
 typedef double dv2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ dv2 ld2(const double *p) { return *reinterpret_cast<const dv2 *>(p); }
@@ -236,9 +377,8 @@ inline bool prec_is_general(const psk_prec *M) {
 // reports a bounded-spin timeout of any triangular solve inside M (syncs the stream)
 int prec_check_error(const psk_prec *M, hipStream_t s);
 int tile_rows_for(int64_t n, int64_t nnz);
-int spmv_grid(const Context *c, const psk_csr *A);
+// one-shot SpMV (grid = tiles of A->tile_rows rows); dot modes write their grid sum to partial[0]
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
-                const double *aux_q, double *partial, const int32_t *done_flag, int grid,
-                hipStream_t s);
+                const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s);
 
 }  // namespace psk

@@ -67,6 +67,56 @@ void DevBuf::release() {
     bytes = 0;
 }
 
+__global__ void gridsum_arm_kernel(uint64_t *slots, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) slots[i] = kGridSumSentinel;
+}
+
+static int gridsum_arm(uint64_t **p, int64_t count, hipStream_t s) {
+    PSK_HIP(hipMalloc(p, (size_t)count * sizeof(uint64_t)));
+    hipLaunchKernelGGL(gridsum_arm_kernel, dim3((unsigned)((count + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, *p,
+                       count);
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
+int gridsum_prepare(Context *c, int64_t nwg, int W, double *out, GridSum *gs) {
+    if (W < 1 || W > kGridSumMaxW || nwg < 1) return fail(PSK_ERR_ARG, "gridsum_prepare: bad geometry");
+    if (!c->gs_err) {
+        PSK_HIP(hipMalloc(&c->gs_err, sizeof(int32_t)));
+        PSK_HIP(hipMemsetAsync(c->gs_err, 0, sizeof(int32_t), c->stream));
+        PSK_TRY(gridsum_arm(&c->gs_gslots, (int64_t)kMaxGrid * kGridSumMaxW, c->stream));
+    }
+    gs->out = out;
+    gs->grp = gridsum_grp(nwg);
+    gs->err = c->gs_err;
+    gs->gslots = c->gs_gslots;
+    gs->slots = nullptr;
+    if (gs->grp == 1) return PSK_OK;
+    const int64_t need = nwg * W;
+    if (need > c->gs_cap) {
+        int64_t cap = c->gs_cap > 0 ? c->gs_cap : (int64_t)1 << 20;
+        while (cap < need) cap *= 2;
+        uint64_t *p = nullptr;
+        PSK_TRY(gridsum_arm(&p, cap, c->stream));
+        if (c->gs_slots) c->gs_retired.push_back(c->gs_slots);
+        c->gs_slots = p;
+        c->gs_cap = cap;
+    }
+    gs->slots = c->gs_slots;
+    return PSK_OK;
+}
+
+int gridsum_check(Context *c) {
+    if (!c->gs_err) return PSK_OK;
+    int32_t h = 0;
+    PSK_HIP(hipMemcpyAsync(&h, c->gs_err, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    if (h == 0) return PSK_OK;
+    PSK_HIP(hipMemsetAsync(c->gs_err, 0, sizeof(int32_t), c->stream));
+    return fail(PSK_ERR_HIP, "grid reduction: a partial sum was never published (bounded wait expired)");
+}
+
 int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s) {
     if (n <= 0) return PSK_OK;
     PSK_HIP(hipMemcpyAsync(dst, src, (size_t)n * sizeof(double),

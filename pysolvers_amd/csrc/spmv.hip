@@ -5,14 +5,14 @@
 // We reproduce that bit for bit: the products are staged through LDS (so no FMA can form) and each
 // row is summed sequentially by one lane in stored order, starting from 0.0.
 //
-// Layout/schedule (gfx950): a workgroup of 256 threads (4 waves) walks a contiguous range of
-// 256-row tiles. Per tile, the tile's nnz range [rowptr[r0], rowptr[r1]) is streamed in
-// 2048-entry chunks with fully coalesced loads of colidx (4 B/lane) and vals (8 B/lane), the x
-// gather is issued branch-free for up to 8 entries per lane (ILP), products land in a 16 KiB LDS
-// slab, and each lane then sums its own row from LDS. Rows longer than a chunk keep their running
-// sum across chunks, so ANY row length is exact. Optional epilogues fuse the dot products the
-// Krylov loops need next (p.Ap for PCG, q_0.u for GMRES, ||b-Ax||^2 for the true residual), each
-// reduced deterministically per workgroup into partial[blockIdx.x].
+// Layout/schedule (gfx950): one workgroup of 256 threads (4 waves) per tile of `trows` rows (256
+// for 5-point rows), grid = tiles (one-shot; see gridsum in psk_internal.hpp for why). The tile's
+// nnz range [rowptr[r0], rowptr[r1]) is streamed in 1280-entry chunks with fully coalesced
+// non-temporal loads of colidx (4 B/lane) and vals (8 B/lane), the x gather is issued branch-free
+// for 5 entries per lane, rounded products land in a 10 KiB LDS slab, and each lane then sums its
+// own row from LDS. Rows longer than a chunk keep their running sum across chunks, so ANY row
+// length is exact. Optional epilogues fuse the dot products the Krylov loops need next (p.Ap for
+// PCG, q_0.u for GMRES, ||b-Ax||^2 for the true residual), reduced deterministically by gridsum.
 #include "psk_internal.hpp"
 
 #include <climits>
@@ -31,134 +31,104 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(
     int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const double *__restrict__ vals, const double *__restrict__ x, double *__restrict__ y,
-    const double *__restrict__ aux_d, const double *__restrict__ aux_q, double *__restrict__ partial,
+    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs,
     const int32_t *__restrict__ done, int32_t nnz) {
     if (done != nullptr && *done != 0) return;
     constexpr int KU = kChunk / kBlock;   // staged entries per lane per chunk
     __shared__ double prod[kChunk + kBlock];   // + a dump row for lanes past the chunk's end
     __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
-    // tiles are dealt round-robin (tile = block + k*grid): the whole grid sweeps one compact window
-    // of rows at a time, so x entries gathered by rows i-m, i and i+m are fetched once and re-served
-    // from L2 / Infinity Cache (spmv_lab A3: +22% over contiguous per-block ranges at n = 268M)
-    const int64_t ntiles = (n + trows - 1) / trows;
-    const int64_t tstep = gridDim.x, t0 = blockIdx.x, t1 = ntiles;
+    const int64_t r0 = (int64_t)blockIdx.x * trows;
+    const int64_t r1 = (r0 + trows < n) ? r0 + trows : n;
     const int32_t last = nnz > 0 ? nnz - 1 : 0;   // colidx/vals hold at least one (dummy) entry
-    double acc = 0.0;
-
-    // The colidx/vals stream of the first chunk of tile t, clamped to valid indices. ALWAYS the same
-    // number of loads (an empty tile re-reads one valid entry): the compiler can then wait for this
-    // tile's gathers with a static vmcnt while the next tile's stream is still in flight.
-    int32_t cc[KU], ncc[KU];
-    double vv[KU], nvv[KU];
-    int32_t e0 = 0, e1 = 0;
-    auto issue = [&](int64_t t, int32_t &a, int32_t &b, int32_t *c_, double *v_) {
-        const int64_t r0 = t * trows, r1 = (r0 + trows < n) ? r0 + trows : n;
-        a = rowptr[r0];
-        b = rowptr[r1];
-        const int32_t c1 = (b - a > kChunk) ? a + kChunk : b;
-        const int32_t base = a < last ? a : last;
+    const int32_t e0 = rowptr[r0], e1 = rowptr[r1];
+    // the first chunk's colidx/vals stream, clamped to valid indices (an empty tile re-reads one
+    // valid entry), issued before anything else
+    int32_t cc[KU];
+    double vv[KU];
+    {
+        const int32_t c1 = (e1 - e0 > kChunk) ? e0 + kChunk : e1;
+        const int32_t base = e0 < last ? e0 : last;
 #pragma unroll
         for (int k = 0; k < KU; ++k) {
-            const int32_t e = a + k * kBlock + tid;
+            const int32_t e = e0 + k * kBlock + tid;
             const int32_t ee = e < c1 ? e : base;
-            c_[k] = ld_stream(colidx + ee);
-            v_[k] = ld_stream(vals + ee);
+            cc[k] = ld_stream(colidx + ee);
+            vv[k] = ld_stream(vals + ee);
         }
-    };
-    if (t0 < t1) issue(t0, e0, e1, cc, vv);
-
-    for (int64_t t = t0; t < t1; t += tstep) {
-        const int64_t r0 = t * trows;
-        const int64_t r1 = (r0 + trows < n) ? r0 + trows : n;
-        const int64_t row = r0 + tid;
-        const bool has = tid < trows && row < r1;
-        const int64_t rowc = has ? row : r0;   // a valid row for the unconditional epilogue loads
-        // row bounds and the epilogue operands, loaded BEFORE the prefetch so that waiting for them
-        // never waits for the next tile's stream
-        const int32_t rs = rowptr[rowc], re = rowptr[rowc + 1];
-        double eq = 0.0;
-        if (MODE == kSpmvDot) eq = x[rowc];
-        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
-            eq = aux_q[rowc];
-        const int32_t ce0 = e0, ce1 = e1;
-        double sum = 0.0;
-        // chunk 0 (its stream was issued one tile ago)
-        {
-            const int32_t c0 = ce0, c1 = (ce1 - c0 > kChunk) ? c0 + kChunk : ce1;
-            double xv[KU], pv[KU];
+    }
+    const int64_t row = r0 + tid;
+    const bool has = tid < trows && row < r1;
+    const int64_t rowc = has ? row : r0;   // a valid row for the unconditional epilogue loads
+    const int32_t rs = rowptr[rowc], re = rowptr[rowc + 1];
+    double eq = 0.0;
+    if (MODE == kSpmvDot) eq = x[rowc];
+    if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+        eq = aux_q[rowc];
+    double sum = 0.0;
+    {   // chunk 0
+        const int32_t c0 = e0, c1 = (e1 - c0 > kChunk) ? c0 + kChunk : e1;
+        double pv[KU];
 #pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                double xx = x[cc[k]];
-                if (MODE == kSpmvJacobiDot) xx = aux_d[cc[k]] * xx;   // (DInv*q)[c], rounded
-                xv[k] = xx;
-            }
-            // software pipeline: the next tile's stream is in flight while this tile's gathers land
-            const int64_t tn = (t + tstep < t1) ? t + tstep : t;
-            issue(tn, e0, e1, ncc, nvv);
-#pragma unroll
-            for (int k = 0; k < KU; ++k) pv[k] = vv[k] * xv[k];   // rounded product
-            // unconditional stores (lanes past the chunk write the dump row): a conditional store
-            // would let the compiler sink that lane's gather behind the prefetch and wait for both
-#pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                const int32_t e = c0 + k * kBlock + tid;
-                prod[(e < c1 ? k * kBlock : kChunk) + tid] = pv[k];
-            }
-            __syncthreads();
-            const int32_t a = rs > c0 ? rs : c0;
-            const int32_t bnd = re < c1 ? re : c1;
-            if (has)
-                for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
-            __syncthreads();
+        for (int k = 0; k < KU; ++k) {
+            double xx = x[cc[k]];
+            if (MODE == kSpmvJacobiDot) xx = aux_d[cc[k]] * xx;   // (DInv*q)[c], rounded
+            pv[k] = vv[k] * xx;                                   // rounded product
         }
-        // rare: tile longer than one chunk
-        for (int32_t c0 = ce0 + kChunk; c0 < ce1; c0 += kChunk) {
-            const int32_t c1 = (ce1 - c0 > kChunk) ? c0 + kChunk : ce1;
-            double pv[KU];
 #pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                const int32_t e = c0 + k * kBlock + tid;
-                const int32_t ee = e < c1 ? e : c0;
-                const int32_t c = ld_stream(colidx + ee);
-                double xx = x[c];
-                if (MODE == kSpmvJacobiDot) xx = aux_d[c] * xx;
-                pv[k] = ld_stream(vals + ee) * xx;
-            }
+        for (int k = 0; k < KU; ++k) {   // lanes past the chunk write the dump row
+            const int32_t e = c0 + k * kBlock + tid;
+            prod[(e < c1 ? k * kBlock : kChunk) + tid] = pv[k];
+        }
+        __syncthreads();
+        const int32_t a = rs > c0 ? rs : c0;
+        const int32_t bnd = re < c1 ? re : c1;
+        if (has)
+            for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];   // stored order
+        __syncthreads();
+    }
+    // rare: tile longer than one chunk
+    for (int32_t c0 = e0 + kChunk; c0 < e1; c0 += kChunk) {
+        const int32_t c1 = (e1 - c0 > kChunk) ? c0 + kChunk : e1;
+        double pv[KU];
 #pragma unroll
-            for (int k = 0; k < KU; ++k) {
-                const int32_t e = c0 + k * kBlock + tid;
-                if (e < c1) prod[k * kBlock + tid] = pv[k];
-            }
-            __syncthreads();
-            const int32_t a = rs > c0 ? rs : c0;
-            const int32_t bnd = re < c1 ? re : c1;
-            if (has)
-                for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];
-            __syncthreads();
+        for (int k = 0; k < KU; ++k) {
+            const int32_t e = c0 + k * kBlock + tid;
+            const int32_t ee = e < c1 ? e : c0;
+            const int32_t c = ld_stream(colidx + ee);
+            double xx = x[c];
+            if (MODE == kSpmvJacobiDot) xx = aux_d[c] * xx;
+            pv[k] = ld_stream(vals + ee) * xx;
         }
 #pragma unroll
         for (int k = 0; k < KU; ++k) {
-            cc[k] = ncc[k];
-            vv[k] = nvv[k];
+            const int32_t e = c0 + k * kBlock + tid;
+            if (e < c1) prod[k * kBlock + tid] = pv[k];
         }
-        if (has) {
-            if (MODE == kSpmvResid) {
-                const double r = eq - sum;   // b - A*x (GMRESSolver.py:163)
-                y[row] = r;
-                acc = fma(r, r, acc);
-            } else if (MODE == kSpmvAdd) {
-                y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
-            } else {
-                __builtin_nontemporal_store(sum, y + row);
-                if (MODE != kSpmvPlain) acc = fma(eq, sum, acc);   // x.(Ax) or q.(Ax)
-            }
+        __syncthreads();
+        const int32_t a = rs > c0 ? rs : c0;
+        const int32_t bnd = re < c1 ? re : c1;
+        if (has)
+            for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];
+        __syncthreads();
+    }
+    double acc = 0.0;
+    if (has) {
+        if (MODE == kSpmvResid) {
+            const double r = eq - sum;   // b - A*x (GMRESSolver.py:163)
+            y[row] = r;
+            acc = r * r;
+        } else if (MODE == kSpmvAdd) {
+            y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
+        } else {
+            __builtin_nontemporal_store(sum, y + row);
+            if (MODE != kSpmvPlain) acc = eq * sum;   // x.(Ax) or q.(Ax)
         }
     }
     // only the residual mode may be called without partials (AMG smoothing); kernel-uniform test
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || partial != nullptr)) {
-        const double s = block_sum(acc, sh);
-        if (tid == 0) partial[blockIdx.x] = s;
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) {
+        const double bs = block_sum(acc, sh);
+        gridsum_publish<1>(gs, &bs, sh);
     }
 }
 
@@ -170,54 +140,33 @@ int tile_rows_for(int64_t n, int64_t nnz) {
     return r;
 }
 
-int spmv_grid(const Context *c, const psk_csr *A) {
-    const int64_t tiles = (A->n + A->tile_rows - 1) / A->tile_rows;
-    static const int per_cu = [] {   // 3 workgroups per CU streamed best (bench sweep 2..8, r1)
-        const char *e = std::getenv("PSK_SPMV_WG_PER_CU");   // experiments only
-        const int v = e ? std::atoi(e) : 3;
-        return v >= 1 && v <= 8 ? v : 3;
-    }();
-    int cap = c->num_cus * per_cu;
-    cap -= cap % 8;
-    if (cap < 8) cap = 8;
-    if (cap > kMaxGrid) cap = kMaxGrid;
-    return (int)(tiles < cap ? (tiles < 1 ? 1 : tiles) : cap);
-}
+static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) / A->tile_rows; }
 
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
-                const double *aux_q, double *partial, const int32_t *done_flag, int grid,
-                hipStream_t s) {
+                const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s) {
     if (A->n == 0) return PSK_OK;
-    dim3 gd(grid), bd(kBlock);
+    Context *c;
+    PSK_TRY(ctx(&c));
+    const int64_t nwg = spmv_tiles(A);
+    GridSum gs{nullptr, nullptr, nullptr, 1, nullptr};
+    if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
+    dim3 gd((unsigned)nwg), bd(kBlock);
     const int tr = A->tile_rows;
+    const int32_t nz = (int32_t)A->nnz;
+#define PSK_SPMV_LAUNCH(M)                                                                                  \
+    hipLaunchKernelGGL(spmv_kernel<M>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals, x, y, aux_d, \
+                       aux_q, gs, done_flag, nz)
     switch (mode) {
-    case kSpmvPlain:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvPlain>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
-        break;
-    case kSpmvDot:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
-        break;
-    case kSpmvJacobiDot:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvJacobiDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
-                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
-        break;
-    case kSpmvPlainDot:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvPlainDot>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx,
-                           A->vals, x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
-        break;
-    case kSpmvResid:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvResid>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
-        break;
-    case kSpmvAdd:
-        hipLaunchKernelGGL(spmv_kernel<kSpmvAdd>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals,
-                           x, y, aux_d, aux_q, partial, done_flag, (int32_t)A->nnz);
-        break;
+    case kSpmvPlain: PSK_SPMV_LAUNCH(kSpmvPlain); break;
+    case kSpmvDot: PSK_SPMV_LAUNCH(kSpmvDot); break;
+    case kSpmvJacobiDot: PSK_SPMV_LAUNCH(kSpmvJacobiDot); break;
+    case kSpmvPlainDot: PSK_SPMV_LAUNCH(kSpmvPlainDot); break;
+    case kSpmvResid: PSK_SPMV_LAUNCH(kSpmvResid); break;
+    case kSpmvAdd: PSK_SPMV_LAUNCH(kSpmvAdd); break;
     default:
         return fail(PSK_ERR_ARG, "unknown spmv mode");
     }
+#undef PSK_SPMV_LAUNCH
     PSK_HIP(hipGetLastError());
     return PSK_OK;
 }
@@ -508,8 +457,7 @@ int psk_spmv(const psk_csr *Ac, const double *x, double *y, int32_t loc) {
         dx = tx;
         dy = (loc == PSK_HOST) ? tx + A->ncols : y;
     }
-    const int grid = spmv_grid(c, A);
-    PSK_TRY(launch_spmv(A, kSpmvPlain, dx, dy, nullptr, nullptr, nullptr, nullptr, grid, c->stream));
+    PSK_TRY(launch_spmv(A, kSpmvPlain, dx, dy, nullptr, nullptr, nullptr, nullptr, c->stream));
     if (loc == PSK_HOST) PSK_TRY(from_device_vec(dy, PSK_HOST, A->n, y, c->stream));
     PSK_HIP(hipStreamSynchronize(c->stream));
     tmp.release();
@@ -521,14 +469,13 @@ int psk_spmv_timed(const psk_csr *A, const double *x, double *y, int32_t reps, d
     if (A->comm) return fail(PSK_ERR_UNSUPPORTED, "psk_spmv_timed: sharded matrix");
     Context *c;
     PSK_TRY(ctx(&c));
-    const int grid = spmv_grid(c, A);
     hipEvent_t e0, e1;
     PSK_HIP(hipEventCreate(&e0));
     PSK_HIP(hipEventCreate(&e1));
-    int rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, grid, c->stream);   // warm
+    int rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, c->stream);   // warm
     if (rc == PSK_OK && hipEventRecord(e0, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
     for (int r = 0; r < reps && rc == PSK_OK; ++r)
-        rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, grid, c->stream);
+        rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, c->stream);
     if (rc == PSK_OK && hipEventRecord(e1, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
     float ms = 0.f;
     if (rc == PSK_OK && hipEventSynchronize(e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");

@@ -264,6 +264,37 @@ def test_fd4096_spmv_and_first_iterations(psk):
     assert np.linalg.norm(st.soln() - ref["soln"]) <= 1e-12 * np.linalg.norm(ref["soln"])
 
 
+# m chosen so the one-shot grids straddle the gridsum geometry (psk_internal.hpp): SpMV tiles
+# ceil(m^2/256) = 255 / 256 (one level) / 259 (groups) / 4727 (groups with lagged AND own-group
+# reducers); K2/K3 tiles ceil(m^2/512) likewise
+@pytest.mark.parametrize("m", [255, 256, 257, 363, 1100])
+def test_pcg_gridsum_geometries(psk, m):
+    from oracle import fdlap, krylov
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    dA = psk.DeviceCSR.from_scipy(A)
+    b = A @ np.random.default_rng(m).random(m * m)
+    ctl = _ctl(maxiter=12, tau=0.0, failOnMaxiter=False)
+    for prec, oprec in ((psk.Jacobi(), krylov.jacobi_form(A)), (None, krylov.identity_apply)):
+        kw = {"precond": prec} if prec is not None else {}
+        st = psk.PCG(control=ctl, **kw).makeSolver().solve(dA, b)
+        ref = krylov.pcg(A, b, maxiter=12, tau=0.0, fail_on_maxiter=False, precond=oprec)
+        assert st.iters() == ref["iters"] == 12
+        np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=RTOL_RESID)
+        assert np.linalg.norm(st.soln() - ref["soln"]) <= 1e-12 * np.linalg.norm(ref["soln"])
+
+
+def test_pcg_run_to_run_bitwise(psk):
+    """The in-launch reductions have a fixed order: two solves of the same system agree bit for bit."""
+    m = 1100
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    b = psk.mvmult(dA, np.random.default_rng(7).random(m * m))
+    ctl = _ctl(maxiter=50, tau=0.0, failOnMaxiter=False)
+    s1 = psk.PCG(control=ctl, precond=psk.Jacobi()).makeSolver().solve(dA, b)
+    s2 = psk.PCG(control=ctl, precond=psk.Jacobi()).makeSolver().solve(dA, b)
+    assert np.array_equal(s1.soln(), s2.soln())
+    assert np.array_equal(s1.info["hist"], s2.info["hist"])
+
+
 # ---------------------------------------------------------------------------------------------
 # ILUT apply (RightILUTPreconditioner.applyRight = SuperLU ILU.solve) on the device
 

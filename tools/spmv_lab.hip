@@ -265,6 +265,71 @@ __global__ __launch_bounds__(BS) void spmv_A5(int64_t n, const int* __restrict__
     }
 }
 
+// ---------------- O: one-shot — one 256-row tile per workgroup, grid = tiles (hardware dispatch
+// order instead of a persistent loop; many resident workgroups hide the latency chain) ------------
+template <int CH, int TPW = 1>
+__global__ __launch_bounds__(BS) void spmv_O(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
+                                             const double* __restrict__ va, const double* __restrict__ x,
+                                             double* __restrict__ y) {
+    constexpr int KU = CH / BS, TR = 256;
+    __shared__ double prod[CH + BS];
+    const int tid = threadIdx.x;
+    const int64_t nt = (n + TR - 1) / TR;
+    const int last = rp[n] - 1;
+    int cc[TPW][KU]; double vv[TPW][KU];
+    int e0[TPW], e1[TPW];
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        int64_t t = (int64_t)blockIdx.x * TPW + u;
+        t = t < nt ? t : nt - 1;
+        const int64_t r0 = t * TR, r1 = r0 + TR < n ? r0 + TR : n;
+        e0[u] = rp[r0]; e1[u] = rp[r1];
+        const int c1 = e1[u] - e0[u] > CH ? e0[u] + CH : e1[u];
+        const int base = e0[u] < last ? e0[u] : last;
+#pragma unroll
+        for (int k = 0; k < KU; ++k) { int e = e0[u] + k * BS + tid; int ee = e < c1 ? e : base;
+            cc[u][k] = __builtin_nontemporal_load(ci + ee); vv[u][k] = __builtin_nontemporal_load(va + ee); }
+    }
+#pragma unroll
+    for (int u = 0; u < TPW; ++u) {
+        const int64_t t = (int64_t)blockIdx.x * TPW + u;
+        if (t >= nt) break;
+        const int64_t r0 = t * TR, r1 = r0 + TR < n ? r0 + TR : n;
+        const int64_t row = r0 + tid;
+        const bool has = row < r1;
+        const int64_t rowc = has ? row : r0;
+        const int rs = rp[rowc], re = rp[rowc + 1];
+        double sum = 0.0;
+        const int ce0 = e0[u], ce1 = e1[u];
+        {
+            const int c0 = ce0, c1 = ce1 - c0 > CH ? c0 + CH : ce1;
+            double pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) pv[k] = vv[u][k] * x[cc[u][k]];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; prod[(e < c1 ? k * BS : CH) + tid] = pv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            if (has) for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            __syncthreads();
+        }
+        for (int c0 = ce0 + CH; c0 < ce1; c0 += CH) {
+            const int c1 = ce1 - c0 > CH ? c0 + CH : ce1;
+            double pv[KU];
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; int ee = e < c1 ? e : c0;
+                pv[k] = __builtin_nontemporal_load(va + ee) * x[__builtin_nontemporal_load(ci + ee)]; }
+#pragma unroll
+            for (int k = 0; k < KU; ++k) { int e = c0 + k * BS + tid; prod[(e < c1 ? k * BS : CH) + tid] = pv[k]; }
+            __syncthreads();
+            const int a = rs > c0 ? rs : c0, b = re < c1 ? re : c1;
+            if (has) for (int e = a; e < b; ++e) sum = sum + prod[e - c0];
+            __syncthreads();
+        }
+        if (has) __builtin_nontemporal_store(sum, y + row);
+    }
+}
+
 // ---------------- A4: 3-stage pipeline: stream(t+2) | gather(t+1) | sum(t), round-robin tiles -----------
 template <int CH>
 __global__ __launch_bounds__(BS) void spmv_A4(int64_t n, const int* __restrict__ rp, const int* __restrict__ ci,
@@ -656,13 +721,11 @@ int main(int argc, char** argv) {
         std::vector<V> vs = {
             {"A blk256/ch2048", spmv_A, 2048},
             {"A3 interleave g1024", spmv_A3<1280, 2>, 1024},
-            {"A5 g512", spmv_A5<1280>, 512},
-            {"A5 g640", spmv_A5<1280>, 640},
             {"A5 g768", spmv_A5<1280>, 768},
-            {"A5 g896", spmv_A5<1280>, 896},
-            {"A5 tr512 g512", spmv_A5<2560, 512>, 512},
-            {"A5 tr512 g768", spmv_A5<2560, 512>, 768},
-            {"A5 tr512 g1024", spmv_A5<2560, 512>, 1024},
+            {"O oneshot", spmv_O<1280, 1>, (int)((n + 255) / 256)},
+            {"O oneshot tpw2", spmv_O<1280, 2>, (int)((n + 511) / 512)},
+            {"O oneshot tpw4", spmv_O<1280, 4>, (int)((n + 1023) / 1024)},
+            {"A5 g1536", spmv_A5<1280>, 1536},
         };
         // reference result
         spmv_A<<<2048, BS>>>(n, rp, ci, va, x, yr);
