@@ -228,11 +228,29 @@ int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *c, psk_csr
  * (callable without a GPU; the CPU tests check the sharding plan with it). */
 int psk_fd2d_dist_plan(int64_t m, int32_t nranks, int32_t rank, int64_t *row_begin, int64_t *row_end,
                        int64_t *ncols, int64_t *halo_lo, int64_t *halo_hi);
-/* Row block [row_begin,row_end) of a global CSR given with GLOBAL column indices
- * (host arrays of the local rows only: rowptr[nloc+1] starting anywhere, colidx, vals). */
-int psk_csr_create_dist(int64_t n_global, int64_t row_begin, int64_t row_end,
-                        const int64_t *rowptr, const int32_t *colidx, const double *vals,
-                        psk_comm *c, psk_csr **out);
+/* General row-block sharding: rank c->rank's rows [row_starts[rank], row_starts[rank+1]) of a
+ * global n_global x n_global CSR (the row split of every rank in row_starts[nranks+1], 0 ..
+ * n_global). Host arrays of the local rows only, GLOBAL column indices: rowptr[nloc+1] may start
+ * anywhere (entry j of local row i is colidx[rowptr[i]-rowptr[0]+j']); stored order is kept.
+ * Local columns are [owned | halo], the halo being the distinct off-block columns in ascending
+ * global order (psk_csr_halo_cols). The pattern must be structurally symmetric across ranks (as
+ * any matrix PCG runs on): each rank sends a peer the owned rows that reference the peer's block,
+ * which is then exactly what the peer needs; under RCCL every rank checks this at creation and all
+ * of them return PSK_ERR_ARG otherwise. Halo sends that are not a contiguous row range are packed
+ * by one gather kernel before the grouped ncclSend/ncclRecv. Replaces: nothing in the reference
+ * (single-process); the solvers take such a matrix with rank-local b and x. */
+int psk_csr_create_dist(int64_t n_global, const int64_t *row_starts, const int64_t *rowptr,
+                        const int32_t *colidx, const double *vals, psk_comm *c, psk_csr **out);
+/* Global index of every halo column of a sharded matrix, in local column order (cols may be
+ * NULL to query the count). */
+int psk_csr_halo_cols(const psk_csr *A, int64_t *cols, int64_t *count);
+/* Halo plan of a sharded matrix, one entry per peer rank (ascending): what is sent to it and which
+ * segment of the halo it fills. Arrays may be NULL; *npeers <= nranks-1. */
+int psk_csr_halo_peers(const psk_csr *A, int32_t *ranks, int64_t *send_counts, int64_t *recv_counts,
+                       int64_t *recv_offsets, int32_t *npeers);
+/* Validation: the values halo_exchange sends, peer by peer, for the local vector x (device
+ * pointers; out holds sum(send_counts) doubles), packed by the same kernel. No communication. */
+int psk_csr_halo_pack(const psk_csr *A, const double *x, double *out);
 
 #ifdef __cplusplus
 }

@@ -3,9 +3,9 @@
 Row-block distributed restatement of PCG (PCGSolver.py:64-142) with the SAME sharding plan the
 device engine uses (psk_fd2d_dist_plan: whole grid lines per rank, local columns
 [owned | halo_lo | halo_hi]) and the same communication structure: one halo exchange of p per
-iteration with ranks r-1 / r+1, and sum-all-reduces of the local dot partials. Runs on CPU over a
-torch.distributed gloo group; tests/test_dist_gloo.py checks it against the serial oracle, which
-pins the plan, the local column remap and the exchange/reduction schedule on CPU.
+iteration with ranks r-1 / r+1, and rank-order sums of the gathered local dot products
+(allgather). Runs on CPU over a torch.distributed gloo group; tests/test_dist_gloo.py checks it
+against the serial oracle, which pins the plan, the local column remap and the exchange/reduction schedule on CPU.
 """
 import numpy as np
 import numpy.linalg as npla
@@ -32,10 +32,16 @@ def local_block(m, plan, a=-1.0, b=1.0):
 
 
 def _allreduce(dist, vals):
+    """Sum over ranks the way libpsk does it (dist.hip allgather): gather every rank's values, then
+    add them in rank order on every rank, so all ranks hold the same bits."""
     import torch
     t = torch.tensor(vals, dtype=torch.float64)
-    dist.all_reduce(t)
-    return t.numpy()
+    parts = [torch.empty_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(parts, t)
+    acc = parts[0].numpy().copy()
+    for q in parts[1:]:
+        acc = acc + q.numpy()
+    return acc
 
 
 def _halo(dist, p_ext, nloc, m, hlo, hhi, rank):
@@ -59,9 +65,68 @@ def _halo(dist, p_ext, nloc, m, hlo, hhi, rank):
 
 
 def dist_pcg(dist, m, Aloc, b, plan, maxiter, tau, fail_on_maxiter=True, jacobi=True):
+    """FD whole-grid-line shards (psk_csr_create_fd2d_dist)."""
     rank = dist.get_rank()
     rb, re, ncols, hlo, hhi = plan
     nloc = re - rb
+    return _pcg_core(dist, Aloc, b, nloc, ncols, lambda p: _halo(dist, p, nloc, m, hlo, hhi, rank),
+                     maxiter, tau, fail_on_maxiter, jacobi)
+
+
+def shard_plan(A, row_starts, rank):
+    """General row-block plan of psk_csr_create_dist (pysolvers_amd/csrc/dist.hip dist_plan):
+    local columns [owned | halo] with the halo = distinct off-block columns ascending; receive
+    from q = the halo segment q owns; send to q = the owned rows with an entry in q's block
+    (== what q receives from us when the pattern is structurally symmetric)."""
+    A = A.tocsr()
+    rs = np.asarray(row_starts, dtype=np.int64)
+    rb, re = int(rs[rank]), int(rs[rank + 1])
+    nloc = re - rb
+    e0, e1 = int(A.indptr[rb]), int(A.indptr[re])
+    cols = A.indices[e0:e1].astype(np.int64)
+    offm = (cols < rb) | (cols >= re)
+    halo = np.unique(cols[offm])
+    lcol = np.where(offm, nloc + np.searchsorted(halo, cols), cols - rb)
+    indptr = (A.indptr[rb:re + 1] - e0).astype(np.int64)
+    Aloc = sp.csr_matrix((A.data[e0:e1].copy(), lcol, indptr), shape=(nloc, nloc + halo.shape[0]))
+    Aloc.has_sorted_indices = False
+    owner_h = np.searchsorted(rs, halo, side="right") - 1
+    recv = {}
+    for q in np.unique(owner_h):
+        ks = np.nonzero(owner_h == q)[0]
+        recv[int(q)] = (int(ks[0]), int(ks.shape[0]))
+    rows = np.repeat(np.arange(nloc), np.diff(indptr))
+    owner_e = np.searchsorted(rs, cols, side="right") - 1
+    send = {}
+    for q in np.unique(owner_e[offm]):
+        send[int(q)] = np.unique(rows[offm & (owner_e == q)])
+    return dict(rb=rb, re=re, nloc=nloc, ncols=nloc + halo.shape[0], Aloc=Aloc, halo=halo, recv=recv, send=send)
+
+
+def _halo_general(dist, p_ext, plan):
+    import torch
+    reqs, bufs = [], []
+    for q in sorted(set(plan["send"]) | set(plan["recv"])):
+        if q in plan["send"]:
+            reqs.append(dist.isend(torch.from_numpy(np.ascontiguousarray(p_ext[plan["send"][q]])), q))
+        if q in plan["recv"]:
+            off, cnt = plan["recv"][q]
+            t = torch.empty(cnt, dtype=torch.float64)
+            reqs.append(dist.irecv(t, q))
+            bufs.append((plan["nloc"] + off, t))
+    for r in reqs:
+        r.wait()
+    for off, t in bufs:
+        p_ext[off:off + t.shape[0]] = t.numpy()
+
+
+def dist_pcg_general(dist, plan, b, maxiter, tau, fail_on_maxiter=True, jacobi=True):
+    """General shards (psk_csr_create_dist): same loop, halo lists from shard_plan."""
+    return _pcg_core(dist, plan["Aloc"], b, plan["nloc"], plan["ncols"], lambda p: _halo_general(dist, p, plan),
+                     maxiter, tau, fail_on_maxiter, jacobi)
+
+
+def _pcg_core(dist, Aloc, b, nloc, ncols, exchange, maxiter, tau, fail_on_maxiter, jacobi):
     dinv = np.reciprocal(Aloc[:, :nloc].diagonal()) if jacobi else None
     M = (lambda v: np.multiply(dinv, v)) if jacobi else (lambda v: v)
     hist = []
@@ -73,7 +138,7 @@ def dist_pcg(dist, m, Aloc, b, plan, maxiter, tau, fail_on_maxiter=True, jacobi=
     x = np.zeros_like(b)
     uDotR, = _allreduce(dist, [np.dot(p[:nloc], r)])
     for k in range(maxiter):
-        _halo(dist, p, nloc, m, hlo, hhi, rank)
+        exchange(p)
         Ap = Aloc @ p
         pTAp, = _allreduce(dist, [np.dot(p[:nloc], Ap)])
         alpha = uDotR / pTAp

@@ -81,7 +81,10 @@ SIGNATURES = {
     "psk_comm_init_dry": (ctypes.c_int, [I32, I32, PP]),
     "psk_csr_create_fd2d_dist": (ctypes.c_int, [F64, F64, I64, P, PP, ctypes.POINTER(I64),
                                                 ctypes.POINTER(I64)]),
-    "psk_csr_create_dist": (ctypes.c_int, [I64, I64, I64, P, P, P, P, PP]),
+    "psk_csr_create_dist": (ctypes.c_int, [I64, P, P, P, P, P, PP]),
+    "psk_csr_halo_cols": (ctypes.c_int, [P, P, ctypes.POINTER(I64)]),
+    "psk_csr_halo_peers": (ctypes.c_int, [P, P, P, P, P, ctypes.POINTER(I32)]),
+    "psk_csr_halo_pack": (ctypes.c_int, [P, P, P]),
     "psk_fd2d_dist_plan": (ctypes.c_int, [I64, I32, I32] + [ctypes.POINTER(I64)] * 5),
 }
 

@@ -3,26 +3,40 @@
 // No reference counterpart: PySolvers is single-process. The sharded PCG is the same loop as
 // pcg.hip; per iteration it adds (1) a halo exchange of the search direction p with the two
 // neighbouring ranks (grouped ncclSend/ncclRecv of one grid line each way for the 5-point FD
-// matrix: m doubles per side), and (2) two in-place ncclAllReduce(sum) of the per-workgroup dot
-// partials (p.Ap; then r.r and u.r fused). Every rank then re-reduces the summed partials in the
-// same fixed order, so all ranks hold bit-identical scalars and stop on the same iteration
-// without further communication.
+// matrix: m doubles per side), and (2) two ncclAllGather of the ranks' dot products (p.Ap; then
+// r.r and u.r fused). Every rank then sums the gathered values in rank order itself, so all ranks
+// hold bit-identical scalars and stop on the same iteration without further communication (an
+// all-reduce would leave the order of the rank sum to RCCL's algorithm choice).
 #include "psk_internal.hpp"
 
+#include <algorithm>
 #include <climits>
 #include <cmath>
 
 namespace psk {
 
+// sendbuf[k] = x[idx[k]]: the owned entries the peers need, packed peer by peer
+__global__ void halo_pack_kernel(int64_t count, const int32_t *__restrict__ idx, const double *__restrict__ x,
+                                 double *__restrict__ out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < count) out[k] = x[idx[k]];
+}
+
 int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
     if (!A->comm || A->peers.empty()) return PSK_OK;
     if (A->comm->dry) return PSK_OK;   // the caller supplied the halo entries
     ncclComm_t nc = A->comm->nccl;
+    double *sb = A->sendbuf.as<double>();
+    if (A->pack_count > 0) {
+        hipLaunchKernelGGL(halo_pack_kernel, dim3((unsigned)((A->pack_count + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           s, A->pack_count, A->pack_idx, x, sb);
+        PSK_HIP(hipGetLastError());
+    }
     PSK_RCCL(ncclGroupStart());
     for (const HaloPeer &p : A->peers) {
         if (p.send_count > 0) {
-            if (p.send_idx) return fail(PSK_ERR_UNSUPPORTED, "indexed halo sends not built");
-            PSK_RCCL(ncclSend(x + p.send_begin, (size_t)p.send_count, ncclDouble, p.rank, nc, s));
+            const double *src = p.send_idx ? sb + p.pack_off : x + p.send_begin;
+            PSK_RCCL(ncclSend(src, (size_t)p.send_count, ncclDouble, p.rank, nc, s));
         }
         if (p.recv_count > 0)
             PSK_RCCL(ncclRecv(x + A->n + p.recv_offset, (size_t)p.recv_count, ncclDouble, p.rank, nc, s));
@@ -31,10 +45,10 @@ int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
     return PSK_OK;
 }
 
-int allreduce_sum(psk_csr *A, double *buf, int64_t count, hipStream_t s) {
-    if (!A->comm || A->comm->nranks == 1) return PSK_OK;
+int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipStream_t s) {
+    if (!A->comm) return fail(PSK_ERR_ARG, "allgather on an unsharded matrix");
     if (A->comm->dry) return fail(PSK_ERR_UNSUPPORTED, "collective on a dry (RCCL-less) communicator");
-    PSK_RCCL(ncclAllReduce(buf, buf, (size_t)count, ncclDouble, ncclSum, A->comm->nccl, s));
+    PSK_RCCL(ncclAllGather(send, recv, (size_t)count, ncclDouble, A->comm->nccl, s));
     return PSK_OK;
 }
 
@@ -54,6 +68,143 @@ static int fd2d_plan(int64_t m, int P, int r, FdPlan &p) {
     p.halo_lo = l0 > 0 ? m : 0;
     p.halo_hi = l1 < m ? m : 0;
     p.ncols = p.nloc + p.halo_lo + p.halo_hi;
+    return PSK_OK;
+}
+
+
+// ---- general row-block sharding (psk_csr_create_dist) --------------------------------------
+// Host plan of rank r's block, rows [rs[r], rs[r+1]) of a global CSR:
+//  * local columns: owned c -> c - rb; every other referenced column -> nloc + its position in the
+//    ascending list of distinct off-block columns (the halo), which is therefore grouped by owner
+//    rank in rank order: the segment received from rank q is contiguous;
+//  * send to q: the owned rows that have an entry in q's block, ascending. For a structurally
+//    symmetric pattern that is exactly the list q receives from us (A[j][c] != 0 <=> A[c][j] != 0),
+//    so it is built without communication; under RCCL the lists are exchanged once at creation and
+//    compared (dist_verify), and every rank refuses a pattern that is not symmetric across ranks.
+struct DistPlan {
+    int64_t rb = 0, re = 0, nloc = 0;
+    std::vector<int32_t> lcol;                    // local column of every local entry
+    std::vector<int64_t> halo;                    // global ids of the halo columns (ascending)
+    std::vector<int64_t> recv_off, recv_cnt;      // per rank: halo segment it owns
+    std::vector<std::vector<int32_t>> send_rows;  // per rank: owned local rows it needs
+};
+
+static int owner_of(const int64_t *rs, int P, int64_t c) {
+    return (int)(std::upper_bound(rs, rs + P + 1, c) - rs) - 1;   // largest q with rs[q] <= c
+}
+
+static int dist_plan(int64_t n_global, const int64_t *rs, int P, int r, const int64_t *rowptr, const int32_t *colidx,
+                     DistPlan &pl) {
+    pl.rb = rs[r];
+    pl.re = rs[r + 1];
+    pl.nloc = pl.re - pl.rb;
+    const int64_t e0 = rowptr[0], nnz = rowptr[pl.nloc] - e0;
+    std::vector<int64_t> off;
+    for (int64_t j = 0; j < nnz; ++j) {
+        const int64_t c = colidx[j];
+        if (c < 0 || c >= n_global) return fail(PSK_ERR_ARG, "psk_csr_create_dist: column index out of range");
+        if (c < pl.rb || c >= pl.re) off.push_back(c);
+    }
+    std::sort(off.begin(), off.end());
+    off.erase(std::unique(off.begin(), off.end()), off.end());
+    pl.halo.swap(off);
+    if (pl.nloc + (int64_t)pl.halo.size() >= INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "local columns exceed int32");
+    pl.lcol.resize((size_t)nnz);
+    pl.recv_off.assign((size_t)P, 0);
+    pl.recv_cnt.assign((size_t)P, 0);
+    pl.send_rows.assign((size_t)P, {});
+    for (size_t k = 0; k < pl.halo.size(); ++k) {
+        const int q = owner_of(rs, P, pl.halo[k]);
+        if (pl.recv_cnt[(size_t)q] == 0) pl.recv_off[(size_t)q] = (int64_t)k;
+        ++pl.recv_cnt[(size_t)q];
+    }
+    for (int64_t i = 0; i < pl.nloc; ++i)
+        for (int64_t j = rowptr[i] - e0; j < rowptr[i + 1] - e0; ++j) {
+            const int64_t c = colidx[j];
+            if (c >= pl.rb && c < pl.re) {
+                pl.lcol[(size_t)j] = (int32_t)(c - pl.rb);
+                continue;
+            }
+            const int64_t k = std::lower_bound(pl.halo.begin(), pl.halo.end(), c) - pl.halo.begin();
+            pl.lcol[(size_t)j] = (int32_t)(pl.nloc + k);
+            std::vector<int32_t> &sr = pl.send_rows[(size_t)owner_of(rs, P, c)];
+            if (sr.empty() || sr.back() != (int32_t)i) sr.push_back((int32_t)i);
+        }
+    return PSK_OK;
+}
+
+// Creation-time check under RCCL (collective over all ranks, same verdict everywhere): the send
+// and receive counts agree pairwise, then each rank's send list equals what its peer expects.
+static int dist_verify(psk_comm *cm, const int64_t *rs, const DistPlan &pl) {
+    const int P = cm->nranks, r = cm->rank;
+    Context *c;
+    PSK_TRY(ctx(&c));
+    hipStream_t s = c->stream;
+    std::vector<int64_t> mine((size_t)2 * P);
+    for (int q = 0; q < P; ++q) {
+        mine[(size_t)q] = (int64_t)pl.send_rows[(size_t)q].size();
+        mine[(size_t)(P + q)] = pl.recv_cnt[(size_t)q];
+    }
+    int64_t total_recv = 0, total_send = 0;
+    for (int q = 0; q < P; ++q) {
+        total_send += mine[(size_t)q];
+        total_recv += mine[(size_t)(P + q)];
+    }
+    DevBuf d;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } release_d{d};
+    const size_t cnt_bytes = (size_t)2 * P * 8 * (P + 1);
+    PSK_TRY(d.ensure(cnt_bytes + (size_t)(total_send + total_recv + 2) * 8 + 8 * (size_t)P + 64));
+    int64_t *dmine = d.as<int64_t>(), *dall = dmine + 2 * P;
+    PSK_HIP(hipMemcpy(dmine, mine.data(), mine.size() * 8, hipMemcpyHostToDevice));
+    PSK_RCCL(ncclAllGather(dmine, dall, (size_t)2 * P, ncclInt64, cm->nccl, s));
+    std::vector<int64_t> all((size_t)2 * P * P);
+    PSK_HIP(hipMemcpyAsync(all.data(), dall, all.size() * 8, hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    for (int a = 0; a < P; ++a)
+        for (int b = 0; b < P; ++b)
+            if (a != b && all[(size_t)(2 * P * a + b)] != all[(size_t)(2 * P * b + P + a)])
+                return fail(PSK_ERR_ARG, "psk_csr_create_dist: halo counts disagree across ranks (pattern not "
+                                         "structurally symmetric)");
+    // exchange: send the global ids we receive from q; receive the ids q receives from us
+    int64_t *dneed = dall + 2 * P * P, *dgot = dneed + total_recv;
+    int32_t *dflag = reinterpret_cast<int32_t *>(dgot + total_send);
+    int32_t *dflags = dflag + 2;
+    if (total_recv > 0) PSK_HIP(hipMemcpy(dneed, pl.halo.data(), (size_t)total_recv * 8, hipMemcpyHostToDevice));
+    PSK_RCCL(ncclGroupStart());
+    int64_t so = 0;
+    for (int q = 0; q < P; ++q) {
+        if (pl.recv_cnt[(size_t)q] > 0)
+            PSK_RCCL(ncclSend(dneed + pl.recv_off[(size_t)q], (size_t)pl.recv_cnt[(size_t)q], ncclInt64, q, cm->nccl, s));
+        const int64_t ns = (int64_t)pl.send_rows[(size_t)q].size();
+        if (ns > 0) PSK_RCCL(ncclRecv(dgot + so, (size_t)ns, ncclInt64, q, cm->nccl, s));
+        so += ns;
+    }
+    PSK_RCCL(ncclGroupEnd());
+    std::vector<int64_t> got((size_t)total_send);
+    if (total_send > 0) PSK_HIP(hipMemcpyAsync(got.data(), dgot, got.size() * 8, hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    int32_t ok = 1;
+    so = 0;
+    for (int q = 0; q < P && ok; ++q)
+        for (int32_t i : pl.send_rows[(size_t)q])
+            if (got[(size_t)so++] != pl.rb + i) {
+                ok = 0;
+                break;
+            }
+    PSK_HIP(hipMemcpy(dflag, &ok, 4, hipMemcpyHostToDevice));
+    PSK_RCCL(ncclAllGather(dflag, dflags, 1, ncclInt32, cm->nccl, s));
+    std::vector<int32_t> oks((size_t)P);
+    PSK_HIP(hipMemcpyAsync(oks.data(), dflags, (size_t)P * 4, hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    for (int q = 0; q < P; ++q)
+        if (!oks[(size_t)q])
+            return fail(PSK_ERR_ARG, "psk_csr_create_dist: halo lists disagree across ranks (pattern not "
+                                     "structurally symmetric)");
+    (void)rs;
+    (void)r;
     return PSK_OK;
 }
 
@@ -183,15 +334,142 @@ int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *cm, psk_cs
         p.send_idx = nullptr;
         A->peers.push_back(p);
     }
+    if (lo)
+        for (int64_t j = rb - m; j < rb; ++j) A->halo_cols.push_back(j);
+    if (hi)
+        for (int64_t j = re; j < re + m; ++j) A->halo_cols.push_back(j);
     *out = A;
     if (row_begin) *row_begin = rb;
     if (row_end) *row_end = re;
     return PSK_OK;
 }
 
-int psk_csr_create_dist(int64_t, int64_t, int64_t, const int64_t *, const int32_t *, const double *,
-                        psk_comm *, psk_csr **) {
-    return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create_dist: general row-block sharding not built yet");
+int psk_csr_create_dist(int64_t n_global, const int64_t *row_starts, const int64_t *rowptr, const int32_t *colidx,
+                        const double *vals, psk_comm *cm, psk_csr **out) {
+    if (!cm || !out || !row_starts || !rowptr || n_global < 0)
+        return fail(PSK_ERR_ARG, "psk_csr_create_dist: bad arguments");
+    const int P = cm->nranks, r = cm->rank;
+    if (row_starts[0] != 0 || row_starts[P] != n_global)
+        return fail(PSK_ERR_ARG, "psk_csr_create_dist: row_starts must run from 0 to n_global");
+    for (int q = 0; q < P; ++q)
+        if (row_starts[q + 1] < row_starts[q]) return fail(PSK_ERR_ARG, "psk_csr_create_dist: row_starts not monotone");
+    if (n_global >= INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create_dist: int32 columns required");
+    const int64_t nloc = row_starts[r + 1] - row_starts[r];
+    for (int64_t i = 0; i < nloc; ++i)
+        if (rowptr[i + 1] < rowptr[i]) return fail(PSK_ERR_ARG, "psk_csr_create_dist: rowptr not monotone");
+    const int64_t nnz = rowptr[nloc] - rowptr[0];
+    if (nnz > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create_dist: local nnz exceeds int32");
+    if (nnz > 0 && (!colidx || !vals)) return fail(PSK_ERR_ARG, "psk_csr_create_dist: NULL entries");
+    DistPlan pl;
+    PSK_TRY(dist_plan(n_global, row_starts, P, r, rowptr, colidx, pl));
+    if (!cm->dry) PSK_TRY(dist_verify(cm, row_starts, pl));
+    Context *c;
+    PSK_TRY(ctx(&c));
+    psk_csr *A = new psk_csr();
+    A->n = nloc;
+    A->ncols = nloc + (int64_t)pl.halo.size();
+    A->nnz = nnz;
+    A->tile_rows = tile_rows_for(nloc, nnz);
+    A->n_global = n_global;
+    A->row_begin = pl.rb;
+    A->row_end = pl.re;
+    A->comm = cm;
+    A->device = c->device;
+    A->halo_cols = pl.halo;
+    std::vector<int32_t> rp32((size_t)nloc + 1);
+    for (int64_t i = 0; i <= nloc; ++i) rp32[(size_t)i] = (int32_t)(rowptr[i] - rowptr[0]);
+    std::vector<int32_t> pack;
+    for (int q = 0; q < P; ++q) {
+        const std::vector<int32_t> &sr = pl.send_rows[(size_t)q];
+        if (pl.recv_cnt[(size_t)q] == 0 && sr.empty()) continue;
+        HaloPeer p{};
+        p.rank = q;
+        p.recv_count = pl.recv_cnt[(size_t)q];
+        p.recv_offset = pl.recv_off[(size_t)q];
+        p.send_count = (int64_t)sr.size();
+        p.send_idx = nullptr;
+        p.send_begin = sr.empty() ? 0 : sr[0];
+        p.pack_off = 0;
+        const bool contiguous = sr.empty() || (int64_t)sr.back() - sr.front() + 1 == (int64_t)sr.size();
+        if (!contiguous) {
+            p.pack_off = (int64_t)pack.size();
+            pack.insert(pack.end(), sr.begin(), sr.end());
+            p.send_idx = reinterpret_cast<int32_t *>(1);   // resolved after the upload below
+        }
+        A->peers.push_back(p);
+    }
+    int rc = PSK_OK;
+    const size_t mn = nnz > 0 ? (size_t)nnz : 1;
+    if (hipMalloc(&A->rowptr, (size_t)(nloc + 1) * 4) != hipSuccess || hipMalloc(&A->colidx, mn * 4) != hipSuccess ||
+        hipMalloc(&A->vals, mn * 8) != hipSuccess)
+        rc = fail(PSK_ERR_ALLOC, "psk_csr_create_dist: alloc");
+    if (rc == PSK_OK && !pack.empty()) {
+        A->pack_count = (int64_t)pack.size();
+        if (hipMalloc(&A->pack_idx, pack.size() * 4) != hipSuccess) rc = fail(PSK_ERR_ALLOC, "halo pack alloc");
+        else if (hipMemcpy(A->pack_idx, pack.data(), pack.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            rc = fail(PSK_ERR_HIP, "halo pack upload");
+        if (rc == PSK_OK) rc = A->sendbuf.ensure(pack.size() * 8);
+        for (HaloPeer &p : A->peers)
+            if (p.send_idx) p.send_idx = A->pack_idx + p.pack_off;
+    } else {
+        for (HaloPeer &p : A->peers) p.send_idx = nullptr;
+    }
+    if (rc == PSK_OK && (hipMemcpy(A->rowptr, rp32.data(), rp32.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                         (nnz > 0 && hipMemcpy(A->colidx, pl.lcol.data(), (size_t)nnz * 4, hipMemcpyHostToDevice) !=
+                                         hipSuccess) ||
+                         (nnz > 0 && hipMemcpy(A->vals, vals, (size_t)nnz * 8, hipMemcpyHostToDevice) != hipSuccess) ||
+                         (nnz == 0 && (hipMemset(A->colidx, 0, 4) != hipSuccess || hipMemset(A->vals, 0, 8) != hipSuccess))))
+        rc = fail(PSK_ERR_HIP, "psk_csr_create_dist: upload");
+    if (rc != PSK_OK) {
+        psk_csr_destroy(A);
+        return rc;
+    }
+    *out = A;
+    return PSK_OK;
 }
+
+int psk_csr_halo_peers(const psk_csr *A, int32_t *ranks, int64_t *send_counts, int64_t *recv_counts,
+                       int64_t *recv_offsets, int32_t *npeers) {
+    if (!A || !npeers) return fail(PSK_ERR_ARG, "psk_csr_halo_peers: bad arguments");
+    *npeers = (int32_t)A->peers.size();
+    for (size_t k = 0; k < A->peers.size(); ++k) {
+        if (ranks) ranks[k] = A->peers[k].rank;
+        if (send_counts) send_counts[k] = A->peers[k].send_count;
+        if (recv_counts) recv_counts[k] = A->peers[k].recv_count;
+        if (recv_offsets) recv_offsets[k] = A->peers[k].recv_offset;
+    }
+    return PSK_OK;
+}
+
+int psk_csr_halo_pack(const psk_csr *Ac, const double *x, double *out) {
+    if (!Ac || !x || !out) return fail(PSK_ERR_ARG, "psk_csr_halo_pack: NULL argument");
+    psk_csr *A = const_cast<psk_csr *>(Ac);
+    Context *c;
+    PSK_TRY(ctx(&c));
+    hipStream_t s = c->stream;
+    if (A->pack_count > 0) {   // the exact kernel halo_exchange runs
+        hipLaunchKernelGGL(halo_pack_kernel, dim3((unsigned)((A->pack_count + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                           s, A->pack_count, A->pack_idx, x, A->sendbuf.as<double>());
+        PSK_HIP(hipGetLastError());
+    }
+    int64_t o = 0;
+    for (const HaloPeer &p : A->peers) {
+        if (p.send_count > 0) {
+            const double *src = p.send_idx ? A->sendbuf.as<double>() + p.pack_off : x + p.send_begin;
+            PSK_HIP(hipMemcpyAsync(out + o, src, (size_t)p.send_count * 8, hipMemcpyDeviceToDevice, s));
+        }
+        o += p.send_count;
+    }
+    PSK_HIP(hipStreamSynchronize(s));
+    return PSK_OK;
+}
+
+int psk_csr_halo_cols(const psk_csr *A, int64_t *cols, int64_t *count) {
+    if (!A || !count) return fail(PSK_ERR_ARG, "psk_csr_halo_cols: bad arguments");
+    *count = (int64_t)A->halo_cols.size();
+    if (cols) std::copy(A->halo_cols.begin(), A->halo_cols.end(), cols);
+    return PSK_OK;
+}
+
 
 }  // extern "C"

@@ -93,10 +93,11 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
 template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv,
-    const double *__restrict__ pap, GridSum gs, PcgState *st, const double *__restrict__ udr, int64_t k) {
+    const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st, const double *__restrict__ udr,
+    int64_t k) {
     if (st->done) return;
     __shared__ double sh[kWaves];
-    const double pTAp = *pap;                                // np.dot(p, Ap)  :113 (K1's grid sum)
+    const double pTAp = rank_sum(pap, nparts, 1, 0);         // np.dot(p, Ap)  :113 (K1's grid sum)
     if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
@@ -144,10 +145,10 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
 // (K2's expression on the same partials), the convergence test, beta. Returns false when the
 // solve stopped at this iteration; x (which K3 owns) is then still advanced over [i0, i1).
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
-                                             const double *__restrict__ pap, double rr, double ur, PcgState *st,
+                                             double pTAp, double rr, double ur, PcgState *st,
                                              double *__restrict__ udr, double *__restrict__ hist, int64_t k,
                                              int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta) {
-    alpha = udr[k] / *pap;                                   // :118
+    alpha = udr[k] / pTAp;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
     if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
@@ -169,11 +170,13 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
 template <bool JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ r, double *__restrict__ p,
-    const double *__restrict__ dinv, const double *__restrict__ pap, const double *__restrict__ rrur, PcgState *st,
-    double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
+    const double *__restrict__ dinv, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts,
+    PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter,
+    int fail_on_maxiter) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, p, pap, rrur[0], rrur[1], st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+    if (!pcg_direction_scalars(n, x, p, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
+                               rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
                                beta))
         return;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
@@ -255,7 +258,7 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
     double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
     if (st->live != k) return;
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, p, pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
                                beta))
         return;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
@@ -273,10 +276,13 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 
 struct PcgWork {
     double *x, *r, *p, *Ap, *u, *part1, *part2, *part3, *udr, *hist;
+    // sharded (P ranks): the ranks' gathered scalars, [P] p.Ap and [P][2] (r.r, u.r), and the
+    // gathered init partials [P][kMaxGrid][2]; unsharded: part1g/part2g alias part1/part2
+    double *part1g, *part2g, *initg;
     PcgState *st;
 };
 
-static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, PcgWork &w) {
+static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &w) {
     const size_t vec = align_up((size_t)A->n * 8, 256), vecc = align_up((size_t)A->ncols * 8, 256);
     const size_t big = (gen ? 4 : 3) * vec + vecc;
     PSK_TRY(A->ws.ensure(big > 0 ? big : 256));
@@ -289,7 +295,10 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, PcgWork &w) {
     const size_t small = align_up(sizeof(PcgState), 256) + 2 * align_up(kMaxGrid * 8, 256) +
                          align_up(2 * kMaxGrid * 8, 256) + align_up((size_t)(maxiter + 2) * 8, 256) +
                          align_up((size_t)(maxiter + 1) * 8, 256);
-    PSK_TRY(A->ws_small.ensure(small));
+    const size_t gath = P > 1 ? align_up((size_t)P * 8, 256) + align_up((size_t)P * 16, 256) +
+                                    align_up((size_t)P * 2 * kMaxGrid * 8, 256)
+                              : 0;
+    PSK_TRY(A->ws_small.ensure(small + gath));
     char *s = A->ws_small.as<char>();
     w.st = reinterpret_cast<PcgState *>(s);
     s += align_up(sizeof(PcgState), 256);
@@ -302,6 +311,18 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, PcgWork &w) {
     w.udr = reinterpret_cast<double *>(s);
     s += align_up((size_t)(maxiter + 2) * 8, 256);
     w.hist = reinterpret_cast<double *>(s);
+    s += align_up((size_t)(maxiter + 1) * 8, 256);
+    if (P > 1) {
+        w.part1g = reinterpret_cast<double *>(s);
+        s += align_up((size_t)P * 8, 256);
+        w.part2g = reinterpret_cast<double *>(s);
+        s += align_up((size_t)P * 16, 256);
+        w.initg = reinterpret_cast<double *>(s);
+    } else {
+        w.part1g = w.part1;
+        w.part2g = w.part2;
+        w.initg = w.part2;
+    }
     return PSK_OK;
 }
 
@@ -328,8 +349,11 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // general preconditioner (ILU): u = M^-1 r materialised between K2 and K3
     const bool gen = prec_is_general(M);
     if (gen && A->comm) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: ILU preconditioning of a sharded matrix");
+    // sharded: P ranks, scalars gathered (not all-reduced) and summed in rank order on every rank
+    const bool sharded = A->comm != nullptr;
+    const int P = sharded ? A->comm->nranks : 1;
     PcgWork w;
-    PSK_TRY(pcg_workspace(A, maxiter, gen, w));
+    PSK_TRY(pcg_workspace(A, maxiter, gen, P, w));
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
     const int gv = grid_for_rows(c, n, kVecTile);    // persistent grid of the init kernels
     // one-shot grid of K2/K3 (one 512-element tile per workgroup); K1/K2 finish their dot products
@@ -339,9 +363,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     GridSum gs2, gs3;
     PSK_TRY(gridsum_prepare(c, nv, 2, w.part2, &gs2));
     PSK_TRY(gridsum_prepare(c, nv, 1, w.part3, &gs3));
-    // Sharded: the init partials are all-reduced as zero-padded kMaxGrid-long arrays (same RCCL
-    // count on every rank whatever its grid); the loop's grid sums as 1 and 2 values.
-    const bool sharded = A->comm != nullptr;
+    // Sharded: the init partials are gathered as zero-padded kMaxGrid-long arrays (same RCCL count
+    // on every rank whatever its grid); the loop's grid sums as 1 and 2 values per rank.
     const int npi = sharded ? kMaxGrid : gv;
     if (sharded) PSK_HIP(hipMemsetAsync(w.part2, 0, 2 * kMaxGrid * sizeof(double), s));
 
@@ -360,8 +383,9 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
     }
     PSK_HIP(hipGetLastError());
-    if (sharded) PSK_TRY(allreduce_sum(A, w.part2, 2 * npi, s));
-    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.part2, npi, ctl->tau, w.st, w.udr);
+    if (sharded) PSK_TRY(allgather(A, w.part2, w.initg, 2 * npi, s));
+    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.initg, P * npi, ctl->tau, w.st,
+                       w.udr);
     PSK_HIP(hipGetLastError());
 
     // polling ring: flag copies every C iterations, host waits on the copy L chunks back
@@ -420,15 +444,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if ((rc = launch_spmv(A, kSpmvDot, w.p, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s)) != PSK_OK)
             break;
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
-        if (sharded && (rc = allreduce_sum(A, w.part1, 1, s)) != PSK_OK) break;
+        if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
         const dim3 gk((unsigned)nv);
         if (dinv)
-            hipLaunchKernelGGL(pcg_update_kernel<true>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1, gs2,
-                               w.st, w.udr, k);
+            hipLaunchKernelGGL(pcg_update_kernel<true>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1g, P,
+                               gs2, w.st, w.udr, k);
         else
-            hipLaunchKernelGGL(pcg_update_kernel<false>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1, gs2,
-                               w.st, w.udr, k);
-        if (sharded && (rc = allreduce_sum(A, w.part2, 2, s)) != PSK_OK) break;
+            hipLaunchKernelGGL(pcg_update_kernel<false>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1g, P,
+                               gs2, w.st, w.udr, k);
+        if (sharded && (rc = allgather(A, w.part2, w.part2g, 2, s)) != PSK_OK) break;
         if (gen) {
             if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
             hipLaunchKernelGGL(pcg_dot_kernel, gk, dim3(kBlock), 0, s, n, w.u, w.r, gs3, w.st);
@@ -437,10 +461,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         } else {
             if (dinv)
                 hipLaunchKernelGGL(pcg_direction_kernel<true>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
-                                   w.part1, w.part2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                                   ctl->fail_on_maxiter);
             else
                 hipLaunchKernelGGL(pcg_direction_kernel<false>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
-                                   w.part1, w.part2, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                                   ctl->fail_on_maxiter);
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;

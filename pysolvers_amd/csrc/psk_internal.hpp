@@ -80,8 +80,10 @@ struct HaloPeer {
     int64_t send_count;   // owned entries we send to this peer
     int64_t recv_count;   // halo entries we receive from it
     int64_t recv_offset;  // offset inside the halo region
-    int32_t *send_idx;    // device: owned local indices to pack (nullptr when contiguous)
+    int32_t *send_idx;    // device: owned local indices to pack (nullptr when contiguous); points
+                          // into psk_csr::pack_idx (not owned)
     int64_t send_begin;   // contiguous owned range start when send_idx == nullptr
+    int64_t pack_off;     // offset of this peer's packed segment in pack_idx / sendbuf
 };
 
 }  // namespace psk
@@ -108,6 +110,9 @@ struct psk_csr {
     int64_t n_global = 0, row_begin = 0, row_end = 0;
     std::vector<psk::HaloPeer> peers;
     psk::DevBuf sendbuf;  // packed halo sends
+    int32_t *pack_idx = nullptr;   // device: the packed peers' send indices, concatenated
+    int64_t pack_count = 0;
+    std::vector<int64_t> halo_cols;   // global index of each halo column, in local order
     // per-matrix solver workspace (grow-only)
     psk::DevBuf ws;
     psk::DevBuf ws_small;
@@ -180,6 +185,14 @@ __device__ __forceinline__ double block_sum(double v, double *sh) {
 #pragma unroll
     for (int i = 1; i < kWaves; ++i) r += sh[i];
     return r;
+}
+
+// Sum over the ranks of a gathered [nparts][W] array, component c, in rank order: every rank of a
+// sharded solve gets the same bits from its allgather'd copy (nparts == 1: the value itself).
+__device__ __forceinline__ double rank_sum(const double *g, int nparts, int W, int c) {
+    double s = g[c];
+    for (int q = 1; q < nparts; ++q) s += g[q * W + c];
+    return s;
 }
 
 // Sum of np partials laid out with `stride` (identical bits in every workgroup).
@@ -350,7 +363,9 @@ inline int grid_for_rows(const Context *c, int64_t rows, int per_tile) {
 int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
 int from_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
 int halo_exchange(psk_csr *A, double *x_local, hipStream_t s);
-int allreduce_sum(psk_csr *A, double *buf, int64_t count, hipStream_t s);
+// recv[q*count + i] = rank q's send[i]: no arithmetic, so every rank holds the same bits and
+// reduces them in rank order itself (RCCL's reduction order is algorithm- and rank-dependent)
+int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipStream_t s);
 
 // SpMV launch (defined in spmv.hip); modes below
 enum SpmvMode : int {

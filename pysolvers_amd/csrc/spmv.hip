@@ -320,8 +320,9 @@ static void csr_free(psk_csr *A) {
     A->ws.release();
     A->ws_small.release();
     A->sendbuf.release();
-    for (auto &p : A->peers)
-        if (p.send_idx) (void)hipFree(p.send_idx);
+    if (A->pack_idx) (void)hipFree(A->pack_idx);
+    A->pack_idx = nullptr;
+    A->pack_count = 0;
     A->peers.clear();
 }
 

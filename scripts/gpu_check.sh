@@ -18,7 +18,7 @@ echo "== smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smo
 rc=$?; tail -3 $OUT/smoke_$TAG.log; stop_if_crashed $rc
 
 if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  echo "== pytest -m gpu"; timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $OUT/pytest_gpu_$TAG.log 2>&1
+  echo "== pytest -m gpu"; timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
   rc=$?; tail -15 $OUT/pytest_gpu_$TAG.log; stop_if_crashed $rc
 fi
 
