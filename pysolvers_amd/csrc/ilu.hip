@@ -73,30 +73,80 @@ __global__ void fill_sentinel_kernel(int64_t n, double *x) {
 }
 
 // Sync-free: x_i = (rhs_i - sum_j T_ij x_j) / diag_i  (diag == nullptr: unit), rhs_i = rhs[rhs_idx[i]]
-// when rhs_idx is given. Rows are visited in `order`; every wave walks order[wave], order[wave + W], ...
-__global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ rp,
-                                                        const int32_t *__restrict__ ci, const double *__restrict__ va,
+// when rhs_idx is given. The factor is stored in SOLVE ORDER (host-built): position k holds row
+// krow[k] with entries [krp[k], krp[k+1]) of kci/kva, so a wave's rows stream. Wave w takes positions
+// w, w+W, ... and software-pipelines them: while it waits on the dependencies of position k it already
+// has position k+W's row, entries, right-hand side and diagonal in flight (stage B) and position
+// k+2W's row header (stage A), so a row costs one hand-off round trip instead of a chain of dependent
+// HBM loads (order -> rowptr -> entries -> rhs index -> rhs).
+struct SfHead {
+    int32_t row, s, e;
+};
+struct SfBody {
+    int32_t row, s, e, c;
+    double v, b, d;
+};
+
+__global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
+                                                        const int32_t *__restrict__ kci, const double *__restrict__ kva,
                                                         const double *__restrict__ diag, const double *__restrict__ rhs,
                                                         const int32_t *__restrict__ rhs_idx, double *x,
-                                                        int32_t *err, const int32_t *__restrict__ order) {
+                                                        int32_t *err, const int32_t *__restrict__ krow) {
     const int lane = threadIdx.x & 63;
     const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
     const int64_t W = (int64_t)gridDim.x * kWaves;
+    if (wave >= n) return;
+    auto head = [&](int64_t k, SfHead &h) {
+        if (k < n) {
+            h.row = krow[k];
+            h.s = krp[k];
+            h.e = krp[k + 1];
+        }
+    };
+    auto body = [&](int64_t k, const SfHead &h, SfBody &b) {
+        if (k < n) {
+            b.row = h.row;
+            b.s = h.s;
+            b.e = h.e;
+            const int32_t idx = h.s + lane;
+            b.c = idx < h.e ? kci[idx] : -1;
+            b.v = idx < h.e ? kva[idx] : 0.0;
+            if (lane == 0) {
+                b.b = rhs[rhs_idx ? rhs_idx[h.row] : h.row];
+                b.d = diag ? diag[h.row] : 1.0;
+            }
+        }
+    };
+    SfHead ha, hb;
+    SfBody cur, nxt;
+    head(wave, ha);
+    body(wave, ha, cur);
+    head(wave + W, hb);
     for (int64_t k = wave; k < n; k += W) {
-        const int64_t i = order[k];
-        const int32_t s = rp[i], e = rp[i + 1];
+        // the first poll of this row goes out before the prefetches, so waiting for it does not
+        // wait for them (loads complete in order)
+        uint64_t bits = cur.c >= 0 ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(x + cur.c), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0;
+        body(k + W, hb, nxt);       // stage B of k+W (its header arrived an iteration ago)
+        head(k + 2 * W, hb);        // stage A of k+2W
         double acc = 0.0;
-        for (int32_t base = s; base < e; base += 64) {
+        if (cur.c >= 0) {
+            double xv = __longlong_as_double((long long)bits);
+            if (is_sentinel(xv)) xv = wait_pub(x + cur.c, err);
+            acc = fma(cur.v, xv, acc);
+        }
+        for (int32_t base = cur.s + 64; base < cur.e; base += 64) {   // rows longer than a wave
             const int32_t idx = base + lane;
-            if (idx < e) acc = fma(va[idx], wait_pub(x + ci[idx], err), acc);
+            if (idx < cur.e) acc = fma(kva[idx], wait_pub(x + kci[idx], err), acc);
         }
         const double sum = wave_sum(acc);
         if (lane == 0) {
-            const double bi = rhs_idx ? rhs[rhs_idx[i]] : rhs[i];
-            double r = bi - sum;
-            if (diag) r = r / diag[i];
-            store_pub(x + i, r);
+            double r = cur.b - sum;
+            if (diag) r = r / cur.d;
+            store_pub(x + cur.row, r);
         }
+        cur = nxt;
     }
 }
 
@@ -242,6 +292,22 @@ static int coop_grid(const Context *c, const void *kern, size_t lds) {
     return c->num_cus * per_cu;
 }
 
+// Sync-free grid: every resident slot the occupancy API reports minus one workgroup per CU (the
+// hardware admits one fewer than the API at some SGPR counts, MI355X_MICROARCH.md "Residency"); all
+// waves must be co-resident, since a row's wave may wait on any earlier position.
+static int syncfree_grid(const Context *c) {
+    static int per_cu = -1;
+    if (per_cu < 0) {
+        int api = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&api, reinterpret_cast<const void *>(&sptrsv_kernel), kBlock,
+                                                         0) != hipSuccess)
+            api = 2;
+        per_cu = std::max(1, std::min(api, 8) - 1);
+        if (const char *e = std::getenv("PSK_SYNCFREE_PER_CU")) per_cu = std::max(1, std::atoi(e));   // experiments
+    }
+    return c->num_cus * per_cu;
+}
+
 // x = T^-1 rhs[rhs_idx] for one factor, with the factor's schedule
 static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const double *rhs, const int32_t *rhs_idx,
                          double *x, int32_t *err, hipStream_t s) {
@@ -270,7 +336,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         return PSK_OK;
     }
     const void *k = reinterpret_cast<const void *>(&sptrsv_kernel);
-    const int g = coop_grid(c, k, 0);
+    const int g = syncfree_grid(c);
     const int32_t *ord = T.order;
     void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
     PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, 0, s));
@@ -558,7 +624,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     std::vector<int32_t> order, lev;
     int64_t nlev = 0;
     level_order(F, order, lev, nlev);
-    const int64_t G = (int64_t)c->num_cus * 2, waves = G * kWaves;
+    const int64_t waves = (int64_t)syncfree_grid(c) * kWaves;
     T.est_syncfree_us = simulate_syncfree(F, order, waves);
     // band candidates: one block per workgroup, and 2x / 4x / 8x more blocks. Eligible: at most 8
     // off-diagonal entries per row (record width K), levels at most one chunk wide, LDS fits a CU.
@@ -621,9 +687,18 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
                 }
         }
     }
-    int rc = upload(&T.rowptr, F.rp);
-    if (rc == PSK_OK) rc = upload(&T.colidx, F.ci);
-    if (rc == PSK_OK) rc = upload(&T.vals, ova);
+    // the sync-free kernel's copy of the factor, in solve order (position k = row order[k])
+    std::vector<int32_t> krp((size_t)n + 1, 0), kci(F.ci.size());
+    std::vector<double> kva(ova.size());
+    for (int64_t k = 0; k < n; ++k) {
+        const int32_t i = order[(size_t)k], a = F.rp[(size_t)i], e = F.rp[(size_t)i + 1];
+        std::copy(F.ci.begin() + a, F.ci.begin() + e, kci.begin() + krp[(size_t)k]);
+        std::copy(ova.begin() + a, ova.begin() + e, kva.begin() + krp[(size_t)k]);
+        krp[(size_t)k + 1] = krp[(size_t)k] + (e - a);
+    }
+    int rc = upload(&T.rowptr, krp);
+    if (rc == PSK_OK) rc = upload(&T.colidx, kci);
+    if (rc == PSK_OK) rc = upload(&T.vals, kva);
     if (rc == PSK_OK) rc = upload(&T.diag, dg);
     if (rc == PSK_OK) rc = upload(&T.order, order);
     if (rc == PSK_OK) rc = upload(&T.rec_row, rrow);

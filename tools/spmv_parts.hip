@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                                                  \
@@ -106,6 +107,61 @@ __global__ void fillx(int64_t n, double *x) {
     if (i < n) x[i] = 1.0 + (double)(i % 7) * 0.125;
 }
 
+
+// SELL-256 (sliced ELL, one 256-row slice per workgroup, slot-major inside a slice): entry j of
+// row 256t+l at off[t] + j*256 + l; row lengths as uint8. Each lane sums its own row over slots
+// 0..len-1 in stored order (bit-identical to csr_matvec), no LDS.
+template <int W>
+__global__ __launch_bounds__(BS) void spmv_sell(int64_t n, const int64_t *__restrict__ off,
+                                                const unsigned char *__restrict__ len, const int *__restrict__ sc,
+                                                const double *__restrict__ sv, const double *__restrict__ x,
+                                                double *__restrict__ y) {
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x, row = t * TR + tid;
+    const bool has = row < n;
+    const int64_t o = off[t];
+    const int w = (int)((off[t + 1] - o) / TR);
+    const int L = has ? len[row] : 0;
+    double sum = 0.0;
+    if (w <= W) {
+        int cc[W];
+        double vv[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+            if (j < L) {
+                cc[j] = __builtin_nontemporal_load(sc + o + (int64_t)j * TR + tid);
+                vv[j] = __builtin_nontemporal_load(sv + o + (int64_t)j * TR + tid);
+            }
+        double xv[W];
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+            if (j < L) xv[j] = x[cc[j]];
+#pragma unroll
+        for (int j = 0; j < W; ++j)
+            if (j < L) sum = sum + vv[j] * xv[j];
+    } else {
+        for (int j = 0; j < L; ++j)
+            sum = sum + __builtin_nontemporal_load(sv + o + (int64_t)j * TR + tid) *
+                            x[__builtin_nontemporal_load(sc + o + (int64_t)j * TR + tid)];
+    }
+    if (has) __builtin_nontemporal_store(sum, y + row);
+}
+
+__global__ void sell_fill(int64_t n, const int *rp, const int *ci, const double *va, const int64_t *off,
+                          unsigned char *len, int *sc, double *sv) {
+    const int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (row >= n) return;
+    const int64_t t = row / TR, l = row % TR, o = off[t];
+    const int w = (int)((off[t + 1] - o) / TR);
+    const int a = rp[row], b = rp[row + 1];
+    len[row] = (unsigned char)(b - a);
+    for (int j = 0; j < w; ++j) {
+        const bool in = j < b - a;
+        sc[o + (int64_t)j * TR + l] = in ? ci[a + j] : (int)row;
+        sv[o + (int64_t)j * TR + l] = in ? va[a + j] : 0.0;
+    }
+}
+
 typedef void (*Kern)(int64_t, const int *, const int *, const double *, const double *, double *);
 
 int main(int argc, char **argv) {
@@ -184,6 +240,63 @@ int main(int argc, char **argv) {
             const double s = t[i][0] * 1e-3;
             std::printf("m=%-6lld %-10s %9.1f us  moved %6.2f GB  %6.0f GB/s  %5.1f%% of 8 TB/s\n", (long long)m,
                         vs[i].name, s * 1e6, vs[i].bytes / 1e9, vs[i].bytes / s / 1e9, vs[i].bytes / s / 8e12 * 100);
+        }
+        {   // SELL-256 of the same matrix (FD: width 5 in every slice)
+            const int64_t nt = (n + TR - 1) / TR;
+            std::vector<int> hrp(n + 1);
+            CK(hipMemcpy(hrp.data(), rp, (n + 1) * 4, hipMemcpyDeviceToHost));
+            std::vector<int64_t> hoff(nt + 1);
+            hoff[0] = 0;
+            for (int64_t tt = 0; tt < nt; ++tt) {
+                int w = 0;
+                for (int64_t r = tt * TR; r < std::min(n, tt * TR + TR); ++r) w = std::max(w, hrp[r + 1] - hrp[r]);
+                hoff[tt + 1] = hoff[tt] + (int64_t)w * TR;
+            }
+            int64_t *doff;
+            unsigned char *dlen;
+            int *dsc;
+            double *dsv, *y2;
+            CK(hipMalloc(&doff, (nt + 1) * 8));
+            CK(hipMalloc(&dlen, n));
+            CK(hipMalloc(&dsc, hoff[nt] * 4));
+            CK(hipMalloc(&dsv, hoff[nt] * 8));
+            CK(hipMalloc(&y2, n * 8));
+            CK(hipMemcpy(doff, hoff.data(), (nt + 1) * 8, hipMemcpyHostToDevice));
+            sell_fill<<<(unsigned)((n + 255) / 256), 256>>>(n, rp, ci, va, doff, dlen, dsc, dsv);
+            spmv_v<0><<<grid, BS>>>(n, rp, ci, va, x, y);
+            spmv_sell<8><<<(unsigned)nt, BS>>>(n, doff, dlen, dsc, dsv, x, y2);
+            CK(hipDeviceSynchronize());
+            std::vector<double> h1(n), h2(n);
+            CK(hipMemcpy(h1.data(), y, n * 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(h2.data(), y2, n * 8, hipMemcpyDeviceToHost));
+            const bool same = std::equal(h1.begin(), h1.end(), h2.begin(), [](double a, double b) {
+                return std::memcmp(&a, &b, 8) == 0;
+            });
+            float best = 1e30f, bestc = 1e30f;
+            for (int r = 0; r < 5; ++r) {
+                for (int v = 0; v < 2; ++v) {
+                    CK(hipEventRecord(e0));
+                    for (int l = 0; l < L; ++l) {
+                        if (v == 0) spmv_sell<8><<<(unsigned)nt, BS>>>(n, doff, dlen, dsc, dsv, x, y2);
+                        else spmv_v<0><<<grid, BS>>>(n, rp, ci, va, x, y);
+                    }
+                    CK(hipEventRecord(e1));
+                    CK(hipEventSynchronize(e1));
+                    float f;
+                    CK(hipEventElapsedTime(&f, e0, e1));
+                    if (v == 0) best = std::min(best, f / L); else bestc = std::min(bestc, f / L);
+                }
+            }
+            const double moved = 12.0 * hoff[nt] + 1.0 * n + 8.0 * (nt + 1) + 16.0 * n;
+            std::printf("m=%-6lld sell256    %9.1f us  csr-alg %6.0f GB/s (%5.1f%%)  moved %6.2f GB -> %6.0f GB/s  "
+                        "bitwise=%s   [csr full interleaved %9.1f us]\n",
+                        (long long)m, best * 1e3, full / (best * 1e-3) / 1e9, full / (best * 1e-3) / 8e12 * 100,
+                        moved / 1e9, moved / (best * 1e-3) / 1e9, same ? "yes" : "NO", bestc * 1e3);
+            CK(hipFree(doff));
+            CK(hipFree(dlen));
+            CK(hipFree(dsc));
+            CK(hipFree(dsv));
+            CK(hipFree(y2));
         }
         CK(hipFree(rp));
         CK(hipFree(ci));
