@@ -91,7 +91,12 @@ def main():
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
 
     from pysolvers_amd import _native as N
-    dev = int(os.environ.get("PSK_BENCH_DEVICE", local_rank))   # override only for rehearsals
+    # one GPU per rank: LOCAL_RANK when every GPU is visible to every rank; a launcher that narrows
+    # visibility per rank leaves one device (ordinal 0) per process
+    ndev = N.device_count()
+    if ndev < 1:
+        raise SystemExit("bench.py: no GPU visible")
+    dev = int(os.environ.get("PSK_BENCH_DEVICE", local_rank if local_rank < ndev else local_rank % ndev))
     N.check(N.lib.psk_set_device(dev), "psk_set_device")
 
     dist = None
@@ -109,7 +114,14 @@ def main():
     # ---- operator, preconditioner, right-hand side (all resident in HBM before timing) -----------
     comm = ctypes.c_void_p()
     A = ctypes.c_void_p()
-    if world > 1:
+    # PSK_BENCH_TRANSPORT=host: rehearsal of the N>1 path with all ranks on ONE GPU (collectives over
+    # host shared memory, psk_comm_init_host); never a measurement
+    transport = os.environ.get("PSK_BENCH_TRANSPORT", "rccl")
+    if world > 1 and transport == "host":
+        obj = [("/psk_bench_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        N.check(N.lib.psk_comm_init_host(world, rank, obj[0], ctypes.byref(comm)), "psk_comm_init_host")
+    elif world > 1:
         uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES)()
         if rank == 0:
             N.check(N.lib.psk_comm_unique_id(uid), "psk_comm_unique_id")
@@ -117,6 +129,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
         N.check(N.lib.psk_comm_init(world, rank, uid, ctypes.byref(comm)), "psk_comm_init")
+    if world > 1:
         rb, re_ = ctypes.c_int64(), ctypes.c_int64()
         N.check(N.lib.psk_csr_create_fd2d_dist(-1.0, 1.0, m, comm, ctypes.byref(A), ctypes.byref(rb),
                                                ctypes.byref(re_)), "psk_csr_create_fd2d_dist")
@@ -194,7 +207,7 @@ def main():
                     "generator), b = A @ default_rng(12345).random(n)",
             "config": {"workload": "PCG+Jacobi, FDLaplacian2D %dx%d (n=%d, nnz=%d), tau=0 fixed-iteration"
                                    % (m, m, n, nnz),
-                       "m": m, "precond": "jacobi", "parallelism": "row-block x%d (RCCL)" % world
+                       "m": m, "precond": "jacobi", "parallelism": "row-block x%d (%s)" % (world, "RCCL" if transport == "rccl" else "host-shm rehearsal")
                        if world > 1 else "single GPU"},
             "roofline": {"bound": "hbm", "kernel": "spmv_kernel<kSpmvDot> (rank 0)",
                          "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -207,6 +220,8 @@ def main():
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
             "setup_s": setup_s,
         }
+        if transport == "host" and world > 1:
+            out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
         if world == 1 and args.spmv10m and m != 3163:
             out["spmv_N10M"] = spmv_10m(N)
         if world == 1 and args.config1 and m != 4096:

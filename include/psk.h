@@ -219,6 +219,12 @@ int psk_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, psk_comm **ou
  * built on ONE GPU for any rank and psk_spmv then takes the full local [owned | halo] x from the
  * caller; collectives (and hence sharded solves) return PSK_ERR_UNSUPPORTED. */
 int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out);
+/* Validation only: a communicator whose collectives run through a POSIX shared-memory segment
+ * `name` ("/..."; the same on every rank, unique per job) between nranks processes of ONE host,
+ * stream-ordered like the RCCL calls they stand in for (D2H, host barrier, H2D). Lets the sharded
+ * solvers run with nranks > 1 on a single GPU, where RCCL refuses duplicate devices. Slow; never
+ * used for timing. */
+int psk_comm_init_host(int32_t nranks, int32_t rank, const char *name, psk_comm **out);
 int psk_comm_destroy(psk_comm *c);
 /* Rank `rank`'s row block of FDLaplacian2D(a,b,m): rows [row_begin,row_end) split on
  * whole grid lines; local columns are [owned | halo_lo | halo_hi]. */

@@ -21,14 +21,23 @@ from .DeviceMatrix import DeviceCSR
 
 
 class Communicator:
-    """A psk_comm: RCCL communicator of `nranks` (or a dry one: shards without collectives, for
-    validating the sharding on one GPU)."""
+    """A psk_comm: RCCL communicator of `nranks` (production), a dry one (shards without
+    collectives) or a host shared-memory one (transport="host": the collectives of P processes on
+    ONE GPU, for validating the multi-rank path where RCCL refuses duplicate devices)."""
 
-    def __init__(self, nranks, rank, unique_id=None, dry=False):
+    def __init__(self, nranks, rank, unique_id=None, dry=False, transport="rccl"):
         self.nranks, self.rank, self.dry = int(nranks), int(rank), bool(dry)
+        self.transport = "dry" if dry else transport
         h = ctypes.c_void_p()
         if dry:
             N.check(N.lib.psk_comm_init_dry(self.nranks, self.rank, ctypes.byref(h)), "psk_comm_init_dry")
+        elif transport == "host":
+            if not unique_id:
+                raise ValueError("Communicator(transport='host'): unique_id = shared segment name '/...'")
+            name = unique_id if isinstance(unique_id, bytes) else str(unique_id).encode()
+            N.check(N.lib.psk_comm_init_host(self.nranks, self.rank, name, ctypes.byref(h)), "psk_comm_init_host")
+        elif transport != "rccl":
+            raise ValueError("transport must be 'rccl' or 'host'")
         else:
             if unique_id is None:
                 raise ValueError("Communicator: unique_id required (Communicator.unique_id() on rank 0)")
@@ -43,14 +52,17 @@ class Communicator:
         return bytes(uid)
 
     @classmethod
-    def from_torch_distributed(cls, group=None):
+    def from_torch_distributed(cls, group=None, transport="rccl"):
         """Collective over the torch.distributed group (any backend; gloo is enough, it only
-        carries the RCCL unique id)."""
+        carries the RCCL unique id / the shared segment name)."""
+        import os
         import torch.distributed as dist
         rank, world = dist.get_rank(group), dist.get_world_size(group)
-        obj = [cls.unique_id() if rank == 0 else None]
+        if rank == 0:
+            uid = cls.unique_id() if transport == "rccl" else ("/psk_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode()
+        obj = [uid if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0, group=group)
-        return cls(world, rank, obj[0])
+        return cls(world, rank, obj[0], transport=transport)
 
     @property
     def handle(self):

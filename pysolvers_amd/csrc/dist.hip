@@ -32,6 +32,20 @@ int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
                            s, A->pack_count, A->pack_idx, x, sb);
         PSK_HIP(hipGetLastError());
     }
+    if (A->comm->shm) {
+        std::vector<int> pr;
+        std::vector<const double *> sd;
+        std::vector<double *> rv;
+        std::vector<int64_t> sc, rc;
+        for (const HaloPeer &p : A->peers) {
+            pr.push_back(p.rank);
+            sd.push_back(p.send_idx ? sb + p.pack_off : x + p.send_begin);
+            sc.push_back(p.send_count);
+            rv.push_back(x + A->n + p.recv_offset);
+            rc.push_back(p.recv_count);
+        }
+        return shm_exchange(A->comm, (int)pr.size(), pr.data(), sd.data(), sc.data(), rv.data(), rc.data(), s);
+    }
     PSK_RCCL(ncclGroupStart());
     for (const HaloPeer &p : A->peers) {
         if (p.send_count > 0) {
@@ -48,6 +62,7 @@ int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
 int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipStream_t s) {
     if (!A->comm) return fail(PSK_ERR_ARG, "allgather on an unsharded matrix");
     if (A->comm->dry) return fail(PSK_ERR_UNSUPPORTED, "collective on a dry (RCCL-less) communicator");
+    if (A->comm->shm) return shm_allgather(A->comm, send, recv, count, s);
     PSK_RCCL(ncclAllGather(send, recv, (size_t)count, ncclDouble, A->comm->nccl, s));
     return PSK_OK;
 }
@@ -133,78 +148,109 @@ static int dist_plan(int64_t n_global, const int64_t *rs, int P, int r, const in
     return PSK_OK;
 }
 
-// Creation-time check under RCCL (collective over all ranks, same verdict everywhere): the send
-// and receive counts agree pairwise, then each rank's send list equals what its peer expects.
-static int dist_verify(psk_comm *cm, const int64_t *rs, const DistPlan &pl) {
-    const int P = cm->nranks, r = cm->rank;
+// Synchronous host-buffer collectives for creation-time checks, over the communicator's transport
+// (RCCL: staged through device memory on libpsk's stream; shared memory: shmcomm.hip).
+static int host_allgather(psk_comm *cm, const void *mine, void *all, size_t bytes) {
+    if (cm->shm) return shm_allgather_host(cm, mine, all, bytes);
     Context *c;
     PSK_TRY(ctx(&c));
     hipStream_t s = c->stream;
-    std::vector<int64_t> mine((size_t)2 * P);
-    for (int q = 0; q < P; ++q) {
-        mine[(size_t)q] = (int64_t)pl.send_rows[(size_t)q].size();
-        mine[(size_t)(P + q)] = pl.recv_cnt[(size_t)q];
-    }
-    int64_t total_recv = 0, total_send = 0;
-    for (int q = 0; q < P; ++q) {
-        total_send += mine[(size_t)q];
-        total_recv += mine[(size_t)(P + q)];
-    }
     DevBuf d;
     struct Release {
         DevBuf &b;
         ~Release() { b.release(); }
-    } release_d{d};
-    const size_t cnt_bytes = (size_t)2 * P * 8 * (P + 1);
-    PSK_TRY(d.ensure(cnt_bytes + (size_t)(total_send + total_recv + 2) * 8 + 8 * (size_t)P + 64));
-    int64_t *dmine = d.as<int64_t>(), *dall = dmine + 2 * P;
-    PSK_HIP(hipMemcpy(dmine, mine.data(), mine.size() * 8, hipMemcpyHostToDevice));
-    PSK_RCCL(ncclAllGather(dmine, dall, (size_t)2 * P, ncclInt64, cm->nccl, s));
-    std::vector<int64_t> all((size_t)2 * P * P);
-    PSK_HIP(hipMemcpyAsync(all.data(), dall, all.size() * 8, hipMemcpyDeviceToHost, s));
+    } rel{d};
+    PSK_TRY(d.ensure(bytes * (size_t)(cm->nranks + 1) + 64));
+    char *dm = d.as<char>(), *da = dm + bytes;
+    PSK_HIP(hipMemcpy(dm, mine, bytes, hipMemcpyHostToDevice));
+    PSK_RCCL(ncclAllGather(dm, da, bytes, ncclUint8, cm->nccl, s));
+    PSK_HIP(hipMemcpyAsync(all, da, bytes * (size_t)cm->nranks, hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
+    return PSK_OK;
+}
+
+static int host_exchange(psk_comm *cm, const std::vector<int> &peers, const std::vector<const void *> &sends,
+                         const std::vector<size_t> &sb, const std::vector<void *> &recvs, const std::vector<size_t> &rb) {
+    const int np = (int)peers.size();
+    if (cm->shm) return shm_exchange_host(cm, np, peers.data(), sends.data(), sb.data(), recvs.data(), rb.data());
+    Context *c;
+    PSK_TRY(ctx(&c));
+    hipStream_t s = c->stream;
+    size_t tot = 0;
+    for (int k = 0; k < np; ++k) tot += sb[(size_t)k] + rb[(size_t)k];
+    DevBuf d;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } rel{d};
+    PSK_TRY(d.ensure(tot + 64));
+    char *p = d.as<char>();
+    std::vector<char *> dr((size_t)np);
+    PSK_RCCL(ncclGroupStart());
+    for (int k = 0; k < np; ++k) {
+        if (sb[(size_t)k]) {
+            PSK_HIP(hipMemcpy(p, sends[(size_t)k], sb[(size_t)k], hipMemcpyHostToDevice));
+            PSK_RCCL(ncclSend(p, sb[(size_t)k], ncclUint8, peers[(size_t)k], cm->nccl, s));
+            p += sb[(size_t)k];
+        }
+        dr[(size_t)k] = p;
+        if (rb[(size_t)k]) {
+            PSK_RCCL(ncclRecv(p, rb[(size_t)k], ncclUint8, peers[(size_t)k], cm->nccl, s));
+            p += rb[(size_t)k];
+        }
+    }
+    PSK_RCCL(ncclGroupEnd());
+    for (int k = 0; k < np; ++k)
+        if (rb[(size_t)k]) PSK_HIP(hipMemcpyAsync(recvs[(size_t)k], dr[(size_t)k], rb[(size_t)k], hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    return PSK_OK;
+}
+
+// Creation-time check (collective over all ranks, same verdict everywhere): the send and receive
+// counts agree pairwise, then each rank's send list equals what its peer expects to receive.
+static int dist_verify(psk_comm *cm, const DistPlan &pl) {
+    const int P = cm->nranks;
+    std::vector<int64_t> mine((size_t)2 * P), all((size_t)2 * P * P);
+    for (int q = 0; q < P; ++q) {
+        mine[(size_t)q] = (int64_t)pl.send_rows[(size_t)q].size();
+        mine[(size_t)(P + q)] = pl.recv_cnt[(size_t)q];
+    }
+    PSK_TRY(host_allgather(cm, mine.data(), all.data(), mine.size() * 8));
     for (int a = 0; a < P; ++a)
         for (int b = 0; b < P; ++b)
             if (a != b && all[(size_t)(2 * P * a + b)] != all[(size_t)(2 * P * b + P + a)])
                 return fail(PSK_ERR_ARG, "psk_csr_create_dist: halo counts disagree across ranks (pattern not "
                                          "structurally symmetric)");
-    // exchange: send the global ids we receive from q; receive the ids q receives from us
-    int64_t *dneed = dall + 2 * P * P, *dgot = dneed + total_recv;
-    int32_t *dflag = reinterpret_cast<int32_t *>(dgot + total_send);
-    int32_t *dflags = dflag + 2;
-    if (total_recv > 0) PSK_HIP(hipMemcpy(dneed, pl.halo.data(), (size_t)total_recv * 8, hipMemcpyHostToDevice));
-    PSK_RCCL(ncclGroupStart());
-    int64_t so = 0;
+    // send each owner the global ids we receive from it; receive the ids each peer receives from us
+    std::vector<int> peers;
+    std::vector<const void *> sends;
+    std::vector<void *> recvs;
+    std::vector<size_t> sb, rb;
+    std::vector<std::vector<int64_t>> got((size_t)P);
     for (int q = 0; q < P; ++q) {
-        if (pl.recv_cnt[(size_t)q] > 0)
-            PSK_RCCL(ncclSend(dneed + pl.recv_off[(size_t)q], (size_t)pl.recv_cnt[(size_t)q], ncclInt64, q, cm->nccl, s));
-        const int64_t ns = (int64_t)pl.send_rows[(size_t)q].size();
-        if (ns > 0) PSK_RCCL(ncclRecv(dgot + so, (size_t)ns, ncclInt64, q, cm->nccl, s));
-        so += ns;
+        const size_t ns = pl.send_rows[(size_t)q].size(), nr = (size_t)pl.recv_cnt[(size_t)q];
+        if (ns == 0 && nr == 0) continue;
+        got[(size_t)q].resize(ns);
+        peers.push_back(q);
+        sends.push_back(pl.halo.data() + (nr ? pl.recv_off[(size_t)q] : 0));
+        sb.push_back(nr * 8);
+        recvs.push_back(got[(size_t)q].data());
+        rb.push_back(ns * 8);
     }
-    PSK_RCCL(ncclGroupEnd());
-    std::vector<int64_t> got((size_t)total_send);
-    if (total_send > 0) PSK_HIP(hipMemcpyAsync(got.data(), dgot, got.size() * 8, hipMemcpyDeviceToHost, s));
-    PSK_HIP(hipStreamSynchronize(s));
+    PSK_TRY(host_exchange(cm, peers, sends, sb, recvs, rb));
     int32_t ok = 1;
-    so = 0;
     for (int q = 0; q < P && ok; ++q)
-        for (int32_t i : pl.send_rows[(size_t)q])
-            if (got[(size_t)so++] != pl.rb + i) {
+        for (size_t k = 0; k < pl.send_rows[(size_t)q].size(); ++k)
+            if (got[(size_t)q][k] != pl.rb + pl.send_rows[(size_t)q][k]) {
                 ok = 0;
                 break;
             }
-    PSK_HIP(hipMemcpy(dflag, &ok, 4, hipMemcpyHostToDevice));
-    PSK_RCCL(ncclAllGather(dflag, dflags, 1, ncclInt32, cm->nccl, s));
     std::vector<int32_t> oks((size_t)P);
-    PSK_HIP(hipMemcpyAsync(oks.data(), dflags, (size_t)P * 4, hipMemcpyDeviceToHost, s));
-    PSK_HIP(hipStreamSynchronize(s));
+    PSK_TRY(host_allgather(cm, &ok, oks.data(), 4));
     for (int q = 0; q < P; ++q)
         if (!oks[(size_t)q])
             return fail(PSK_ERR_ARG, "psk_csr_create_dist: halo lists disagree across ranks (pattern not "
                                      "structurally symmetric)");
-    (void)rs;
-    (void)r;
     return PSK_OK;
 }
 
@@ -272,6 +318,7 @@ int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out) {
 int psk_comm_destroy(psk_comm *c) {
     if (!c) return PSK_OK;
     if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    shm_close(c);
     delete c;
     return PSK_OK;
 }
@@ -362,7 +409,7 @@ int psk_csr_create_dist(int64_t n_global, const int64_t *row_starts, const int64
     if (nnz > 0 && (!colidx || !vals)) return fail(PSK_ERR_ARG, "psk_csr_create_dist: NULL entries");
     DistPlan pl;
     PSK_TRY(dist_plan(n_global, row_starts, P, r, rowptr, colidx, pl));
-    if (!cm->dry) PSK_TRY(dist_verify(cm, row_starts, pl));
+    if (!cm->dry) PSK_TRY(dist_verify(cm, pl));
     Context *c;
     PSK_TRY(ctx(&c));
     psk_csr *A = new psk_csr();

@@ -86,6 +86,7 @@ struct HaloPeer {
     int64_t pack_off;     // offset of this peer's packed segment in pack_idx / sendbuf
 };
 
+struct ShmComm;
 }  // namespace psk
 
 struct psk_comm {
@@ -94,7 +95,20 @@ struct psk_comm {
     int device = 0;
     ncclComm_t nccl = nullptr;
     bool dry = false;     // psk_comm_init_dry: builds shards, no collectives (single-GPU validation)
+    psk::ShmComm *shm = nullptr;   // psk_comm_init_host: shared-memory transport (shmcomm.hip)
 };
+
+namespace psk {
+// shared-memory transport (shmcomm.hip): stream-ordered like the RCCL calls they stand in for
+int shm_allgather(psk_comm *c, const double *send, double *recv, int64_t count, hipStream_t s);
+int shm_exchange(psk_comm *c, int npeers, const int *peers, const double *const *sends, const int64_t *send_counts,
+                 double *const *recvs, const int64_t *recv_counts, hipStream_t s);
+int shm_allgather_host(psk_comm *c, const void *mine, void *all, size_t bytes);
+int shm_exchange_host(psk_comm *c, int npeers, const int *peers, const void *const *sends, const size_t *send_bytes,
+                      void *const *recvs, const size_t *recv_bytes);
+int shm_error(const psk_comm *c);
+void shm_close(psk_comm *c);
+}  // namespace psk
 
 struct psk_csr {
     int64_t n = 0;        // local (owned) rows
