@@ -122,6 +122,19 @@ int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out);
 int psk_csr_create_rect(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
                         const double *vals, int32_t loc, psk_csr **out);
 int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
+/* SpMV storage layout of A (same y bit for bit either way; the CSR arrays are always kept):
+ *   PSK_LAYOUT_CSR    one workgroup per tile of rows, the tile's entries streamed in stored order
+ *                     and the products staged through LDS;
+ *   PSK_LAYOUT_SLICED a sliced copy: 256-row slices, slot-major inside a slice, one row per lane,
+ *                     padding slots (column -1) up to the slice's widest row.
+ * Every creation path picks SLICED when its padded stream is no larger than the CSR stream
+ * (12 B/slot <= 12 B/entry + 4 B/row); env PSK_SPMV_LAYOUT=csr|sliced overrides. set = -1
+ * queries, PSK_LAYOUT_CSR / PSK_LAYOUT_SLICED switches (building or freeing the copy); *slots =
+ * padded entries of the sliced copy (0 without one). Out pointers may be NULL. Replaces nothing in
+ * the reference (scipy keeps CSR); it is a device storage choice under mvmult (IterativeLinearSolver.py:94-106). */
+#define PSK_LAYOUT_CSR    0
+#define PSK_LAYOUT_SLICED 1
+int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots);
 /* Copy the arrays back to host buffers (any pointer may be NULL). */
 int psk_csr_download(const psk_csr *A, int32_t *rowptr, int32_t *colidx, double *vals);
 int psk_csr_destroy(psk_csr *A);

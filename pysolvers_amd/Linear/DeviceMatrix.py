@@ -126,6 +126,20 @@ class DeviceCSR:
     def handle(self):
         return self._h
 
+    @property
+    def layout(self):
+        """SpMV storage layout: "csr" or "sliced" (psk_csr_layout; y is bit-identical either way)."""
+        k = N.I32()
+        N.check(N.lib.psk_csr_layout(self._h, -1, ctypes.byref(k), None), "psk_csr_layout")
+        return "sliced" if k.value == N.PSK_LAYOUT_SLICED else "csr"
+
+    def set_layout(self, layout):
+        """Switch the SpMV storage layout ("csr" or "sliced"); returns the padded slot count."""
+        k = {"csr": N.PSK_LAYOUT_CSR, "sliced": N.PSK_LAYOUT_SLICED}[layout]
+        slots = N.I64()
+        N.check(N.lib.psk_csr_layout(self._h, k, None, ctypes.byref(slots)), "psk_csr_layout")
+        return slots.value
+
     def to_scipy(self):
         indptr = np.empty(self.n + 1, dtype=np.int32)
         indices = np.empty(self.nnz, dtype=np.int32)

@@ -357,6 +357,7 @@ int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *cm, psk_cs
         rc = fail(PSK_ERR_ALLOC, "fd2d_dist alloc");
     if (rc == PSK_OK) rc = fd2d_fill(A, m, a, b, rb, re, lo ? rb - m : rb, c->stream);
     if (rc == PSK_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "fd2d_dist sync");
+    if (rc == PSK_OK) rc = csr_choose_layout(A, c->stream);
     if (rc != PSK_OK) {
         psk_csr_destroy(A);
         return rc;
@@ -467,6 +468,7 @@ int psk_csr_create_dist(int64_t n_global, const int64_t *row_starts, const int64
                          (nnz > 0 && hipMemcpy(A->vals, vals, (size_t)nnz * 8, hipMemcpyHostToDevice) != hipSuccess) ||
                          (nnz == 0 && (hipMemset(A->colidx, 0, 4) != hipSuccess || hipMemset(A->vals, 0, 8) != hipSuccess))))
         rc = fail(PSK_ERR_HIP, "psk_csr_create_dist: upload");
+    if (rc == PSK_OK) rc = csr_choose_layout(A, c->stream);
     if (rc != PSK_OK) {
         psk_csr_destroy(A);
         return rc;

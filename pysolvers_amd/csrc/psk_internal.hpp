@@ -119,6 +119,13 @@ struct psk_csr {
     int32_t *colidx = nullptr;
     double *vals = nullptr;
     int device = 0;
+    // sliced copy of the same entries (spmv.hip, "sliced layout"): slices of kSlice rows, slot-major
+    // inside a slice (slot j of lane l at sl_off[t] + j*kSlice + l), padding slots hold column -1.
+    // Present when the SpMV uses it (psk_csr_layout); the CSR arrays above are always kept.
+    int64_t *sl_off = nullptr;   // [nslices + 1] slot offsets
+    int32_t *sl_col = nullptr;
+    double *sl_val = nullptr;
+    int64_t sl_slots = 0;
     // distributed
     psk_comm *comm = nullptr;
     int64_t n_global = 0, row_begin = 0, row_end = 0;
@@ -406,6 +413,10 @@ inline bool prec_is_general(const psk_prec *M) {
 // reports a bounded-spin timeout of any triangular solve inside M (syncs the stream)
 int prec_check_error(const psk_prec *M, hipStream_t s);
 int tile_rows_for(int64_t n, int64_t nnz);
+// SpMV layout of a freshly created matrix: the sliced copy when it streams no more bytes than the
+// CSR arrays (PSK_SPMV_LAYOUT=csr|sliced overrides); called at the end of every creation path
+int csr_choose_layout(psk_csr *A, hipStream_t s);
+void sliced_free(psk_csr *A);
 // one-shot SpMV (grid = tiles of A->tile_rows rows); dot modes write their grid sum to partial[0]
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s);

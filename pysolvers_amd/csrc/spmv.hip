@@ -132,6 +132,188 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Sliced layout (SELL-256): the same entries regrouped so that one workgroup owns a slice of
+// kSlice = 256 rows, ONE ROW PER LANE, and slot j of the slice's rows is contiguous (slot-major).
+// The stream loads stay coalesced, and each x gather instruction of a wave now reads the j-th
+// entries of 64 consecutive rows: for the 5-point matrix 512 contiguous bytes of x per slot, where
+// a CSR tile's gather instruction mixes the 5 neighbour offsets of ~13 rows (more cache lines and
+// address work per load). Each lane still sums ITS row in stored order from 0.0 with rounded
+// products, so y is bit-identical to csr_matvec and to spmv_kernel. Padding slots (rows shorter
+// than the slice's widest row) hold column -1 and are skipped. No rowptr stream, no LDS staging.
+// tools/spmv_parts.hip / tools/sell_lab.hip: 3.48 ms vs 3.57-3.92 ms (CSR) at 16384^2.
+constexpr int kSlice = kBlock;
+constexpr int kSliceRegs = 8;   // slots held in registers; wider slices take the loop below
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
+    int64_t n, const int64_t *__restrict__ soff, const int32_t *__restrict__ scol,
+    const double *__restrict__ sval, const double *__restrict__ x, double *__restrict__ y,
+    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs,
+    const int32_t *__restrict__ done) {
+    if (done != nullptr && *done != 0) return;
+    __shared__ double sh[kWaves];
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x, row = t * kSlice + tid;
+    const bool has = row < n;
+    const int64_t o = soff[t];
+    const int w = (int)((soff[t + 1] - o) / kSlice);
+    const int32_t *sc = scol + o + tid;
+    const double *sv = sval + o + tid;
+    double eq = 0.0;
+    if (has) {
+        if (MODE == kSpmvDot) eq = x[row];
+        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+            eq = aux_q[row];
+    }
+    double sum = 0.0;
+    if (w <= kSliceRegs) {
+        int32_t cc[kSliceRegs];
+        double vv[kSliceRegs], xv[kSliceRegs];
+#pragma unroll
+        for (int j = 0; j < kSliceRegs; ++j) {   // the slice's whole stream first (w is uniform)
+            cc[j] = -1;
+            vv[j] = 0.0;
+            if (j < w) {
+                cc[j] = ld_stream(sc + j * kSlice);
+                vv[j] = ld_stream(sv + j * kSlice);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kSliceRegs; ++j) {   // then every gather
+            xv[j] = 0.0;
+            if (cc[j] >= 0) {
+                xv[j] = x[cc[j]];
+                if (MODE == kSpmvJacobiDot) xv[j] = aux_d[cc[j]] * xv[j];   // (DInv*q)[c], rounded
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kSliceRegs; ++j)
+            if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
+    } else {
+        for (int j = 0; j < w; ++j) {
+            const int32_t c = ld_stream(sc + (int64_t)j * kSlice);
+            if (c < 0) break;   // only padding follows a row's last entry
+            double xx = x[c];
+            if (MODE == kSpmvJacobiDot) xx = aux_d[c] * xx;
+            sum = sum + ld_stream(sv + (int64_t)j * kSlice) * xx;
+        }
+    }
+    double acc = 0.0;
+    if (has) {
+        if (MODE == kSpmvResid) {
+            const double r = eq - sum;
+            y[row] = r;
+            acc = r * r;
+        } else if (MODE == kSpmvAdd) {
+            y[row] = eq + sum;
+        } else {
+            __builtin_nontemporal_store(sum, y + row);
+            if (MODE != kSpmvPlain) acc = eq * sum;
+        }
+    }
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) {
+        const double bs = block_sum(acc, sh);
+        gridsum_publish<1>(gs, &bs, sh);
+    }
+}
+
+// widest row of every slice
+__global__ __launch_bounds__(kBlock) void sliced_width_kernel(int64_t n, const int32_t *__restrict__ rowptr,
+                                                              int32_t *__restrict__ width) {
+    __shared__ int32_t sh[kWaves];
+    const int64_t row = (int64_t)blockIdx.x * kSlice + threadIdx.x;
+    int32_t len = row < n ? rowptr[row + 1] - rowptr[row] : 0;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int32_t v = __shfl_xor(len, o, 64);
+        len = v > len ? v : len;
+    }
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = len;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int32_t m = sh[0];
+        for (int i = 1; i < kWaves; ++i) m = sh[i] > m ? sh[i] : m;
+        width[blockIdx.x] = m;
+    }
+}
+
+// one workgroup per slice, one lane per row (lanes past n write padding): coalesced stores
+__global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const int32_t *__restrict__ rowptr,
+                                                             const int32_t *__restrict__ colidx,
+                                                             const double *__restrict__ vals,
+                                                             const int64_t *__restrict__ soff,
+                                                             int32_t *__restrict__ scol, double *__restrict__ sval) {
+    const int64_t t = blockIdx.x, row = t * kSlice + threadIdx.x;
+    const int64_t o = soff[t], w = (soff[t + 1] - o) / kSlice;
+    const int64_t a = row < n ? rowptr[row] : 0;
+    const int64_t len = row < n ? rowptr[row + 1] - a : 0;
+    for (int64_t j = 0; j < w; ++j) {
+        const int64_t s = o + j * kSlice + threadIdx.x;
+        scol[s] = j < len ? colidx[a + j] : -1;
+        sval[s] = j < len ? vals[a + j] : 0.0;
+    }
+}
+
+void sliced_free(psk_csr *A) {
+    if (A->sl_off) (void)hipFree(A->sl_off);
+    if (A->sl_col) (void)hipFree(A->sl_col);
+    if (A->sl_val) (void)hipFree(A->sl_val);
+    A->sl_off = nullptr;
+    A->sl_col = nullptr;
+    A->sl_val = nullptr;
+    A->sl_slots = 0;
+}
+
+// Builds the sliced copy of A. Unless `force`, only when its stream (12 B per slot) is no larger
+// than the CSR stream (12 B per entry + 4 B per row), i.e. padding costs nothing, and quietly
+// keeps CSR if HBM cannot hold the copy.
+static int sliced_build(psk_csr *A, hipStream_t s, bool force) {
+    sliced_free(A);
+    const int64_t nt = (A->n + kSlice - 1) / kSlice;
+    if (nt == 0) return PSK_OK;   // nothing to multiply (launch_spmv returns early)
+    if (nt > INT32_MAX) return force ? fail(PSK_ERR_UNSUPPORTED, "sliced layout: too many slices") : PSK_OK;
+    DevBuf tmp;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } rel{tmp};
+    PSK_TRY(tmp.ensure((size_t)nt * sizeof(int32_t)));
+    hipLaunchKernelGGL(sliced_width_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, tmp.as<int32_t>());
+    PSK_HIP(hipGetLastError());
+    std::vector<int32_t> wd((size_t)nt);
+    PSK_HIP(hipMemcpyAsync(wd.data(), tmp.p, (size_t)nt * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    std::vector<int64_t> off((size_t)nt + 1);
+    off[0] = 0;
+    for (int64_t t = 0; t < nt; ++t) off[(size_t)t + 1] = off[(size_t)t] + (int64_t)wd[(size_t)t] * kSlice;
+    const int64_t slots = off[(size_t)nt];
+    if (!force && 12 * slots > 12 * A->nnz + 4 * (A->n + 1)) return PSK_OK;
+    const size_t ms = slots > 0 ? (size_t)slots : 1;
+    if (hipMalloc(&A->sl_off, (size_t)(nt + 1) * 8) != hipSuccess || hipMalloc(&A->sl_col, ms * 4) != hipSuccess ||
+        hipMalloc(&A->sl_val, ms * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        sliced_free(A);
+        return force ? fail(PSK_ERR_ALLOC, "sliced layout: hipMalloc") : PSK_OK;
+    }
+    PSK_HIP(hipMemcpyAsync(A->sl_off, off.data(), (size_t)(nt + 1) * 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(sliced_fill_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, A->vals,
+                       A->sl_off, A->sl_col, A->sl_val);
+    PSK_HIP(hipGetLastError());
+    PSK_HIP(hipStreamSynchronize(s));
+    A->sl_slots = slots;
+    return PSK_OK;
+}
+
+int csr_choose_layout(psk_csr *A, hipStream_t s) {
+    const char *e = std::getenv("PSK_SPMV_LAYOUT");
+    if (e && std::strcmp(e, "csr") == 0) return PSK_OK;
+    const bool force = e && std::strcmp(e, "sliced") == 0;
+    int rc = sliced_build(A, s, force);
+    if (rc != PSK_OK) sliced_free(A);
+    return rc;
+}
+
 int tile_rows_for(int64_t n, int64_t nnz) {
     // rows per tile so that a typical tile's entries fit one LDS chunk
     const double avg = n > 0 ? (double)nnz / (double)n : 1.0;
@@ -147,10 +329,29 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     if (A->n == 0) return PSK_OK;
     Context *c;
     PSK_TRY(ctx(&c));
-    const int64_t nwg = spmv_tiles(A);
+    const bool sliced = A->sl_off != nullptr;
+    const int64_t nwg = sliced ? (A->n + kSlice - 1) / kSlice : spmv_tiles(A);
     GridSum gs{nullptr, nullptr, nullptr, 1, nullptr};
     if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
     dim3 gd((unsigned)nwg), bd(kBlock);
+    if (sliced) {
+#define PSK_SLICED_LAUNCH(M)                                                                                 \
+    hipLaunchKernelGGL(spmv_sliced_kernel<M>, gd, bd, 0, s, A->n, A->sl_off, A->sl_col, A->sl_val, x, y, aux_d, \
+                       aux_q, gs, done_flag)
+        switch (mode) {
+        case kSpmvPlain: PSK_SLICED_LAUNCH(kSpmvPlain); break;
+        case kSpmvDot: PSK_SLICED_LAUNCH(kSpmvDot); break;
+        case kSpmvJacobiDot: PSK_SLICED_LAUNCH(kSpmvJacobiDot); break;
+        case kSpmvPlainDot: PSK_SLICED_LAUNCH(kSpmvPlainDot); break;
+        case kSpmvResid: PSK_SLICED_LAUNCH(kSpmvResid); break;
+        case kSpmvAdd: PSK_SLICED_LAUNCH(kSpmvAdd); break;
+        default:
+            return fail(PSK_ERR_ARG, "unknown spmv mode");
+        }
+#undef PSK_SLICED_LAUNCH
+        PSK_HIP(hipGetLastError());
+        return PSK_OK;
+    }
     const int tr = A->tile_rows;
     const int32_t nz = (int32_t)A->nnz;
 #define PSK_SPMV_LAUNCH(M)                                                                                  \
@@ -317,6 +518,7 @@ static void csr_free(psk_csr *A) {
     A->rowptr = nullptr;
     A->colidx = nullptr;
     A->vals = nullptr;
+    sliced_free(A);
     A->ws.release();
     A->ws_small.release();
     A->sendbuf.release();
@@ -377,6 +579,12 @@ int psk_csr_create_rect(int64_t n, int64_t ncols, int64_t nnz, const int32_t *ro
         delete A;
         return fail(PSK_ERR_HIP, std::string("psk_csr_create copy: ") + hipGetErrorString(e));
     }
+    rc = csr_choose_layout(A, c->stream);
+    if (rc != PSK_OK) {
+        csr_free(A);
+        delete A;
+        return rc;
+    }
     *out = A;
     return PSK_OK;
 }
@@ -402,6 +610,7 @@ int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out) {
         hipError_t e = hipStreamSynchronize(c->stream);
         if (e != hipSuccess) rc = fail(PSK_ERR_HIP, std::string("fd2d: ") + hipGetErrorString(e));
     }
+    if (rc == PSK_OK) rc = csr_choose_layout(A, c->stream);
     if (rc != PSK_OK) {
         csr_free(A);
         delete A;
@@ -415,6 +624,22 @@ int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz) {
     if (!A) return fail(PSK_ERR_ARG, "NULL matrix");
     if (n) *n = A->n;
     if (nnz) *nnz = A->nnz;
+    return PSK_OK;
+}
+
+int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots) {
+    if (!A) return fail(PSK_ERR_ARG, "psk_csr_layout: NULL matrix");
+    if (set != -1 && set != PSK_LAYOUT_CSR && set != PSK_LAYOUT_SLICED)
+        return fail(PSK_ERR_ARG, "psk_csr_layout: set must be -1, PSK_LAYOUT_CSR or PSK_LAYOUT_SLICED");
+    if (set == PSK_LAYOUT_CSR) sliced_free(A);
+    if (set == PSK_LAYOUT_SLICED && !A->sl_off && A->n > 0) {
+        Context *c;
+        PSK_TRY(ctx(&c));
+        PSK_HIP(hipStreamSynchronize(c->stream));   // queued launches may still read the layout
+        PSK_TRY(sliced_build(A, c->stream, true));
+    }
+    if (layout) *layout = A->sl_off ? PSK_LAYOUT_SLICED : PSK_LAYOUT_CSR;
+    if (slots) *slots = A->sl_slots;
     return PSK_OK;
 }
 

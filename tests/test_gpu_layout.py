@@ -1,0 +1,131 @@
+"""The two SpMV storage layouts (psk_csr_layout: CSR tiles / 256-row slices) give bit-identical y
+— and therefore bit-identical solver trajectories — on every SpMV mode the solvers use.
+
+Bar: bit-exact (scipy csr_matvec sums each row in stored order from 0.0 with rounded products;
+both layouts do exactly that, IterativeLinearSolver.py:94-106).
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import case_precond, golden_matrix, load_golden, product_prec_type, solver_cases
+
+from test_gpu_parity import _check_against_golden, _ragged_matrix
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def psk():
+    import pysolvers_amd
+    from pysolvers_amd import _native as N
+    assert N.device_count() >= 1, "no GPU visible to libpsk"
+    return pysolvers_amd
+
+
+def _ctl(**kw):
+    from pysolvers_amd import CommonSolverArgs
+    kw.setdefault("showIters", False)
+    kw.setdefault("showFinal", False)
+    return CommonSolverArgs(**kw)
+
+
+def test_layout_auto_choice(psk):
+    """FD rows fill every slot of a slice (sliced chosen); random ragged rows would pad (CSR kept)."""
+    assert psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, 64).layout == "sliced"
+    assert psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, 2).layout == "csr"      # one mostly empty slice
+    rng = np.random.default_rng(5)
+    assert psk.DeviceCSR.from_scipy(_ragged_matrix(rng, 5000)).layout == "csr"
+
+
+@pytest.mark.parametrize("n,long_rows,empty_rows", [
+    (1, (), ()), (7, (), (3,)), (257, (), (0, 256)), (5000, (17, 4096), (5, 6, 7)), (70001, (300,), (69999,)),
+])
+def test_spmv_both_layouts_bitwise(psk, n, long_rows, empty_rows):
+    """Ragged rows, empty rows, rows longer than the register slots (loop path), partial last slice."""
+    rng = np.random.default_rng(n + 11)
+    A = _ragged_matrix(rng, n, long_rows, empty_rows)
+    x = rng.standard_normal(n)
+    x[rng.integers(0, n, size=max(1, n // 50))] = -0.0
+    ref = A @ x
+    dA = psk.DeviceCSR.from_scipy(A)
+    for lay in ("sliced", "csr", "sliced"):
+        slots = dA.set_layout(lay)
+        assert dA.layout == lay
+        if lay == "sliced":
+            assert slots >= A.nnz
+        y = psk.mvmult(dA, x)
+        assert np.array_equal(y.view(np.uint64), ref.view(np.uint64)), lay
+
+
+def test_spmv_rectangular_both_layouts(psk):
+    """AMG transfer operators are rectangular (x has ncols entries)."""
+    rng = np.random.default_rng(3)
+    A = sp.random(3000, 700, density=0.004, random_state=4, format="csr")
+    x = rng.standard_normal(700)
+    dA = psk.DeviceCSR.from_scipy(A, rectangular=True)
+    for lay in ("csr", "sliced"):
+        dA.set_layout(lay)
+        assert np.array_equal(psk.mvmult(dA, x), A @ x)
+
+
+def test_fd_large_layouts_bitwise(psk):
+    """FD 3163^2 (the metric's N = 10M): the sliced y equals the C oracle's csr_matvec."""
+    from oracle import fdlap, native
+    m = 3163
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    assert dA.layout == "sliced"
+    x = np.random.default_rng(1).random(m * m)
+    ys = psk.mvmult(dA, x)
+    dA.set_layout("csr")
+    yc = psk.mvmult(dA, x)
+    assert np.array_equal(ys, yc)
+    assert np.array_equal(ys, native.csr_matvec(fdlap.fd_laplacian_2d(-1.0, 1.0, m), x))
+
+
+def _solve_case(psk, case, d, monkeypatch, layout):
+    """The golden case solved with every matrix (A and any AMG hierarchy operator) in `layout`."""
+    monkeypatch.setenv("PSK_SPMV_LAYOUT", layout)
+    ctl = _ctl(maxiter=case["maxiter"], tau=case["tau"], failOnMaxiter=bool(case["fail_on_maxiter"]))
+    f = psk.PCG if case["kind"] == "pcg" else psk.GMRES
+    return f(control=ctl, precond=product_prec_type(psk, case_precond(case))).makeSolver().solve(golden_matrix(d),
+                                                                                                 d["b"])
+
+
+@pytest.mark.parametrize("layout", ["csr", "sliced"])
+@pytest.mark.parametrize("case", solver_cases(), ids=lambda c: c["file"][:-4])
+def test_solver_matches_reference_each_layout(psk, case, layout, monkeypatch):
+    """Every golden solver case meets the parity bar with either layout forced everywhere. (The dot
+    products fused into the SpMV are summed per workgroup, so where a CSR tile is not 256 rows — DH
+    matrices, longer rows — the two layouts round p.Ap differently, like any other reduction order.)"""
+    d = load_golden(case["file"])
+    _check_against_golden(_solve_case(psk, case, d, monkeypatch, layout), d, case)
+
+
+@pytest.mark.parametrize("file", ["pcg_fd64_jacobi.npz", "pcg_fd128_jacobi.npz", "pcg_fd32_identity.npz",
+                                  "gmres_fd16_identity.npz", "gmres_fd32_jacobi.npz", "gmres_fd32_ilut.npz"])
+def test_fd_trajectories_bitwise_across_layouts(psk, file, monkeypatch):
+    """FD rows: a CSR tile is 256 rows, exactly one slice, so even the fused dot products (kSpmvDot,
+    kSpmvPlainDot, kSpmvJacobiDot, kSpmvResid) are summed in the same order: identical bits."""
+    case = next(c for c in solver_cases() if c["file"] == file)
+    d = load_golden(file)
+    s1 = _solve_case(psk, case, d, monkeypatch, "csr")
+    s2 = _solve_case(psk, case, d, monkeypatch, "sliced")
+    assert s1.iters() == s2.iters() and s1.success() == s2.success()
+    assert np.array_equal(s1.soln(), s2.soln())
+    assert np.array_equal(s1.info["hist"], s2.info["hist"])
+
+
+def test_amg_identical_across_layouts(psk, monkeypatch):
+    """AMG hierarchy operators (kSpmvResid, kSpmvPlain on R, kSpmvAdd on P) built under each layout."""
+    d = load_golden("pcg_negfd32_ic.npz")
+    A = golden_matrix(d)
+    out = []
+    for lay in ("csr", "sliced"):
+        monkeypatch.setenv("PSK_SPMV_LAYOUT", lay)
+        st = psk.PCG(control=_ctl(maxiter=200, tau=1e-8), precond=psk.AMG(numIters=2, numLevels=3)).makeSolver() \
+            .solve(A, d["b"])
+        out.append(st)
+    assert out[0].iters() == out[1].iters()
+    assert np.array_equal(out[0].soln(), out[1].soln())
+    assert np.array_equal(out[0].info["hist"], out[1].info["hist"])

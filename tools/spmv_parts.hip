@@ -64,7 +64,12 @@ __global__ __launch_bounds__(BS) void spmv_v(int64_t n, const int *__restrict__ 
     }
     double pv[KU];
 #pragma unroll
-    for (int k = 0; k < KU; ++k) pv[k] = vv[k] * (V == 1 ? 1.0 : x[cc[k]]);
+    for (int k = 0; k < KU; ++k) {
+        // V == 5: the gather stays inside the tile's own 256-row x window (dependent on colidx, but
+        // every load an L1/L2 hit) — separates the dependent round trip from where x comes from
+        const int64_t gi = V == 5 ? r0 + ((cc[k] & 255) < (r1 - r0) ? (cc[k] & 255) : 0) : (int64_t)cc[k];
+        pv[k] = vv[k] * (V == 1 ? 1.0 : x[gi]);
+    }
     if (V == 2) {
 #pragma unroll
         for (int k = 0; k < KU; ++k) sum += pv[k];
@@ -191,7 +196,8 @@ int main(int argc, char **argv) {
                              {"nogather", spmv_v<1>, full - 8.0 * n},
                              {"nolds", spmv_v<2>, full},
                              {"stream", spmv_v<3>, full - 8.0 * n},
-                             {"rowptr", spmv_v<4>, 4.0 * (n + 1) + 8.0 * n}};
+                             {"rowptr", spmv_v<4>, 4.0 * (n + 1) + 8.0 * n},
+                             {"owngather", spmv_v<5>, full}};
         const unsigned grid = (unsigned)((n + TR - 1) / TR);
         // working-set probe: the same kernels over the first n/16 rows of the big matrix
         {
