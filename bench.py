@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1c_pmc_traffic_16384.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1d_pmc_traffic_16384.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same kernel and side")
     args = ap.parse_args()
 
@@ -189,6 +189,10 @@ def main():
         nnz_loc = ctypes.c_int64()
         N.check(N.lib.psk_csr_info(A, None, ctypes.byref(nnz_loc)), "info")
         bspmv = spmv_bytes(nloc_r0, nnz_loc.value)
+        lay, slots = N.I32(), N.I64()
+        N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), ctypes.byref(slots)), "psk_csr_layout")
+        sliced = lay.value == N.PSK_LAYOUT_SLICED
+        kname = "spmv_sliced_kernel<kSpmvDot>" if sliced else "spmv_kernel<kSpmvDot>"
         ach = bspmv / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
         biter = pcg_iter_bytes(n, nnz)
         out = {
@@ -209,12 +213,14 @@ def main():
                                    % (m, m, n, nnz),
                        "m": m, "precond": "jacobi", "parallelism": "row-block x%d (%s)" % (world, "RCCL" if transport == "rccl" else "host-shm rehearsal")
                        if world > 1 else "single GPU"},
-            "roofline": {"bound": "hbm", "kernel": "spmv_kernel<kSpmvDot> (rank 0)",
+            "roofline": {"bound": "hbm", "kernel": kname + " (rank 0)",
                          "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (ach / HBM_PEAK_GBPS) if ach else None,
-                         **pmc_traffic(args.traffic_json, m, world),
+                         **pmc_traffic(args.traffic_json, m, world, sliced),
                          "algorithmic_bytes_per_launch": bspmv, "avg_launch_ms": res.spmv_ms,
-                         "launches": res.spmv_launches},
+                         "launches": res.spmv_launches,
+                         "layout": "sliced" if sliced else "csr",
+                         "layout_bytes_per_launch": sliced_bytes(nloc_r0, slots.value) if sliced else bspmv},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
@@ -245,7 +251,12 @@ def main():
         dist.destroy_process_group()
 
 
-def pmc_traffic(path, m, world):
+def sliced_bytes(n, slots):
+    """Compulsory bytes of the sliced-layout SpMV: 12 B per padded slot, slice offsets, x once, y."""
+    return 12 * slots + 8 * ((n + 255) // 256 + 1) + 16 * n
+
+
+def pmc_traffic(path, m, world, sliced):
     """HBM bytes per SpMV launch measured by rocprofv3 PMC passes on the same kernel and matrix
     (scripts/gpu_pmc.sh -> tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections
     calibrated by tools/pmc_calib.hip). Counters cannot be read from inside the timed run."""
@@ -256,8 +267,9 @@ def pmc_traffic(path, m, world):
         return {"traffic": None}
     if d.get("config", {}).get("side") != m or world != 1:
         return {"traffic": None}
+    want = "void psk::spmv_sliced_kernel<1>" if sliced else "void psk::spmv_kernel<1>"
     for k, v in d["kernels"].items():
-        if k.startswith("void psk::spmv_kernel<1>"):
+        if k.startswith(want):
             return {"traffic": v["hbm_bytes_per_launch"],
                     "traffic_source": os.path.relpath(path, REPO) + " (rocprofv3 PMC, same kernel/config)"}
     return {"traffic": None}
