@@ -189,9 +189,10 @@ def main():
         nnz_loc = ctypes.c_int64()
         N.check(N.lib.psk_csr_info(A, None, ctypes.byref(nnz_loc)), "info")
         bspmv = spmv_bytes(nloc_r0, nnz_loc.value)
-        lay, slots = N.I32(), N.I64()
-        N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), ctypes.byref(slots)), "psk_csr_layout")
-        sliced = lay.value == N.PSK_LAYOUT_SLICED
+        lay, slots, packed, stream = N.I32(), N.I64(), N.I64(), N.I64()
+        N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), ctypes.byref(slots), ctypes.byref(packed),
+                                     ctypes.byref(stream)), "psk_csr_layout")
+        sliced = lay.value != N.PSK_LAYOUT_CSR
         kname = "spmv_sliced_kernel<kSpmvDot>" if sliced else "spmv_kernel<kSpmvDot>"
         ach = bspmv / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
         biter = pcg_iter_bytes(n, nnz)
@@ -219,8 +220,9 @@ def main():
                          **pmc_traffic(args.traffic_json, m, world, sliced),
                          "algorithmic_bytes_per_launch": bspmv, "avg_launch_ms": res.spmv_ms,
                          "launches": res.spmv_launches,
-                         "layout": "sliced" if sliced else "csr",
-                         "layout_bytes_per_launch": sliced_bytes(nloc_r0, slots.value) if sliced else bspmv},
+                         "layout": {N.PSK_LAYOUT_CSR: "csr", N.PSK_LAYOUT_SLICED: "sliced",
+                                    N.PSK_LAYOUT_SLICED_WIDE: "sliced_wide"}[lay.value],
+                         "layout_bytes_per_launch": stream.value + 16 * nloc_r0},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
@@ -249,11 +251,6 @@ def main():
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
-
-
-def sliced_bytes(n, slots):
-    """Compulsory bytes of the sliced-layout SpMV: 12 B per padded slot, slice offsets, x once, y."""
-    return 12 * slots + 8 * ((n + 255) // 256 + 1) + 16 * n
 
 
 def pmc_traffic(path, m, world, sliced):

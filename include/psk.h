@@ -123,18 +123,26 @@ int psk_csr_create_rect(int64_t nrows, int64_t ncols, int64_t nnz, const int32_t
                         const double *vals, int32_t loc, psk_csr **out);
 int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
 /* SpMV storage layout of A (same y bit for bit either way; the CSR arrays are always kept):
- *   PSK_LAYOUT_CSR    one workgroup per tile of rows, the tile's entries streamed in stored order
- *                     and the products staged through LDS;
- *   PSK_LAYOUT_SLICED a sliced copy: 256-row slices, slot-major inside a slice, one row per lane,
- *                     padding slots (column -1) up to the slice's widest row.
- * Every creation path picks SLICED when its padded stream is no larger than the CSR stream
- * (12 B/slot <= 12 B/entry + 4 B/row); env PSK_SPMV_LAYOUT=csr|sliced overrides. set = -1
- * queries, PSK_LAYOUT_CSR / PSK_LAYOUT_SLICED switches (building or freeing the copy); *slots =
- * padded entries of the sliced copy (0 without one). Out pointers may be NULL. Replaces nothing in
- * the reference (scipy keeps CSR); it is a device storage choice under mvmult (IterativeLinearSolver.py:94-106). */
-#define PSK_LAYOUT_CSR    0
-#define PSK_LAYOUT_SLICED 1
-int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots);
+ *   PSK_LAYOUT_CSR          one workgroup per tile of rows, the tile's entries streamed in stored
+ *                           order and the products staged through LDS;
+ *   PSK_LAYOUT_SLICED       a sliced copy: 256-row slices, slot-major inside a slice, one row per
+ *                           lane, padding slots up to the slice's widest row, values in slot pairs
+ *                           (16-B loads); a slice whose columns all lie within +-32767 of their rows
+ *                           stores 16-bit column deltas two to a 32-bit word, any other slice 32-bit
+ *                           columns;
+ *   PSK_LAYOUT_SLICED_WIDE  the same with 32-bit columns in every slice.
+ * Every creation path picks SLICED when its stream is no larger than the CSR stream (12 B/entry +
+ * 4 B/row); env PSK_SPMV_LAYOUT=csr|sliced|sliced_wide overrides. set = -1 queries, a PSK_LAYOUT_*
+ * value switches (building or freeing the copy). Out: *slots = padded slots of the sliced copy (0
+ * without one), *packed_slots = those in 16-bit slices, *stream_bytes = matrix bytes one SpMV
+ * streams in the current layout (CSR: 12 nnz + 4 (n+1)). Out pointers may be NULL. Replaces
+ * nothing in the reference (scipy keeps CSR): a device storage choice under mvmult
+ * (IterativeLinearSolver.py:94-106). */
+#define PSK_LAYOUT_CSR         0
+#define PSK_LAYOUT_SLICED      1
+#define PSK_LAYOUT_SLICED_WIDE 2
+int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int64_t *packed_slots,
+                   int64_t *stream_bytes);
 /* Copy the arrays back to host buffers (any pointer may be NULL). */
 int psk_csr_download(const psk_csr *A, int32_t *rowptr, int32_t *colidx, double *vals);
 int psk_csr_destroy(psk_csr *A);

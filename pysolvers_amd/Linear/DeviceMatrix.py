@@ -126,19 +126,22 @@ class DeviceCSR:
     def handle(self):
         return self._h
 
+    _LAYOUTS = {"csr": 0, "sliced": 1, "sliced_wide": 2}
+
     @property
     def layout(self):
-        """SpMV storage layout: "csr" or "sliced" (psk_csr_layout; y is bit-identical either way)."""
+        """SpMV storage layout: "csr", "sliced" (16-bit column deltas where they fit) or
+        "sliced_wide" (psk_csr_layout; y is bit-identical in every layout)."""
         k = N.I32()
-        N.check(N.lib.psk_csr_layout(self._h, -1, ctypes.byref(k), None), "psk_csr_layout")
-        return "sliced" if k.value == N.PSK_LAYOUT_SLICED else "csr"
+        N.check(N.lib.psk_csr_layout(self._h, -1, ctypes.byref(k), None, None, None), "psk_csr_layout")
+        return {v: n for n, v in self._LAYOUTS.items()}[k.value]
 
     def set_layout(self, layout):
-        """Switch the SpMV storage layout ("csr" or "sliced"); returns the padded slot count."""
-        k = {"csr": N.PSK_LAYOUT_CSR, "sliced": N.PSK_LAYOUT_SLICED}[layout]
-        slots = N.I64()
-        N.check(N.lib.psk_csr_layout(self._h, k, None, ctypes.byref(slots)), "psk_csr_layout")
-        return slots.value
+        """Switch the SpMV storage layout; returns (padded slots, slots in 16-bit slices)."""
+        slots, packed = N.I64(), N.I64()
+        N.check(N.lib.psk_csr_layout(self._h, self._LAYOUTS[layout], None, ctypes.byref(slots), ctypes.byref(packed),
+                                     None), "psk_csr_layout")
+        return slots.value, packed.value
 
     def to_scipy(self):
         indptr = np.empty(self.n + 1, dtype=np.int32)

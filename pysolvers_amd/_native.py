@@ -15,7 +15,7 @@ PSK_OK = 0
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_HOST, PSK_DEVICE = 0, 1
 PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
-PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED = 0, 1
+PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE = 0, 1, 2
 PSK_UNIQUE_ID_BYTES = 128
 
 STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOWN: "breakdown",
@@ -54,7 +54,7 @@ SIGNATURES = {
     "psk_csr_create_fd2d": (ctypes.c_int, [F64, F64, I64, PP]),
     "psk_csr_create_rect": (ctypes.c_int, [I64, I64, I64, P, P, P, I32, PP]),
     "psk_csr_info": (ctypes.c_int, [P, ctypes.POINTER(I64), ctypes.POINTER(I64)]),
-    "psk_csr_layout": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I64)]),
+    "psk_csr_layout": (ctypes.c_int, [P, I32, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 3),
     "psk_csr_download": (ctypes.c_int, [P, P, P, P]),
     "psk_csr_destroy": (ctypes.c_int, [P]),
     "psk_spmv": (ctypes.c_int, [P, P, P, I32]),

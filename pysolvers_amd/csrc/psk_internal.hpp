@@ -120,12 +120,16 @@ struct psk_csr {
     double *vals = nullptr;
     int device = 0;
     // sliced copy of the same entries (spmv.hip, "sliced layout"): slices of kSlice rows, slot-major
-    // inside a slice (slot j of lane l at sl_off[t] + j*kSlice + l), padding slots hold column -1.
-    // Present when the SpMV uses it (psk_csr_layout); the CSR arrays above are always kept.
+    // inside a slice (values in slot pairs), per slice either packed int16 column-delta pairs
+    // (sl_fmt[t] = 1, sl_pcol) or int32 columns (sl_col); every array is addressed from the slice's
+    // slot offset sl_off[t]. Present when the SpMV uses it (psk_csr_layout); the CSR arrays above
+    // are always kept.
     int64_t *sl_off = nullptr;   // [nslices + 1] slot offsets
-    int32_t *sl_col = nullptr;
+    int8_t *sl_fmt = nullptr;    // [nslices] 1 = packed (int16 deltas)
+    int32_t *sl_col = nullptr;   // nullptr when every slice is packed
+    int32_t *sl_pcol = nullptr;  // nullptr when no slice is packed (2 int16 deltas per word)
     double *sl_val = nullptr;
-    int64_t sl_slots = 0;
+    int64_t sl_slots = 0, sl_packed_slots = 0, sl_stream_bytes = 0;
     // distributed
     psk_comm *comm = nullptr;
     int64_t n_global = 0, row_begin = 0, row_end = 0;

@@ -140,16 +140,33 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
 // a CSR tile's gather instruction mixes the 5 neighbour offsets of ~13 rows (more cache lines and
 // address work per load). Each lane still sums ITS row in stored order from 0.0 with rounded
 // products, so y is bit-identical to csr_matvec and to spmv_kernel. Padding slots (rows shorter
-// than the slice's widest row) hold column -1 and are skipped. No rowptr stream, no LDS staging.
-// tools/spmv_parts.hip / tools/sell_lab.hip: 3.48 ms vs 3.57-3.92 ms (CSR) at 16384^2.
+// than the slice's widest row) are skipped. No rowptr stream, no LDS staging.
+// Storage of a slice of width w (slot offset o = sl_off[t], all arrays indexed from o):
+//  * values in slot PAIRS: slots 2p, 2p+1 of lane l adjacent at o + 2p*256 + 2l (one 16-B load per
+//    pair); an odd last slot at o + (w-1)*256 + l;
+//  * columns, by sl_fmt[t]: a "packed" slice (every column within +-32767 of its row) stores the
+//    int16 deltas c - row of slots 2p, 2p+1 in ONE int32 word at o + p*256 + l (kPad16 = padding),
+//    i.e. 2 B per slot in full 256-B wave loads; any other slice int32 columns at o + j*256 + l
+//    (-1 = padding). FD: 10.4 B per slot instead of 12 (every slice but a shard's halo lines).
+// tools/sell_lab.hip, tools/sell_pack_lab.hip (16384^2, back to back): CSR 3.61 ms, int32 columns
+// 3.20-3.39 ms, 16-bit pairs + paired values 2.87 ms; all bit-identical.
 constexpr int kSlice = kBlock;
-constexpr int kSliceRegs = 8;   // slots held in registers; wider slices take the loop below
+constexpr int kSliceRegs = 8;             // slots held in registers; wider slices take the loop below
+constexpr int16_t kPad16 = INT16_MIN;     // padding slot of a packed slice
+constexpr int64_t kMaxDelta16 = 32767;
+
+// value of slot j (of w) of lane l in a slice at slot offset o
+__device__ __forceinline__ int64_t sliced_vpos(int64_t o, int j, int w, int l) {
+    return (j | 1) < w ? o + (int64_t)(j & ~1) * kSlice + 2 * l + (j & 1) : o + (int64_t)j * kSlice + l;
+}
+
+__device__ __forceinline__ int32_t unpack_delta(int32_t row, int16_t d) { return d == kPad16 ? -1 : row + (int32_t)d; }
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
-    int64_t n, const int64_t *__restrict__ soff, const int32_t *__restrict__ scol,
-    const double *__restrict__ sval, const double *__restrict__ x, double *__restrict__ y,
-    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs,
+    int64_t n, const int64_t *__restrict__ soff, const int8_t *__restrict__ sfmt, const int32_t *__restrict__ scol,
+    const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ x,
+    double *__restrict__ y, const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs,
     const int32_t *__restrict__ done) {
     if (done != nullptr && *done != 0) return;
     __shared__ double sh[kWaves];
@@ -158,8 +175,8 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const bool has = row < n;
     const int64_t o = soff[t];
     const int w = (int)((soff[t + 1] - o) / kSlice);
-    const int32_t *sc = scol + o + tid;
-    const double *sv = sval + o + tid;
+    const bool packed = sfmt[t] != 0;   // uniform across the workgroup
+    const int32_t row32 = (int32_t)row;
     double eq = 0.0;
     if (has) {
         if (MODE == kSpmvDot) eq = x[row];
@@ -171,13 +188,33 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
         int32_t cc[kSliceRegs];
         double vv[kSliceRegs], xv[kSliceRegs];
 #pragma unroll
-        for (int j = 0; j < kSliceRegs; ++j) {   // the slice's whole stream first (w is uniform)
+        for (int j = 0; j < kSliceRegs; ++j) {
             cc[j] = -1;
             vv[j] = 0.0;
-            if (j < w) {
-                cc[j] = ld_stream(sc + j * kSlice);
-                vv[j] = ld_stream(sv + j * kSlice);
+        }
+        // the slice's whole stream first (w and packed are uniform): values by pairs, then columns
+#pragma unroll
+        for (int p = 0; p < kSliceRegs / 2; ++p) {
+            if (2 * p + 1 < w) {
+                const dv2 v2 = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(sval + o + 2 * p * kSlice) + tid);
+                vv[2 * p] = v2.x;
+                vv[2 * p + 1] = v2.y;
+            } else if (2 * p < w) {
+                vv[2 * p] = ld_stream(sval + o + 2 * p * kSlice + tid);
             }
+        }
+        if (packed) {
+#pragma unroll
+            for (int p = 0; p < kSliceRegs / 2; ++p)
+                if (2 * p < w) {
+                    const int32_t word = ld_stream(spcol + o + p * kSlice + tid);
+                    cc[2 * p] = unpack_delta(row32, (int16_t)(word & 0xffff));
+                    cc[2 * p + 1] = unpack_delta(row32, (int16_t)(word >> 16));
+                }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kSliceRegs; ++j)
+                if (j < w) cc[j] = ld_stream(scol + o + j * kSlice + tid);
         }
 #pragma unroll
         for (int j = 0; j < kSliceRegs; ++j) {   // then every gather
@@ -192,11 +229,17 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
     } else {
         for (int j = 0; j < w; ++j) {
-            const int32_t c = ld_stream(sc + (int64_t)j * kSlice);
+            int32_t c;
+            if (packed) {
+                const int32_t word = ld_stream(spcol + o + (int64_t)(j >> 1) * kSlice + tid);
+                c = unpack_delta(row32, (int16_t)((j & 1) ? (word >> 16) : (word & 0xffff)));
+            } else {
+                c = ld_stream(scol + o + (int64_t)j * kSlice + tid);
+            }
             if (c < 0) break;   // only padding follows a row's last entry
             double xx = x[c];
             if (MODE == kSpmvJacobiDot) xx = aux_d[c] * xx;
-            sum = sum + ld_stream(sv + (int64_t)j * kSlice) * xx;
+            sum = sum + ld_stream(sval + sliced_vpos(o, j, w, tid)) * xx;
         }
     }
     double acc = 0.0;
@@ -218,23 +261,42 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     }
 }
 
-// widest row of every slice
-__global__ __launch_bounds__(kBlock) void sliced_width_kernel(int64_t n, const int32_t *__restrict__ rowptr,
-                                                              int32_t *__restrict__ width) {
-    __shared__ int32_t sh[kWaves];
+// per slice: widest row, and the largest |column - row| of its entries (saturated to int32)
+__global__ __launch_bounds__(kBlock) void sliced_shape_kernel(int64_t n, const int32_t *__restrict__ rowptr,
+                                                              const int32_t *__restrict__ colidx,
+                                                              int32_t *__restrict__ width, int32_t *__restrict__ span) {
+    __shared__ int32_t sh[2 * kWaves];
     const int64_t row = (int64_t)blockIdx.x * kSlice + threadIdx.x;
-    int32_t len = row < n ? rowptr[row + 1] - rowptr[row] : 0;
+    int32_t len = 0, dmax = 0;
+    if (row < n) {
+        const int32_t a = rowptr[row], b = rowptr[row + 1];
+        len = b - a;
+        for (int32_t e = a; e < b; ++e) {
+            int64_t d = (int64_t)colidx[e] - row;
+            d = d < 0 ? -d : d;
+            const int32_t ds = d > INT32_MAX ? INT32_MAX : (int32_t)d;
+            dmax = ds > dmax ? ds : dmax;
+        }
+    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-        const int32_t v = __shfl_xor(len, o, 64);
+        const int32_t v = __shfl_xor(len, o, 64), u = __shfl_xor(dmax, o, 64);
         len = v > len ? v : len;
+        dmax = u > dmax ? u : dmax;
     }
-    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = len;
+    if ((threadIdx.x & 63) == 0) {
+        sh[threadIdx.x >> 6] = len;
+        sh[kWaves + (threadIdx.x >> 6)] = dmax;
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
-        int32_t m = sh[0];
-        for (int i = 1; i < kWaves; ++i) m = sh[i] > m ? sh[i] : m;
+        int32_t m = sh[0], dm = sh[kWaves];
+        for (int i = 1; i < kWaves; ++i) {
+            m = sh[i] > m ? sh[i] : m;
+            dm = sh[kWaves + i] > dm ? sh[kWaves + i] : dm;
+        }
         width[blockIdx.x] = m;
+        span[blockIdx.x] = dm;
     }
 }
 
@@ -243,32 +305,46 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
                                                              const int32_t *__restrict__ colidx,
                                                              const double *__restrict__ vals,
                                                              const int64_t *__restrict__ soff,
-                                                             int32_t *__restrict__ scol, double *__restrict__ sval) {
-    const int64_t t = blockIdx.x, row = t * kSlice + threadIdx.x;
-    const int64_t o = soff[t], w = (soff[t + 1] - o) / kSlice;
+                                                             const int8_t *__restrict__ sfmt, int32_t *__restrict__ scol,
+                                                             int32_t *__restrict__ spcol, double *__restrict__ sval) {
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x, row = t * kSlice + tid;
+    const int64_t o = soff[t];
+    const int w = (int)((soff[t + 1] - o) / kSlice);
+    const bool packed = sfmt[t] != 0;
     const int64_t a = row < n ? rowptr[row] : 0;
     const int64_t len = row < n ? rowptr[row + 1] - a : 0;
-    for (int64_t j = 0; j < w; ++j) {
-        const int64_t s = o + j * kSlice + threadIdx.x;
-        scol[s] = j < len ? colidx[a + j] : -1;
-        sval[s] = j < len ? vals[a + j] : 0.0;
+    for (int j = 0; j < w; ++j) {
+        sval[sliced_vpos(o, j, w, tid)] = j < len ? vals[a + j] : 0.0;
+        if (!packed) scol[o + (int64_t)j * kSlice + tid] = j < len ? colidx[a + j] : -1;
     }
+    if (packed)
+        for (int p = 0; 2 * p < w; ++p) {
+            const int j0 = 2 * p, j1 = 2 * p + 1;
+            const int16_t d0 = j0 < len ? (int16_t)(colidx[a + j0] - row) : kPad16;
+            const int16_t d1 = j1 < len ? (int16_t)(colidx[a + j1] - row) : kPad16;
+            spcol[o + (int64_t)p * kSlice + tid] = (int32_t)(uint16_t)d0 | ((int32_t)d1 * 65536);
+        }
 }
 
 void sliced_free(psk_csr *A) {
-    if (A->sl_off) (void)hipFree(A->sl_off);
-    if (A->sl_col) (void)hipFree(A->sl_col);
-    if (A->sl_val) (void)hipFree(A->sl_val);
+    void *ptrs[] = {A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val};
+    for (void *p : ptrs)
+        if (p) (void)hipFree(p);
     A->sl_off = nullptr;
+    A->sl_fmt = nullptr;
     A->sl_col = nullptr;
+    A->sl_pcol = nullptr;
     A->sl_val = nullptr;
     A->sl_slots = 0;
+    A->sl_packed_slots = 0;
+    A->sl_stream_bytes = 0;
 }
 
-// Builds the sliced copy of A. Unless `force`, only when its stream (12 B per slot) is no larger
-// than the CSR stream (12 B per entry + 4 B per row), i.e. padding costs nothing, and quietly
-// keeps CSR if HBM cannot hold the copy.
-static int sliced_build(psk_csr *A, hipStream_t s, bool force) {
+// Builds the sliced copy of A (pack = allow int16 column deltas). Unless `force`, only when its
+// stream (10 or 12 B per slot) is no larger than the CSR stream (12 B per entry + 4 B per row),
+// i.e. padding costs nothing, and quietly keeps CSR if HBM cannot hold the copy.
+static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack) {
     sliced_free(A);
     const int64_t nt = (A->n + kSlice - 1) / kSlice;
     if (nt == 0) return PSK_OK;   // nothing to multiply (launch_spmv returns early)
@@ -278,38 +354,59 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force) {
         DevBuf &b;
         ~Release() { b.release(); }
     } rel{tmp};
-    PSK_TRY(tmp.ensure((size_t)nt * sizeof(int32_t)));
-    hipLaunchKernelGGL(sliced_width_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, tmp.as<int32_t>());
+    PSK_TRY(tmp.ensure((size_t)nt * 2 * sizeof(int32_t)));
+    int32_t *dw = tmp.as<int32_t>(), *dspan = dw + nt;
+    hipLaunchKernelGGL(sliced_shape_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, dw,
+                       dspan);
     PSK_HIP(hipGetLastError());
-    std::vector<int32_t> wd((size_t)nt);
-    PSK_HIP(hipMemcpyAsync(wd.data(), tmp.p, (size_t)nt * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    std::vector<int32_t> wd((size_t)nt * 2);
+    PSK_HIP(hipMemcpyAsync(wd.data(), tmp.p, (size_t)nt * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
     std::vector<int64_t> off((size_t)nt + 1);
+    std::vector<int8_t> fmt((size_t)nt);
     off[0] = 0;
-    for (int64_t t = 0; t < nt; ++t) off[(size_t)t + 1] = off[(size_t)t] + (int64_t)wd[(size_t)t] * kSlice;
+    int64_t packed_slots = 0, col_bytes = 0;
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t w = wd[(size_t)t];
+        off[(size_t)t + 1] = off[(size_t)t] + w * kSlice;
+        fmt[(size_t)t] = (pack && wd[(size_t)(nt + t)] <= kMaxDelta16) ? 1 : 0;
+        if (fmt[(size_t)t]) packed_slots += w * kSlice;
+        col_bytes += (fmt[(size_t)t] ? 4 * ((w + 1) / 2) : 4 * w) * kSlice;
+    }
     const int64_t slots = off[(size_t)nt];
-    if (!force && 12 * slots > 12 * A->nnz + 4 * (A->n + 1)) return PSK_OK;
+    const int64_t wide_slots = slots - packed_slots;
+    // matrix bytes one SpMV streams: values, columns, slice offsets and formats
+    const int64_t stream = 8 * slots + col_bytes + 9 * nt + 8;
+    if (!force && stream > 12 * A->nnz + 4 * (A->n + 1)) return PSK_OK;
     const size_t ms = slots > 0 ? (size_t)slots : 1;
-    if (hipMalloc(&A->sl_off, (size_t)(nt + 1) * 8) != hipSuccess || hipMalloc(&A->sl_col, ms * 4) != hipSuccess ||
-        hipMalloc(&A->sl_val, ms * 8) != hipSuccess) {
+    bool ok = hipMalloc(&A->sl_off, (size_t)(nt + 1) * 8) == hipSuccess &&
+              hipMalloc(&A->sl_fmt, (size_t)nt) == hipSuccess && hipMalloc(&A->sl_val, ms * 8) == hipSuccess;
+    if (ok && wide_slots > 0) ok = hipMalloc(&A->sl_col, ms * 4) == hipSuccess;      // indexed by slot
+    if (ok && packed_slots > 0) ok = hipMalloc(&A->sl_pcol, ms * 4) == hipSuccess;   // words from each slice's o
+    if (!ok) {
         (void)hipGetLastError();
         sliced_free(A);
         return force ? fail(PSK_ERR_ALLOC, "sliced layout: hipMalloc") : PSK_OK;
     }
     PSK_HIP(hipMemcpyAsync(A->sl_off, off.data(), (size_t)(nt + 1) * 8, hipMemcpyHostToDevice, s));
+    PSK_HIP(hipMemcpyAsync(A->sl_fmt, fmt.data(), (size_t)nt, hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(sliced_fill_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, A->vals,
-                       A->sl_off, A->sl_col, A->sl_val);
+                       A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val);
     PSK_HIP(hipGetLastError());
     PSK_HIP(hipStreamSynchronize(s));
     A->sl_slots = slots;
+    A->sl_packed_slots = packed_slots;
+    A->sl_stream_bytes = stream;
+    (void)wide_slots;
     return PSK_OK;
 }
 
 int csr_choose_layout(psk_csr *A, hipStream_t s) {
     const char *e = std::getenv("PSK_SPMV_LAYOUT");
     if (e && std::strcmp(e, "csr") == 0) return PSK_OK;
-    const bool force = e && std::strcmp(e, "sliced") == 0;
-    int rc = sliced_build(A, s, force);
+    const bool wide = e && std::strcmp(e, "sliced_wide") == 0;
+    const bool force = e && (std::strcmp(e, "sliced") == 0 || wide);
+    int rc = sliced_build(A, s, force, !wide);
     if (rc != PSK_OK) sliced_free(A);
     return rc;
 }
@@ -336,8 +433,8 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     dim3 gd((unsigned)nwg), bd(kBlock);
     if (sliced) {
 #define PSK_SLICED_LAUNCH(M)                                                                                 \
-    hipLaunchKernelGGL(spmv_sliced_kernel<M>, gd, bd, 0, s, A->n, A->sl_off, A->sl_col, A->sl_val, x, y, aux_d, \
-                       aux_q, gs, done_flag)
+    hipLaunchKernelGGL(spmv_sliced_kernel<M>, gd, bd, 0, s, A->n, A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, \
+                       A->sl_val, x, y, aux_d, aux_q, gs, done_flag)
         switch (mode) {
         case kSpmvPlain: PSK_SLICED_LAUNCH(kSpmvPlain); break;
         case kSpmvDot: PSK_SLICED_LAUNCH(kSpmvDot); break;
@@ -627,19 +724,23 @@ int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz) {
     return PSK_OK;
 }
 
-int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots) {
+int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int64_t *packed_slots,
+                   int64_t *stream_bytes) {
     if (!A) return fail(PSK_ERR_ARG, "psk_csr_layout: NULL matrix");
-    if (set != -1 && set != PSK_LAYOUT_CSR && set != PSK_LAYOUT_SLICED)
-        return fail(PSK_ERR_ARG, "psk_csr_layout: set must be -1, PSK_LAYOUT_CSR or PSK_LAYOUT_SLICED");
-    if (set == PSK_LAYOUT_CSR) sliced_free(A);
-    if (set == PSK_LAYOUT_SLICED && !A->sl_off && A->n > 0) {
+    if (set != -1 && set != PSK_LAYOUT_CSR && set != PSK_LAYOUT_SLICED && set != PSK_LAYOUT_SLICED_WIDE)
+        return fail(PSK_ERR_ARG, "psk_csr_layout: set must be -1 or a PSK_LAYOUT_* value");
+    if (set != -1) {
         Context *c;
         PSK_TRY(ctx(&c));
-        PSK_HIP(hipStreamSynchronize(c->stream));   // queued launches may still read the layout
-        PSK_TRY(sliced_build(A, c->stream, true));
+        PSK_HIP(hipStreamSynchronize(c->stream));   // queued launches may still read the old layout
+        if (set == PSK_LAYOUT_CSR) sliced_free(A);
+        else PSK_TRY(sliced_build(A, c->stream, true, set == PSK_LAYOUT_SLICED));
     }
-    if (layout) *layout = A->sl_off ? PSK_LAYOUT_SLICED : PSK_LAYOUT_CSR;
+    if (layout) *layout = !A->sl_off ? PSK_LAYOUT_CSR : (A->sl_col && !A->sl_pcol ? PSK_LAYOUT_SLICED_WIDE
+                                                                                 : PSK_LAYOUT_SLICED);
     if (slots) *slots = A->sl_slots;
+    if (packed_slots) *packed_slots = A->sl_packed_slots;
+    if (stream_bytes) *stream_bytes = A->sl_off ? A->sl_stream_bytes : 12 * A->nnz + 4 * (A->n + 1);
     return PSK_OK;
 }
 

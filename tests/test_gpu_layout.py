@@ -41,30 +41,53 @@ def test_layout_auto_choice(psk):
 @pytest.mark.parametrize("n,long_rows,empty_rows", [
     (1, (), ()), (7, (), (3,)), (257, (), (0, 256)), (5000, (17, 4096), (5, 6, 7)), (70001, (300,), (69999,)),
 ])
-def test_spmv_both_layouts_bitwise(psk, n, long_rows, empty_rows):
-    """Ragged rows, empty rows, rows longer than the register slots (loop path), partial last slice."""
+def test_spmv_every_layout_bitwise(psk, n, long_rows, empty_rows):
+    """Ragged rows, empty rows, rows longer than the register slots (loop path), partial last slice;
+    n <= 32768 packs every slice (16-bit deltas), n = 70001 leaves most slices wide."""
     rng = np.random.default_rng(n + 11)
     A = _ragged_matrix(rng, n, long_rows, empty_rows)
     x = rng.standard_normal(n)
     x[rng.integers(0, n, size=max(1, n // 50))] = -0.0
     ref = A @ x
     dA = psk.DeviceCSR.from_scipy(A)
-    for lay in ("sliced", "csr", "sliced"):
-        slots = dA.set_layout(lay)
-        assert dA.layout == lay
-        if lay == "sliced":
+    for lay in ("sliced", "csr", "sliced_wide", "sliced"):
+        slots, packed = dA.set_layout(lay)
+        assert dA.layout == lay or (lay == "sliced" and packed == 0 and dA.layout == "sliced_wide")
+        if lay != "csr":
             assert slots >= A.nnz
+        if lay == "sliced" and n <= 32768:
+            assert packed == slots
+        if lay == "sliced_wide":
+            assert packed == 0
         y = psk.mvmult(dA, x)
         assert np.array_equal(y.view(np.uint64), ref.view(np.uint64)), lay
 
 
-def test_spmv_rectangular_both_layouts(psk):
+def test_spmv_mixed_packed_and_wide_slices(psk):
+    """A banded matrix with a few far-off entries: the slices holding them stay 32-bit, the rest pack."""
+    rng = np.random.default_rng(21)
+    n = 100000
+    A = sp.diags([rng.standard_normal(n - 300), rng.standard_normal(n), rng.standard_normal(n - 1)], [-300, 0, 1],
+                 format="lil")
+    for i in (10, 40000, 99999):
+        A[i, (i + 50000) % n] = 2.5
+        A[i, (i + 32767) % n] = -1.5
+    A = A.tocsr()
+    x = rng.standard_normal(n)
+    dA = psk.DeviceCSR.from_scipy(A)
+    assert dA.layout == "sliced"
+    slots, packed = dA.set_layout("sliced")
+    assert 0 < packed < slots
+    assert np.array_equal(psk.mvmult(dA, x), A @ x)
+
+
+def test_spmv_rectangular_every_layout(psk):
     """AMG transfer operators are rectangular (x has ncols entries)."""
     rng = np.random.default_rng(3)
     A = sp.random(3000, 700, density=0.004, random_state=4, format="csr")
     x = rng.standard_normal(700)
     dA = psk.DeviceCSR.from_scipy(A, rectangular=True)
-    for lay in ("csr", "sliced"):
+    for lay in ("csr", "sliced", "sliced_wide"):
         dA.set_layout(lay)
         assert np.array_equal(psk.mvmult(dA, x), A @ x)
 
@@ -76,11 +99,15 @@ def test_fd_large_layouts_bitwise(psk):
     dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
     assert dA.layout == "sliced"
     x = np.random.default_rng(1).random(m * m)
+    slots, packed = dA.set_layout("sliced")
+    nnz = 5 * m * m - 4 * m
+    assert packed == slots and nnz <= slots < nnz + 4 * m + 5 * 256   # all 16-bit; pads: boundary rows, last slice
     ys = psk.mvmult(dA, x)
-    dA.set_layout("csr")
-    yc = psk.mvmult(dA, x)
-    assert np.array_equal(ys, yc)
-    assert np.array_equal(ys, native.csr_matvec(fdlap.fd_laplacian_2d(-1.0, 1.0, m), x))
+    ref = native.csr_matvec(fdlap.fd_laplacian_2d(-1.0, 1.0, m), x)
+    assert np.array_equal(ys, ref)
+    for lay in ("csr", "sliced_wide"):
+        dA.set_layout(lay)
+        assert np.array_equal(psk.mvmult(dA, x), ref)
 
 
 def _solve_case(psk, case, d, monkeypatch, layout):
@@ -92,7 +119,7 @@ def _solve_case(psk, case, d, monkeypatch, layout):
                                                                                                  d["b"])
 
 
-@pytest.mark.parametrize("layout", ["csr", "sliced"])
+@pytest.mark.parametrize("layout", ["csr", "sliced", "sliced_wide"])
 @pytest.mark.parametrize("case", solver_cases(), ids=lambda c: c["file"][:-4])
 def test_solver_matches_reference_each_layout(psk, case, layout, monkeypatch):
     """Every golden solver case meets the parity bar with either layout forced everywhere. (The dot
@@ -110,10 +137,11 @@ def test_fd_trajectories_bitwise_across_layouts(psk, file, monkeypatch):
     case = next(c for c in solver_cases() if c["file"] == file)
     d = load_golden(file)
     s1 = _solve_case(psk, case, d, monkeypatch, "csr")
-    s2 = _solve_case(psk, case, d, monkeypatch, "sliced")
-    assert s1.iters() == s2.iters() and s1.success() == s2.success()
-    assert np.array_equal(s1.soln(), s2.soln())
-    assert np.array_equal(s1.info["hist"], s2.info["hist"])
+    for lay in ("sliced", "sliced_wide"):
+        s2 = _solve_case(psk, case, d, monkeypatch, lay)
+        assert s1.iters() == s2.iters() and s1.success() == s2.success()
+        assert np.array_equal(s1.soln(), s2.soln())
+        assert np.array_equal(s1.info["hist"], s2.info["hist"])
 
 
 def test_amg_identical_across_layouts(psk, monkeypatch):
@@ -121,11 +149,12 @@ def test_amg_identical_across_layouts(psk, monkeypatch):
     d = load_golden("pcg_negfd32_ic.npz")
     A = golden_matrix(d)
     out = []
-    for lay in ("csr", "sliced"):
+    for lay in ("csr", "sliced", "sliced_wide"):
         monkeypatch.setenv("PSK_SPMV_LAYOUT", lay)
         st = psk.PCG(control=_ctl(maxiter=200, tau=1e-8), precond=psk.AMG(numIters=2, numLevels=3)).makeSolver() \
             .solve(A, d["b"])
         out.append(st)
-    assert out[0].iters() == out[1].iters()
-    assert np.array_equal(out[0].soln(), out[1].soln())
-    assert np.array_equal(out[0].info["hist"], out[1].info["hist"])
+    for o in out[1:]:
+        assert out[0].iters() == o.iters()
+        assert np.array_equal(out[0].soln(), o.soln())
+        assert np.array_equal(out[0].info["hist"], o.info["hist"])
