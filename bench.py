@@ -80,7 +80,7 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1d_pmc_traffic_16384.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1e_pmc_traffic_16384.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same kernel and side")
     args = ap.parse_args()
 
