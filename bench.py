@@ -228,6 +228,14 @@ def main():
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
             "setup_s": setup_s,
         }
+        if world == 1:
+            # the same matrix, plain y = A x launches back to back (no dot epilogue, no solver kernels
+            # in between): how much of the in-loop SpMV time is the PCG context
+            bms = ctypes.c_double()
+            N.check(N.lib.psk_spmv_timed(A, db, dsol, 20, ctypes.byref(bms)), "psk_spmv_timed")
+            out["spmv_plain_batch20"] = {"avg_launch_ms": bms.value,
+                                         "achieved_GBps": bspmv / (bms.value * 1e-3) / 1e9,
+                                         "frac": bspmv / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS}
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
         if world == 1 and args.spmv10m and m != 3163:
