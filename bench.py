@@ -304,7 +304,7 @@ def spmv_10m(N, iters=30):
     out = {"n": n, "nnz": nnz, "avg_launch_ms": res.spmv_ms, "achieved_GBps": gbps,
            "frac": gbps / HBM_PEAK_GBPS, "pcg_it_per_s": iters / (res.loop_ms * 1e-3),
            "algorithmic_bytes_per_launch": b,
-           "batch50": {"kernel": "spmv_kernel<kSpmvPlain>", "avg_launch_ms": bms.value, "achieved_GBps": bb,
+           "batch50": {"kernel": "SpMV, plain mode, the matrix's default layout", "avg_launch_ms": bms.value, "achieved_GBps": bb,
                        "frac": bb / HBM_PEAK_GBPS,
                        "how": "50 back-to-back launches between two HIP events on the library stream"}}
     for p in (db, dx):
