@@ -236,6 +236,7 @@ def main():
             out["spmv_plain_batch20"] = {"avg_launch_ms": bms.value,
                                          "achieved_GBps": bspmv / (bms.value * 1e-3) / 1e9,
                                          "frac": bspmv / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            out["spmv_csr_layout_batch20"] = csr_layout_batch(N, A, db, dsol, bspmv)
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
         if world == 1 and args.spmv10m and m != 3163:
@@ -259,6 +260,18 @@ def main():
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
+
+
+def csr_layout_batch(N, A, x, y, bspmv, reps=20):
+    """The same matrix switched to the CSR layout (tile kernel, LDS-staged products) and multiplied
+    `reps` times back to back: the CSR SpMV the north star names, beside the default layout. The
+    matrix is left in CSR layout afterwards (call last)."""
+    N.check(N.lib.psk_csr_layout(A, N.PSK_LAYOUT_CSR, None, None, None, None), "psk_csr_layout")
+    ms = ctypes.c_double()
+    N.check(N.lib.psk_spmv_timed(A, x, y, reps, ctypes.byref(ms)), "psk_spmv_timed")
+    gbps = bspmv / (ms.value * 1e-3) / 1e9
+    return {"kernel": "spmv_kernel<kSpmvPlain> (CSR layout)", "avg_launch_ms": ms.value, "achieved_GBps": gbps,
+            "frac": gbps / HBM_PEAK_GBPS}
 
 
 def pmc_traffic(path, m, world, sliced):
@@ -301,12 +314,14 @@ def spmv_10m(N, iters=30):
     bms = ctypes.c_double()
     N.check(N.lib.psk_spmv_timed(A, dx, db, 50, ctypes.byref(bms)), "psk_spmv_timed")
     bb = b / (bms.value * 1e-3) / 1e9
+    csr = csr_layout_batch(N, A, dx, db, b, reps=50)
     out = {"n": n, "nnz": nnz, "avg_launch_ms": res.spmv_ms, "achieved_GBps": gbps,
            "frac": gbps / HBM_PEAK_GBPS, "pcg_it_per_s": iters / (res.loop_ms * 1e-3),
            "algorithmic_bytes_per_launch": b,
            "batch50": {"kernel": "SpMV, plain mode, the matrix's default layout", "avg_launch_ms": bms.value, "achieved_GBps": bb,
                        "frac": bb / HBM_PEAK_GBPS,
-                       "how": "50 back-to-back launches between two HIP events on the library stream"}}
+                       "how": "50 back-to-back launches between two HIP events on the library stream"},
+           "batch50_csr_layout": csr}
     for p in (db, dx):
         N.lib.psk_dfree(p)
     N.lib.psk_prec_destroy(M)
