@@ -30,15 +30,19 @@ def main():
     M = TriangularSolveChain(U.shape[0], U=U)
     v = psk.DeviceVector.from_numpy(np.random.default_rng(0).standard_normal(U.shape[0]))
     out = {"side": m, "blocks_env": os.environ.get("PSK_BAND_BLOCKS"), "info": M.schedule("U")}
+    res = {}
     for sched in ("band", "syncfree"):
         M.schedule("U", set=sched)
-        M.apply(v)
+        res[sched] = M.apply(v).numpy()
         N.check(N.lib.psk_synchronize(), "sync")
         t = time.perf_counter()
         for _ in range(args.reps):
             M.apply(v)
         N.check(N.lib.psk_synchronize(), "sync")
         out[sched + "_ms"] = (time.perf_counter() - t) * 1e3 / args.reps
+    out["band_vs_syncfree_maxrel"] = float(np.max(np.abs(res["band"] - res["syncfree"])) /
+                                           np.max(np.abs(res["syncfree"])))
+    out["gate_env"] = os.environ.get("PSK_BAND_GATE")
     print(json.dumps(out), flush=True)
 
 
