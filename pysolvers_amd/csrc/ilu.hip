@@ -241,25 +241,42 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
                 const int cb = (int)((r / kBandChunk) & 1), sl = (int)(r % kBandChunk);
                 const double *db = dbuf + cb * kD * kBandChunk;
                 const int32_t *ib = ibuf + cb * (K + 2) * kBandChunk;
+                // every LDS read of the record first (one round trip), then every ring read (a
+                // second one; entries that are not in-block read slot 0, unused), then the sum in
+                // stored order: a local level is ~3 dependent LDS round trips instead of ~10
                 const int32_t row = ib[sl];
+                int32_t cc[K];
+                int64_t pc[K];
+                double vv[K], ee[K], rg[K];
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    cc[k] = ib[(2 + k) * kBandChunk + sl];
+                    vv[k] = db[k * kBandChunk + sl];
+                    ee[k] = db[(K + 2 + k) * kBandChunk + sl];
+                }
+                const double bb = db[(K + 1) * kBandChunk + sl];
+                const double dd = rec_d ? db[K * kBandChunk + sl] : 1.0;
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    pc[k] = upper ? (n - 1 - cc[k]) : cc[k];
+                    rg[k] = ring_mask >= 0 ? ring[(cc[k] >= 0 && pc[k] >= p_lo ? pc[k] : 0) & ring_mask] : 0.0;
+                }
                 double acc = 0.0;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
-                    const int32_t c = ib[(2 + k) * kBandChunk + sl];
-                    if (c >= 0) {
-                        const int64_t pc = upper ? (n - 1 - c) : c;
+                    if (cc[k] >= 0) {
                         double xv;
-                        if (pc < p_lo) {   // earlier block: the staged snapshot, else wait for it
-                            xv = db[(K + 2 + k) * kBandChunk + sl];
-                            if (is_sentinel(xv)) xv = wait_pub(x + c, err);
+                        if (pc[k] < p_lo) {   // earlier block: the staged snapshot, else wait for it
+                            xv = ee[k];
+                            if (is_sentinel(xv)) xv = wait_pub(x + cc[k], err);
                         } else {
-                            xv = ring_mask >= 0 ? ring[pc & ring_mask] : wait_pub(x + c, err);
+                            xv = ring_mask >= 0 ? rg[k] : wait_pub(x + cc[k], err);
                         }
-                        acc = fma(db[k * kBandChunk + sl], xv, acc);
+                        acc = fma(vv[k], xv, acc);
                     }
                 }
-                double res = db[(K + 1) * kBandChunk + sl] - acc;
-                if (rec_d) res = res / db[K * kBandChunk + sl];
+                double res = bb - acc;
+                if (rec_d) res = res / dd;
                 if (ring_mask >= 0) ring[(upper ? (n - 1 - row) : row) & ring_mask] = res;
                 store_pub(x + row, res);
             }
