@@ -160,6 +160,12 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
 // go to an LDS ring (position & ring_mask, host-verified reuse distance) as well as to x; dependencies
 // on earlier blocks are waited on through x.
 constexpr int kBandChunk = kBlock;   // records per staged chunk = widest level = threads
+#ifdef PSK_BAND_PROF
+__device__ unsigned long long g_band_prof[8];   // development probe: cycles per phase of block 100's levels
+extern "C" int psk_band_prof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_band_prof), sizeof(g_band_prof)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 template <int K>
 struct BandChunkRegs {
@@ -231,11 +237,18 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
             __syncthreads();
         };
         while (a < nrec) {
+#ifdef PSK_BAND_PROF
+            const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
             if (a / kBandChunk >= have) advance();                      // level starts in the next chunk
             const int64_t ca = a / kBandChunk;
             const int32_t *iba = ibuf + (ca & 1) * (K + 2) * kBandChunk;
             const int64_t bnd = iba[kBandChunk + (a % kBandChunk)];   // end of this level (relative)
             if ((bnd - 1) / kBandChunk >= have) advance();              // level reaches into the next chunk
+#ifdef PSK_BAND_PROF
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            uint64_t t2 = t1;
+#endif
             const int64_t r = a + tid;
             if (r < bnd) {
                 const int cb = (int)((r / kBandChunk) & 1), sl = (int)(r % kBandChunk);
@@ -261,6 +274,10 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
                     pc[k] = upper ? (n - 1 - cc[k]) : cc[k];
                     rg[k] = ring_mask >= 0 ? ring[(cc[k] >= 0 && pc[k] >= p_lo ? pc[k] : 0) & ring_mask] : 0.0;
                 }
+#ifdef PSK_BAND_PROF
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                t2 = __builtin_amdgcn_s_memtime();
+#endif
                 double acc = 0.0;
 #pragma unroll
                 for (int k = 0; k < K; ++k) {
@@ -280,13 +297,257 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
                 if (ring_mask >= 0) ring[(upper ? (n - 1 - row) : row) & ring_mask] = res;
                 store_pub(x + row, res);
             }
+#ifdef PSK_BAND_PROF
+            const uint64_t t3 = __builtin_amdgcn_s_memtime();
+#endif
             // LDS results of this level visible to the next; x stores may still be in flight
             __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0)
             __builtin_amdgcn_s_barrier();
+#ifdef PSK_BAND_PROF
+            if (tid == 0 && blk == 100) {
+                const uint64_t t4 = __builtin_amdgcn_s_memtime();
+                g_band_prof[0] += t1 - t0;
+                g_band_prof[1] += t2 - t1;
+                g_band_prof[2] += t3 - t2;
+                g_band_prof[3] += t4 - t3;
+                g_band_prof[4] += 1;
+            }
+#endif
             a = bnd;
         }
         __syncthreads();   // ring and buffers reused by the next block of this workgroup
     }
+}
+
+// Narrow band: the band schedule for factors whose local levels are at most one wave wide (the
+// Gauss-Seidel factor triu(A) of a 2-D grid, any block of lines). Wave 0 solves the block's levels
+// alone, with no workgroup barrier between levels (LDS traffic of one wave is in order); waves 1-3
+// stage the record chunks into kNarrowBufs LDS buffers ahead of it and, while they wait for a free
+// buffer, re-poll the external snapshots still holding the sentinel, so the solving wave finds its
+// dependencies on earlier blocks in LDS instead of paying an agent-scope load round trip per level
+// (tools/band_prof.py: that round trip was ~60% of a band level). Hand-shakes through LDS counters:
+// ctl[b] = stager waves that finished staging buffer b (3 per round), ctl[NB] = last chunk the solver
+// finished, ctl[NB+1] = block done.
+constexpr int kNarrowBufs = 3;
+constexpr int kNarrowChunk = 128;   // records per buffer
+constexpr int kNarrowWidth = 64;    // widest local level (one wave)
+
+__device__ __forceinline__ int32_t lds_load_acq(int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int K>
+__global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
+    int64_t n, int upper, const double *__restrict__ rhs, const int32_t *__restrict__ rhs_idx, double *x,
+    int32_t *err, const int32_t *__restrict__ rec_row, const int32_t *__restrict__ rec_end,
+    const int32_t *__restrict__ rec_c, const double *__restrict__ rec_v, const double *__restrict__ rec_d,
+    int64_t nblocks, int64_t B, int ring_mask) {
+    constexpr int C = kNarrowChunk, NB = kNarrowBufs, kD = 2 * K + 2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int ring_words = ring_mask + 1;
+    double *ring = reinterpret_cast<double *>(smem);
+    double *dbuf = ring + ring_words;                                        // NB x [v[K], d, b, e[K]] x C
+    int32_t *ibuf = reinterpret_cast<int32_t *>(dbuf + NB * kD * C);         // NB x [row, end, c[K]] x C
+    int32_t *ctl = ibuf + NB * (K + 2) * C;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const double sentinel = __longlong_as_double((long long)kSentinel);
+    for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+        const int64_t p_lo = blk * B, p_hi = (p_lo + B < n) ? p_lo + B : n, nrec = p_hi - p_lo;
+        const int64_t nchunks = (nrec + C - 1) / C;
+        if (tid <= NB + 1) ctl[tid] = tid == NB ? -1 : 0;
+        __syncthreads();
+        if (wave == 0) {
+            int64_t seen = -1, cur = 0, a = 0;
+            auto wait_chunk = [&](int64_t q) {
+                if (q <= seen) return;
+                const int32_t need = 3 * (int32_t)(q / NB + 1);
+                int64_t spins = 0;
+                while (lds_load_acq(&ctl[q % NB]) < need) {
+                    if (++spins > kMaxSpins) {
+                        atomicExch(err, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                seen = q;
+            };
+            while (a < nrec) {
+#ifdef PSK_BAND_PROF
+                const uint64_t t0 = __builtin_amdgcn_s_memtime();
+                int hits = 0;
+#endif
+                const int64_t q = a / C;
+                if (q > cur) {   // every level of chunks < q is done: their buffers may be restaged
+                    if (lane == 0) __hip_atomic_store(&ctl[NB], (int32_t)(q - 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    cur = q;
+                }
+                wait_chunk(q);
+                const int64_t bnd = ibuf[(q % NB) * (K + 2) * C + C + (a % C)];
+                if ((bnd - 1) / C > q) wait_chunk(q + 1);
+#ifdef PSK_BAND_PROF
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                uint64_t t2 = t1;
+#endif
+                const int64_t r = a + lane;
+                if (r < bnd) {
+                    const int bf = (int)((r / C) % NB), sl = (int)(r % C);
+                    const double *db = dbuf + bf * kD * C;
+                    const int32_t *ib = ibuf + bf * (K + 2) * C;
+                    const int32_t row = ib[sl];
+                    int32_t cc[K];
+                    int64_t pc[K];
+                    double vv[K], ee[K], rg[K];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        cc[k] = ib[(2 + k) * C + sl];
+                        vv[k] = db[k * C + sl];
+                        ee[k] = __longlong_as_double((long long)__hip_atomic_load(
+                            reinterpret_cast<const uint64_t *>(db + (K + 2 + k) * C + sl), __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_WORKGROUP));
+                    }
+                    const double bb = db[(K + 1) * C + sl];
+                    const double dd = rec_d ? db[K * C + sl] : 1.0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        pc[k] = upper ? (n - 1 - cc[k]) : cc[k];
+                        rg[k] = ring[(cc[k] >= 0 && pc[k] >= p_lo ? pc[k] : 0) & ring_mask];
+                    }
+#ifdef PSK_BAND_PROF
+                    __builtin_amdgcn_s_waitcnt(0xc07f);
+                    t2 = __builtin_amdgcn_s_memtime();
+#endif
+                    double acc = 0.0;
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        if (cc[k] >= 0) {
+                            double xv;
+                            if (pc[k] < p_lo) {
+                                xv = ee[k];
+#ifdef PSK_BAND_PROF
+                                if (is_sentinel(xv)) ++hits;
+#endif
+                                if (is_sentinel(xv)) xv = wait_pub(x + cc[k], err);
+                            } else {
+                                xv = rg[k];
+                            }
+                            acc = fma(vv[k], xv, acc);
+                        }
+                    }
+                    double res = bb - acc;
+                    if (rec_d) res = res / dd;
+                    ring[(upper ? (n - 1 - row) : row) & ring_mask] = res;
+                    store_pub(x + row, res);
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // this level's ring writes before the next level's reads
+                __builtin_amdgcn_wave_barrier();
+#ifdef PSK_BAND_PROF
+                {
+                    const uint64_t t3 = __builtin_amdgcn_s_memtime();
+                    t2 = __shfl(t2, 0, 64);
+                    hits = __reduce_add_sync(0xffffffffffffffffull, hits);
+                    if (lane == 0 && blk == 100) {
+                        g_band_prof[0] += t1 - t0;
+                        g_band_prof[1] += t2 - t1;
+                        g_band_prof[2] += t3 - t2;
+                        g_band_prof[3] += (uint64_t)hits;
+                        g_band_prof[4] += 1;
+                    }
+                }
+#endif
+                a = bnd;
+            }
+            if (lane == 0) {
+                __hip_atomic_store(&ctl[NB], (int32_t)(nchunks - 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(&ctl[NB + 1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        } else {
+            // stager thread st owns slot st of every buffer (and slot st + 192 < C: none for C = 128)
+            const int st = tid - 64;
+            const bool owns = st < C;
+            int64_t last_q[NB];
+            uint32_t pending[NB];   // bit k: entry k of the owned slot still holds the sentinel
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                last_q[b] = -1;
+                pending[b] = 0;
+            }
+            auto refresh = [&]() {
+                const int32_t done_q = lds_load_acq(&ctl[NB]);
+#pragma unroll
+                for (int b = 0; b < NB; ++b) {
+                    if (pending[b] == 0 || last_q[b] <= done_q) continue;
+                    const int32_t *ib = ibuf + b * (K + 2) * C;
+                    double *db = dbuf + b * kD * C;
+#pragma unroll
+                    for (int k = 0; k < K; ++k)
+                        if (pending[b] & (1u << k)) {
+                            const double v = load_pub(x + ib[(2 + k) * C + st]);
+                            if (!is_sentinel(v)) {
+                                __hip_atomic_store(reinterpret_cast<uint64_t *>(db + (K + 2 + k) * C + st),
+                                                   (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                                pending[b] &= ~(1u << k);
+                            }
+                        }
+                }
+            };
+            for (int64_t q = 0; q < nchunks; ++q) {
+                const int b = (int)(q % NB);
+                int64_t spins = 0;
+                while (lds_load_acq(&ctl[NB]) < q - NB) {   // buffer b still holds chunk q - NB
+                    refresh();
+                    if (++spins > kMaxSpins) {
+                        atomicExch(err, 1);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                const int64_t rq = p_lo + q * C + st;
+                pending[b] = 0;
+                last_q[b] = q;
+                if (owns && rq < p_hi) {
+                    double *db = dbuf + b * kD * C;
+                    int32_t *ib = ibuf + b * (K + 2) * C;
+                    const int32_t row = rec_row[rq];
+                    ib[st] = row;
+                    ib[C + st] = rec_end[rq];
+#pragma unroll
+                    for (int k = 0; k < K; ++k) {
+                        const int32_t c = rec_c[(int64_t)k * n + rq];
+                        ib[(2 + k) * C + st] = c;
+                        db[k * C + st] = rec_v[(int64_t)k * n + rq];
+                        double e = sentinel;
+                        if (c >= 0 && (upper ? (n - 1 - c) : c) < p_lo) {
+                            e = load_pub(x + c);
+                            if (is_sentinel(e)) pending[b] |= 1u << k;
+                        }
+                        db[(K + 2 + k) * C + st] = e;
+                    }
+                    db[K * C + st] = rec_d ? rec_d[rq] : 1.0;
+                    db[(K + 1) * C + st] = rhs_idx ? rhs[rhs_idx[row]] : rhs[row];
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's LDS writes done
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) __hip_atomic_fetch_add(&ctl[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            int64_t spins = 0;
+            while (lds_load_acq(&ctl[NB + 1]) == 0) {
+                refresh();
+                if (++spins > kMaxSpins) {
+                    atomicExch(err, 1);
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        __syncthreads();   // ring, buffers and counters reused by the next block of this workgroup
+    }
+}
+
+static size_t narrow_lds_bytes(int ring_words, int K) {
+    return (size_t)ring_words * sizeof(double) +
+           (size_t)kNarrowBufs * kNarrowChunk * ((2 * K + 2) * sizeof(double) + (K + 2) * sizeof(int32_t)) +
+           (kNarrowBufs + 2) * sizeof(int32_t);
 }
 
 // out[i] = z[perm[i]] (perm == nullptr: copy)
@@ -332,6 +593,26 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
     const int32_t *rp = T.rowptr, *ci = T.colidx;
     const double *va = T.vals, *dg = T.diag;
     (void)rp;
+    if (T.schedule == kSchedBand && T.band_narrow) {
+        const void *k = nullptr;
+        switch (T.band_K) {
+        case 1: k = reinterpret_cast<const void *>(&sptrsv_band_narrow_kernel<1>); break;
+        case 2: k = reinterpret_cast<const void *>(&sptrsv_band_narrow_kernel<2>); break;
+        case 4: k = reinterpret_cast<const void *>(&sptrsv_band_narrow_kernel<4>); break;
+        case 8: k = reinterpret_cast<const void *>(&sptrsv_band_narrow_kernel<8>); break;
+        default: return fail(PSK_ERR_ARG, "band schedule: bad record width");
+        }
+        const size_t lds = narrow_lds_bytes(T.ring_words, T.band_K);
+        const int g = coop_grid(c, k, lds);
+        int upper = T.upper ? 1 : 0;
+        const int32_t *rr = T.rec_row, *re = T.rec_end, *rc = T.rec_c;
+        const double *rv = T.rec_v, *rd = T.diag ? T.rec_d : nullptr;
+        int64_t nb = T.band_nblocks, B = T.band_B;
+        int mask = T.ring_words - 1;
+        void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask};
+        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
+        return PSK_OK;
+    }
     if (T.schedule == kSchedBand) {
         const void *k = nullptr;
         switch (T.band_K) {
@@ -423,6 +704,7 @@ namespace {
 // costs ~0.9 us with the ring (it is paced by the one external load of the block's boundary row;
 // FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
 constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
+constexpr double kNarrowLevelUs = 0.35;   // narrow band local level (provisional)
 
 struct HostFactor {
     int64_t n = 0;
@@ -669,6 +951,16 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         }
         if (B == 64) break;
     }
+    // narrow band (one solving wave, staging waves): every local level at most one wave wide, ring present
+    bool narrow = false;
+    if (band_ok && best.ring_words > 0 && narrow_lds_bytes(best.ring_words, K) <= 160 * 1024) {
+        int64_t wmax = 0;
+        for (size_t L = 0; L + 1 < best.lvl_ptr.size(); ++L) wmax = std::max(wmax, best.lvl_ptr[L + 1] - best.lvl_ptr[L]);
+        const char *ne = std::getenv("PSK_BAND_NARROW");
+        narrow = wmax <= kNarrowWidth && !(ne && std::atoi(ne) == 0);
+        if (narrow) best.est *= kNarrowLevelUs / kBandLevelRingUs;   // levels dominate the simulated time
+    }
+    T.band_narrow = narrow;
     T.est_band_us = band_ok ? best.est : -1.0;
     T.schedule = (band_ok && best.est < T.est_syncfree_us) ? kSchedBand : kSchedSyncFree;
     T.present = true;

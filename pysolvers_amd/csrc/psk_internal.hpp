@@ -170,6 +170,7 @@ struct TriFactor {
     int band_K = 0;
     int64_t band_B = 0, band_nblocks = 0, band_levels = 0;
     int32_t ring_words = 0;
+    bool band_narrow = false;   // band run by sptrsv_band_narrow_kernel (local levels <= one wave wide)
     double est_syncfree_us = 0.0, est_band_us = 0.0;
     void release();
 };
