@@ -160,6 +160,28 @@ def test_trisolve_rejects_bad_factors(psk):
         TriangularSolveChain(2, L=L, l_unit=True, gather_in=np.array([0, 0]))   # not a permutation
 
 
+def test_gauss_seidel_narrow_band_large(psk, monkeypatch):
+    """FD 1024^2 triu: 256 blocks of 4 grid lines, 32 staged chunks each — the narrow band kernel
+    (one solving wave, staging waves re-polling the external snapshots) and the barrier band kernel
+    (PSK_BAND_NARROW=0) both match spsolve_triangular, and each other bit for bit."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    m = 1024
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    U = sp.triu(A).tocsr()
+    v = np.random.default_rng(5).standard_normal(A.shape[0])
+    ref = spla.spsolve_triangular(U, v, lower=False)
+    outs = []
+    for narrow in ("1", "0"):
+        monkeypatch.setenv("PSK_BAND_NARROW", narrow)
+        M = TriangularSolveChain(A.shape[0], U=U)
+        M.schedule("U", set="band")
+        outs.append(M.apply(v))
+        assert _rel(outs[-1], ref) <= 1e-12, narrow
+        assert _rel(M.apply(v), ref) <= 1e-12, narrow   # re-apply (sentinel refill)
+    assert np.array_equal(outs[0], outs[1])   # same per-row arithmetic in both kernels
+
+
 @pytest.mark.parametrize("m", [64, 300])
 def test_gauss_seidel_factor_schedules(psk, m):
     """triu(-FD2D) (the GS smoother's factor, ClassicSmoothers.py:33): band and sync-free schedules
