@@ -704,7 +704,7 @@ namespace {
 // costs ~0.9 us with the ring (it is paced by the one external load of the block's boundary row;
 // FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
 constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
-constexpr double kNarrowLevelUs = 0.35;   // narrow band local level (provisional)
+constexpr double kNarrowLevelUs = 0.8;    // narrow band local level (FD 8192^2 Gauss-Seidel: 12.6 ms / 16128 levels)
 
 struct HostFactor {
     int64_t n = 0;
