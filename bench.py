@@ -102,7 +102,17 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
+        # control plane only. Gloo's C++ connection log goes to fd 1; keep stdout for the ONE JSON
+        # line the driver parses by pointing fd 1 at stderr while the group connects
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
 
     def barrier():
         if dist is not None:
