@@ -158,3 +158,33 @@ def test_amg_identical_across_layouts(psk, monkeypatch):
         assert out[0].iters() == o.iters()
         assert np.array_equal(out[0].soln(), o.soln())
         assert np.array_equal(out[0].info["hist"], o.info["hist"])
+
+
+def _fd_rows_reference(m, x, rows):
+    """csr_matvec of FDLaplacian2D(-1, 1, m) restricted to `rows`: each row summed from 0.0 in its
+    stored order [diag, -m, +m, -1, +1] (absent neighbours skipped), products rounded."""
+    h = abs(1.0 - (-1.0)) / float(m + 1)
+    dval, oval = -4.0 / h / h, 1.0 / h / h
+    ix, iy = rows % m, rows // m
+    s = 0.0 + dval * x[rows]
+    for ok, off in ((iy > 0, -m), (iy < m - 1, m), (ix > 0, -1), (ix < m - 1, 1)):
+        nb = np.where(ok, rows + off, rows)
+        s = np.where(ok, s + oval * x[nb], s)
+    return s
+
+
+def test_fd16384_spmv_full_size(psk):
+    """configs[3]'s matrix (n = 268M) on one GPU: the default sliced SpMV equals the CSR-layout kernel
+    bit for bit over all rows, and both equal csr_matvec on 400k sampled rows plus every boundary row."""
+    m = 16384
+    n = m * m
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    assert dA.layout == "sliced"
+    x = np.random.default_rng(12345).random(n)
+    y = psk.mvmult(dA, x)
+    rng = np.random.default_rng(2)
+    edge = np.arange(m, dtype=np.int64)
+    rows = np.unique(np.concatenate([rng.integers(0, n, 400_000), edge, n - m + edge, edge * m, edge * m + m - 1]))
+    assert np.array_equal(y[rows], _fd_rows_reference(m, x, rows))
+    dA.set_layout("csr")
+    assert np.array_equal(psk.mvmult(dA, x), y)
