@@ -82,9 +82,10 @@ __global__ void fill_sentinel_kernel(int64_t n, double *x) {
 struct SfHead {
     int32_t row, s, e;
 };
+constexpr int kSfChunks = 3;   // 64-entry chunks of a row held in registers (longer rows loop)
 struct SfBody {
-    int32_t row, s, e, c;
-    double v, b, d;
+    int32_t row, s, e, c[kSfChunks];
+    double v[kSfChunks], b, d;
 };
 
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
@@ -108,9 +109,12 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
             b.row = h.row;
             b.s = h.s;
             b.e = h.e;
-            const int32_t idx = h.s + lane;
-            b.c = idx < h.e ? kci[idx] : -1;
-            b.v = idx < h.e ? kva[idx] : 0.0;
+#pragma unroll
+            for (int j = 0; j < kSfChunks; ++j) {
+                const int32_t idx = h.s + 64 * j + lane;
+                b.c[j] = idx < h.e ? kci[idx] : -1;
+                b.v[j] = idx < h.e ? kva[idx] : 0.0;
+            }
             if (lane == 0) {
                 b.b = rhs[rhs_idx ? rhs_idx[h.row] : h.row];
                 b.d = diag ? diag[h.row] : 1.0;
@@ -125,18 +129,23 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
     for (int64_t k = wave; k < n; k += W) {
         // the first poll of this row goes out before the prefetches, so waiting for it does not
         // wait for them (loads complete in order)
-        uint64_t bits = cur.c >= 0 ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(x + cur.c), __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)
-                                   : 0;
+        uint64_t bits[kSfChunks];
+#pragma unroll
+        for (int j = 0; j < kSfChunks; ++j)
+            bits[j] = cur.c[j] >= 0 ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(x + cur.c[j]),
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : 0;
         body(k + W, hb, nxt);       // stage B of k+W (its header arrived an iteration ago)
         head(k + 2 * W, hb);        // stage A of k+2W
         double acc = 0.0;
-        if (cur.c >= 0) {
-            double xv = __longlong_as_double((long long)bits);
-            if (is_sentinel(xv)) xv = wait_pub(x + cur.c, err);
-            acc = fma(cur.v, xv, acc);
-        }
-        for (int32_t base = cur.s + 64; base < cur.e; base += 64) {   // rows longer than a wave
+#pragma unroll
+        for (int j = 0; j < kSfChunks; ++j)   // lane's entries in stored order: lane, lane+64, ...
+            if (cur.c[j] >= 0) {
+                double xv = __longlong_as_double((long long)bits[j]);
+                if (is_sentinel(xv)) xv = wait_pub(x + cur.c[j], err);
+                acc = fma(cur.v[j], xv, acc);
+            }
+        for (int32_t base = cur.s + 64 * kSfChunks; base < cur.e; base += 64) {   // longer rows
             const int32_t idx = base + lane;
             if (idx < cur.e) acc = fma(kva[idx], wait_pub(x + kci[idx], err), acc);
         }
