@@ -61,7 +61,7 @@ __device__ __forceinline__ double wait_pub(const double *p, int32_t *err) {
             atomicExch(err, 1);
             return 0.0;
         }
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(4);   // sleep 1 / 4 / 12 between polls: AMG 8192^2 2.90 / 2.92 / 2.90 it/s
         xv = load_pub(p);
     }
     return xv;
