@@ -60,8 +60,10 @@ def _worker(rank, world, port, name, kind, out_dir):
     dist.destroy_process_group()
 
 
+# fd512 x 2: shards of 128 slices whose first/last slices (halo lines) keep 32-bit columns while the
+# rest are packed — the sliced SpMV layout across the halo
 @pytest.mark.parametrize("name,kind,world", [("fd64", "fd", 2), ("fd96", "fd", 3), ("dh12", "general", 3),
-                                             ("fd50", "general", 4)])
+                                             ("fd50", "general", 4), ("fd512", "fd", 2)])
 def test_multirank_pcg_on_one_gpu(tmp_path, name, kind, world):
     import torch.multiprocessing as mp
     from oracle import fdlap, krylov
