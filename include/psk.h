@@ -192,8 +192,9 @@ int psk_prec_create_amg(int32_t num_levels, psk_csr *const *A, psk_csr *const *P
                         int32_t nu_post, double tau, psk_prec **out);
 /* Schedule of factor `which` (0 = L, 1 = U) of a triangular-solve chain: 0 = sync-free (one wave per
  * row, global dependency levels), 1 = band (one workgroup per block of the solve order, local levels
- * behind barriers, LDS ring of ring_words doubles). The library picks the faster by a host simulation
- * (est_*_us); set = 0 / 1 forces one, -1 only queries. Any out pointer may be NULL. */
+ * behind barriers, LDS ring of ring_words doubles), 2 = LDS (factors of at most 18432 rows: one
+ * workgroup, sync-free inside it with x in LDS). The library picks the fastest by host cost models
+ * (est_*_us); set = 0 / 1 / 2 forces one, -1 only queries. Any out pointer may be NULL. */
 int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t *schedule, int64_t *blocks,
                                int32_t *ring_words, double *est_syncfree_us, double *est_band_us);
 /* kind, size and triangular-solve shape of a preconditioner (any out pointer may be NULL). */

@@ -88,6 +88,8 @@ struct SfBody {
     double v[kSfChunks], b, d;
 };
 
+constexpr int kSfTail = 4;
+
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
                                                         const int32_t *__restrict__ kci, const double *__restrict__ kva,
                                                         const double *__restrict__ diag, const double *__restrict__ rhs,
@@ -145,9 +147,29 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
                 if (is_sentinel(xv)) xv = wait_pub(x + cur.c[j], err);
                 acc = fma(cur.v[j], xv, acc);
             }
-        for (int32_t base = cur.s + 64 * kSfChunks; base < cur.e; base += 64) {   // longer rows
-            const int32_t idx = base + lane;
-            if (idx < cur.e) acc = fma(kva[idx], wait_pub(x + kci[idx], err), acc);
+        // longer rows: kSfTail chunks of entries, then their x values, in flight at once
+        for (int32_t base = cur.s + 64 * kSfChunks; base < cur.e; base += 64 * kSfTail) {
+            int32_t tc[kSfTail];
+            double tv[kSfTail];
+            uint64_t tb[kSfTail];
+#pragma unroll
+            for (int t = 0; t < kSfTail; ++t) {
+                const int32_t idx = base + 64 * t + lane;
+                tc[t] = idx < cur.e ? kci[idx] : -1;
+                tv[t] = idx < cur.e ? kva[idx] : 0.0;
+            }
+#pragma unroll
+            for (int t = 0; t < kSfTail; ++t)
+                tb[t] = tc[t] >= 0 ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(x + tc[t]), __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0;
+#pragma unroll
+            for (int t = 0; t < kSfTail; ++t)
+                if (tc[t] >= 0) {
+                    double xv = __longlong_as_double((long long)tb[t]);
+                    if (is_sentinel(xv)) xv = wait_pub(x + tc[t], err);
+                    acc = fma(tv[t], xv, acc);
+                }
         }
         const double sum = wave_sum(acc);
         if (lane == 0) {
@@ -157,6 +179,132 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
         }
         cur = nxt;
     }
+}
+
+// LDS-resident: a factor small enough for x to live in LDS (the AMG coarse LU: 16.6k rows, 3008
+// levels, ~140 entries per row) is solved by ONE workgroup of 16 waves running the sync-free
+// schedule above with x in LDS: a dependency hand-off is an LDS write seen by another wave's LDS
+// poll (~0.1 us) instead of a device-scope store seen by a polling load (~1-2 us). Each wave still
+// prefetches its next rows' entries from HBM while it waits. x is copied out at the end.
+constexpr int kLdsThreads = 1024;
+constexpr int kLdsTail = 8;
+constexpr int kLdsDepth = 3;   // rows in flight per wave (PSK_LDS_DEPTH=1..3 overrides)
+constexpr int64_t kLdsMaxRows = 18432;   // 144 KiB of x
+
+template <int D>
+__global__ __launch_bounds__(kLdsThreads) void sptrsv_lds_kernel(int64_t n, const int32_t *__restrict__ krp,
+                                                                 const int32_t *__restrict__ kci,
+                                                                 const double *__restrict__ kva,
+                                                                 const double *__restrict__ diag,
+                                                                 const double *__restrict__ rhs,
+                                                                 const int32_t *__restrict__ rhs_idx, double *x,
+                                                                 int32_t *err, const int32_t *__restrict__ krow) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    uint64_t *xs = reinterpret_cast<uint64_t *>(smem);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t wave = tid >> 6, W = kLdsThreads / 64;
+    for (int64_t i = tid; i < n; i += kLdsThreads) xs[i] = kSentinel;
+    __syncthreads();
+    auto lds_wait = [&](int32_t c) -> double {
+        uint64_t b = __hip_atomic_load(xs + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        int64_t spins = 0;
+        while (b == kSentinel) {
+            if (++spins > kMaxSpins) {
+                atomicExch(err, 1);
+                return 0.0;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            b = __hip_atomic_load(xs + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        return __longlong_as_double((long long)b);
+    };
+    auto head = [&](int64_t k, SfHead &h) {
+        if (k < n) {
+            h.row = krow[k];
+            h.s = krp[k];
+            h.e = krp[k + 1];
+        }
+    };
+    auto body = [&](int64_t k, const SfHead &h, SfBody &b) {
+        if (k < n) {
+            b.row = h.row;
+            b.s = h.s;
+            b.e = h.e;
+#pragma unroll
+            for (int j = 0; j < kSfChunks; ++j) {
+                const int32_t idx = h.s + 64 * j + lane;
+                b.c[j] = idx < h.e ? kci[idx] : -1;
+                b.v[j] = idx < h.e ? kva[idx] : 0.0;
+            }
+            if (lane == 0) {
+                b.b = rhs[rhs_idx ? rhs_idx[h.row] : h.row];
+                b.d = diag ? diag[h.row] : 1.0;
+            }
+        }
+    };
+    // register ring of D rows per wave: row k's entries are loaded D rows (D*W positions) before
+    // it is solved and its header 2D rows before, so a wave keeps D rows of HBM loads in flight
+    // while it waits on LDS hand-offs (one row in flight cost one HBM round trip per row)
+    SfHead hq[D];
+    SfBody bq[D];
+#pragma unroll
+    for (int t = 0; t < D; ++t) head(wave + t * W, hq[t]);
+#pragma unroll
+    for (int t = 0; t < D; ++t) body(wave + t * W, hq[t], bq[t]);
+#pragma unroll
+    for (int t = 0; t < D; ++t) head(wave + (D + t) * W, hq[t]);
+    for (int64_t k0 = wave; k0 < n; k0 += D * W) {
+#pragma unroll
+        for (int t = 0; t < D; ++t) {
+            const int64_t k = k0 + t * W;
+            if (k >= n) break;
+            const SfBody cur = bq[t];
+            body(k + D * W, hq[t], bq[t]);
+            head(k + 2 * D * W, hq[t]);
+            // all of this row's first LDS reads go out together; only a sentinel among them waits
+            uint64_t bits[kSfChunks];
+#pragma unroll
+            for (int j = 0; j < kSfChunks; ++j)
+                bits[j] = cur.c[j] >= 0
+                              ? __hip_atomic_load(xs + cur.c[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
+                              : 0;
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < kSfChunks; ++j)   // lane's entries in stored order: lane, lane+64, ...
+                if (cur.c[j] >= 0)
+                    acc = fma(cur.v[j],
+                              bits[j] == kSentinel ? lds_wait(cur.c[j]) : __longlong_as_double((long long)bits[j]), acc);
+            // longer rows (the dense tail of an LU factor): kLdsTail chunks of entries in flight at once
+            for (int32_t base = cur.s + 64 * kSfChunks; base < cur.e; base += 64 * kLdsTail) {
+                int32_t tc[kLdsTail];
+                double tv[kLdsTail];
+                uint64_t tb[kLdsTail];
+#pragma unroll
+                for (int u = 0; u < kLdsTail; ++u) {
+                    const int32_t idx = base + 64 * u + lane;
+                    tc[u] = idx < cur.e ? kci[idx] : -1;
+                    tv[u] = idx < cur.e ? kva[idx] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kLdsTail; ++u)
+                    tb[u] = tc[u] >= 0 ? __hip_atomic_load(xs + tc[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+#pragma unroll
+                for (int u = 0; u < kLdsTail; ++u)
+                    if (tc[u] >= 0)
+                        acc = fma(tv[u], tb[u] == kSentinel ? lds_wait(tc[u]) : __longlong_as_double((long long)tb[u]),
+                                  acc);
+            }
+            const double sum = wave_sum(acc);
+            if (lane == 0) {
+                double r = cur.b - sum;
+                if (diag) r = r / cur.d;
+                __hip_atomic_store(xs + cur.row, (uint64_t)__double_as_longlong(r), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    }
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += kLdsThreads) x[i] = __longlong_as_double((long long)xs[i]);
 }
 
 // Band: workgroup g takes blocks g, g+G, ... in solve order. Position of row i in solve order: i
@@ -602,6 +750,19 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
     const int32_t *rp = T.rowptr, *ci = T.colidx;
     const double *va = T.vals, *dg = T.diag;
     (void)rp;
+    if (T.schedule == kSchedLds) {
+        static const int depth = [] {
+            const char *e = std::getenv("PSK_LDS_DEPTH");
+            return e ? std::atoi(e) : kLdsDepth;
+        }();
+        const void *k = depth <= 1   ? reinterpret_cast<const void *>(&sptrsv_lds_kernel<1>)
+                        : depth == 2 ? reinterpret_cast<const void *>(&sptrsv_lds_kernel<2>)
+                                     : reinterpret_cast<const void *>(&sptrsv_lds_kernel<3>);   // 4 spills
+        const int32_t *ord = T.order;
+        void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
+        PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(kLdsThreads), args, (size_t)n * sizeof(double), s));
+        return PSK_OK;
+    }
     if (T.schedule == kSchedBand && T.band_narrow) {
         const void *k = nullptr;
         switch (T.band_K) {
@@ -713,6 +874,7 @@ namespace {
 // costs ~0.9 us with the ring (it is paced by the one external load of the block's boundary row;
 // FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
 constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
+constexpr double kLdsLevelUs = 0.15, kLdsBytesPerUs = 40e3;   // LDS schedule (provisional)
 constexpr double kNarrowLevelUs = 0.8;    // narrow band local level (FD 8192^2 Gauss-Seidel: 12.6 ms / 16128 levels)
 
 struct HostFactor {
@@ -972,6 +1134,14 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     T.band_narrow = narrow;
     T.est_band_us = band_ok ? best.est : -1.0;
     T.schedule = (band_ok && best.est < T.est_syncfree_us) ? kSchedBand : kSchedSyncFree;
+    // one workgroup with x in LDS: a level costs an LDS hand-off, the entries stream through one CU
+    T.est_lds_us = -1.0;
+    if (n > 0 && n <= kLdsMaxRows) {
+        T.est_lds_us = (double)nlev * kLdsLevelUs + (double)F.ci.size() * 12.0 / kLdsBytesPerUs;
+        const double other = T.schedule == kSchedBand ? T.est_band_us : T.est_syncfree_us;
+        const char *le = std::getenv("PSK_TRISOLVE_LDS");
+        if (T.est_lds_us < other && !(le && std::atoi(le) == 0)) T.schedule = kSchedLds;
+    }
     T.present = true;
     T.upper = upper;
     T.nnz = (int64_t)F.ci.size();
@@ -1085,8 +1255,10 @@ extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t se
     if (set == kSchedBand && T.band_K == 0)
         return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor not eligible for the band schedule "
                                          "(more than 8 entries in a row or a level wider than a chunk)");
-    if (set == kSchedSyncFree || set == kSchedBand) T.schedule = set;
-    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0 or 1");
+    if (set == kSchedLds && (M->n > kLdsMaxRows || M->n == 0))
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor too large for the LDS schedule");
+    if (set == kSchedSyncFree || set == kSchedBand || set == kSchedLds) T.schedule = set;
+    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1 or 2");
     if (schedule) *schedule = T.schedule;
     if (blocks) *blocks = T.band_nblocks;
     if (ring_words) *ring_words = T.ring_words;

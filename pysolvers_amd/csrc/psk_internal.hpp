@@ -154,8 +154,9 @@ struct AmgHierarchy;
 //    per block walking the block's LOCAL levels (dependencies inside the block) with a barrier
 //    between levels; dependencies on earlier blocks are waited on through the published values;
 //    an LDS ring of `ring_words` doubles (0 = none) serves the in-block dependencies.
-// `schedule` picks one (kSchedSyncFree / kSchedBand), chosen by a host simulation of both.
-enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1 };
+//  * LDS: small factors (x fits LDS) solved by one workgroup, sync-free inside it with x in LDS.
+// `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds), chosen by host cost models.
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2 };
 struct TriFactor {
     bool present = false, upper = false;
     int64_t nnz = 0;
@@ -171,7 +172,7 @@ struct TriFactor {
     int64_t band_B = 0, band_nblocks = 0, band_levels = 0;
     int32_t ring_words = 0;
     bool band_narrow = false;   // band run by sptrsv_band_narrow_kernel (local levels <= one wave wide)
-    double est_syncfree_us = 0.0, est_band_us = 0.0;
+    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0;
     void release();
 };
 }  // namespace psk

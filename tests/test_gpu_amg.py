@@ -132,9 +132,10 @@ def test_trisolve_chain_random(psk, n, seed):
         ref = spla.spsolve_triangular(Ud, spla.spsolve_triangular(Ld, v[gin], lower=True), lower=False)[gout]
         M = TriangularSolveChain(n, L=L, l_unit=l_unit, U=U, u_unit=u_unit, gather_in=gin, gather_out=gout)
         assert _rel(M.apply(v), ref) <= 1e-12
-        for sched in ("syncfree", "band"):                   # both schedules, forced where eligible
+        for sched in ("syncfree", "band", "lds"):            # every schedule, forced where eligible
             for f in ("L", "U"):
-                if sched == "syncfree" or M.schedule(f)["est_band_us"] >= 0:
+                if sched == "syncfree" or (sched == "band" and M.schedule(f)["est_band_us"] >= 0) or \
+                        (sched == "lds" and n <= 18432):
                     M.schedule(f, set=sched)
             assert _rel(M.apply(v), ref) <= 1e-12, sched
     # single factors, no permutations
@@ -195,7 +196,38 @@ def test_gauss_seidel_factor_schedules(psk, m):
     M = TriangularSolveChain(A.shape[0], U=U)
     info = M.schedule("U")
     assert info["est_band_us"] > 0 and info["est_syncfree_us"] > 0
-    for sched in ("band", "syncfree"):
+    outs = {}
+    for sched in ("band", "syncfree", "lds") if A.shape[0] <= 18432 else ("band", "syncfree"):
         M.schedule("U", set=sched)
-        assert _rel(M.apply(v), ref) <= 1e-12, sched
+        outs[sched] = M.apply(v)
+        assert _rel(outs[sched], ref) <= 1e-12, sched
         assert _rel(M.apply(v), ref) <= 1e-12, sched          # re-apply (sentinel refill)
+    if "lds" in outs:   # the LDS schedule runs the sync-free row arithmetic: bit-identical
+        assert np.array_equal(outs["lds"], outs["syncfree"])
+
+
+@pytest.mark.parametrize("n,dens", [(3000, 0.08), (18432, 0.002)])
+def test_lds_schedule_matches_syncfree(psk, n, dens):
+    """The single-workgroup LDS schedule (x in LDS) on coarse-LU-like factors: long rows (> 3 chunks
+    of 64 entries at n=3000) and the largest eligible size. Bit-identical to the sync-free kernel
+    (same per-row arithmetic), within 1e-12 of spsolve_triangular; a larger factor is refused."""
+    from pysolvers_amd import _native as N
+    from pysolvers_amd.Linear import TriangularSolveChain
+    rng = np.random.default_rng(n)
+    Lo = sp.tril(sp.random(n, n, density=dens, random_state=rng), k=-1).tocsr() * (2.0 / (dens * n))
+    L = (Lo + sp.diags(1.0 + rng.random(n))).tocsr()
+    U = L.T.tocsr()
+    v = rng.standard_normal(n)
+    ref = spla.spsolve_triangular(U, spla.spsolve_triangular(L, v, lower=True), lower=False)
+    M = TriangularSolveChain(n, L=L, U=U)
+    outs = {}
+    for sched in ("syncfree", "lds"):
+        for f in ("L", "U"):
+            M.schedule(f, set=sched)
+        outs[sched] = M.apply(v)
+        assert _rel(outs[sched], ref) <= 1e-12, sched
+        assert _rel(M.apply(v), ref) <= 1e-12, sched
+    assert np.array_equal(outs["lds"], outs["syncfree"])
+    big = TriangularSolveChain(18433, L=sp.eye(18433, format="csr"))
+    with pytest.raises(N.PskError):
+        big.schedule("L", set="lds")

@@ -104,6 +104,14 @@ def main():
     per.append(dict(level=0, n=M.levels()[0], coarse_solve_ms=timed(co, v0), L=co.schedule("L"), U=co.schedule("U"),
                     dep_levels=[co.device_info()["levels_l"], co.device_info()["levels_u"]],
                     nnz=[co.device_info()["nnz_l"], co.device_info()["nnz_u"]]))
+    if M.levels()[0] <= 18432:   # coarse solve under each schedule it can run, then back to the chosen one
+        chosen = (co.schedule("L")["schedule"], co.schedule("U")["schedule"])
+        for sched in ("syncfree", "lds"):
+            co.schedule("L", set=sched)
+            co.schedule("U", set=sched)
+            per[-1]["coarse_solve_ms_" + sched] = timed(co, v0)
+        co.schedule("L", set=chosen[0])
+        co.schedule("U", set=chosen[1])
     out["per_level"] = per
     out["setup_s"] = time.time() - t
     sol = psk.DeviceVector(n)
