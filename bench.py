@@ -44,9 +44,22 @@ def spmv_bytes(n, nnz):
     return 12 * nnz + 4 * (n + 1) + 16 * n
 
 
+PCG_VEC_BYTES_PER_ROW = 80   # K2 (r, Ap, dinv in; r out) + K3 (r, p, x, dinv in; x, p out), Jacobi
+LAYOUT_NAMES = {0: "csr", 1: "sliced", 2: "sliced_wide", 3: "sliced_dict"}   # PSK_LAYOUT_*
+
+
 def pcg_iter_bytes(n, nnz, jacobi=True):
-    """Compulsory bytes of one PCG iteration in libpsk's 3-launch schedule."""
-    return spmv_bytes(n, nnz) + (80 if jacobi else 64) * n
+    """Compulsory bytes of one PCG iteration in libpsk's 3-launch schedule with a CSR SpMV
+    (SURVEY.md §8d)."""
+    return spmv_bytes(n, nnz) + (PCG_VEC_BYTES_PER_ROW if jacobi else 64) * n
+
+
+def layout_bytes(N, A, n):
+    """Bytes one SpMV of A must move in its current storage layout — the matrix stream
+    (psk_csr_layout) + x read once + y written — and the layout's name."""
+    lay, stream = N.I32(), N.I64()
+    N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), None, None, ctypes.byref(stream)), "psk_csr_layout")
+    return stream.value + 16 * n, LAYOUT_NAMES[lay.value]
 
 
 def cpu_baseline(m, iters):
@@ -80,7 +93,7 @@ def main():
     ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1e_pmc_traffic_16384.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1h_pmc_traffic_16384.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same kernel and side")
     args = ap.parse_args()
 
@@ -204,8 +217,12 @@ def main():
                                      ctypes.byref(stream)), "psk_csr_layout")
         sliced = lay.value != N.PSK_LAYOUT_CSR
         kname = "spmv_sliced_kernel<kSpmvDot>" if sliced else "spmv_kernel<kSpmvDot>"
-        ach = bspmv / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
-        biter = pcg_iter_bytes(n, nnz)
+        # the bytes this launch must move in its storage layout (matrix stream + x read + y written;
+        # DESIGN.md "Roofline accounting"); with a value dictionary far fewer than CSR's 12 B/entry
+        blay = stream.value + 16 * nloc_r0
+        ach = blay / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
+        csr_eq = bspmv / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
+        biter = blay * world + PCG_VEC_BYTES_PER_ROW * n
         out = {
             "metric": METRIC,
             "value": it_s,
@@ -228,11 +245,9 @@ def main():
                          "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (ach / HBM_PEAK_GBPS) if ach else None,
                          **pmc_traffic(args.traffic_json, m, world, sliced),
-                         "algorithmic_bytes_per_launch": bspmv, "avg_launch_ms": res.spmv_ms,
-                         "launches": res.spmv_launches,
-                         "layout": {N.PSK_LAYOUT_CSR: "csr", N.PSK_LAYOUT_SLICED: "sliced",
-                                    N.PSK_LAYOUT_SLICED_WIDE: "sliced_wide"}[lay.value],
-                         "layout_bytes_per_launch": stream.value + 16 * nloc_r0},
+                         "algorithmic_bytes_per_launch": blay, "avg_launch_ms": res.spmv_ms,
+                         "launches": res.spmv_launches, "layout": LAYOUT_NAMES[lay.value],
+                         "csr_bytes_per_launch": bspmv, "csr_equivalent_GBps": csr_eq},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
@@ -244,8 +259,8 @@ def main():
             bms = ctypes.c_double()
             N.check(N.lib.psk_spmv_timed(A, db, dsol, 20, ctypes.byref(bms)), "psk_spmv_timed")
             out["spmv_plain_batch20"] = {"avg_launch_ms": bms.value,
-                                         "achieved_GBps": bspmv / (bms.value * 1e-3) / 1e9,
-                                         "frac": bspmv / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+                                         "achieved_GBps": blay / (bms.value * 1e-3) / 1e9,
+                                         "frac": blay / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS}
             out["spmv_csr_layout_batch20"] = csr_layout_batch(N, A, db, dsol, bspmv)
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
@@ -319,15 +334,17 @@ def spmv_10m(N, iters=30):
     res = N.PskResult()
     N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
     b = spmv_bytes(n, nnz)
-    gbps = b / (res.spmv_ms * 1e-3) / 1e9
+    bl, lname = layout_bytes(N, A, n)
+    gbps = bl / (res.spmv_ms * 1e-3) / 1e9
     # back-to-back launches between two events (no per-launch event in between)
     bms = ctypes.c_double()
     N.check(N.lib.psk_spmv_timed(A, dx, db, 50, ctypes.byref(bms)), "psk_spmv_timed")
-    bb = b / (bms.value * 1e-3) / 1e9
+    bb = bl / (bms.value * 1e-3) / 1e9
     csr = csr_layout_batch(N, A, dx, db, b, reps=50)
-    out = {"n": n, "nnz": nnz, "avg_launch_ms": res.spmv_ms, "achieved_GBps": gbps,
+    out = {"n": n, "nnz": nnz, "layout": lname, "avg_launch_ms": res.spmv_ms, "achieved_GBps": gbps,
            "frac": gbps / HBM_PEAK_GBPS, "pcg_it_per_s": iters / (res.loop_ms * 1e-3),
-           "algorithmic_bytes_per_launch": b,
+           "algorithmic_bytes_per_launch": bl, "csr_bytes_per_launch": b,
+           "csr_equivalent_GBps": b / (res.spmv_ms * 1e-3) / 1e9,
            "batch50": {"kernel": "SpMV, plain mode, the matrix's default layout", "avg_launch_ms": bms.value, "achieved_GBps": bb,
                        "frac": bb / HBM_PEAK_GBPS,
                        "how": "50 back-to-back launches between two HIP events on the library stream"},
@@ -364,10 +381,10 @@ def pcg_4096(N, iters=300):
     N.check(N.lib.psk_synchronize(), "sync")
     dt = time.perf_counter() - t0
     res = run(50, 1)
-    b = spmv_bytes(n, nnz)
-    out = {"n": n, "nnz": nnz, "iters": iters, "pcg_it_per_s": iters / dt,
-           "pcg_iteration_frac_of_peak": pcg_iter_bytes(n, nnz) * iters / dt / 1e9 / HBM_PEAK_GBPS,
-           "spmv_avg_launch_ms": res.spmv_ms, "spmv_frac": b / (res.spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    bl, lname = layout_bytes(N, A, n)
+    out = {"n": n, "nnz": nnz, "iters": iters, "layout": lname, "pcg_it_per_s": iters / dt,
+           "pcg_iteration_frac_of_peak": (bl + PCG_VEC_BYTES_PER_ROW * n) * iters / dt / 1e9 / HBM_PEAK_GBPS,
+           "spmv_avg_launch_ms": res.spmv_ms, "spmv_frac": bl / (res.spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     for p in (db, dx):
         N.lib.psk_dfree(p)
     N.lib.psk_prec_destroy(M)

@@ -130,9 +130,14 @@ int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
  *                           (16-B loads); a slice whose columns all lie within +-32767 of their rows
  *                           stores 16-bit column deltas two to a 32-bit word, any other slice 32-bit
  *                           columns;
- *   PSK_LAYOUT_SLICED_WIDE  the same with 32-bit columns in every slice.
- * Every creation path picks SLICED when its stream is no larger than the CSR stream (12 B/entry +
- * 4 B/row); env PSK_SPMV_LAYOUT=csr|sliced|sliced_wide overrides. set = -1 queries, a PSK_LAYOUT_*
+ *   PSK_LAYOUT_SLICED_WIDE  the same with 32-bit columns in every slice;
+ *   PSK_LAYOUT_SLICED_DICT  SLICED with the values replaced by one-byte indices into a dictionary of
+ *                           the matrix's distinct values (at most 8 bit patterns: stencils, graph
+ *                           Laplacians), 3 B per slot with 16-bit columns.
+ * Every creation path picks SLICED_DICT (values permitting) or SLICED when its stream is no larger
+ * than the CSR stream (12 B/entry + 4 B/row); env PSK_SPMV_LAYOUT=csr|sliced|sliced_wide|sliced_dict
+ * overrides (sliced: no dictionary). Forcing SLICED_DICT on a matrix with more than 8 distinct
+ * values fails with PSK_ERR_UNSUPPORTED. set = -1 queries, a PSK_LAYOUT_*
  * value switches (building or freeing the copy). Out: *slots = padded slots of the sliced copy (0
  * without one), *packed_slots = those in 16-bit slices, *stream_bytes = matrix bytes one SpMV
  * streams in the current layout (CSR: 12 nnz + 4 (n+1)). Out pointers may be NULL. Replaces
@@ -141,6 +146,7 @@ int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
 #define PSK_LAYOUT_CSR         0
 #define PSK_LAYOUT_SLICED      1
 #define PSK_LAYOUT_SLICED_WIDE 2
+#define PSK_LAYOUT_SLICED_DICT 3
 int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int64_t *packed_slots,
                    int64_t *stream_bytes);
 /* Copy the arrays back to host buffers (any pointer may be NULL). */

@@ -126,12 +126,13 @@ class DeviceCSR:
     def handle(self):
         return self._h
 
-    _LAYOUTS = {"csr": 0, "sliced": 1, "sliced_wide": 2}
+    _LAYOUTS = {"csr": 0, "sliced": 1, "sliced_wide": 2, "sliced_dict": 3}
 
     @property
     def layout(self):
-        """SpMV storage layout: "csr", "sliced" (16-bit column deltas where they fit) or
-        "sliced_wide" (psk_csr_layout; y is bit-identical in every layout)."""
+        """SpMV storage layout: "csr", "sliced" (16-bit column deltas where they fit), "sliced_wide"
+        or "sliced_dict" (sliced + one-byte value indices into the matrix's <= 8 distinct values)
+        (psk_csr_layout; y is bit-identical in every layout)."""
         k = N.I32()
         N.check(N.lib.psk_csr_layout(self._h, -1, ctypes.byref(k), None, None, None), "psk_csr_layout")
         return {v: n for n, v in self._LAYOUTS.items()}[k.value]

@@ -15,7 +15,7 @@ PSK_OK = 0
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_HOST, PSK_DEVICE = 0, 1
 PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
-PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE = 0, 1, 2
+PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE, PSK_LAYOUT_SLICED_DICT = 0, 1, 2, 3
 PSK_UNIQUE_ID_BYTES = 128
 
 STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOWN: "breakdown",

@@ -128,7 +128,9 @@ struct psk_csr {
     int8_t *sl_fmt = nullptr;    // [nslices] 1 = packed (int16 deltas)
     int32_t *sl_col = nullptr;   // nullptr when every slice is packed
     int32_t *sl_pcol = nullptr;  // nullptr when no slice is packed (2 int16 deltas per word)
-    double *sl_val = nullptr;
+    double *sl_val = nullptr;    // values, or (sl_dict) one byte index per slot, 4 per word
+    double *sl_dict = nullptr;   // value dictionary (<= 8 distinct values, padded to 8), nullptr = none
+    int32_t sl_dict_n = 0;
     int64_t sl_slots = 0, sl_packed_slots = 0, sl_stream_bytes = 0;
     // distributed
     psk_comm *comm = nullptr;

@@ -15,6 +15,7 @@
 // PCG, q_0.u for GMRES, ||b-Ax||^2 for the true residual), reduced deterministically by gridsum.
 #include "psk_internal.hpp"
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -148,9 +149,20 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
 //    int16 deltas c - row of slots 2p, 2p+1 in ONE int32 word at o + p*256 + l (kPad16 = padding),
 //    i.e. 2 B per slot in full 256-B wave loads; any other slice int32 columns at o + j*256 + l
 //    (-1 = padding). FD: 10.4 B per slot instead of 12 (every slice but a shard's halo lines).
+//  * values, when the whole matrix holds at most kDictMax distinct values (bit patterns; stencils,
+//    graph Laplacians, FEM on uniform meshes): a value DICTIONARY (sl_dict) and one byte per slot,
+//    the indices of slots 4q..4q+3 of lane l in one 32-bit word at word o*2 + q*256 + l of the
+//    value buffer (inside the slice's own value region, so no extra offsets); 3 B per slot with
+//    packed columns instead of 10. The kernel keeps the dictionary in scalar registers and picks a
+//    slot's value with a select tree (no memory instruction per slot: tools/dict_lab.hip, FD
+//    16384^2: doubles 2.96 ms, indices + dict[idx] loads 2.24 ms, indices + selects 1.70 ms). The
+//    dictionary entries are the matrix's own doubles, so every product, and y, is unchanged bit for
+//    bit (Kourtis et al., "CSR-VI" value compression).
 // tools/sell_lab.hip, tools/sell_pack_lab.hip (16384^2, back to back): CSR 3.61 ms, int32 columns
 // 3.20-3.39 ms, 16-bit pairs + paired values 2.87 ms; all bit-identical.
 constexpr int kSlice = kBlock;
+constexpr int kDictMax = 8;      // distinct values a dictionary may hold (held in scalar registers)
+constexpr int kDictCand = 64;    // candidates one detection pass collects
 constexpr int kSliceRegs = 8;             // slots held in registers; wider slices take the loop below
 constexpr int16_t kPad16 = INT16_MIN;     // padding slot of a packed slice
 constexpr int64_t kMaxDelta16 = 32767;
@@ -162,12 +174,28 @@ __device__ __forceinline__ int64_t sliced_vpos(int64_t o, int j, int w, int l) {
 
 __device__ __forceinline__ int32_t unpack_delta(int32_t row, int16_t d) { return d == kPad16 ? -1 : row + (int32_t)d; }
 
-template <int MODE>
+__device__ __forceinline__ bool same_bits(double a, double b) {
+    return __double_as_longlong(a) == __double_as_longlong(b);
+}
+
+// dictionary entry idx (< DK) by selects on the index bits; dv lives in scalar registers
+template <int DK>
+__device__ __forceinline__ double dict_pick(const double *dv, uint32_t idx) {
+    if (DK == 2) return (idx & 1) ? dv[1] : dv[0];
+    const double a0 = (idx & 1) ? dv[1] : dv[0], a1 = (idx & 1) ? dv[3] : dv[2];
+    const double b0 = (idx & 2) ? a1 : a0;
+    if (DK == 4) return b0;
+    const double a2 = (idx & 1) ? dv[5] : dv[4], a3 = (idx & 1) ? dv[7] : dv[6];
+    const double b1 = (idx & 2) ? a3 : a2;
+    return (idx & 4) ? b1 : b0;
+}
+
+template <int MODE, int DK>   // DK: dictionary size class (0 = double values, 2 / 4 / 8 entries)
 __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     int64_t n, const int64_t *__restrict__ soff, const int8_t *__restrict__ sfmt, const int32_t *__restrict__ scol,
-    const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ x,
-    double *__restrict__ y, const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs,
-    const int32_t *__restrict__ done) {
+    const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ sdict,
+    const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
+    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
     if (done != nullptr && *done != 0) return;
     __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
@@ -176,6 +204,10 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const int64_t o = soff[t];
     const int w = (int)((soff[t + 1] - o) / kSlice);
     const bool packed = sfmt[t] != 0;   // uniform across the workgroup
+    const int32_t *vword = reinterpret_cast<const int32_t *>(sval) + 2 * o;   // dictionary indices
+    double dv[DK > 0 ? DK : 1];
+#pragma unroll
+    for (int k = 0; k < DK; ++k) dv[k] = sdict[k];   // uniform: scalar loads
     const int32_t row32 = (int32_t)row;
     double eq = 0.0;
     if (has) {
@@ -192,15 +224,23 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             cc[j] = -1;
             vv[j] = 0.0;
         }
-        // the slice's whole stream first (w and packed are uniform): values by pairs, then columns
+        // the slice's whole stream first (w and packed are uniform): values by pairs (or dictionary
+        // index words), then columns
+        int32_t vw[kSliceRegs / 4];
+        if (DK > 0) {
 #pragma unroll
-        for (int p = 0; p < kSliceRegs / 2; ++p) {
-            if (2 * p + 1 < w) {
-                const dv2 v2 = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(sval + o + 2 * p * kSlice) + tid);
-                vv[2 * p] = v2.x;
-                vv[2 * p + 1] = v2.y;
-            } else if (2 * p < w) {
-                vv[2 * p] = ld_stream(sval + o + 2 * p * kSlice + tid);
+            for (int q = 0; q < kSliceRegs / 4; ++q) vw[q] = 4 * q < w ? ld_stream(vword + q * kSlice + tid) : 0;
+        } else {
+#pragma unroll
+            for (int p = 0; p < kSliceRegs / 2; ++p) {
+                if (2 * p + 1 < w) {
+                    const dv2 v2 =
+                        __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(sval + o + 2 * p * kSlice) + tid);
+                    vv[2 * p] = v2.x;
+                    vv[2 * p + 1] = v2.y;
+                } else if (2 * p < w) {
+                    vv[2 * p] = ld_stream(sval + o + 2 * p * kSlice + tid);
+                }
             }
         }
         if (packed) {
@@ -215,6 +255,11 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
 #pragma unroll
             for (int j = 0; j < kSliceRegs; ++j)
                 if (j < w) cc[j] = ld_stream(scol + o + j * kSlice + tid);
+        }
+        if (DK > 0) {
+#pragma unroll
+            for (int j = 0; j < kSliceRegs; ++j)
+                if (j < w) vv[j] = dict_pick<DK>(dv, ((uint32_t)vw[j >> 2] >> (8 * (j & 3))) & 0xff);
         }
 #pragma unroll
         for (int j = 0; j < kSliceRegs; ++j) {   // then every gather
@@ -239,7 +284,11 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             if (c < 0) break;   // only padding follows a row's last entry
             double xx = x[c];
             if (MODE == kSpmvJacobiDot) xx = aux_d[c] * xx;
-            sum = sum + ld_stream(sval + sliced_vpos(o, j, w, tid)) * xx;
+            const double v =
+                DK > 0 ? dict_pick<DK>(dv, ((uint32_t)ld_stream(vword + (int64_t)(j >> 2) * kSlice + tid) >> (8 * (j & 3))) &
+                                               0xff)
+                       : ld_stream(sval + sliced_vpos(o, j, w, tid));
+            sum = sum + v * xx;
         }
     }
     double acc = 0.0;
@@ -300,13 +349,42 @@ __global__ __launch_bounds__(kBlock) void sliced_shape_kernel(int64_t n, const i
     }
 }
 
+// One detection pass for the value dictionary: every wave that meets a value (bit pattern) not in
+// dict[0, nd) offers its first such value; the first kDictCand offers land in cand. No offers =
+// the dictionary is complete.
+__global__ __launch_bounds__(kBlock) void dict_scan_kernel(int64_t nnz, const double *__restrict__ vals,
+                                                           const double *__restrict__ dict, int nd,
+                                                           int32_t *__restrict__ ncand, double *__restrict__ cand) {
+    __shared__ double dl[kDictMax];
+    if (threadIdx.x < nd) dl[threadIdx.x] = dict[threadIdx.x];
+    __syncthreads();
+    double mine = 0.0;
+    bool has = false;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < nnz; i += (int64_t)gridDim.x * kBlock) {
+        const double v = vals[i];
+        bool found = false;
+        for (int k = 0; k < nd && !found; ++k) found = same_bits(v, dl[k]);
+        if (!found) {
+            mine = v;
+            has = true;
+            break;
+        }
+    }
+    const uint64_t m = __ballot(has);
+    if (m != 0 && (threadIdx.x & 63) == __builtin_ctzll(m)) {
+        const int32_t slot = atomicAdd(ncand, 1);
+        if (slot < kDictCand) cand[slot] = mine;
+    }
+}
+
 // one workgroup per slice, one lane per row (lanes past n write padding): coalesced stores
 __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const int32_t *__restrict__ rowptr,
                                                              const int32_t *__restrict__ colidx,
                                                              const double *__restrict__ vals,
                                                              const int64_t *__restrict__ soff,
                                                              const int8_t *__restrict__ sfmt, int32_t *__restrict__ scol,
-                                                             int32_t *__restrict__ spcol, double *__restrict__ sval) {
+                                                             int32_t *__restrict__ spcol, double *__restrict__ sval,
+                                                             const double *__restrict__ sdict, int nd) {
     const int tid = threadIdx.x;
     const int64_t t = blockIdx.x, row = t * kSlice + tid;
     const int64_t o = soff[t];
@@ -315,8 +393,22 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
     const int64_t a = row < n ? rowptr[row] : 0;
     const int64_t len = row < n ? rowptr[row + 1] - a : 0;
     for (int j = 0; j < w; ++j) {
-        sval[sliced_vpos(o, j, w, tid)] = j < len ? vals[a + j] : 0.0;
+        if (!sdict) sval[sliced_vpos(o, j, w, tid)] = j < len ? vals[a + j] : 0.0;
         if (!packed) scol[o + (int64_t)j * kSlice + tid] = j < len ? colidx[a + j] : -1;
+    }
+    if (sdict) {   // index words; padding slots index entry 0 (never read: their column is padding)
+        int32_t *vword = reinterpret_cast<int32_t *>(sval) + 2 * o;
+        for (int q = 0; 4 * q < w; ++q) {
+            uint32_t word = 0;
+            for (int b = 0; b < 4; ++b) {
+                const int j = 4 * q + b;
+                uint32_t k = 0;
+                if (j < len)
+                    while (k + 1 < (uint32_t)nd && !same_bits(sdict[k], vals[a + j])) ++k;
+                word |= k << (8 * b);
+            }
+            vword[(int64_t)q * kSlice + tid] = (int32_t)word;
+        }
     }
     if (packed)
         for (int p = 0; 2 * p < w; ++p) {
@@ -328,7 +420,7 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
 }
 
 void sliced_free(psk_csr *A) {
-    void *ptrs[] = {A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val};
+    void *ptrs[] = {A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     A->sl_off = nullptr;
@@ -336,16 +428,65 @@ void sliced_free(psk_csr *A) {
     A->sl_col = nullptr;
     A->sl_pcol = nullptr;
     A->sl_val = nullptr;
+    A->sl_dict = nullptr;
+    A->sl_dict_n = 0;
     A->sl_slots = 0;
     A->sl_packed_slots = 0;
     A->sl_stream_bytes = 0;
 }
 
-// Builds the sliced copy of A (pack = allow int16 column deltas). Unless `force`, only when its
-// stream (10 or 12 B per slot) is no larger than the CSR stream (12 B per entry + 4 B per row),
-// i.e. padding costs nothing, and quietly keeps CSR if HBM cannot hold the copy.
-static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack) {
+// The distinct values of A (bit patterns) when there are at most kDictMax of them, else empty:
+// detection passes over A->vals, each adding every new value it was offered (<= kDictMax + 1 passes,
+// one for a matrix of arbitrary values).
+static int find_value_dict(const psk_csr *A, hipStream_t s, std::vector<double> &dict) {
+    dict.clear();
+    if (A->nnz == 0) return PSK_OK;
+    DevBuf tmp;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } rel{tmp};
+    PSK_TRY(tmp.ensure((size_t)(kDictMax + kDictCand + 1) * sizeof(double)));
+    double *ddict = tmp.as<double>(), *dcand = ddict + kDictMax;
+    int32_t *dn = reinterpret_cast<int32_t *>(dcand + kDictCand);
+    const int64_t blocks = std::min<int64_t>((A->nnz + kBlock - 1) / kBlock, 2048);
+    std::vector<double> cand(kDictCand);
+    for (int pass = 0; pass <= kDictMax; ++pass) {
+        if (!dict.empty())
+            PSK_HIP(hipMemcpyAsync(ddict, dict.data(), dict.size() * sizeof(double), hipMemcpyHostToDevice, s));
+        PSK_HIP(hipMemsetAsync(dn, 0, sizeof(int32_t), s));
+        hipLaunchKernelGGL(dict_scan_kernel, dim3((unsigned)blocks), dim3(kBlock), 0, s, A->nnz, A->vals, ddict,
+                           (int)dict.size(), dn, dcand);
+        PSK_HIP(hipGetLastError());
+        int32_t nc = 0;
+        PSK_HIP(hipMemcpyAsync(&nc, dn, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        PSK_HIP(hipMemcpyAsync(cand.data(), dcand, kDictCand * sizeof(double), hipMemcpyDeviceToHost, s));
+        PSK_HIP(hipStreamSynchronize(s));
+        if (nc == 0) return PSK_OK;   // every value is in the dictionary
+        for (int i = 0; i < std::min(nc, kDictCand); ++i) {
+            bool seen = false;
+            for (double d : dict) seen = seen || std::memcmp(&d, &cand[(size_t)i], sizeof(double)) == 0;
+            if (!seen) dict.push_back(cand[(size_t)i]);
+            if ((int)dict.size() > kDictMax) {
+                dict.clear();
+                return PSK_OK;
+            }
+        }
+    }
+    dict.clear();
+    return PSK_OK;
+}
+
+// Builds the sliced copy of A (pack = allow int16 column deltas, use_dict = index values through a
+// dictionary when A has at most kDictMax distinct values; force_dict fails when it has more).
+// Unless `force`, only when its stream is no larger than the CSR stream (12 B per entry + 4 B per
+// row), i.e. padding costs nothing, and quietly keeps CSR if HBM cannot hold the copy.
+static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool use_dict, bool force_dict) {
     sliced_free(A);
+    std::vector<double> dict;
+    if (use_dict) PSK_TRY(find_value_dict(A, s, dict));
+    if (force_dict && dict.empty())
+        return fail(PSK_ERR_UNSUPPORTED, "sliced layout: more than 8 distinct values, no value dictionary");
     const int64_t nt = (A->n + kSlice - 1) / kSlice;
     if (nt == 0) return PSK_OK;   // nothing to multiply (launch_spmv returns early)
     if (nt > INT32_MAX) return force ? fail(PSK_ERR_UNSUPPORTED, "sliced layout: too many slices") : PSK_OK;
@@ -365,24 +506,28 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack) {
     std::vector<int64_t> off((size_t)nt + 1);
     std::vector<int8_t> fmt((size_t)nt);
     off[0] = 0;
-    int64_t packed_slots = 0, col_bytes = 0;
+    int64_t packed_slots = 0, col_bytes = 0, val_bytes = 0;
     for (int64_t t = 0; t < nt; ++t) {
         const int64_t w = wd[(size_t)t];
         off[(size_t)t + 1] = off[(size_t)t] + w * kSlice;
         fmt[(size_t)t] = (pack && wd[(size_t)(nt + t)] <= kMaxDelta16) ? 1 : 0;
         if (fmt[(size_t)t]) packed_slots += w * kSlice;
         col_bytes += (fmt[(size_t)t] ? 4 * ((w + 1) / 2) : 4 * w) * kSlice;
+        val_bytes += (dict.empty() ? 8 * w : 4 * ((w + 3) / 4)) * kSlice;
     }
     const int64_t slots = off[(size_t)nt];
     const int64_t wide_slots = slots - packed_slots;
-    // matrix bytes one SpMV streams: values, columns, slice offsets and formats
-    const int64_t stream = 8 * slots + col_bytes + 9 * nt + 8;
+    // matrix bytes one SpMV streams: values (or value indices + dictionary), columns, slice offsets
+    // and formats
+    const int64_t stream = val_bytes + 8 * (int64_t)dict.size() + col_bytes + 9 * nt + 8;
     if (!force && stream > 12 * A->nnz + 4 * (A->n + 1)) return PSK_OK;
     const size_t ms = slots > 0 ? (size_t)slots : 1;
     bool ok = hipMalloc(&A->sl_off, (size_t)(nt + 1) * 8) == hipSuccess &&
               hipMalloc(&A->sl_fmt, (size_t)nt) == hipSuccess && hipMalloc(&A->sl_val, ms * 8) == hipSuccess;
     if (ok && wide_slots > 0) ok = hipMalloc(&A->sl_col, ms * 4) == hipSuccess;      // indexed by slot
     if (ok && packed_slots > 0) ok = hipMalloc(&A->sl_pcol, ms * 4) == hipSuccess;   // words from each slice's o
+    if (ok && !dict.empty()) ok = hipMalloc(&A->sl_dict, kDictMax * 8) == hipSuccess;   // padded: the kernel
+                                                                                         // reads its size class
     if (!ok) {
         (void)hipGetLastError();
         sliced_free(A);
@@ -390,8 +535,14 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack) {
     }
     PSK_HIP(hipMemcpyAsync(A->sl_off, off.data(), (size_t)(nt + 1) * 8, hipMemcpyHostToDevice, s));
     PSK_HIP(hipMemcpyAsync(A->sl_fmt, fmt.data(), (size_t)nt, hipMemcpyHostToDevice, s));
+    if (!dict.empty()) {
+        std::vector<double> padded(dict);
+        padded.resize(kDictMax, 0.0);
+        PSK_HIP(hipMemcpyAsync(A->sl_dict, padded.data(), kDictMax * 8, hipMemcpyHostToDevice, s));
+    }
+    A->sl_dict_n = (int32_t)dict.size();
     hipLaunchKernelGGL(sliced_fill_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, A->vals,
-                       A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val);
+                       A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, A->sl_dict_n);
     PSK_HIP(hipGetLastError());
     PSK_HIP(hipStreamSynchronize(s));
     A->sl_slots = slots;
@@ -405,8 +556,10 @@ int csr_choose_layout(psk_csr *A, hipStream_t s) {
     const char *e = std::getenv("PSK_SPMV_LAYOUT");
     if (e && std::strcmp(e, "csr") == 0) return PSK_OK;
     const bool wide = e && std::strcmp(e, "sliced_wide") == 0;
-    const bool force = e && (std::strcmp(e, "sliced") == 0 || wide);
-    int rc = sliced_build(A, s, force, !wide);
+    const bool plain = e && std::strcmp(e, "sliced") == 0;
+    const bool force = e && (plain || wide || std::strcmp(e, "sliced_dict") == 0);
+    // auto and sliced_dict: a dictionary when the values allow one (never an error here)
+    int rc = sliced_build(A, s, force, !wide, !wide && !plain, false);
     if (rc != PSK_OK) sliced_free(A);
     return rc;
 }
@@ -432,9 +585,17 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
     dim3 gd((unsigned)nwg), bd(kBlock);
     if (sliced) {
-#define PSK_SLICED_LAUNCH(M)                                                                                 \
-    hipLaunchKernelGGL(spmv_sliced_kernel<M>, gd, bd, 0, s, A->n, A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, \
-                       A->sl_val, x, y, aux_d, aux_q, gs, done_flag)
+        const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
+#define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
+    hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_fmt, A->sl_col,        \
+                       A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag)
+#define PSK_SLICED_LAUNCH(M)                                                                                   \
+    do {                                                                                                       \
+        if (dk == 0) PSK_SLICED_LAUNCH_DK(M, 0);                                                               \
+        else if (dk == 2) PSK_SLICED_LAUNCH_DK(M, 2);                                                          \
+        else if (dk == 4) PSK_SLICED_LAUNCH_DK(M, 4);                                                          \
+        else PSK_SLICED_LAUNCH_DK(M, 8);                                                                       \
+    } while (0)
         switch (mode) {
         case kSpmvPlain: PSK_SLICED_LAUNCH(kSpmvPlain); break;
         case kSpmvDot: PSK_SLICED_LAUNCH(kSpmvDot); break;
@@ -446,6 +607,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
             return fail(PSK_ERR_ARG, "unknown spmv mode");
         }
 #undef PSK_SLICED_LAUNCH
+#undef PSK_SLICED_LAUNCH_DK
         PSK_HIP(hipGetLastError());
         return PSK_OK;
     }
@@ -727,17 +889,23 @@ int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz) {
 int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int64_t *packed_slots,
                    int64_t *stream_bytes) {
     if (!A) return fail(PSK_ERR_ARG, "psk_csr_layout: NULL matrix");
-    if (set != -1 && set != PSK_LAYOUT_CSR && set != PSK_LAYOUT_SLICED && set != PSK_LAYOUT_SLICED_WIDE)
+    if (set != -1 && set != PSK_LAYOUT_CSR && set != PSK_LAYOUT_SLICED && set != PSK_LAYOUT_SLICED_WIDE &&
+        set != PSK_LAYOUT_SLICED_DICT)
         return fail(PSK_ERR_ARG, "psk_csr_layout: set must be -1 or a PSK_LAYOUT_* value");
     if (set != -1) {
         Context *c;
         PSK_TRY(ctx(&c));
         PSK_HIP(hipStreamSynchronize(c->stream));   // queued launches may still read the old layout
         if (set == PSK_LAYOUT_CSR) sliced_free(A);
-        else PSK_TRY(sliced_build(A, c->stream, true, set == PSK_LAYOUT_SLICED));
+        else
+            PSK_TRY(sliced_build(A, c->stream, true, set != PSK_LAYOUT_SLICED_WIDE, set == PSK_LAYOUT_SLICED_DICT,
+                                 set == PSK_LAYOUT_SLICED_DICT));
     }
-    if (layout) *layout = !A->sl_off ? PSK_LAYOUT_CSR : (A->sl_col && !A->sl_pcol ? PSK_LAYOUT_SLICED_WIDE
-                                                                                 : PSK_LAYOUT_SLICED);
+    if (layout)
+        *layout = !A->sl_off                  ? PSK_LAYOUT_CSR
+                  : A->sl_dict                ? PSK_LAYOUT_SLICED_DICT
+                  : A->sl_col && !A->sl_pcol ? PSK_LAYOUT_SLICED_WIDE
+                                              : PSK_LAYOUT_SLICED;
     if (slots) *slots = A->sl_slots;
     if (packed_slots) *packed_slots = A->sl_packed_slots;
     if (stream_bytes) *stream_bytes = A->sl_off ? A->sl_stream_bytes : 12 * A->nnz + 4 * (A->n + 1);

@@ -31,8 +31,9 @@ def _ctl(**kw):
 
 
 def test_layout_auto_choice(psk):
-    """FD rows fill every slot of a slice (sliced chosen); random ragged rows would pad (CSR kept)."""
-    assert psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, 64).layout == "sliced"
+    """FD rows fill every slot of a slice and hold 2 distinct values (sliced with a value dictionary
+    chosen); random ragged rows would pad (CSR kept)."""
+    assert psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, 64).layout == "sliced_dict"
     assert psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, 2).layout == "csr"      # one mostly empty slice
     rng = np.random.default_rng(5)
     assert psk.DeviceCSR.from_scipy(_ragged_matrix(rng, 5000)).layout == "csr"
@@ -75,7 +76,7 @@ def test_spmv_mixed_packed_and_wide_slices(psk):
     A = A.tocsr()
     x = rng.standard_normal(n)
     dA = psk.DeviceCSR.from_scipy(A)
-    assert dA.layout == "sliced"
+    assert dA.layout == "sliced"          # random values: no dictionary
     slots, packed = dA.set_layout("sliced")
     assert 0 < packed < slots
     assert np.array_equal(psk.mvmult(dA, x), A @ x)
@@ -97,7 +98,7 @@ def test_fd_large_layouts_bitwise(psk):
     from oracle import fdlap, native
     m = 3163
     dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
-    assert dA.layout == "sliced"
+    assert dA.layout == "sliced_dict"
     x = np.random.default_rng(1).random(m * m)
     slots, packed = dA.set_layout("sliced")
     nnz = 5 * m * m - 4 * m
@@ -105,8 +106,9 @@ def test_fd_large_layouts_bitwise(psk):
     ys = psk.mvmult(dA, x)
     ref = native.csr_matvec(fdlap.fd_laplacian_2d(-1.0, 1.0, m), x)
     assert np.array_equal(ys, ref)
-    for lay in ("csr", "sliced_wide"):
+    for lay in ("csr", "sliced_wide", "sliced_dict"):
         dA.set_layout(lay)
+        assert dA.layout == lay
         assert np.array_equal(psk.mvmult(dA, x), ref)
 
 
@@ -119,7 +121,7 @@ def _solve_case(psk, case, d, monkeypatch, layout):
                                                                                                  d["b"])
 
 
-@pytest.mark.parametrize("layout", ["csr", "sliced", "sliced_wide"])
+@pytest.mark.parametrize("layout", ["csr", "sliced", "sliced_wide", "sliced_dict"])
 @pytest.mark.parametrize("case", solver_cases(), ids=lambda c: c["file"][:-4])
 def test_solver_matches_reference_each_layout(psk, case, layout, monkeypatch):
     """Every golden solver case meets the parity bar with either layout forced everywhere. (The dot
@@ -137,7 +139,7 @@ def test_fd_trajectories_bitwise_across_layouts(psk, file, monkeypatch):
     case = next(c for c in solver_cases() if c["file"] == file)
     d = load_golden(file)
     s1 = _solve_case(psk, case, d, monkeypatch, "csr")
-    for lay in ("sliced", "sliced_wide"):
+    for lay in ("sliced", "sliced_wide", "sliced_dict"):
         s2 = _solve_case(psk, case, d, monkeypatch, lay)
         assert s1.iters() == s2.iters() and s1.success() == s2.success()
         assert np.array_equal(s1.soln(), s2.soln())
@@ -149,7 +151,7 @@ def test_amg_identical_across_layouts(psk, monkeypatch):
     d = load_golden("pcg_negfd32_ic.npz")
     A = golden_matrix(d)
     out = []
-    for lay in ("csr", "sliced", "sliced_wide"):
+    for lay in ("csr", "sliced", "sliced_wide", "sliced_dict"):
         monkeypatch.setenv("PSK_SPMV_LAYOUT", lay)
         st = psk.PCG(control=_ctl(maxiter=200, tau=1e-8), precond=psk.AMG(numIters=2, numLevels=3)).makeSolver() \
             .solve(A, d["b"])
@@ -179,12 +181,43 @@ def test_fd16384_spmv_full_size(psk):
     m = 16384
     n = m * m
     dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
-    assert dA.layout == "sliced"
+    assert dA.layout == "sliced_dict"
     x = np.random.default_rng(12345).random(n)
     y = psk.mvmult(dA, x)
     rng = np.random.default_rng(2)
     edge = np.arange(m, dtype=np.int64)
     rows = np.unique(np.concatenate([rng.integers(0, n, 400_000), edge, n - m + edge, edge * m, edge * m + m - 1]))
     assert np.array_equal(y[rows], _fd_rows_reference(m, x, rows))
-    dA.set_layout("csr")
-    assert np.array_equal(psk.mvmult(dA, x), y)
+    for lay in ("csr", "sliced"):
+        dA.set_layout(lay)
+        assert np.array_equal(psk.mvmult(dA, x), y), lay
+
+
+@pytest.mark.parametrize("nvals", [1, 2, 3, 4, 5, 8, 9])
+def test_value_dictionary(psk, nvals):
+    """Ragged rows (register and loop paths, empty rows, partial last slice) whose values come from
+    `nvals` distinct doubles, including -0.0 next to +0.0 and a subnormal: up to 8 (every select-tree
+    size class: 2, 4, 8) the auto layout indexes them through a dictionary and y equals scipy bit for
+    bit; at 9 there is no dictionary and forcing one fails."""
+    from pysolvers_amd import _native as N
+    rng = np.random.default_rng(nvals)
+    n = 20000
+    A = _ragged_matrix(rng, n, (17, 4096), (5, 6, 7))
+    pool = np.concatenate([[-0.0, 0.0, 5e-324, 1.0, -1.0 / 3.0], rng.standard_normal(64)])[:nvals]
+    A.data = pool[rng.integers(0, nvals, size=A.nnz)]
+    x = rng.standard_normal(n)
+    ref = A @ x
+    dA = psk.DeviceCSR.from_scipy(A)
+    if nvals <= 8:
+        assert dA.layout in ("csr", "sliced_dict")   # auto: whichever streams fewer bytes
+        dA.set_layout("sliced_dict")
+        assert dA.layout == "sliced_dict"
+        assert np.array_equal(psk.mvmult(dA, x).view(np.uint64), ref.view(np.uint64))
+        dA.set_layout("sliced")
+        assert dA.layout == "sliced"
+        assert np.array_equal(psk.mvmult(dA, x).view(np.uint64), ref.view(np.uint64))
+    else:
+        with pytest.raises(N.PskError):
+            dA.set_layout("sliced_dict")
+        assert dA.layout == "csr"        # a failed switch leaves no sliced copy
+        assert np.array_equal(psk.mvmult(dA, x), ref)
