@@ -125,10 +125,11 @@ struct psk_csr {
     // slot offset sl_off[t]. Present when the SpMV uses it (psk_csr_layout); the CSR arrays above
     // are always kept.
     int64_t *sl_off = nullptr;   // [nslices + 1] slot offsets
+    int64_t *sl_woff = nullptr;  // [nslices + 1] word offsets into sl_pcol (packed columns, value indices)
     int8_t *sl_fmt = nullptr;    // [nslices] 1 = packed (int16 deltas)
     int32_t *sl_col = nullptr;   // nullptr when every slice is packed
-    int32_t *sl_pcol = nullptr;  // nullptr when no slice is packed (2 int16 deltas per word)
-    double *sl_val = nullptr;    // values, or (sl_dict) one byte index per slot, 4 per word
+    int32_t *sl_pcol = nullptr;  // word stream: 2 int16 deltas per word, then 4 value indices per word
+    double *sl_val = nullptr;    // values (nullptr with a dictionary)
     double *sl_dict = nullptr;   // value dictionary (<= 8 distinct values, padded to 8), nullptr = none
     int32_t sl_dict_n = 0;
     int64_t sl_slots = 0, sl_packed_slots = 0, sl_stream_bytes = 0;

@@ -146,14 +146,16 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
 //  * values in slot PAIRS: slots 2p, 2p+1 of lane l adjacent at o + 2p*256 + 2l (one 16-B load per
 //    pair); an odd last slot at o + (w-1)*256 + l;
 //  * columns, by sl_fmt[t]: a "packed" slice (every column within +-32767 of its row) stores the
-//    int16 deltas c - row of slots 2p, 2p+1 in ONE int32 word at o + p*256 + l (kPad16 = padding),
-//    i.e. 2 B per slot in full 256-B wave loads; any other slice int32 columns at o + j*256 + l
-//    (-1 = padding). FD: 10.4 B per slot instead of 12 (every slice but a shard's halo lines).
+//    int16 deltas c - row of slots 2p, 2p+1 in ONE int32 word at word wo + p*256 + l of the word
+//    stream sl_pcol (wo = sl_woff[t]; kPad16 = padding), i.e. 2 B per slot in full 256-B wave
+//    loads; any other slice int32 columns at o + j*256 + l of sl_col (-1 = padding). FD: 10.4 B per
+//    slot instead of 12 (every slice but a shard's halo lines).
 //  * values, when the whole matrix holds at most kDictMax distinct values (bit patterns; stencils,
 //    graph Laplacians, FEM on uniform meshes): a value DICTIONARY (sl_dict) and one byte per slot,
-//    the indices of slots 4q..4q+3 of lane l in one 32-bit word at word o*2 + q*256 + l of the
-//    value buffer (inside the slice's own value region, so no extra offsets); 3 B per slot with
-//    packed columns instead of 10. The kernel keeps the dictionary in scalar registers and picks a
+//    the indices of slots 4q..4q+3 of lane l in one 32-bit word of the word stream, after the
+//    slice's column words (word wo + ceil(w/2)*256 + q*256 + l; wo + q*256 + l in a wide slice), so
+//    a slice's whole stream is one contiguous run; 3 B per slot with packed columns instead of 10
+//    (no sl_val then). The kernel keeps the dictionary in scalar registers and picks a
 //    slot's value with a select tree (no memory instruction per slot: tools/dict_lab.hip, FD
 //    16384^2: doubles 2.96 ms, indices + dict[idx] loads 2.24 ms, indices + selects 1.70 ms). The
 //    dictionary entries are the matrix's own doubles, so every product, and y, is unchanged bit for
@@ -192,8 +194,9 @@ __device__ __forceinline__ double dict_pick(const double *dv, uint32_t idx) {
 
 template <int MODE, int DK>   // DK: dictionary size class (0 = double values, 2 / 4 / 8 entries)
 __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
-    int64_t n, const int64_t *__restrict__ soff, const int8_t *__restrict__ sfmt, const int32_t *__restrict__ scol,
-    const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ sdict,
+    int64_t n, const int64_t *__restrict__ soff, const int64_t *__restrict__ swoff, const int8_t *__restrict__ sfmt,
+    const int32_t *__restrict__ scol, const int32_t *__restrict__ spcol, const double *__restrict__ sval,
+    const double *__restrict__ sdict,
     const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
     const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
     if (done != nullptr && *done != 0) return;
@@ -204,7 +207,8 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const int64_t o = soff[t];
     const int w = (int)((soff[t + 1] - o) / kSlice);
     const bool packed = sfmt[t] != 0;   // uniform across the workgroup
-    const int32_t *vword = reinterpret_cast<const int32_t *>(sval) + 2 * o;   // dictionary indices
+    const int32_t *pword = spcol + swoff[t];                                   // packed column words
+    const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
     double dv[DK > 0 ? DK : 1];
 #pragma unroll
     for (int k = 0; k < DK; ++k) dv[k] = sdict[k];   // uniform: scalar loads
@@ -247,7 +251,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
 #pragma unroll
             for (int p = 0; p < kSliceRegs / 2; ++p)
                 if (2 * p < w) {
-                    const int32_t word = ld_stream(spcol + o + p * kSlice + tid);
+                    const int32_t word = ld_stream(pword + p * kSlice + tid);
                     cc[2 * p] = unpack_delta(row32, (int16_t)(word & 0xffff));
                     cc[2 * p + 1] = unpack_delta(row32, (int16_t)(word >> 16));
                 }
@@ -276,7 +280,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
         for (int j = 0; j < w; ++j) {
             int32_t c;
             if (packed) {
-                const int32_t word = ld_stream(spcol + o + (int64_t)(j >> 1) * kSlice + tid);
+                const int32_t word = ld_stream(pword + (int64_t)(j >> 1) * kSlice + tid);
                 c = unpack_delta(row32, (int16_t)((j & 1) ? (word >> 16) : (word & 0xffff)));
             } else {
                 c = ld_stream(scol + o + (int64_t)j * kSlice + tid);
@@ -382,6 +386,7 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
                                                              const int32_t *__restrict__ colidx,
                                                              const double *__restrict__ vals,
                                                              const int64_t *__restrict__ soff,
+                                                             const int64_t *__restrict__ swoff,
                                                              const int8_t *__restrict__ sfmt, int32_t *__restrict__ scol,
                                                              int32_t *__restrict__ spcol, double *__restrict__ sval,
                                                              const double *__restrict__ sdict, int nd) {
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
         if (!packed) scol[o + (int64_t)j * kSlice + tid] = j < len ? colidx[a + j] : -1;
     }
     if (sdict) {   // index words; padding slots index entry 0 (never read: their column is padding)
-        int32_t *vword = reinterpret_cast<int32_t *>(sval) + 2 * o;
+        int32_t *vword = spcol + swoff[t] + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);
         for (int q = 0; 4 * q < w; ++q) {
             uint32_t word = 0;
             for (int b = 0; b < 4; ++b) {
@@ -415,15 +420,16 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
             const int j0 = 2 * p, j1 = 2 * p + 1;
             const int16_t d0 = j0 < len ? (int16_t)(colidx[a + j0] - row) : kPad16;
             const int16_t d1 = j1 < len ? (int16_t)(colidx[a + j1] - row) : kPad16;
-            spcol[o + (int64_t)p * kSlice + tid] = (int32_t)(uint16_t)d0 | ((int32_t)d1 * 65536);
+            spcol[swoff[t] + (int64_t)p * kSlice + tid] = (int32_t)(uint16_t)d0 | ((int32_t)d1 * 65536);
         }
 }
 
 void sliced_free(psk_csr *A) {
-    void *ptrs[] = {A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict};
+    void *ptrs[] = {A->sl_off, A->sl_woff, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     A->sl_off = nullptr;
+    A->sl_woff = nullptr;
     A->sl_fmt = nullptr;
     A->sl_col = nullptr;
     A->sl_pcol = nullptr;
@@ -503,9 +509,10 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
     std::vector<int32_t> wd((size_t)nt * 2);
     PSK_HIP(hipMemcpyAsync(wd.data(), tmp.p, (size_t)nt * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
-    std::vector<int64_t> off((size_t)nt + 1);
+    std::vector<int64_t> off((size_t)nt + 1), woff((size_t)nt + 1);
     std::vector<int8_t> fmt((size_t)nt);
     off[0] = 0;
+    woff[0] = 0;
     int64_t packed_slots = 0, col_bytes = 0, val_bytes = 0;
     for (int64_t t = 0; t < nt; ++t) {
         const int64_t w = wd[(size_t)t];
@@ -514,18 +521,23 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
         if (fmt[(size_t)t]) packed_slots += w * kSlice;
         col_bytes += (fmt[(size_t)t] ? 4 * ((w + 1) / 2) : 4 * w) * kSlice;
         val_bytes += (dict.empty() ? 8 * w : 4 * ((w + 3) / 4)) * kSlice;
+        // the word stream: packed column words, then dictionary index words
+        const int64_t words = (fmt[(size_t)t] ? (w + 1) / 2 : 0) + (dict.empty() ? 0 : (w + 3) / 4);
+        woff[(size_t)t + 1] = woff[(size_t)t] + words * kSlice;
     }
-    const int64_t slots = off[(size_t)nt];
+    const int64_t slots = off[(size_t)nt], nwords = woff[(size_t)nt];
     const int64_t wide_slots = slots - packed_slots;
     // matrix bytes one SpMV streams: values (or value indices + dictionary), columns, slice offsets
-    // and formats
-    const int64_t stream = val_bytes + 8 * (int64_t)dict.size() + col_bytes + 9 * nt + 8;
+    // (two arrays) and formats
+    const int64_t stream = val_bytes + 8 * (int64_t)dict.size() + col_bytes + 17 * nt + 16;
     if (!force && stream > 12 * A->nnz + 4 * (A->n + 1)) return PSK_OK;
     const size_t ms = slots > 0 ? (size_t)slots : 1;
     bool ok = hipMalloc(&A->sl_off, (size_t)(nt + 1) * 8) == hipSuccess &&
-              hipMalloc(&A->sl_fmt, (size_t)nt) == hipSuccess && hipMalloc(&A->sl_val, ms * 8) == hipSuccess;
-    if (ok && wide_slots > 0) ok = hipMalloc(&A->sl_col, ms * 4) == hipSuccess;      // indexed by slot
-    if (ok && packed_slots > 0) ok = hipMalloc(&A->sl_pcol, ms * 4) == hipSuccess;   // words from each slice's o
+              hipMalloc(&A->sl_woff, (size_t)(nt + 1) * 8) == hipSuccess &&
+              hipMalloc(&A->sl_fmt, (size_t)nt) == hipSuccess;
+    if (ok && dict.empty()) ok = hipMalloc(&A->sl_val, ms * 8) == hipSuccess;              // indexed by slot
+    if (ok && wide_slots > 0) ok = hipMalloc(&A->sl_col, ms * 4) == hipSuccess;            // indexed by slot
+    if (ok && nwords > 0) ok = hipMalloc(&A->sl_pcol, (size_t)nwords * 4) == hipSuccess;   // from sl_woff[t]
     if (ok && !dict.empty()) ok = hipMalloc(&A->sl_dict, kDictMax * 8) == hipSuccess;   // padded: the kernel
                                                                                          // reads its size class
     if (!ok) {
@@ -534,6 +546,7 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
         return force ? fail(PSK_ERR_ALLOC, "sliced layout: hipMalloc") : PSK_OK;
     }
     PSK_HIP(hipMemcpyAsync(A->sl_off, off.data(), (size_t)(nt + 1) * 8, hipMemcpyHostToDevice, s));
+    PSK_HIP(hipMemcpyAsync(A->sl_woff, woff.data(), (size_t)(nt + 1) * 8, hipMemcpyHostToDevice, s));
     PSK_HIP(hipMemcpyAsync(A->sl_fmt, fmt.data(), (size_t)nt, hipMemcpyHostToDevice, s));
     if (!dict.empty()) {
         std::vector<double> padded(dict);
@@ -542,7 +555,8 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
     }
     A->sl_dict_n = (int32_t)dict.size();
     hipLaunchKernelGGL(sliced_fill_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, A->vals,
-                       A->sl_off, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, A->sl_dict_n);
+                       A->sl_off, A->sl_woff, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict,
+                       A->sl_dict_n);
     PSK_HIP(hipGetLastError());
     PSK_HIP(hipStreamSynchronize(s));
     A->sl_slots = slots;
@@ -587,8 +601,8 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
-    hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_fmt, A->sl_col,        \
-                       A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag)
+    hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff, A->sl_fmt,       \
+                       A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag)
 #define PSK_SLICED_LAUNCH(M)                                                                                   \
     do {                                                                                                       \
         if (dk == 0) PSK_SLICED_LAUNCH_DK(M, 0);                                                               \
@@ -904,7 +918,7 @@ int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int
     if (layout)
         *layout = !A->sl_off                  ? PSK_LAYOUT_CSR
                   : A->sl_dict                ? PSK_LAYOUT_SLICED_DICT
-                  : A->sl_col && !A->sl_pcol ? PSK_LAYOUT_SLICED_WIDE
+                  : A->sl_packed_slots == 0   ? PSK_LAYOUT_SLICED_WIDE
                                               : PSK_LAYOUT_SLICED;
     if (slots) *slots = A->sl_slots;
     if (packed_slots) *packed_slots = A->sl_packed_slots;
