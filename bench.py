@@ -54,6 +54,14 @@ def pcg_iter_bytes(n, nnz, jacobi=True):
     return spmv_bytes(n, nnz) + (PCG_VEC_BYTES_PER_ROW if jacobi else 64) * n
 
 
+def vec_bytes_per_row(N, M):
+    """K2 + K3 bytes per row: 80 with a streamed DInv, 64 when the Jacobi diagonal is one scalar
+    (psk_prec_jacobi_uniform)."""
+    u = N.I32()
+    N.check(N.lib.psk_prec_jacobi_uniform(M, ctypes.byref(u), None), "psk_prec_jacobi_uniform")
+    return PCG_VEC_BYTES_PER_ROW - (16 if u.value else 0)
+
+
 def layout_bytes(N, A, n):
     """Bytes one SpMV of A must move in its current storage layout — the matrix stream
     (psk_csr_layout) + x read once + y written — and the layout's name."""
@@ -222,7 +230,8 @@ def main():
         blay = stream.value + 16 * nloc_r0
         ach = blay / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
         csr_eq = bspmv / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
-        biter = blay * world + PCG_VEC_BYTES_PER_ROW * n
+        vb = vec_bytes_per_row(N, M)
+        biter = blay * world + vb * n
         out = {
             "metric": METRIC,
             "value": it_s,
@@ -248,7 +257,7 @@ def main():
                          "algorithmic_bytes_per_launch": blay, "avg_launch_ms": res.spmv_ms,
                          "launches": res.spmv_launches, "layout": LAYOUT_NAMES[lay.value],
                          "csr_bytes_per_launch": bspmv, "csr_equivalent_GBps": csr_eq},
-            "pcg_iteration_roofline": {"bytes_per_iteration": biter,
+            "pcg_iteration_roofline": {"bytes_per_iteration": biter, "vector_bytes_per_row": vb,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
             "setup_s": setup_s,
@@ -310,7 +319,9 @@ def pmc_traffic(path, m, world, sliced):
         return {"traffic": None}
     if d.get("config", {}).get("side") != m or world != 1:
         return {"traffic": None}
-    want = "void psk::spmv_sliced_kernel<1>" if sliced else "void psk::spmv_kernel<1>"
+    # kSpmvDot = 1; the sliced kernel's second template argument is the dictionary size class
+    want = ("void psk::spmv_sliced_kernel<1>", "void psk::spmv_sliced_kernel<1,") if sliced \
+        else ("void psk::spmv_kernel<1>",)
     for k, v in d["kernels"].items():
         if k.startswith(want):
             return {"traffic": v["hbm_bytes_per_launch"],
@@ -383,7 +394,7 @@ def pcg_4096(N, iters=300):
     res = run(50, 1)
     bl, lname = layout_bytes(N, A, n)
     out = {"n": n, "nnz": nnz, "iters": iters, "layout": lname, "pcg_it_per_s": iters / dt,
-           "pcg_iteration_frac_of_peak": (bl + PCG_VEC_BYTES_PER_ROW * n) * iters / dt / 1e9 / HBM_PEAK_GBPS,
+           "pcg_iteration_frac_of_peak": (bl + vec_bytes_per_row(N, M) * n) * iters / dt / 1e9 / HBM_PEAK_GBPS,
            "spmv_avg_launch_ms": res.spmv_ms, "spmv_frac": bl / (res.spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     for p in (db, dx):
         N.lib.psk_dfree(p)

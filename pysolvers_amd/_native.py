@@ -64,6 +64,7 @@ SIGNATURES = {
     "psk_axpy": (ctypes.c_int, [I64, F64, P, P, I32]),
     "psk_prec_create": (ctypes.c_int, [P, I32, PP]),
     "psk_prec_apply": (ctypes.c_int, [P, I64, P, P, I32]),
+    "psk_prec_jacobi_uniform": (ctypes.c_int, [P, ctypes.POINTER(I32), ctypes.POINTER(ctypes.c_double)]),
     "psk_prec_create_ilu": (ctypes.c_int, [I64, P, P, P, P, P, P, P, P, PP]),
     "psk_prec_destroy": (ctypes.c_int, [P]),
     "psk_prec_create_trisolve": (ctypes.c_int, [I64, P, P, P, I32, P, P, P, I32, P, P, PP]),

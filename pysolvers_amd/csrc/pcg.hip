@@ -89,10 +89,11 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
 
 // ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
 // One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses). JAC: Jacobi
-// preconditioner fused (dinv != nullptr).
-template <bool JAC>
+// preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
+// diagonal matrices such as stencils: the same products, 8 B/row less per kernel).
+template <int JAC>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
-    int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv,
+    int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv, double ds,
     const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st, const double *__restrict__ udr,
     int64_t k) {
     if (st->done) return;
@@ -115,8 +116,8 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     // cache policy: Ap is dead after this kernel (non-temporal); r and dinv are re-read by K3
     if (i + 1 < n) {
         const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
-        dv2 d{};
-        if (JAC) d = ld2(dinv + i);
+        dv2 d{ds, ds};
+        if (JAC == 1) d = ld2(dinv + i);
         dv2 rn;
         rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
         rn.y = ro.y - alpha * a.y;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
         const double rn = r[i] - alpha * Ap[i];
-        const double u0 = JAC ? dinv[i] * rn : rn;
+        const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
         rr = rn * rn;
         ur = u0 * rn;
@@ -167,10 +168,10 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
 }
 
 // ---- K3: x += alpha p, convergence test, beta, p = u + beta p (one-shot, as K2) -------------
-template <bool JAC>
+template <int JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ r, double *__restrict__ p,
-    const double *__restrict__ dinv, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts,
+    const double *__restrict__ dinv, double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts,
     PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter,
     int fail_on_maxiter) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
@@ -183,8 +184,8 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
     if (i + 1 < n) {
         const dv2 ro = ld2nt(r + i), po = ld2(p + i), xo = ld2nt(x + i);
-        dv2 d{};
-        if (JAC) d = ld2nt(dinv + i);
+        dv2 d{ds, ds};
+        if (JAC == 1) d = ld2nt(dinv + i);
         double u0 = ro.x, u1 = ro.y;
         if (JAC) {
             u0 = d.x * ro.x;
@@ -198,7 +199,7 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
         st2nt(x + i, xn);
         st2(p + i, pn);
     } else if (i < n) {
-        const double u0 = JAC ? dinv[i] * r[i] : r[i];
+        const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
         const double pi = p[i];
         x[i] = x[i] + alpha * pi;
         p[i] = u0 + beta * pi;
@@ -355,6 +356,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     PcgWork w;
     PSK_TRY(pcg_workspace(A, maxiter, gen, P, w));
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
+    const int jac = !dinv ? 0 : M->dinv_uniform ? 2 : 1;
+    const double ds = jac == 2 ? M->dinv_value : 0.0;
     const int gv = grid_for_rows(c, n, kVecTile);    // persistent grid of the init kernels
     // one-shot grid of K2/K3 (one 512-element tile per workgroup); K1/K2 finish their dot products
     // in-launch (gridsum), so the loop's scalars are part1[0] = p.Ap and part2[0..1] = (r.r, u.r)
@@ -446,11 +449,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
         const dim3 gk((unsigned)nv);
-        if (dinv)
-            hipLaunchKernelGGL(pcg_update_kernel<true>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1g, P,
+        if (jac == 2)
+            hipLaunchKernelGGL(pcg_update_kernel<2>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
+                               gs2, w.st, w.udr, k);
+        else if (jac == 1)
+            hipLaunchKernelGGL(pcg_update_kernel<1>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
                                gs2, w.st, w.udr, k);
         else
-            hipLaunchKernelGGL(pcg_update_kernel<false>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, w.part1g, P,
+            hipLaunchKernelGGL(pcg_update_kernel<0>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
                                gs2, w.st, w.udr, k);
         if (sharded && (rc = allgather(A, w.part2, w.part2g, 2, s)) != PSK_OK) break;
         if (gen) {
@@ -459,12 +465,16 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             hipLaunchKernelGGL(pcg_gen_direction_kernel, gk, dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, w.part2,
                                w.part3, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         } else {
-            if (dinv)
-                hipLaunchKernelGGL(pcg_direction_kernel<true>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
+            if (jac == 2)
+                hipLaunchKernelGGL(pcg_direction_kernel<2>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
+                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                                   ctl->fail_on_maxiter);
+            else if (jac == 1)
+                hipLaunchKernelGGL(pcg_direction_kernel<1>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
                                    w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
                                    ctl->fail_on_maxiter);
             else
-                hipLaunchKernelGGL(pcg_direction_kernel<false>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv,
+                hipLaunchKernelGGL(pcg_direction_kernel<0>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
                                    w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
                                    ctl->fail_on_maxiter);
         }

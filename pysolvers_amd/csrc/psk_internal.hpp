@@ -120,10 +120,11 @@ struct psk_csr {
     double *vals = nullptr;
     int device = 0;
     // sliced copy of the same entries (spmv.hip, "sliced layout"): slices of kSlice rows, slot-major
-    // inside a slice (values in slot pairs), per slice either packed int16 column-delta pairs
-    // (sl_fmt[t] = 1, sl_pcol) or int32 columns (sl_col); every array is addressed from the slice's
-    // slot offset sl_off[t]. Present when the SpMV uses it (psk_csr_layout); the CSR arrays above
-    // are always kept.
+    // inside a slice (values in slot pairs, or byte indices into sl_dict), per slice either packed
+    // int16 column-delta pairs (sl_fmt[t] = 1) or int32 columns (sl_col); sl_col and sl_val are
+    // addressed from the slice's slot offset sl_off[t], the word stream sl_pcol (packed columns,
+    // then value indices) from sl_woff[t]. Present when the SpMV uses it (psk_csr_layout); the CSR
+    // arrays above are always kept.
     int64_t *sl_off = nullptr;   // [nslices + 1] slot offsets
     int64_t *sl_woff = nullptr;  // [nslices + 1] word offsets into sl_pcol (packed columns, value indices)
     int8_t *sl_fmt = nullptr;    // [nslices] 1 = packed (int16 deltas)
@@ -132,6 +133,7 @@ struct psk_csr {
     double *sl_val = nullptr;    // values (nullptr with a dictionary)
     double *sl_dict = nullptr;   // value dictionary (<= 8 distinct values, padded to 8), nullptr = none
     int32_t sl_dict_n = 0;
+    int32_t sl_uniform_w = 0;    // > 0: every slice this wide and packed (offsets computed, not loaded)
     int64_t sl_slots = 0, sl_packed_slots = 0, sl_stream_bytes = 0;
     // distributed
     psk_comm *comm = nullptr;
@@ -184,6 +186,8 @@ struct psk_prec {
     int kind = PSK_PREC_IDENTITY;
     int64_t n = 0;
     double *dinv = nullptr;   // JACOBI
+    bool dinv_uniform = false;   // every DInv entry the same bits (constant diagonal): PCG reads dinv_value
+    double dinv_value = 0.0;
     // PSK_PREC_ILU = triangular-solve chain: out = (U^-1 L^-1 v[gather_in])[gather_out]
     psk::TriFactor lo, up;
     int32_t *gather_in = nullptr, *gather_out = nullptr;

@@ -196,7 +196,7 @@ template <int MODE, int DK>   // DK: dictionary size class (0 = double values, 2
 __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     int64_t n, const int64_t *__restrict__ soff, const int64_t *__restrict__ swoff, const int8_t *__restrict__ sfmt,
     const int32_t *__restrict__ scol, const int32_t *__restrict__ spcol, const double *__restrict__ sval,
-    const double *__restrict__ sdict,
+    const double *__restrict__ sdict, int uw,
     const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
     const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
     if (done != nullptr && *done != 0) return;
@@ -204,10 +204,13 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const int tid = threadIdx.x;
     const int64_t t = blockIdx.x, row = t * kSlice + tid;
     const bool has = row < n;
-    const int64_t o = soff[t];
-    const int w = (int)((soff[t + 1] - o) / kSlice);
-    const bool packed = sfmt[t] != 0;   // uniform across the workgroup
-    const int32_t *pword = spcol + swoff[t];                                   // packed column words
+    // a uniform layout (uw > 0: every slice uw wide and packed) needs no per-slice header loads, so
+    // the stream loads do not wait for them
+    const int64_t o = uw ? t * uw * kSlice : soff[t];
+    const int w = uw ? uw : (int)((soff[t + 1] - o) / kSlice);
+    const bool packed = uw ? true : sfmt[t] != 0;   // uniform across the workgroup
+    const int64_t wo = uw ? t * ((uw + 1) / 2 + (DK > 0 ? (uw + 3) / 4 : 0)) * kSlice : swoff[t];
+    const int32_t *pword = spcol + wo;                                         // packed column words
     const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
     double dv[DK > 0 ? DK : 1];
 #pragma unroll
@@ -436,6 +439,7 @@ void sliced_free(psk_csr *A) {
     A->sl_val = nullptr;
     A->sl_dict = nullptr;
     A->sl_dict_n = 0;
+    A->sl_uniform_w = 0;
     A->sl_slots = 0;
     A->sl_packed_slots = 0;
     A->sl_stream_bytes = 0;
@@ -509,6 +513,21 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
     std::vector<int32_t> wd((size_t)nt * 2);
     PSK_HIP(hipMemcpyAsync(wd.data(), tmp.p, (size_t)nt * 2 * sizeof(int32_t), hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
+    // uniform: every slice padded to the widest when all pack and that pads at most 1% more slots
+    // (FD: only the first and last grid lines are narrower) — the kernel then computes every
+    // offset from the slice index (PSK_SPMV_UNIFORM=0 disables)
+    int64_t wmax = 0, wsum = 0;
+    bool all_pack = pack;
+    for (int64_t t = 0; t < nt; ++t) {
+        wmax = std::max<int64_t>(wmax, wd[(size_t)t]);
+        wsum += wd[(size_t)t];
+        all_pack = all_pack && wd[(size_t)(nt + t)] <= kMaxDelta16;
+    }
+    const char *ue = std::getenv("PSK_SPMV_UNIFORM");
+    const bool uniform =
+        all_pack && wmax > 0 && wmax <= 64 && wmax * nt * 100 <= wsum * 101 && !(ue && std::atoi(ue) == 0);
+    if (uniform)
+        for (int64_t t = 0; t < nt; ++t) wd[(size_t)t] = (int32_t)wmax;
     std::vector<int64_t> off((size_t)nt + 1), woff((size_t)nt + 1);
     std::vector<int8_t> fmt((size_t)nt);
     off[0] = 0;
@@ -529,7 +548,7 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
     const int64_t wide_slots = slots - packed_slots;
     // matrix bytes one SpMV streams: values (or value indices + dictionary), columns, slice offsets
     // (two arrays) and formats
-    const int64_t stream = val_bytes + 8 * (int64_t)dict.size() + col_bytes + 17 * nt + 16;
+    const int64_t stream = val_bytes + 8 * (int64_t)dict.size() + col_bytes + (uniform ? 0 : 17 * nt + 16);
     if (!force && stream > 12 * A->nnz + 4 * (A->n + 1)) return PSK_OK;
     const size_t ms = slots > 0 ? (size_t)slots : 1;
     bool ok = hipMalloc(&A->sl_off, (size_t)(nt + 1) * 8) == hipSuccess &&
@@ -554,6 +573,7 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
         PSK_HIP(hipMemcpyAsync(A->sl_dict, padded.data(), kDictMax * 8, hipMemcpyHostToDevice, s));
     }
     A->sl_dict_n = (int32_t)dict.size();
+    A->sl_uniform_w = uniform ? (int32_t)wmax : 0;
     hipLaunchKernelGGL(sliced_fill_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, A->vals,
                        A->sl_off, A->sl_woff, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict,
                        A->sl_dict_n);
@@ -602,7 +622,8 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
     hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff, A->sl_fmt,       \
-                       A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag)
+                       A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, A->sl_uniform_w, x, y, aux_d, aux_q, gs,   \
+                       done_flag)
 #define PSK_SLICED_LAUNCH(M)                                                                                   \
     do {                                                                                                       \
         if (dk == 0) PSK_SLICED_LAUNCH_DK(M, 0);                                                               \
@@ -1057,6 +1078,12 @@ int psk_axpy(int64_t n, double alpha, const double *x, double *y, int32_t loc) {
     return PSK_OK;
 }
 
+// flag = 1 when some v[i] differs from v[0] bit for bit
+__global__ void differs_from_first_kernel(int64_t n, const double *__restrict__ v, int32_t *flag) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && __double_as_longlong(v[i]) != __double_as_longlong(v[0])) *flag = 1;
+}
+
 int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out) {
     if (!A || !out) return fail(PSK_ERR_ARG, "psk_prec_create: NULL argument");
     if (kind != PSK_PREC_IDENTITY && kind != PSK_PREC_JACOBI)
@@ -1075,7 +1102,23 @@ int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out) {
         hipLaunchKernelGGL(jacobi_dinv_kernel, dim3((unsigned)((A->n + kBlock - 1) / kBlock)), dim3(kBlock),
                            0, c->stream, A->n, A->rowptr, A->colidx, A->vals, M->dinv);
         e = hipGetLastError();
+        // a constant diagonal (stencils) gives one DInv value: the PCG kernels then use the scalar
+        int32_t *dflag = nullptr;
+        if (e == hipSuccess) e = hipMalloc(&dflag, sizeof(int32_t));
+        if (e == hipSuccess) e = hipMemsetAsync(dflag, 0, sizeof(int32_t), c->stream);
+        if (e == hipSuccess) {
+            hipLaunchKernelGGL(differs_from_first_kernel, dim3((unsigned)((A->n + kBlock - 1) / kBlock)), dim3(kBlock),
+                               0, c->stream, A->n, M->dinv, dflag);
+            e = hipGetLastError();
+        }
+        int32_t differs = 1;
+        if (e == hipSuccess) e = hipMemcpyAsync(&differs, dflag, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess)
+            e = hipMemcpyAsync(&M->dinv_value, M->dinv, sizeof(double), hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (dflag) (void)hipFree(dflag);
+        const char *ue = std::getenv("PSK_JACOBI_UNIFORM");
+        M->dinv_uniform = e == hipSuccess && differs == 0 && !(ue && std::atoi(ue) == 0);
         if (e != hipSuccess) {
             (void)hipFree(M->dinv);
             delete M;
@@ -1083,6 +1126,13 @@ int psk_prec_create(const psk_csr *A, int32_t kind, psk_prec **out) {
         }
     }
     *out = M;
+    return PSK_OK;
+}
+
+int psk_prec_jacobi_uniform(const psk_prec *M, int32_t *uniform, double *value) {
+    if (!M || M->kind != PSK_PREC_JACOBI) return fail(PSK_ERR_ARG, "psk_prec_jacobi_uniform: not a Jacobi preconditioner");
+    if (uniform) *uniform = M->dinv_uniform ? 1 : 0;
+    if (value) *value = M->dinv_uniform ? M->dinv_value : 0.0;
     return PSK_OK;
 }
 

@@ -221,3 +221,35 @@ def test_value_dictionary(psk, nvals):
             dA.set_layout("sliced_dict")
         assert dA.layout == "csr"        # a failed switch leaves no sliced copy
         assert np.array_equal(psk.mvmult(dA, x), ref)
+
+
+def test_uniform_jacobi_diagonal(psk, monkeypatch):
+    """A constant diagonal (FD) makes DInv one scalar the PCG kernels read instead of a stream: the
+    trajectory is bit-identical to the streamed DInv (PSK_JACOBI_UNIFORM=0); a varying diagonal keeps
+    the stream."""
+    import ctypes
+    from pysolvers_amd import _native as N
+    from oracle import fdlap
+    m = 128
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    varied = (A + sp.diags(np.arange(m * m) * 1e-3)).tocsr()        # a non-constant diagonal
+    for mat, expect in ((dA, 1), (psk.DeviceCSR.from_scipy(varied), 0)):
+        M = ctypes.c_void_p()
+        N.check(N.lib.psk_prec_create(mat.handle, N.PSK_PREC_JACOBI, ctypes.byref(M)), "psk_prec_create")
+        u, v = N.I32(), ctypes.c_double()
+        N.check(N.lib.psk_prec_jacobi_uniform(M, ctypes.byref(u), ctypes.byref(v)), "psk_prec_jacobi_uniform")
+        N.lib.psk_prec_destroy(M)
+        assert u.value == expect
+        if expect:
+            assert v.value == 1.0 / A.diagonal()[0]
+    b = A @ np.random.default_rng(3).random(m * m)
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PSK_JACOBI_UNIFORM", flag)
+        st = psk.PCG(control=_ctl(maxiter=2000, tau=1e-10), precond=psk.Jacobi()).makeSolver().solve(dA, b)
+        assert st.success()
+        out.append(st)
+    assert out[0].iters() == out[1].iters()
+    assert np.array_equal(out[0].soln(), out[1].soln())
+    assert np.array_equal(out[0].info["hist"], out[1].info["hist"])
