@@ -192,24 +192,41 @@ __device__ __forceinline__ double dict_pick(const double *dv, uint32_t idx) {
     return (idx & 4) ? b1 : b0;
 }
 
-template <int MODE, int DK>   // DK: dictionary size class (0 = double values, 2 / 4 / 8 entries)
+// a done flag that is never set, for launches without one (the kernel reads the flag without a
+// branch on the pointer, so its load goes out with the slice header)
+__device__ int32_t g_spmv_never_done = 0;
+
+// DK: dictionary size class (0 = double values, 2 / 4 / 8 entries); UNI: uniform layout (every slice
+// uw wide and packed: offsets computed from the slice index, no header loads)
+template <int MODE, int DK, bool UNI>
 __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     int64_t n, const int64_t *__restrict__ soff, const int64_t *__restrict__ swoff, const int8_t *__restrict__ sfmt,
     const int32_t *__restrict__ scol, const int32_t *__restrict__ spcol, const double *__restrict__ sval,
     const double *__restrict__ sdict, int uw,
     const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
     const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
-    if (done != nullptr && *done != 0) return;
+    // every scalar the launch needs goes out in one batch: the done flag (tested only after this
+    // slice's stream loads are in flight — reading is harmless, nothing is stored before the test),
+    // the slice header (non-uniform layouts) and the dictionary
+    const int32_t dn = *(done ? done : &g_spmv_never_done);
     __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
     const int64_t t = blockIdx.x, row = t * kSlice + tid;
     const bool has = row < n;
-    // a uniform layout (uw > 0: every slice uw wide and packed) needs no per-slice header loads, so
-    // the stream loads do not wait for them
-    const int64_t o = uw ? t * uw * kSlice : soff[t];
-    const int w = uw ? uw : (int)((soff[t + 1] - o) / kSlice);
-    const bool packed = uw ? true : sfmt[t] != 0;   // uniform across the workgroup
-    const int64_t wo = uw ? t * ((uw + 1) / 2 + (DK > 0 ? (uw + 3) / 4 : 0)) * kSlice : swoff[t];
+    int64_t o, wo;
+    int w;
+    bool packed;
+    if (UNI) {
+        w = uw;
+        o = t * uw * kSlice;
+        packed = true;
+        wo = t * ((uw + 1) / 2 + (DK > 0 ? (uw + 3) / 4 : 0)) * kSlice;
+    } else {
+        o = soff[t];
+        w = (int)((soff[t + 1] - o) / kSlice);
+        packed = sfmt[t] != 0;   // uniform across the workgroup
+        wo = swoff[t];
+    }
     const int32_t *pword = spcol + wo;                                         // packed column words
     const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
     double dv[DK > 0 ? DK : 1];
@@ -217,6 +234,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     for (int k = 0; k < DK; ++k) dv[k] = sdict[k];   // uniform: scalar loads
     const int32_t row32 = (int32_t)row;
     double eq = 0.0;
+    if (!UNI && dn != 0) return;   // (uniform: tested below, after the stream loads)
     if (has) {
         if (MODE == kSpmvDot) eq = x[row];
         if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
@@ -263,6 +281,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             for (int j = 0; j < kSliceRegs; ++j)
                 if (j < w) cc[j] = ld_stream(scol + o + j * kSlice + tid);
         }
+        if (UNI && dn != 0) return;   // the stream loads are in flight
         if (DK > 0) {
 #pragma unroll
             for (int j = 0; j < kSliceRegs; ++j)
@@ -280,6 +299,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
         for (int j = 0; j < kSliceRegs; ++j)
             if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
     } else {
+        if (UNI && dn != 0) return;
         for (int j = 0; j < w; ++j) {
             int32_t c;
             if (packed) {
@@ -620,10 +640,16 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     dim3 gd((unsigned)nwg), bd(kBlock);
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
-#define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
-    hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff, A->sl_fmt,       \
+        const bool uni = A->sl_uniform_w > 0;
+#define PSK_SLICED_LAUNCH_DKU(M, DK, U)                                                                        \
+    hipLaunchKernelGGL((spmv_sliced_kernel<M, DK, U>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff, A->sl_fmt,    \
                        A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, A->sl_uniform_w, x, y, aux_d, aux_q, gs,   \
                        done_flag)
+#define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
+    do {                                                                                                       \
+        if (uni) PSK_SLICED_LAUNCH_DKU(M, DK, true);                                                           \
+        else PSK_SLICED_LAUNCH_DKU(M, DK, false);                                                              \
+    } while (0)
 #define PSK_SLICED_LAUNCH(M)                                                                                   \
     do {                                                                                                       \
         if (dk == 0) PSK_SLICED_LAUNCH_DK(M, 0);                                                               \
@@ -643,6 +669,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         }
 #undef PSK_SLICED_LAUNCH
 #undef PSK_SLICED_LAUNCH_DK
+#undef PSK_SLICED_LAUNCH_DKU
         PSK_HIP(hipGetLastError());
         return PSK_OK;
     }
