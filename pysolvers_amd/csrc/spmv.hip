@@ -180,14 +180,19 @@ __device__ __forceinline__ bool same_bits(double a, double b) {
     return __double_as_longlong(a) == __double_as_longlong(b);
 }
 
-// dictionary entry idx (< DK) by selects on the index bits; dv lives in scalar registers
+// the dictionary as named scalars (an array here was promoted to per-thread LDS copies)
+struct DictRegs {
+    double d0, d1, d2, d3, d4, d5, d6, d7;
+};
+
+// dictionary entry idx (< DK) by selects on the index bits; the entries live in scalar registers
 template <int DK>
-__device__ __forceinline__ double dict_pick(const double *dv, uint32_t idx) {
-    if (DK == 2) return (idx & 1) ? dv[1] : dv[0];
-    const double a0 = (idx & 1) ? dv[1] : dv[0], a1 = (idx & 1) ? dv[3] : dv[2];
+__device__ __forceinline__ double dict_pick(const DictRegs dv, uint32_t idx) {
+    if (DK == 2) return (idx & 1) ? dv.d1 : dv.d0;
+    const double a0 = (idx & 1) ? dv.d1 : dv.d0, a1 = (idx & 1) ? dv.d3 : dv.d2;
     const double b0 = (idx & 2) ? a1 : a0;
     if (DK == 4) return b0;
-    const double a2 = (idx & 1) ? dv[5] : dv[4], a3 = (idx & 1) ? dv[7] : dv[6];
+    const double a2 = (idx & 1) ? dv.d5 : dv.d4, a3 = (idx & 1) ? dv.d7 : dv.d6;
     const double b1 = (idx & 2) ? a3 : a2;
     return (idx & 4) ? b1 : b0;
 }
@@ -229,9 +234,21 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     }
     const int32_t *pword = spcol + wo;                                         // packed column words
     const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
-    double dv[DK > 0 ? DK : 1];
-#pragma unroll
-    for (int k = 0; k < DK; ++k) dv[k] = sdict[k];   // uniform: scalar loads
+    DictRegs dv{};
+    if (DK >= 2) {   // uniform: scalar loads (the buffer is padded to 8 entries)
+        dv.d0 = sdict[0];
+        dv.d1 = sdict[1];
+    }
+    if (DK >= 4) {
+        dv.d2 = sdict[2];
+        dv.d3 = sdict[3];
+    }
+    if (DK >= 8) {
+        dv.d4 = sdict[4];
+        dv.d5 = sdict[5];
+        dv.d6 = sdict[6];
+        dv.d7 = sdict[7];
+    }
     const int32_t row32 = (int32_t)row;
     double eq = 0.0;
     if (!UNI && dn != 0) return;   // (uniform: tested below, after the stream loads)
