@@ -113,7 +113,8 @@ int psk_dmemset0(void *dst, int64_t bytes);
 
 /* ---- CSR matrices ---------------------------------------------------------------------- */
 /* Copy a CSR matrix (rowptr[n+1], colidx[nnz], vals[nnz]; stored entry order is kept,
- * sorted or not) into HBM. loc says where the three arrays live. */
+ * sorted or not) into HBM. loc says where the three arrays live. int32 indices:
+ * nnz <= 2^31 - 1 - 1536 (PSK_ERR_UNSUPPORTED beyond; FD 16384^2 has 1.34e9). */
 int psk_csr_create(int64_t n, int64_t nnz, const int32_t *rowptr, const int32_t *colidx,
                    const double *vals, int32_t loc, psk_csr **out);
 /* FDLaplacian2D(a, b, m) generated on the device (examples/FDLaplacian2D.py:5-23). */

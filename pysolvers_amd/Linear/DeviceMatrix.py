@@ -63,6 +63,20 @@ def is_device_vector(v):
     return (hasattr(v, "is_cuda") and getattr(v, "is_cuda", False))
 
 
+def torch_stream_ready(*tensors):
+    """Order libpsk after torch for the torch tensors about to be handed to it.
+
+    libpsk runs on its own non-blocking stream (runtime.hip), which nothing orders after torch's
+    current stream: an input may still be written by a queued torch kernel, and an output fresh
+    from the caching allocator may still be read by torch work on its previous use. So wait for
+    torch's current stream on every device involved (allocate the outputs first). Every libpsk
+    entry point synchronises its own stream before returning, so torch may use the results at
+    once."""
+    import torch
+    for dev in {t.device for t in tensors if not isinstance(t, DeviceVector)}:
+        torch.cuda.current_stream(dev).synchronize()
+
+
 class DeviceCSR:
     """CSR matrix (int32 rowptr/colidx, float64 vals) in HBM; stored entry order is preserved."""
 
@@ -180,6 +194,7 @@ def spmv(A, x):
     if is_device_vector(x):
         import torch
         y = torch.empty(dA.n, dtype=torch.float64, device=x.device)
+        torch_stream_ready(x, y)
         N.check(N.lib.psk_spmv(dA.handle, N.ptr(x), N.ptr(y), N.PSK_DEVICE), "psk_spmv")
         return y
     x = np.ascontiguousarray(x, dtype=np.float64)

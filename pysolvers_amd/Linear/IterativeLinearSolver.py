@@ -13,7 +13,7 @@ import scipy.sparse as sp
 
 from .. import _native as N
 from ..IterativeSolver import CommonSolverArgs, IterativeSolver, SolveStatus
-from .DeviceMatrix import DeviceCSR, DeviceVector, as_device_matrix, is_device_vector, spmv
+from .DeviceMatrix import DeviceCSR, DeviceVector, as_device_matrix, is_device_vector, spmv, torch_stream_ready
 from .LinearSolver import LinearSolver, LinearSolverType
 from .PreconditionerType import IdentityPreconditionerType
 
@@ -104,6 +104,7 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
             if b.dtype != torch.float64 or not b.is_contiguous():
                 raise TypeError("device right-hand side must be a contiguous float64 tensor")
             x, loc, bp = torch.empty_like(b), N.PSK_DEVICE, b
+            torch_stream_ready(b, x)
         else:
             bp = np.ascontiguousarray(b, dtype=np.float64)
             x, loc = np.empty_like(bp), N.PSK_HOST

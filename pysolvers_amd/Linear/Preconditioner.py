@@ -10,7 +10,7 @@ from abc import ABC, abstractmethod
 import numpy as np
 
 from .. import _native as N
-from .DeviceMatrix import DeviceVector, as_device_matrix, is_device_vector
+from .DeviceMatrix import DeviceVector, as_device_matrix, is_device_vector, torch_stream_ready
 
 
 class Preconditioner(ABC):
@@ -90,6 +90,7 @@ class DeviceOperator:
         if is_device_vector(vec):
             import torch
             out = torch.empty_like(vec)
+            torch_stream_ready(vec, out)
             N.check(N.lib.psk_prec_apply(self._h, self.n, N.ptr(vec), N.ptr(out), N.PSK_DEVICE), "psk_prec_apply")
             return out
         v = np.ascontiguousarray(vec, dtype=np.float64)

@@ -327,7 +327,7 @@ int psk_csr_create_fd2d_dist(double a, double b, int64_t m, psk_comm *cm, psk_cs
                              int64_t *row_begin, int64_t *row_end) {
     if (!cm || !out || m < 1) return fail(PSK_ERR_ARG, "psk_csr_create_fd2d_dist: bad arguments");
     const int r = cm->rank;
-    if ((m == 1 ? 1 : 5 * m * m - 4 * m) > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "nnz > int32");
+    if ((m == 1 ? 1 : 5 * m * m - 4 * m) > kMaxNnz) return fail(PSK_ERR_UNSUPPORTED, "nnz > int32");
     FdPlan plan;
     PSK_TRY(fd2d_plan(m, cm->nranks, r, plan));
     Context *c;
@@ -406,7 +406,7 @@ int psk_csr_create_dist(int64_t n_global, const int64_t *row_starts, const int64
     for (int64_t i = 0; i < nloc; ++i)
         if (rowptr[i + 1] < rowptr[i]) return fail(PSK_ERR_ARG, "psk_csr_create_dist: rowptr not monotone");
     const int64_t nnz = rowptr[nloc] - rowptr[0];
-    if (nnz > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create_dist: local nnz exceeds int32");
+    if (nnz > kMaxNnz) return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create_dist: local nnz exceeds int32");
     if (nnz > 0 && (!colidx || !vals)) return fail(PSK_ERR_ARG, "psk_csr_create_dist: NULL entries");
     DistPlan pl;
     PSK_TRY(dist_plan(n_global, row_starts, P, r, rowptr, colidx, pl));

@@ -131,7 +131,7 @@ int mm_coo(const MMFile &f, std::vector<int64_t> &ri, std::vector<int64_t> &ci, 
 
 // COO -> canonical CSR (per-row column sort, duplicates summed in stored order after the sort)
 int mm_csr(const MMFile &f, std::vector<int32_t> &rp, std::vector<int32_t> &cols, std::vector<double> &vals) {
-    if (f.nrows >= INT32_MAX || f.ncols >= INT32_MAX || nnz_max(f) >= INT32_MAX)
+    if (f.nrows >= INT32_MAX || f.ncols >= INT32_MAX || nnz_max(f) > kMaxNnz)
         return fail(PSK_ERR_UNSUPPORTED, "MatrixMarket: int32 CSR required");
     std::vector<int64_t> ri, ci;
     std::vector<double> va;

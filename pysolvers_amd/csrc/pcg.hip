@@ -495,13 +495,16 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         (void)hipEventElapsedTime(&ms, ev0, ev1);
         res->loop_ms = ms;
         res->norm_b = hs.normB;
-        int64_t nk = 0;   // iterations whose kernels did real work
+        // nk: iterations whose SpMV ran (the timing count); nhist: iterations that reported a
+        // residual (K3 wrote hist[k]) — a dot(p,Ap) breakdown at k ran the SpMV of k but reports
+        // only 0..k-1, as the reference's loop does (PCGSolver.py:114-115 returns before :126)
+        int64_t nk = 0, nhist = 0;
         if (hs.done == 1) {
             res->status = PSK_CONVERGED;
             res->success = 1;
             res->iters = hs.iters;
             res->resid = hs.resid;
-            nk = hs.normB == 0.0 ? 0 : hs.iters;
+            nk = nhist = hs.normB == 0.0 ? 0 : hs.iters;
         } else if (hs.done == 2) {
             res->status = PSK_BREAKDOWN;
             res->success = 0;
@@ -509,16 +512,17 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             res->resid = NAN;
             set_msg(res, hs.brk_kind == 1 ? "breakdown dot(u,r)==0" : "breakdown dot(p, Ap)==0");
             nk = hs.brk_kind == 1 ? 0 : hs.iters + 1;
+            nhist = hs.brk_kind == 1 ? 0 : hs.iters;
         } else {
             // handleMaxiter(k=maxiter-1, ...) (IterativeSolver.py:115-129); maxiter==0 -> k unset
             res->status = PSK_MAXITER;
             res->success = 0;
             res->iters = maxiter > 0 ? maxiter - 1 : 0;
             set_msg(res, "failure to converge");
-            nk = launched;
+            nk = nhist = launched;
         }
         // residual history, the recursive residual and the solution
-        const int64_t nh = nk < maxiter ? nk : maxiter;
+        const int64_t nh = nhist < maxiter ? nhist : maxiter;
         std::vector<double> hh((size_t)nh);
         if (nh > 0 && hipMemcpy(hh.data(), w.hist, (size_t)nh * 8, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(PSK_ERR_HIP, "hist copy");

@@ -20,6 +20,9 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kChunk = 1280;           // SpMV LDS-staged products per chunk (10 KiB of f64) = 256 FD rows
 constexpr int kMaxGrid = 2048;         // 256 CUs x 8 resident workgroups; partial arrays sized for it
 constexpr int kVecTile = 2 * kBlock;   // elementwise tile: 2 doubles (16 B) per lane
+// largest nnz of a device CSR: the CSR SpMV kernel forms entry indices e0 + k*kBlock + tid and the
+// next chunk start in int32, which must stay below INT32_MAX in every tile
+constexpr int64_t kMaxNnz = (int64_t)INT32_MAX - kChunk - kBlock;
 
 // ---------------------------------------------------------------------------------------------
 // errors
@@ -208,6 +211,31 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
+// One DPP step on a double (both halves moved by the same lane pattern CTRL)
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// Wave total without LDS traffic: DPP inside each 16-lane row (pairs, quads, then row_ror 4 and 8,
+// after which lane 0 of a row holds ((Q0+Q3)+(Q2+Q1)) of its four quad sums), then the four row
+// totals read from lanes 0/16/32/48 and added in that order. Fixed order; the result is uniform
+// (scalar) across the wave. Used where only one lane publishes the sum (the SpMV dot epilogue): a
+// butterfly of ds_bpermute shuffles holds each wave longer at the end of its slice.
+__device__ __forceinline__ double wave_total(double v) {
+    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f64<0x124>(v);   // row_ror:4
+    v += dpp_f64<0x128>(v);   // row_ror:8
+    auto lane = [](double x, int l) {
+        return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                                __builtin_amdgcn_readlane(__double2loint(x), l));
+    };
+    return ((lane(v, 0) + lane(v, 16)) + lane(v, 32)) + lane(v, 48);
+}
+
 // Block-wide sum; all threads get the same value. `sh` must hold kWaves doubles.
 __device__ __forceinline__ double block_sum(double v, double *sh) {
     v = wave_sum(v);
@@ -263,18 +291,21 @@ struct GridSum {
     uint64_t *slots;    // nwg*W workgroup partials (grp > 1)
     uint64_t *gslots;   // ngroups*W group sums
     double *out;        // the W grid sums
-    int64_t grp;        // workgroups per group
+    int64_t grp;        // units (workgroups / waves) per group: a power of two
+    int32_t grp_log2;   // log2(grp): every producer finds its roles with shifts and masks
     int32_t *err;       // set when a bounded wait expires (reported by gridsum_check)
 };
 
-// grp ~ sqrt(nwg): the launch's tail waits for one group reduction (grp/256 loads per lane) and
-// the final one (ngroups/256), so both are kept short; ngroups <= kMaxGrid
-inline int64_t gridsum_grp(int64_t nwg) {
-    if (nwg <= kBlock) return 1;
-    int64_t g = 1;
-    while (g * g < nwg) ++g;
-    const int64_t gmin = (nwg + kMaxGrid - 1) / kMaxGrid;
-    return g > gmin ? g : gmin;
+// grp ~ sqrt(nwg), a power of two: the launch's tail waits for one group reduction (grp/256 loads
+// per lane) and the final one (ngroups/256), so both are kept short; ngroups <= kMaxGrid. A power
+// of two because every producer tests its roles: 64-bit (or even 32-bit) division and modulo are
+// long SALU sequences at the end of every wave (the SpMV's dot epilogue).
+inline int32_t gridsum_grp_log2(int64_t nwg) {
+    if (nwg <= kBlock) return 0;
+    int32_t l = 0;
+    while (((int64_t)1 << (2 * l)) < nwg) ++l;   // (2^l)^2 >= nwg
+    while (((int64_t)kMaxGrid << l) < nwg) ++l;  // ngroups <= kMaxGrid
+    return l;
 }
 
 __device__ __forceinline__ void gridsum_put(uint64_t *sl, double v) {
@@ -330,7 +361,8 @@ __device__ __forceinline__ void gridsum_take_range(uint64_t *src, int64_t j0, in
 template <int W>
 __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double *v, double *sh) {
     const int64_t b = blockIdx.x, nwg = gridDim.x, grp = gs.grp;
-    const int64_t ngroups = (nwg + grp - 1) / grp;
+    const int sh2 = gs.grp_log2;
+    const int64_t ngroups = (nwg + grp - 1) >> sh2;
     double r[W];
     if (grp == 1) {
         if (threadIdx.x == 0)
@@ -341,14 +373,14 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
 #pragma unroll
             for (int c = 0; c < W; ++c) gridsum_put(gs.slots + b * W + c, v[c]);
         const int64_t t = b - (grp - 1) - kGridSumLag;   // lagged role: group t/grp
-        if (t >= 0 && t % grp == 0) {
-            const int64_t g = t / grp;
+        if (t >= 0 && (t & (grp - 1)) == 0) {
+            const int64_t g = t >> sh2;
             gridsum_take_range<W>(gs.slots, g * grp, g * grp + grp, gs.err, sh, r);
             if (threadIdx.x == 0)
 #pragma unroll
                 for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
         }
-        const int64_t g = b / grp, lastm = (g * grp + grp - 1 < nwg) ? g * grp + grp - 1 : nwg - 1;
+        const int64_t g = b >> sh2, lastm = (g * grp + grp - 1 < nwg) ? g * grp + grp - 1 : nwg - 1;
         if (b == lastm && g * grp + grp - 1 + kGridSumLag >= nwg) {   // own-group role
             gridsum_take_range<W>(gs.slots, g * grp, lastm + 1, gs.err, sh, r);
             if (threadIdx.x == 0)
@@ -364,8 +396,84 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
     }
 }
 
-// host: a GridSum for a one-shot launch of nwg workgroups with W (<= kGridSumMaxW) sums, written
-// to out[0..W)
+// Wave-level gridsum: every WAVE of the launch is a unit (u = blockIdx * kWaves + wave) and
+// publishes its own wave sum, so a producer needs no workgroup barrier at all (the SpMV's dot
+// epilogue: one butterfly, one store by lane 0, and the wave is gone). The roles are those of
+// gridsum_publish over units instead of workgroups (a reducer is one wave: lane-strided by 64, then
+// the butterfly); a unit still only waits for lower units — earlier workgroups, or lower waves of its
+// own workgroup, which are resident beside it and never wait for it. The host prepares it with
+// nwg * kWaves units (gridsum_prepare). Every kernel that must give bit-identical sums to another
+// (the SpMV layouts) uses the same variant over the same rows per wave.
+template <int W>
+__device__ __forceinline__ void gridsum_take_range_wave(uint64_t *src, int64_t j0, int64_t j1, int32_t *err,
+                                                        double *res) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+        double a = 0.0;
+        bool ok = true;
+#pragma unroll 4
+        for (int64_t j = j0 + lane; j < j1; j += 64) {
+            const uint64_t v = __hip_atomic_load(src + j * W + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = ok && v != kGridSumSentinel;
+            a += __longlong_as_double((long long)v);
+        }
+        if (!ok) {
+            a = 0.0;
+            for (int64_t j = j0 + lane; j < j1; j += 64)
+                a += __longlong_as_double((long long)gridsum_wait(src + j * W + c, err));
+        }
+        for (int64_t j = j0 + lane; j < j1; j += 64) src[j * W + c] = kGridSumSentinel;
+        res[c] = wave_total(a);
+    }
+}
+
+// Called by every lane of every wave with the wave's W sums (identical in all lanes, e.g. from
+// wave_sum). No barrier; control flow is uniform per wave.
+template <int W>
+__device__ __forceinline__ void gridsum_publish_wave(const GridSum &gs, const double *v) {
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    const int64_t u = (int64_t)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t nu = (int64_t)gridDim.x * kWaves, grp = gs.grp;
+    const int sh2 = gs.grp_log2;
+    const int64_t ngroups = (nu + grp - 1) >> sh2;
+    constexpr int64_t lag = kGridSumLag * kWaves;
+    double r[W];
+    if (grp == 1) {
+        if (lane0)
+#pragma unroll
+            for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + u * W + c, v[c]);
+    } else {
+        if (lane0)
+#pragma unroll
+            for (int c = 0; c < W; ++c) gridsum_put(gs.slots + u * W + c, v[c]);
+        const int64_t t = u - (grp - 1) - lag;   // lagged role: group t/grp
+        if (t >= 0 && (t & (grp - 1)) == 0) {
+            const int64_t g = t >> sh2;
+            gridsum_take_range_wave<W>(gs.slots, g * grp, g * grp + grp, gs.err, r);
+            if (lane0)
+#pragma unroll
+                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
+        }
+        const int64_t g = u >> sh2;
+        const int64_t lastm = (g * grp + grp - 1 < nu) ? g * grp + grp - 1 : nu - 1;
+        if (u == lastm && g * grp + grp - 1 + lag >= nu) {   // own-group role
+            gridsum_take_range_wave<W>(gs.slots, g * grp, lastm + 1, gs.err, r);
+            if (lane0)
+#pragma unroll
+                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
+        }
+    }
+    if (u == nu - 1) {   // final role
+        gridsum_take_range_wave<W>(gs.gslots, 0, ngroups, gs.err, r);
+        if (lane0)
+#pragma unroll
+            for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+    }
+}
+
+// host: a GridSum for a one-shot launch of nwg workgroups (or, for gridsum_publish_wave, nwg *
+// kWaves waves) with W (<= kGridSumMaxW) sums, written to out[0..W)
 int gridsum_prepare(Context *c, int64_t nwg, int W, double *out, GridSum *gs);
 // reports (and clears) an expired gridsum wait; syncs the stream
 int gridsum_check(Context *c);

@@ -88,7 +88,8 @@ int gridsum_prepare(Context *c, int64_t nwg, int W, double *out, GridSum *gs) {
         PSK_TRY(gridsum_arm(&c->gs_gslots, (int64_t)kMaxGrid * kGridSumMaxW, c->stream));
     }
     gs->out = out;
-    gs->grp = gridsum_grp(nwg);
+    gs->grp_log2 = gridsum_grp_log2(nwg);
+    gs->grp = (int64_t)1 << gs->grp_log2;
     gs->err = c->gs_err;
     gs->gslots = c->gs_gslots;
     gs->slots = nullptr;

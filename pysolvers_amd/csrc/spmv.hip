@@ -28,6 +28,24 @@ namespace psk {
 __device__ __forceinline__ int32_t ld_stream(const int32_t *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ double ld_stream(const double *p) { return __builtin_nontemporal_load(p); }
 
+// The dot epilogue of every SpMV kernel (p.Ap, q_0.u, ||b-Ax||^2): one partial per WAVE, published
+// by gridsum_publish_wave — no workgroup barrier at the end of a slice. Both layouts sum 64 rows per
+// wave in the same lanes (256-row tiles / slices), so their grid sums are bit-identical.
+// (PSK_SPMV_BLOCK_PARTIALS: the previous per-workgroup epilogue, kept for same-box A/B runs.)
+#ifdef PSK_SPMV_BLOCK_PARTIALS
+constexpr int kSpmvUnitsPerWg = 1;
+__device__ __forceinline__ void spmv_publish(const GridSum &gs, double acc, double *sh) {
+    const double bs = block_sum(acc, sh);
+    gridsum_publish<1>(gs, &bs, sh);
+}
+#else
+constexpr int kSpmvUnitsPerWg = kWaves;
+__device__ __forceinline__ void spmv_publish(const GridSum &gs, double acc, double *) {
+    const double ws = wave_total(acc);
+    gridsum_publish_wave<1>(gs, &ws);
+}
+#endif
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(
     int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
@@ -127,10 +145,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
         }
     }
     // only the residual mode may be called without partials (AMG smoothing); kernel-uniform test
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) {
-        const double bs = block_sum(acc, sh);
-        gridsum_publish<1>(gs, &bs, sh);
-    }
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) spmv_publish(gs, acc, sh);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -201,41 +216,11 @@ __device__ __forceinline__ double dict_pick(const DictRegs dv, uint32_t idx) {
 // branch on the pointer, so its load goes out with the slice header)
 __device__ int32_t g_spmv_never_done = 0;
 
-// DK: dictionary size class (0 = double values, 2 / 4 / 8 entries); UNI: uniform layout (every slice
-// uw wide and packed: offsets computed from the slice index, no header loads)
-template <int MODE, int DK, bool UNI>
-__global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
-    int64_t n, const int64_t *__restrict__ soff, const int64_t *__restrict__ swoff, const int8_t *__restrict__ sfmt,
-    const int32_t *__restrict__ scol, const int32_t *__restrict__ spcol, const double *__restrict__ sval,
-    const double *__restrict__ sdict, int uw,
-    const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
-    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
-    // every scalar the launch needs goes out in one batch: the done flag (tested only after this
-    // slice's stream loads are in flight — reading is harmless, nothing is stored before the test),
-    // the slice header (non-uniform layouts) and the dictionary
-    const int32_t dn = *(done ? done : &g_spmv_never_done);
-    __shared__ double sh[kWaves];
-    const int tid = threadIdx.x;
-    const int64_t t = blockIdx.x, row = t * kSlice + tid;
-    const bool has = row < n;
-    int64_t o, wo;
-    int w;
-    bool packed;
-    if (UNI) {
-        w = uw;
-        o = t * uw * kSlice;
-        packed = true;
-        wo = t * ((uw + 1) / 2 + (DK > 0 ? (uw + 3) / 4 : 0)) * kSlice;
-    } else {
-        o = soff[t];
-        w = (int)((soff[t + 1] - o) / kSlice);
-        packed = sfmt[t] != 0;   // uniform across the workgroup
-        wo = swoff[t];
-    }
-    const int32_t *pword = spcol + wo;                                         // packed column words
-    const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
+// The dictionary entries DK needs, as scalar loads (the buffer is padded to kDictMax entries).
+template <int DK>
+__device__ __forceinline__ DictRegs load_dict(const double *__restrict__ sdict) {
     DictRegs dv{};
-    if (DK >= 2) {   // uniform: scalar loads (the buffer is padded to 8 entries)
+    if (DK >= 2) {
         dv.d0 = sdict[0];
         dv.d1 = sdict[1];
     }
@@ -249,11 +234,151 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
         dv.d6 = sdict[6];
         dv.d7 = sdict[7];
     }
+    return dv;
+}
+
+// y[row] (and the dot partial of the mode) from the row's sum
+template <int MODE>
+__device__ __forceinline__ double spmv_finish_row(bool has, int64_t row, double sum, double eq, double *__restrict__ y) {
+    double acc = 0.0;
+    if (has) {
+        if (MODE == kSpmvResid) {
+            const double r = eq - sum;   // b - A*x (GMRESSolver.py:163)
+            y[row] = r;
+            acc = r * r;
+        } else if (MODE == kSpmvAdd) {
+            y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
+        } else {
+            __builtin_nontemporal_store(sum, y + row);
+            if (MODE != kSpmvPlain) acc = eq * sum;   // x.(Ax) or q.(Ax)
+        }
+    }
+    return acc;
+}
+
+// x[row] for the PCG dot p.Ap (kSpmvDot): the gathered value of the row's diagonal slot when it
+// stores one (every 5-point row does: x[c] with c == row is the same double), else a load (rare:
+// the branch is taken by the lanes whose row has no stored diagonal). Loading x[row] up front with
+// the stream cost 7% of the in-loop SpMV at FD 16384^2 (one more load in the first round trip).
+template <int NS>
+__device__ __forceinline__ double diag_x(const int32_t *cc, const double *xv, int32_t row, const double *__restrict__ x,
+                                         bool has) {
+    double d = 0.0;
+    bool found = false;
+#pragma unroll
+    for (int j = 0; j < NS; ++j)
+        if (cc[j] == row) {
+            d = xv[j];
+            found = true;
+        }
+    if (!found && has) d = x[row];
+    return d;
+}
+
+// Uniform layout (every slice UW wide and packed — FD and other constant-width banded matrices):
+// the width is a template parameter, so the slice's whole stream is issued as one batch of
+// unconditional loads (a runtime width put a branch between consecutive loads and the compiler
+// then waited on each one: four memory round trips per slice instead of two), the offsets are
+// computed from the slice index, and every slot's gather is issued unconditionally (padding slots
+// gather x[0], and their product is skipped). DK: dictionary size class (0 = double values in slot
+// pairs, 2 / 4 / 8 entries).
+template <int MODE, int DK, int UW>
+__global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
+    int64_t n, const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ sdict,
+    const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
+    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
+    constexpr int NP = (UW + 1) / 2;                 // packed column words per lane
+    constexpr int NI = DK > 0 ? (UW + 3) / 4 : 0;    // dictionary index words per lane
+    __shared__ double sh[kWaves];
+    const int32_t dn = *(done ? done : &g_spmv_never_done);   // tested once the stream is in flight
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x, row = t * kSlice + tid;
+    const bool has = row < n;
+    const int32_t *pword = spcol + t * (int64_t)((NP + NI) * kSlice) + tid;
+    uint32_t cw[NP], iw[NI > 0 ? NI : 1];
+    double vv[UW];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) cw[p] = (uint32_t)ld_stream(pword + p * kSlice);
+    if (DK > 0) {
+#pragma unroll
+        for (int q = 0; q < NI; ++q) iw[q] = (uint32_t)ld_stream(pword + (NP + q) * kSlice);
+    } else {
+        const double *v0 = sval + t * (int64_t)(UW * kSlice);
+#pragma unroll
+        for (int p = 0; p < UW / 2; ++p) {
+            const dv2 v2 = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(v0 + 2 * p * kSlice) + tid);
+            vv[2 * p] = v2.x;
+            vv[2 * p + 1] = v2.y;
+        }
+        if (UW & 1) vv[UW - 1] = ld_stream(v0 + (UW - 1) * kSlice + tid);
+    }
+    const int64_t rowc = has ? row : 0;
+    double eq = 0.0;
+    // kSpmvDot's x[row] is not loaded here: a row that stores its diagonal gathers it below
+    if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot) eq = aux_q[rowc];
+    const DictRegs dv = load_dict<DK>(sdict);
+    if (dn != 0) {   // uniform over the launch: no barrier has been passed
+        // the stream loads are consumed on this path too, so the compiler issues them ahead of the
+        // test instead of sinking them below it (every slice would wait on the flag first)
+#pragma unroll
+        for (int p = 0; p < NP; ++p) __asm__ volatile("" ::"v"(cw[p]));
+        if (DK > 0) {
+#pragma unroll
+            for (int q = 0; q < NI; ++q) __asm__ volatile("" ::"v"(iw[q]));
+        } else {
+#pragma unroll
+            for (int j = 0; j < UW; ++j) __asm__ volatile("" ::"v"(vv[j]));
+        }
+        return;
+    }
+    const int32_t row32 = (int32_t)row;
+    int32_t cc[UW];
+    double xv[UW];
+#pragma unroll
+    for (int j = 0; j < UW; ++j) {
+        cc[j] = unpack_delta(row32, (int16_t)((j & 1) ? (cw[j >> 1] >> 16) : (cw[j >> 1] & 0xffff)));
+        const int32_t cl = cc[j] >= 0 ? cc[j] : 0;
+        xv[j] = x[cl];
+        if (MODE == kSpmvJacobiDot) xv[j] = aux_d[cl] * xv[j];   // (DInv*q)[c], rounded
+    }
+    if (DK > 0) {
+#pragma unroll
+        for (int j = 0; j < UW; ++j) vv[j] = dict_pick<DK>(dv, (iw[j >> 2] >> (8 * (j & 3))) & 0xff);
+    }
+    double sum = 0.0;
+#pragma unroll
+    for (int j = 0; j < UW; ++j)
+        if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
+    if (MODE == kSpmvDot) eq = diag_x<UW>(cc, xv, row32, x, has);
+    const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) spmv_publish(gs, acc, sh);
+}
+
+// General sliced layout (per-slice widths, offsets and formats loaded from the slice header).
+// DK: dictionary size class (0 = double values, 2 / 4 / 8 entries).
+template <int MODE, int DK>
+__global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
+    int64_t n, const int64_t *__restrict__ soff, const int64_t *__restrict__ swoff, const int8_t *__restrict__ sfmt,
+    const int32_t *__restrict__ scol, const int32_t *__restrict__ spcol, const double *__restrict__ sval,
+    const double *__restrict__ sdict,
+    const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
+    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
+    if (done != nullptr && *done != 0) return;
+    __shared__ double sh[kWaves];
+    const int tid = threadIdx.x;
+    const int64_t t = blockIdx.x, row = t * kSlice + tid;
+    const bool has = row < n;
+    const int64_t o = soff[t];
+    const int w = (int)((soff[t + 1] - o) / kSlice);
+    const bool packed = sfmt[t] != 0;   // uniform across the workgroup
+    const int64_t wo = swoff[t];
+    const int32_t *pword = spcol + wo;                                         // packed column words
+    const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
+    const DictRegs dv = load_dict<DK>(sdict);
     const int32_t row32 = (int32_t)row;
     double eq = 0.0;
-    if (!UNI && dn != 0) return;   // (uniform: tested below, after the stream loads)
     if (has) {
-        if (MODE == kSpmvDot) eq = x[row];
+        if (MODE == kSpmvDot && w > kSliceRegs) eq = x[row];   // register path: diag_x below
         if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
             eq = aux_q[row];
     }
@@ -298,7 +423,6 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             for (int j = 0; j < kSliceRegs; ++j)
                 if (j < w) cc[j] = ld_stream(scol + o + j * kSlice + tid);
         }
-        if (UNI && dn != 0) return;   // the stream loads are in flight
         if (DK > 0) {
 #pragma unroll
             for (int j = 0; j < kSliceRegs; ++j)
@@ -315,8 +439,8 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
 #pragma unroll
         for (int j = 0; j < kSliceRegs; ++j)
             if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
+        if (MODE == kSpmvDot) eq = diag_x<kSliceRegs>(cc, xv, row32, x, has);
     } else {
-        if (UNI && dn != 0) return;
         for (int j = 0; j < w; ++j) {
             int32_t c;
             if (packed) {
@@ -335,23 +459,8 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             sum = sum + v * xx;
         }
     }
-    double acc = 0.0;
-    if (has) {
-        if (MODE == kSpmvResid) {
-            const double r = eq - sum;
-            y[row] = r;
-            acc = r * r;
-        } else if (MODE == kSpmvAdd) {
-            y[row] = eq + sum;
-        } else {
-            __builtin_nontemporal_store(sum, y + row);
-            if (MODE != kSpmvPlain) acc = eq * sum;
-        }
-    }
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) {
-        const double bs = block_sum(acc, sh);
-        gridsum_publish<1>(gs, &bs, sh);
-    }
+    const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) spmv_publish(gs, acc, sh);
 }
 
 // per slice: widest row, and the largest |column - row| of its entries (saturated to int32)
@@ -562,7 +671,7 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
     }
     const char *ue = std::getenv("PSK_SPMV_UNIFORM");
     const bool uniform =
-        all_pack && wmax > 0 && wmax <= 64 && wmax * nt * 100 <= wsum * 101 && !(ue && std::atoi(ue) == 0);
+        all_pack && wmax > 0 && wmax <= kSliceRegs && wmax * nt * 100 <= wsum * 101 && !(ue && std::atoi(ue) == 0);
     if (uniform)
         for (int64_t t = 0; t < nt; ++t) wd[(size_t)t] = (int32_t)wmax;
     std::vector<int64_t> off((size_t)nt + 1), woff((size_t)nt + 1);
@@ -652,20 +761,32 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     PSK_TRY(ctx(&c));
     const bool sliced = A->sl_off != nullptr;
     const int64_t nwg = sliced ? (A->n + kSlice - 1) / kSlice : spmv_tiles(A);
-    GridSum gs{nullptr, nullptr, nullptr, 1, nullptr};
-    if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
+    GridSum gs{nullptr, nullptr, nullptr, 1, 0, nullptr};
+    if (partial) PSK_TRY(gridsum_prepare(c, nwg * kSpmvUnitsPerWg, 1, partial, &gs));
     dim3 gd((unsigned)nwg), bd(kBlock);
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
-        const bool uni = A->sl_uniform_w > 0;
-#define PSK_SLICED_LAUNCH_DKU(M, DK, U)                                                                        \
-    hipLaunchKernelGGL((spmv_sliced_kernel<M, DK, U>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff, A->sl_fmt,    \
-                       A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, A->sl_uniform_w, x, y, aux_d, aux_q, gs,   \
-                       done_flag)
+        const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
+#define PSK_UNI_LAUNCH(M, DK, UW)                                                                              \
+    hipLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, A->n, A->sl_pcol, A->sl_val, A->sl_dict, \
+                       x, y, aux_d, aux_q, gs, done_flag)
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
     do {                                                                                                       \
-        if (uni) PSK_SLICED_LAUNCH_DKU(M, DK, true);                                                           \
-        else PSK_SLICED_LAUNCH_DKU(M, DK, false);                                                              \
+        switch (uw) {                                                                                          \
+        case 0:                                                                                                \
+            hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff,         \
+                               A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, \
+                               done_flag);                                                                     \
+            break;                                                                                             \
+        case 1: PSK_UNI_LAUNCH(M, DK, 1); break;                                                               \
+        case 2: PSK_UNI_LAUNCH(M, DK, 2); break;                                                               \
+        case 3: PSK_UNI_LAUNCH(M, DK, 3); break;                                                               \
+        case 4: PSK_UNI_LAUNCH(M, DK, 4); break;                                                               \
+        case 5: PSK_UNI_LAUNCH(M, DK, 5); break;                                                               \
+        case 6: PSK_UNI_LAUNCH(M, DK, 6); break;                                                               \
+        case 7: PSK_UNI_LAUNCH(M, DK, 7); break;                                                               \
+        default: PSK_UNI_LAUNCH(M, DK, 8); break;                                                              \
+        }                                                                                                      \
     } while (0)
 #define PSK_SLICED_LAUNCH(M)                                                                                   \
     do {                                                                                                       \
@@ -686,7 +807,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         }
 #undef PSK_SLICED_LAUNCH
 #undef PSK_SLICED_LAUNCH_DK
-#undef PSK_SLICED_LAUNCH_DKU
+#undef PSK_UNI_LAUNCH
         PSK_HIP(hipGetLastError());
         return PSK_OK;
     }
@@ -877,8 +998,8 @@ int psk_csr_create_rect(int64_t n, int64_t ncols, int64_t nnz, const int32_t *ro
                         const double *vals, int32_t loc, psk_csr **out) {
     if (!out || n < 0 || ncols < 0 || nnz < 0 || !rowptr || (nnz > 0 && (!colidx || !vals)))
         return fail(PSK_ERR_ARG, "psk_csr_create: bad arguments");
-    if (nnz > INT32_MAX || n >= INT32_MAX || ncols >= INT32_MAX)
-        return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create: int32 CSR indices required (nnz < 2^31)");
+    if (nnz > kMaxNnz || n >= INT32_MAX || ncols >= INT32_MAX)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_csr_create: int32 CSR indices required (nnz < 2^31 - 1536)");
     if (loc == PSK_HOST) {
         // a malformed CSR would make the gather fault on the device: validate it here, O(nnz)
         if (rowptr[0] != 0 || rowptr[n] != nnz)
@@ -931,7 +1052,7 @@ int psk_csr_create_fd2d(double a, double b, int64_t m, psk_csr **out) {
     if (!out || m < 1) return fail(PSK_ERR_ARG, "psk_csr_create_fd2d: m must be >= 1");
     const int64_t n = m * m;
     const int64_t nnz = (m == 1) ? 1 : 5 * n - 4 * m;
-    if (nnz > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "FD2D: nnz exceeds int32 CSR");
+    if (nnz > kMaxNnz) return fail(PSK_ERR_UNSUPPORTED, "FD2D: nnz exceeds int32 CSR");
     Context *c;
     PSK_TRY(ctx(&c));
     psk_csr *A = new psk_csr();

@@ -180,6 +180,54 @@ def test_pcg_breakdown_zero_matrix(psk):
     A = sp.csr_matrix((5, 5))
     st = psk.PCG(control=_ctl(maxiter=10)).makeSolver().solve(A, np.ones(5))
     assert not st.success() and st.iters() == 0 and st.soln() is None and "p, Ap" in st.msg()
+    # the reference reports no residual before breaking down at k = 0 (PCGSolver.py:114-115 returns
+    # before :126): empty history, recursive residual = ||b||
+    assert len(st.info["hist"]) == 0
+    assert st.info["resid_recursive"] == np.sqrt(5.0)
+
+
+def test_pcg_breakdown_later_history(psk):
+    """dot(p, Ap) == 0 at k > 0: the history holds exactly the k residuals reported before it."""
+    # A = diag(2, 0, 0), b = (1, 1, 0): step 0 runs (p.Ap = 2) and reports ||r|| = sqrt(2); the next
+    # direction lies in the null space, so dot(p, Ap) == 0 at k = 1
+    A = sp.csr_matrix(np.array([[2.0, 0.0, 0.0], [0.0, 0.0, 0.0], [0.0, 0.0, 0.0]]))
+    b = np.array([1.0, 1.0, 0.0])
+    from oracle import krylov
+    ref = krylov.pcg(A, b, maxiter=10, tau=1e-8)
+    st = psk.PCG(control=_ctl(maxiter=10)).makeSolver().solve(A, b)
+    assert st.iters() == ref["iters"] and bool(st.success()) == bool(ref["success"])
+    assert len(st.info["hist"]) == len(ref["hist"])
+    np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=1e-14)
+
+
+def test_torch_tensors_ordered_after_torch_stream(psk):
+    """b, x and SpMV/preconditioner operands as torch tensors written by still-queued torch kernels:
+    libpsk waits for torch's stream first (same answers as the numpy path)."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("torch without a GPU")
+    d = load_golden("pcg_fd64_jacobi.npz")
+    A = golden_matrix(d)
+    dA = psk.DeviceCSR.from_scipy(A)
+    s = psk.PCG(control=_ctl(maxiter=4000), precond=psk.Jacobi()).makeSolver()
+    st_h = s.solve(dA, d["b"])
+
+    def queued(v):
+        # a long chain of torch kernels ahead of the copy that produces the operand
+        busy = torch.ones(1 << 24, dtype=torch.float64, device="cuda")
+        for _ in range(30):
+            busy = busy * 1.0000001
+        out = torch.zeros(len(v), dtype=torch.float64, device="cuda")
+        out.add_(torch.from_numpy(v).to("cuda", non_blocking=True))
+        return out
+
+    st_d = s.solve(dA, queued(d["b"]))
+    assert st_d.iters() == st_h.iters()
+    assert np.array_equal(st_d.soln().cpu().numpy(), st_h.soln())
+    x = np.random.default_rng(5).random(A.shape[0])
+    assert np.array_equal(psk.mvmult(dA, queued(x)).cpu().numpy(), A @ x)
+    M = psk.Jacobi().form(dA)
+    assert np.array_equal(M.applyRight(queued(x)).cpu().numpy(), M.applyRight(x))
 
 
 def test_pcg_maxiter_zero(psk):

@@ -29,14 +29,17 @@
         }                                                                               \
     } while (0)
 
-// K3-shaped stream: reads a, b, writes a (32 B/element traffic with 2 loads + 1 store of 16 B)
+// K3-shaped stream: reads a, b, writes a (32 B/element traffic with 2 loads + 1 store of 16 B);
+// NT = the store non-temporal
+template <bool NT>
 __global__ __launch_bounds__(256) void k3like(int64_t n, double *__restrict__ a, const double *__restrict__ b) {
     const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
     if (i + 1 < n) {
         psk::dv2 va = psk::ld2(a + i), vb = psk::ld2nt(b + i);
         va.x = va.x * 0.5 + vb.x * 0.25;
         va.y = va.y * 0.5 + vb.y * 0.25;
-        psk::st2(a + i, va);
+        if (NT) psk::st2nt(a + i, va);
+        else psk::st2(a + i, va);
     }
 }
 
@@ -84,6 +87,7 @@ int main(int argc, char **argv) {
             const char *name;
             int mode;
             bool dot, flag, per_launch, interleave;
+            int k3 = 0;   // interleaved kernel: 0 k3like on x, 1 k3like-nt on x, 2 k3like on z (not gathered)
         };
         const Case cases[] = {
             {"plain batch", psk::kSpmvPlain, false, false, false, false},
@@ -93,6 +97,9 @@ int main(int argc, char **argv) {
             {"dot+flag per-launch ev", psk::kSpmvDot, true, true, true, false},
             {"plain after k3like", psk::kSpmvPlain, false, false, true, true},
             {"dot+flag after k3like", psk::kSpmvDot, true, true, true, true},
+            {"dot+flag after k3like-nt", psk::kSpmvDot, true, true, true, true, 1},
+            {"dot+flag after k3like(z)", psk::kSpmvDot, true, true, true, true, 2},
+            {"plain after k3like-nt", psk::kSpmvPlain, false, false, true, true, 1},
         };
         for (int round = 0; round < 3; ++round)
             for (const Case &cs : cases) {
@@ -112,8 +119,10 @@ int main(int argc, char **argv) {
                     ms = f / reps;
                 } else {
                     for (int r = 0; r < reps; ++r) {
-                        if (cs.interleave)
-                            hipLaunchKernelGGL(k3like, dim3((unsigned)((n / 2 + 255) / 256)), dim3(256), 0, s, n, x, z);
+                        const dim3 g3((unsigned)((n / 2 + 255) / 256));
+                        if (cs.interleave && cs.k3 == 0) hipLaunchKernelGGL(k3like<false>, g3, dim3(256), 0, s, n, x, z);
+                        if (cs.interleave && cs.k3 == 1) hipLaunchKernelGGL(k3like<true>, g3, dim3(256), 0, s, n, x, z);
+                        if (cs.interleave && cs.k3 == 2) hipLaunchKernelGGL(k3like<false>, g3, dim3(256), 0, s, n, z, y);
                         CK(hipEventRecord(ta[r], s));
                         launch();
                         CK(hipEventRecord(tb[r], s));
