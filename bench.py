@@ -14,8 +14,12 @@ split on whole grid lines across ranks (one process per GPU), halo lines are exc
 ncclSend/Recv and the dot partials all-reduced with RCCL over xGMI, all inside libpsk.
 
 Timed region: barrier + device sync, ONE psk_pcg call of K iterations, device sync + barrier;
-max over ranks. `roofline` prices the SpMV kernel (the dominant kernel) from HIP events
-recorded by libpsk on its own stream around every SpMV launch of the timed solve.
+max over ranks; --repeats such regions, value = the median one. `roofline` prices the SpMV kernel
+(the metric's kernel) from HIP events recorded by libpsk on its own stream around every SpMV launch
+of the median region; `traffic` comes from a rocprofv3 PMC profile of the SAME libpsk.so build
+(sha256-checked) or is null. On rank 0 at N = 1 the extra keys time the general-matrix path,
+N = 10M (`roofline_N10M`), configs[1] (4096^2), configs[2] (GMRES(30)+ILUT, 2896^2), configs[4]
+(PCG+AMG, 8192^2) and the CPU oracle (`cpu_baseline`), after the 16384^2 operands are freed.
 """
 import argparse
 import ctypes
@@ -70,39 +74,25 @@ def layout_bytes(N, A, n):
     return stream.value + 16 * n, LAYOUT_NAMES[lay.value]
 
 
-def cpu_baseline(m, iters):
-    """The oracle (op-for-op restatement of PCGSolver.solve, bit-identical to the reference) on the
-    host, 1 BLAS thread: a bounded sample of `iters` iterations of the same workload."""
-    from threadpoolctl import threadpool_limits
-    from oracle import fdlap, krylov
-    t0 = time.time()
-    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
-    x = np.random.default_rng(12345).random(m * m)
-    b = A @ x
-    del x
-    setup = time.time() - t0
-    with threadpool_limits(limits=1):
-        t = time.perf_counter()
-        st = krylov.pcg(A, b, maxiter=iters, tau=0.0, fail_on_maxiter=False, precond=krylov.jacobi_form(A))
-        dt = time.perf_counter() - t
-    assert st["iters"] == iters
-    return dict(value=iters / dt, unit="CG iterations/s", cores=1, kind="port",
-                sample="%d PCG+Jacobi iterations of the oracle (numpy/scipy restatement of PCGSolver.py:64-142, "
-                       "bit-identical to the reference) on the same FDLaplacian2D m=%d system, 1 BLAS thread; "
-                       "%.1f s timed, %.0f s setup" % (iters, m, dt, setup))
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--side", type=int, default=16384, help="grid side m of FDLaplacian2D (n = m^2 rows)")
-    ap.add_argument("--cpu-iters", type=int, default=2, help="oracle iterations for cpu_baseline (0 = skip)")
+    ap.add_argument("--repeats", type=int, default=5,
+                    help="timed regions of --steps iterations each; value = the median (SURVEY.md §8d)")
+    ap.add_argument("--cpu-iters", type=int, default=5, help="timed oracle iterations for cpu_baseline (0 = skip)")
+    ap.add_argument("--general", type=int, default=1,
+                    help="also time the general-matrix path (double values, streamed DInv) on rank 0")
+    ap.add_argument("--config2", type=int, default=1, help="also time configs[2] (GMRES(30)+ILUT, FD 2896^2) on rank 0")
+    ap.add_argument("--config4", type=int, default=1, help="also time configs[4] (PCG+AMG, -FD 8192^2) on rank 0")
     ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r1h_pmc_traffic_16384.json"),
-                    help="PMC traffic summary (tools/pmc_summary.py) of the same kernel and side")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r2_pmc_traffic_16384.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py) of the same build, kernel and side")
+    ap.add_argument("--traffic-json-10m", default=os.path.join(REPO, "profiles", "r2_pmc_traffic_3163.json"),
+                    help="PMC traffic summary of the same build at m = 3163 (N = 10M)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,21 +188,27 @@ def main():
     if args.warmup > 0:
         r = run(args.warmup, False)
         assert r.iters == args.warmup, r.iters
-    barrier()
-    N.check(N.lib.psk_synchronize(), "sync")
-    t0 = time.perf_counter()
-    res = run(args.steps, True)
-    N.check(N.lib.psk_synchronize(), "sync")
-    barrier()
-    dt = time.perf_counter() - t0
-    assert res.iters == args.steps and res.success == 1, (res.iters, res.success)
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt, res.spmv_ms], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt, spmv_ms_max = float(t[0]), float(t[1])
-    else:
-        spmv_ms_max = res.spmv_ms
+    # R timed regions of exactly K iterations, each bracketed by barrier + device sync; per region
+    # the max over ranks; value = the median region (warm median of >= 5 runs)
+    regions = []
+    for _ in range(max(1, args.repeats)):
+        barrier()
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        res = run(args.steps, True)
+        N.check(N.lib.psk_synchronize(), "sync")
+        barrier()
+        dt = time.perf_counter() - t0
+        assert res.iters == args.steps and res.success == 1, (res.iters, res.success)
+        spmv_ms = res.spmv_ms
+        if dist is not None:
+            import torch
+            t = torch.tensor([dt, spmv_ms], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt, spmv_ms = float(t[0]), float(t[1])
+        regions.append((dt, spmv_ms, res.spmv_launches))
+    order = sorted(range(len(regions)), key=lambda i: regions[i][0])
+    dt, spmv_ms_med, spmv_launches = regions[order[len(order) // 2]]
 
     if rank == 0:
         it_s = args.steps / dt
@@ -223,15 +219,14 @@ def main():
         lay, slots, packed, stream = N.I32(), N.I64(), N.I64(), N.I64()
         N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), ctypes.byref(slots), ctypes.byref(packed),
                                      ctypes.byref(stream)), "psk_csr_layout")
-        sliced = lay.value != N.PSK_LAYOUT_CSR
-        kname = "spmv_sliced_kernel<kSpmvDot>" if sliced else "spmv_kernel<kSpmvDot>"
         # the bytes this launch must move in its storage layout (matrix stream + x read + y written;
-        # DESIGN.md "Roofline accounting"); with a value dictionary far fewer than CSR's 12 B/entry
+        # DESIGN.md §5); with a value dictionary far fewer than CSR's 12 B/entry
         blay = stream.value + 16 * nloc_r0
-        ach = blay / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
-        csr_eq = bspmv / (res.spmv_ms * 1e-3) / 1e9 if res.spmv_ms > 0 else None
+        ach = blay / (spmv_ms_med * 1e-3) / 1e9 if spmv_ms_med > 0 else None
+        csr_eq = bspmv / (spmv_ms_med * 1e-3) / 1e9 if spmv_ms_med > 0 else None
         vb = vec_bytes_per_row(N, M)
         biter = blay * world + vb * n
+        pmc = pmc_traffic(args.traffic_json, m, world, mode=1, sliced=lay.value != N.PSK_LAYOUT_CSR)
         out = {
             "metric": METRIC,
             "value": it_s,
@@ -250,13 +245,21 @@ def main():
                                    % (m, m, n, nnz),
                        "m": m, "precond": "jacobi", "parallelism": "row-block x%d (%s)" % (world, "RCCL" if transport == "rccl" else "host-shm rehearsal")
                        if world > 1 else "single GPU"},
-            "roofline": {"bound": "hbm", "kernel": kname + " (rank 0)",
+            "repeats": {"regions": len(regions), "value_is": "median region",
+                        "it_s": [args.steps / r[0] for r in regions],
+                        "spmv_avg_launch_ms": [r[1] for r in regions]},
+            "roofline": {"bound": "hbm", "kernel": pmc.pop("kernel", None) or spmv_kernel_label(lay.value, 1),
                          "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (ach / HBM_PEAK_GBPS) if ach else None,
-                         **pmc_traffic(args.traffic_json, m, world, sliced),
-                         "algorithmic_bytes_per_launch": blay, "avg_launch_ms": res.spmv_ms,
-                         "launches": res.spmv_launches, "layout": LAYOUT_NAMES[lay.value],
-                         "csr_bytes_per_launch": bspmv, "csr_equivalent_GBps": csr_eq},
+                         **pmc,
+                         "algorithmic_bytes_per_launch": blay, "avg_launch_ms": spmv_ms_med,
+                         "launches": spmv_launches, "layout": LAYOUT_NAMES[lay.value],
+                         "timing": "HIP events libpsk records on its own stream around every SpMV launch of the "
+                                   "median timed region (rank 0's events; max over ranks at N > 1)",
+                         "csr_bytes_per_launch": bspmv,
+                         "csr_count_over_time_GBps": csr_eq,
+                         "csr_count_note": "SURVEY §8d's CSR byte count (12 nnz + 4(n+1) + 16n) over the same time: "
+                                           "NOT a bandwidth — the layout streams fewer bytes than CSR"},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter, "vector_bytes_per_row": vb,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
@@ -270,30 +273,143 @@ def main():
             out["spmv_plain_batch20"] = {"avg_launch_ms": bms.value,
                                          "achieved_GBps": blay / (bms.value * 1e-3) / 1e9,
                                          "frac": blay / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+            if args.general:
+                out["general_path"] = general_path(N, A, db, dsol, m, args.steps)
             out["spmv_csr_layout_batch20"] = csr_layout_batch(N, A, db, dsol, bspmv)
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
-        if world == 1 and args.spmv10m and m != 3163:
-            out["spmv_N10M"] = spmv_10m(N)
-        if world == 1 and args.config1 and m != 4096:
-            out["configs1_pcg_jacobi_4096"] = pcg_4096(N)
-        if world == 1 and args.cpu_iters > 0:
-            cb = cpu_baseline(m, args.cpu_iters)
-            cb["threads_note"] = "scipy csr_matvec and numpy ufuncs are single-threaded; BLAS limited to 1"
-            out["cpu_baseline"] = cb
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out), flush=True)
-
+    # the 16384^2 operands are no longer needed: free them before the other configs
     N.lib.psk_dfree(dx)
     N.lib.psk_dfree(db)
     N.lib.psk_dfree(dsol)
     N.lib.psk_prec_destroy(M)
     N.lib.psk_csr_destroy(A)
+    if rank == 0:
+        if world == 1 and args.spmv10m and m != 3163:
+            out["spmv_N10M"] = spmv_10m(N, args.traffic_json_10m)
+            out["roofline_N10M"] = out["spmv_N10M"].pop("roofline")
+        if world == 1 and args.config1 and m != 4096:
+            out["configs1_pcg_jacobi_4096"] = pcg_4096(N)
+        if world == 1 and args.config2:
+            out["configs2_gmres30_ilut"] = gmres_ilut(N)
+        if world == 1 and args.config4:
+            out["configs4_pcg_amg_8192"] = pcg_amg(N)
+        if world == 1 and args.cpu_iters > 0:
+            out["cpu_baseline"] = cpu_baseline(m, args.cpu_iters)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+
     if world > 1:
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
+
+
+def median(v):
+    s = sorted(v)
+    return s[len(s) // 2] if len(s) % 2 else 0.5 * (s[len(s) // 2 - 1] + s[len(s) // 2])
+
+
+def spmv_kernel_label(layout, mode):
+    """Descriptive name of the SpMV kernel a layout runs when no PMC profile of the build names it."""
+    return ("spmv_kernel<%d> (CSR layout)" % mode) if layout == 0 else \
+        ("spmv_uniform_kernel / spmv_sliced_kernel <MODE=%d> (%s layout)" % (mode, LAYOUT_NAMES[layout]))
+
+
+def lib_sha256():
+    """sha256 of the libpsk.so this process loaded (a PMC profile is only used for the same build)."""
+    import hashlib
+    from pysolvers_amd import _native as N
+    with open(N.LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()
+
+
+def host_info():
+    """nproc, the CPU model name (lscpu's 'Model name' comes from /proc/cpuinfo) and OPENBLAS_NUM_THREADS."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = None
+    return {"nproc": os.cpu_count(), "affinity_cpus": affinity, "cpu_model": model,
+            "OPENBLAS_NUM_THREADS": os.environ.get("OPENBLAS_NUM_THREADS", "unset (= all cores)"),
+            "OMP_NUM_THREADS": os.environ.get("OMP_NUM_THREADS", "unset")}
+
+
+def cpu_baseline(m, iters):
+    """The oracle (op-for-op restatement of PCGSolver.solve, bit-identical to the reference) on the
+    host, 1 BLAS thread: a bounded sample of the same workload. iters + 1 iterations run; the first
+    (cold) one is dropped and each of the other `iters` is one timed sample; value = 1 / median."""
+    from threadpoolctl import threadpool_limits
+    from oracle import fdlap, krylov
+    t0 = time.time()
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    x = np.random.default_rng(12345).random(m * m)
+    b = A @ x
+    del x
+    setup = time.time() - t0
+    marks = []
+    with threadpool_limits(limits=1):
+        st = krylov.pcg(A, b, maxiter=iters + 1, tau=0.0, fail_on_maxiter=False, precond=krylov.jacobi_form(A),
+                        on_iter=lambda k: marks.append(time.perf_counter()))
+        marks.append(time.perf_counter())
+    assert st["iters"] == iters + 1
+    per = [marks[k + 1] - marks[k] for k in range(1, iters + 1)]
+    return dict(value=1.0 / median(per), unit="CG iterations/s", cores=1, kind="port",
+                samples_s_per_iteration=per, host=host_info(),
+                sample="%d single-iteration samples (after one untimed iteration) of the oracle's PCG+Jacobi "
+                       "(numpy/scipy restatement of PCGSolver.py:64-142, bit-identical to the reference) on the same "
+                       "FDLaplacian2D m=%d system, BLAS limited to 1 thread (scipy csr_matvec and numpy ufuncs are "
+                       "single-threaded anyway); value = 1 / median sample; %.0f s setup" % (iters, m, setup))
+
+
+def general_path(N, A, b, x, m, steps, repeats=3):
+    """The path a general matrix takes (SpMV layout with double values in slot pairs, DInv streamed
+    from HBM) on the same FD system, same iteration count: the headline's value dictionary and
+    scalar DInv apply only to constant-coefficient stencils."""
+    os.environ["PSK_JACOBI_UNIFORM"] = "0"
+    Mg = ctypes.c_void_p()
+    try:
+        N.check(N.lib.psk_prec_create(A, N.PSK_PREC_JACOBI, ctypes.byref(Mg)), "psk_prec_create")
+    finally:
+        del os.environ["PSK_JACOBI_UNIFORM"]
+    N.check(N.lib.psk_csr_layout(A, N.PSK_LAYOUT_SLICED, None, None, None, None), "psk_csr_layout")
+    n = m * m
+
+    def run(k, tk):
+        ctl = N.PskCtl(maxiter=k, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=tk)
+        res = N.PskResult()
+        N.check(N.lib.psk_pcg(A, Mg, b, x, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "psk_pcg")
+        return res
+    run(5, 0)
+    regs = []
+    for _ in range(repeats):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        res = run(steps, 1)
+        N.check(N.lib.psk_synchronize(), "sync")
+        regs.append((time.perf_counter() - t0, res.spmv_ms))
+    regs.sort()
+    dt, sms = regs[len(regs) // 2]
+    bl, lname = layout_bytes(N, A, n)
+    vb = vec_bytes_per_row(N, Mg)
+    N.lib.psk_prec_destroy(Mg)
+    ach = bl / (sms * 1e-3) / 1e9
+    return {"what": "PSK_SPMV_LAYOUT=sliced (double values) + PSK_JACOBI_UNIFORM=0 (streamed DInv), same "
+                    "matrix and iteration count; median of %d regions" % repeats,
+            "pcg_it_per_s": steps / dt, "ms_per_step": dt * 1e3 / steps, "layout": lname,
+            "spmv_avg_launch_ms": sms, "spmv_algorithmic_bytes_per_launch": bl, "spmv_achieved_GBps": ach,
+            "spmv_frac": ach / HBM_PEAK_GBPS, "vector_bytes_per_row": vb,
+            "pcg_iteration_frac_of_peak": (bl + vb * n) * steps / dt / 1e9 / HBM_PEAK_GBPS}
 
 
 def csr_layout_batch(N, A, x, y, bspmv, reps=20):
@@ -308,29 +424,37 @@ def csr_layout_batch(N, A, x, y, bspmv, reps=20):
             "frac": gbps / HBM_PEAK_GBPS}
 
 
-def pmc_traffic(path, m, world, sliced):
-    """HBM bytes per SpMV launch measured by rocprofv3 PMC passes on the same kernel and matrix
-    (scripts/gpu_pmc.sh -> tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections
-    calibrated by tools/pmc_calib.hip). Counters cannot be read from inside the timed run."""
+def pmc_traffic(path, m, world, mode, sliced):
+    """HBM bytes per launch of the SpMV kernel of mode `mode` (1 = kSpmvDot, the PCG loop's; 0 =
+    plain) measured by rocprofv3 PMC passes of THIS build at the same side (scripts/gpu_pmc.sh ->
+    tools/pmc_summary.py: FETCH_SIZE x 2 + WRITE_SIZE, gfx950 corrections calibrated by
+    tools/pmc_calib.hip). The profile must record the sha256 of the same libpsk.so and hold exactly
+    one SpMV kernel of that mode; otherwise traffic is null and the reason is given. Counters
+    cannot be read from inside the timed run."""
+    import re
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return {"traffic": None}
+        return {"traffic": None, "traffic_note": "no PMC profile at %s" % os.path.relpath(path, REPO)}
+    src = os.path.relpath(path, REPO)
     if d.get("config", {}).get("side") != m or world != 1:
-        return {"traffic": None}
-    # kSpmvDot = 1; the sliced kernel's second template argument is the dictionary size class
-    want = ("void psk::spmv_sliced_kernel<1>", "void psk::spmv_sliced_kernel<1,") if sliced \
-        else ("void psk::spmv_kernel<1>",)
-    for k, v in d["kernels"].items():
-        if k.startswith(want):
-            return {"traffic": v["hbm_bytes_per_launch"],
-                    "traffic_source": os.path.relpath(path, REPO) + " (rocprofv3 PMC, same kernel/config)"}
-    return {"traffic": None}
+        return {"traffic": None, "traffic_note": "%s is for another side / rank count" % src}
+    if d.get("libpsk_sha256") != lib_sha256():
+        return {"traffic": None, "traffic_note": "%s was captured with another libpsk.so build" % src}
+    pat = re.compile((r"psk::spmv_(uniform|sliced)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
+    hits = [k for k in d["kernels"] if pat.search(k)]
+    if len(hits) != 1:
+        return {"traffic": None, "traffic_note": "%s holds %d SpMV kernels of mode %d" % (src, len(hits), mode)}
+    v = d["kernels"][hits[0]]
+    return {"kernel": hits[0].split("(")[0].replace("void ", ""), "traffic": v["hbm_bytes_per_launch"],
+            "traffic_source": "%s (rocprofv3 PMC FETCH_SIZE/WRITE_SIZE passes, same libpsk.so sha256, "
+                              "%d launches)" % (src, v["launches"])}
 
 
-def spmv_10m(N, iters=30):
-    """SpMV at the metric's N=10M (m=3163): mean launch time of the PCG SpMV over `iters` iterations."""
+def spmv_10m(N, traffic_json, iters=30):
+    """SpMV at the metric's N=10M (m=3163): mean launch time of the PCG SpMV over `iters` iterations
+    (in the loop) and of 50 plain launches back to back, each priced on the layout's bytes."""
     m = 3163
     n, nnz = fd_sizes(m)
     A, M, db, dx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -341,25 +465,42 @@ def spmv_10m(N, iters=30):
     xe = np.random.default_rng(12345).random(n)
     N.check(N.lib.psk_h2d(dx, N.ptr(xe), n * 8), "h2d")
     N.check(N.lib.psk_spmv(A, dx, db, N.PSK_DEVICE), "spmv")
-    ctl = N.PskCtl(maxiter=iters, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=1)
+    ctl = N.PskCtl(maxiter=10, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=0)
     res = N.PskResult()
     N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
+    regs = []
+    for _ in range(5):
+        ctl = N.PskCtl(maxiter=iters, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=1)
+        res = N.PskResult()
+        N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
+        regs.append((res.spmv_ms, res.loop_ms))
+    regs.sort()
+    spmv_ms, loop_ms = regs[len(regs) // 2]
     b = spmv_bytes(n, nnz)
     bl, lname = layout_bytes(N, A, n)
-    gbps = bl / (res.spmv_ms * 1e-3) / 1e9
+    lay = N.I32()
+    N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), None, None, None), "psk_csr_layout")
+    gbps = bl / (spmv_ms * 1e-3) / 1e9
     # back-to-back launches between two events (no per-launch event in between)
     bms = ctypes.c_double()
     N.check(N.lib.psk_spmv_timed(A, dx, db, 50, ctypes.byref(bms)), "psk_spmv_timed")
     bb = bl / (bms.value * 1e-3) / 1e9
+    sl = lay.value != N.PSK_LAYOUT_CSR
+    pin, pbb = pmc_traffic(traffic_json, m, 1, mode=1, sliced=sl), pmc_traffic(traffic_json, m, 1, mode=0, sliced=sl)
+    roof = {
+        "in_loop": {"bound": "hbm", "kernel": pin.pop("kernel", None) or spmv_kernel_label(lay.value, 1),
+                    "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": gbps / HBM_PEAK_GBPS, **pin,
+                    "algorithmic_bytes_per_launch": bl, "avg_launch_ms": spmv_ms, "layout": lname,
+                    "how": "HIP events around each SpMV launch of a %d-iteration PCG+Jacobi solve; median of 5" % iters},
+        "back_to_back": {"bound": "hbm", "kernel": pbb.pop("kernel", None) or spmv_kernel_label(lay.value, 0),
+                         "achieved": bb, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": bb / HBM_PEAK_GBPS, **pbb,
+                         "algorithmic_bytes_per_launch": bl, "avg_launch_ms": bms.value, "layout": lname,
+                         "how": "50 plain y = A x launches between two HIP events on the library stream"},
+    }
     csr = csr_layout_batch(N, A, dx, db, b, reps=50)
-    out = {"n": n, "nnz": nnz, "layout": lname, "avg_launch_ms": res.spmv_ms, "achieved_GBps": gbps,
-           "frac": gbps / HBM_PEAK_GBPS, "pcg_it_per_s": iters / (res.loop_ms * 1e-3),
-           "algorithmic_bytes_per_launch": bl, "csr_bytes_per_launch": b,
-           "csr_equivalent_GBps": b / (res.spmv_ms * 1e-3) / 1e9,
-           "batch50": {"kernel": "SpMV, plain mode, the matrix's default layout", "avg_launch_ms": bms.value, "achieved_GBps": bb,
-                       "frac": bb / HBM_PEAK_GBPS,
-                       "how": "50 back-to-back launches between two HIP events on the library stream"},
-           "batch50_csr_layout": csr}
+    out = {"n": n, "nnz": nnz, "layout": lname, "pcg_it_per_s": iters / (loop_ms * 1e-3),
+           "csr_bytes_per_launch": b, "csr_count_over_time_GBps_in_loop": b / (spmv_ms * 1e-3) / 1e9,
+           "batch50_csr_layout": csr, "roofline": roof}
     for p in (db, dx):
         N.lib.psk_dfree(p)
     N.lib.psk_prec_destroy(M)
@@ -368,7 +509,7 @@ def spmv_10m(N, iters=30):
 
 
 def pcg_4096(N, iters=300):
-    """configs[1]: PCG+Jacobi on FDLaplacian2D 4096^2, one GPU, `iters` fixed iterations."""
+    """configs[1]: PCG+Jacobi on FDLaplacian2D 4096^2, one GPU, `iters` fixed iterations (median of 5)."""
     m = 4096
     n, nnz = fd_sizes(m)
     A, M, db, dx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
@@ -386,20 +527,165 @@ def pcg_4096(N, iters=300):
         N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
         return res
     run(20, 0)
-    N.check(N.lib.psk_synchronize(), "sync")
-    t0 = time.perf_counter()
-    run(iters, 0)
-    N.check(N.lib.psk_synchronize(), "sync")
-    dt = time.perf_counter() - t0
+    regs = []
+    for _ in range(5):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        run(iters, 0)
+        N.check(N.lib.psk_synchronize(), "sync")
+        regs.append(time.perf_counter() - t0)
+    dt = median(regs)
     res = run(50, 1)
     bl, lname = layout_bytes(N, A, n)
     out = {"n": n, "nnz": nnz, "iters": iters, "layout": lname, "pcg_it_per_s": iters / dt,
+           "regions_it_s": [iters / r for r in regs],
            "pcg_iteration_frac_of_peak": (bl + vec_bytes_per_row(N, M) * n) * iters / dt / 1e9 / HBM_PEAK_GBPS,
            "spmv_avg_launch_ms": res.spmv_ms, "spmv_frac": bl / (res.spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
     for p in (db, dx):
         N.lib.psk_dfree(p)
     N.lib.psk_prec_destroy(M)
     N.lib.psk_csr_destroy(A)
+    return out
+
+
+def trisolve_schedules(N, h):
+    """Schedule the library chose for each factor of a triangular-solve chain."""
+    names = {0: "syncfree", 1: "band", 2: "lds"}
+    out = []
+    for which in (0, 1):
+        s, blocks = N.I32(), N.I64()
+        N.check(N.lib.psk_prec_trisolve_schedule(h, which, -1, ctypes.byref(s), ctypes.byref(blocks), None, None,
+                                                 None), "psk_prec_trisolve_schedule")
+        out.append(names.get(s.value, s.value))
+    return out
+
+
+def gmres_ilut(N, m=2896, restart=30, steps=60, repeats=3):
+    """configs[2]: GMRES(30) + right ILUT (the reference's spilu arguments, ILUTPreconditioner.py:51-53)
+    on FDLaplacian2D m^2, one GPU, exactly `steps` Arnoldi steps per timed solve (tau = 0). m = 2896
+    is the largest side scipy's SuperLU forms this ILUT for (4096^2: SUPERLU_MALLOC fails, in the
+    reference too; profiles/r1_gmres_ilut_4096_unformable.json). Latency model: the ILU apply is two
+    dependency chains; us_per_level = apply time / (levels of L + levels of U)."""
+    import pysolvers_amd as psk
+    n = m * m
+    t = time.time()
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    x = psk.DeviceVector.from_numpy(np.random.default_rng(12345).random(n))
+    b = psk.Linear.spmv(dA, x)
+    del x
+    out = {"workload": "GMRES(%d) + RightILUT(drop_tol=1e-3, fill_factor=15), FDLaplacian2D %dx%d, tau=0, %d Arnoldi "
+                       "steps per solve" % (restart, m, m, steps), "n": n}
+    try:
+        M = psk.RightILUT().form(dA)
+    except RuntimeError as e:
+        out["error"] = "reference ILUT factorization failed: %s" % e
+        return out
+    out["ilut_setup_s"] = time.time() - t
+    info = M.device_info()
+    out.update(nnz_L=info["nnz_l"], nnz_U=info["nnz_u"], levels_L=info["levels_l"], levels_U=info["levels_u"],
+               schedules=trisolve_schedules(N, M.device_handle))
+    v = psk.DeviceVector.from_numpy(np.random.default_rng(1).standard_normal(n))
+    M.applyRight(v)
+    ap = []
+    for _ in range(5):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t2 = time.perf_counter()
+        M.applyRight(v)
+        N.check(N.lib.psk_synchronize(), "sync")
+        ap.append((time.perf_counter() - t2) * 1e3)
+    apply_ms = median(ap)
+    ilu_bytes = 12 * (info["nnz_l"] + info["nnz_u"]) + 80 * n
+    out["ilu_apply"] = {"bound": "latency (dependency chain)", "ms": apply_ms,
+                        "us_per_level": apply_ms * 1e3 / max(1, info["levels_l"] + info["levels_u"]),
+                        "bytes_model": "12 B per factor entry + 80 B per row (gathers, rhs, diagonal, x)",
+                        "bytes": ilu_bytes, "achieved_GBps": ilu_bytes / (apply_ms * 1e-3) / 1e9,
+                        "frac_of_hbm_peak": ilu_bytes / (apply_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    sol = psk.DeviceVector(n)
+
+    def run(k):
+        ctl = N.PskCtl(maxiter=k, tau=0.0, fail_on_maxiter=0, restart=restart, check_every=0, time_kernels=0)
+        res = N.PskResult()
+        N.check(N.lib.psk_gmres(dA.handle, M.device_handle, b._p, sol._p, ctypes.byref(ctl), ctypes.byref(res), None,
+                                N.PSK_DEVICE), "psk_gmres")
+        return res
+    run(restart)
+    regs = []
+    for _ in range(repeats):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        res = run(steps)
+        N.check(N.lib.psk_synchronize(), "sync")
+        regs.append(time.perf_counter() - t0)
+    dt = median(regs)
+    out.update(steps_per_s=steps / dt, ms_per_step=dt * 1e3 / steps, regions_steps_per_s=[steps / r for r in regs],
+               ilu_share_of_step=apply_ms / (dt * 1e3 / steps), status=int(res.status),
+               rec_resid_ratio=res.resid_recursive / res.norm_b, setup_s=time.time() - t)
+    return out
+
+
+def pcg_amg(N, m=8192, levels=5, cycles=2, iters=6, repeats=3):
+    """configs[4]: PCG + AMG(numIters=2, 5 levels, Gauss-Seidel nu = 2 + 2) on -FDLaplacian2D m^2 (the
+    sign FDBratu2D.py:15 uses), one GPU, exactly `iters` PCG iterations per timed solve (PCG+AMG does
+    not converge on this matrix). Latency model: each apply runs cycles x (nuPre +
+    nuPost) fine Gauss-Seidel sweeps, each a dependency chain of 2m - 1 levels."""
+    import pysolvers_amd as psk
+    n = m * m
+    t = time.time()
+    A = -psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m).to_scipy()
+    dA = psk.DeviceCSR.from_scipy(A)
+    x = psk.DeviceVector.from_numpy(np.random.default_rng(12345).random(n))
+    b = psk.Linear.spmv(dA, x)
+    del x
+    out = {"workload": "PCG + AMG(numIters=%d, numLevels=%d, nuPre=2, nuPost=2, GaussSeidelSmoother), "
+                       "-FDLaplacian2D %dx%d, tau=0, %d iterations per solve" % (cycles, levels, m, m, iters), "n": n}
+    t1 = time.time()
+    M = psk.AMG(numIters=cycles, numLevels=levels, smoother=psk.GaussSeidelSmoother).form(dA)
+    del A
+    out["amg_setup_s"] = time.time() - t1
+    out["level_sizes"] = M.levels()
+
+    def timed(fn, reps=3):
+        fn()
+        ts = []
+        for _ in range(reps):
+            N.check(N.lib.psk_synchronize(), "sync")
+            t2 = time.perf_counter()
+            fn()
+            N.check(N.lib.psk_synchronize(), "sync")
+            ts.append((time.perf_counter() - t2) * 1e3)
+        return median(ts)
+    v = psk.DeviceVector.from_numpy(np.random.default_rng(1).standard_normal(n))
+    out["amg_apply_ms"] = timed(lambda: M.apply(v))
+    S = M._S[-1].operator
+    fine_levels = S.device_info()["levels_u"]
+    sweep_ms = timed(lambda: S.apply(v))
+    out["fine_gs_sweep"] = {"bound": "latency (dependency chain)", "ms": sweep_ms, "dep_levels": fine_levels,
+                            "us_per_level": sweep_ms * 1e3 / max(1, fine_levels),
+                            "schedule": S.schedule("U")["schedule"],
+                            "sweeps_per_apply": cycles * 4,
+                            "share_of_apply": cycles * 4 * sweep_ms / out["amg_apply_ms"]}
+    co = M._coarse
+    v0 = psk.DeviceVector.from_numpy(np.random.default_rng(0).standard_normal(M.levels()[0]))
+    out["coarse_solve_ms"] = timed(lambda: co.apply(v0))
+    sol = psk.DeviceVector(n)
+
+    def run(k):
+        ctl = N.PskCtl(maxiter=k, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=0)
+        res = N.PskResult()
+        N.check(N.lib.psk_pcg(dA.handle, M.device_handle, b._p, sol._p, ctypes.byref(ctl), ctypes.byref(res), None,
+                              N.PSK_DEVICE), "psk_pcg")
+        return res
+    run(1)
+    regs = []
+    for _ in range(repeats):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        res = run(iters)
+        N.check(N.lib.psk_synchronize(), "sync")
+        regs.append(time.perf_counter() - t0)
+    dt = median(regs)
+    out.update(pcg_it_per_s=iters / dt, ms_per_it=dt * 1e3 / iters, regions_it_s=[iters / r for r in regs],
+               status=int(res.status), iters_done=int(res.iters), setup_s=time.time() - t)
     return out
 
 

@@ -72,7 +72,9 @@ def _status(success, iters, soln, resid, msg=None, hist=None):
 # ---------------------------------------------------------------------------
 # PCG  (PCGSolver.py:64-142)
 
-def pcg(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_apply):
+def pcg(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_apply, on_iter=None):
+    """on_iter(k): optional hook called at the top of iteration k (bench.py's cpu_baseline times
+    single iterations with it); it sees no solver state."""
     n, nc = A.shape
     assert n == nc                                   # :79-81
     assert n == len(b)                               # :83
@@ -90,6 +92,8 @@ def pcg(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_ap
     k = -1
     normR = None
     for k in range(maxiter):                         # :109
+        if on_iter is not None:
+            on_iter(k)
         Ap = mvmult(A, p)                            # :111
         pTAp = np.dot(p, Ap)                         # :113
         if pTAp == 0.0:                              # :114-115
@@ -198,6 +202,92 @@ def gmres(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_
     if fail_on_maxiter:
         return _status(False, it, x, norm_r_k, 'failure to converge', hist)
     return _status(True, it, x, norm_r_k, hist=hist)
+
+
+# ---------------------------------------------------------------------------
+# Restarted GMRES(m): the reference has no restart (GMRESSolver.py:104 runs one Krylov space of
+# dimension maxiter). GMRES(m) is cycles of the reference's own loop (:87-160) on the residual
+# system A dx = r_c (r_0 = b, r_c = b - A x_c), each at most m steps, with the reference's
+# convergence test against the ORIGINAL ||b|| (tau * ||b||, :158); x_{c+1} = x_c + dx_c.
+# tests/golden/make_restarted.py pins every cycle bit for bit to the reference's own solve on
+# (A, r_c) and writes the fixtures.
+
+def gmres_cycle(A, r0, K, thresh, precond):
+    """One cycle: at most K Arnoldi steps of GMRESSolver.py:87-158 from r0, stopping when |g[k+1]|
+    <= thresh or Arnoldi breaks down. Returns (k, converged, hist, dx) with dx = M^-1 (Q y) (:159-160)
+    over the k+1 basis vectors built."""
+    n = A.shape[0]
+    Q = np.zeros([n, K + 1])                             # :77
+    HBar = np.zeros([K + 1, K])                          # :80
+    CS = np.zeros([K, 2])                                # :83
+    beta = npla.norm(r0)                                 # :90
+    Q[:, 0] = r0 / beta                                  # :91
+    e1 = np.zeros(K + 1)                                 # :95
+    e1[0] = 1.0
+    g = beta * e1                                        # :97
+    hist = []
+    for k in range(K):                                   # :104
+        u = mvmult(A, precond(Q[:, k]))                  # :107
+        for j in range(k + 1):                           # :110-112
+            HBar[j, k] = np.dot(Q[:, j], u)
+            u -= HBar[j, k] * Q[:, j]
+        HBar[k + 1, k] = npla.norm(u)                    # :115
+        hLastColNorm = npla.norm(HBar[0:k + 1, k])       # :121
+        brk = abs(HBar[k + 1, k]) <= 1.0e-16 * hLastColNorm   # :122
+        if not brk:
+            Q[:, k + 1] = u / HBar[k + 1, k]             # :125
+        for j in range(k):                               # :133-135
+            apply_givens_in_place(HBar[:, k], CS[j, 0], CS[j, 1], j)
+        CS[k, :] = find_givens_coefficients(HBar[:, k], k)         # :140
+        apply_givens_in_place(HBar[:, k], CS[k, 0], CS[k, 1], k)   # :145
+        apply_givens_in_place(g, CS[k, 0], CS[k, 1], k)            # :148
+        norm_r_k = np.abs(g[k + 1])                      # :152
+        hist.append(norm_r_k)
+        if brk or norm_r_k <= thresh or k == K - 1:      # :158 (or the cycle's last step)
+            y = npla.solve(HBar[0:k + 1, 0:k + 1], g[0:k + 1])   # :159
+            dx = precond(np.dot(Q[:, 0:k + 1], y))       # :160
+            return k, bool(brk or norm_r_k <= thresh), hist, dx
+    raise ValueError("gmres_cycle: K must be >= 1")
+
+
+def gmres_restarted(A, b, restart, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_apply,
+                    cycles=None):
+    """GMRES(restart) with the reference's status conventions: convergence as :158-174 (iters =
+    steps so far + 1, true residual ||b - A x|| checked); maxiter as the non-restarted solver's
+    handleMaxiter(k, ...) with k = maxiter - 1 (iters = maxiter - 1, resid = last |g[k+1]|).
+    `cycles`, if a list, receives (r_c, steps, dx_c) per cycle (make_restarted.py checks each
+    against the reference)."""
+    n, nc = A.shape
+    assert n == nc and n == len(b)
+    assert restart >= 1 and maxiter >= 1
+    norm_b = npla.norm(b)                                # :66
+    if norm_b == 0.0:                                    # :67-68
+        return _status(True, 1, np.zeros_like(b), 0, hist=[])
+    thresh = tau * norm_b                                # :158
+    hist = []
+    it = 0
+    r = b                                                # :87 (first cycle)
+    x = None
+    while True:
+        Kc = min(maxiter - it, restart)
+        k, conv, h, dx = gmres_cycle(A, r, Kc, thresh, precond)
+        hist += h
+        if cycles is not None:
+            cycles.append((r, k + 1, dx))
+        x = dx if x is None else x + dx
+        if conv:                                         # :159-174
+            resid = b - mvmult(A, x)                     # :163
+            norm_r_true = npla.norm(resid)               # :164
+            if norm_r_true <= thresh:
+                return _status(True, it + k + 1, x, norm_r_true, hist=hist)
+            return _status(False, it + k + 1, x, norm_r_true,
+                           'GMRES failure: true residual did not meet tolerance', hist)
+        it += Kc
+        if it >= maxiter:                                # handleMaxiter(maxiter - 1, ...)
+            if fail_on_maxiter:
+                return _status(False, maxiter - 1, x, h[-1], 'failure to converge', hist)
+            return _status(True, maxiter - 1, x, h[-1], hist=hist)
+        r = b - mvmult(A, x)                             # next cycle's residual system
 
 
 def givens_selftest_matrix():

@@ -309,7 +309,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
 
     int rc = PSK_OK;
     int64_t it = 0;          // global iterations completed before this cycle
-    bool first = true, finished = false;
+    bool first = true, finished = false, hit_maxiter = false;
     GmresState hs{};
     std::vector<double> hR, hg, y;
     int64_t spmv_count = 0;
@@ -438,6 +438,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             if ((rc = run_finalize((int)Kc - 1, it - Kc > 0)) != PSK_OK) break;
             if (it >= maxiter) {
                 // maxiter reached (reference: NameError at :180) -> handleMaxiter(k, x, |g|, ...)
+                hit_maxiter = true;
                 res->iters = maxiter > 0 ? maxiter - 1 : 0;
                 res->resid = hs.rec;
                 res->resid_recursive = hs.rec;
@@ -468,7 +469,8 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             res->iters = 1;
             res->resid = 0.0;
         }
-        const int64_t nh = res->iters + (res->status == PSK_MAXITER ? 1 : 0);
+        // every step reported one residual (reportIter, :155): iters + 1 entries at maxiter (k = maxiter - 1)
+        const int64_t nh = res->iters + (hit_maxiter ? 1 : 0);
         const int64_t nhc = hs.zero_b ? 0 : (nh < maxiter ? nh : maxiter);
         res->hist_len = nhc;
         if (hist && nhc > 0 &&

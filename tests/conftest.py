@@ -64,3 +64,10 @@ def product_prec_type(psk, name):
         return psk.AMG(numIters=it, numLevels=lv, **kw)
     return {"identity": psk.IdentityPreconditionerType, "jacobi": psk.JacobiPreconditionerType,
             "ilut": psk.RightILUT, "ic": psk.RightIC}[name]()
+
+
+def restarted_cases():
+    """GMRES(m) golden cases (tests/golden/make_restarted.py: every cycle pinned to the reference's
+    own GMRES solve on the residual system)."""
+    with open(os.path.join(GOLDEN, "manifest_restarted.json")) as f:
+        return json.load(f)["cases"]

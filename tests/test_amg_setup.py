@@ -146,3 +146,16 @@ def test_coarse_factorisation_is_spsolve(fix, key):
     y = spla.spsolve_triangular(Ut, f[inverse_permutation(lu.perm_c)], lower=True)
     z = spla.spsolve_triangular(Lt, y, lower=False, unit_diagonal=True)
     np.testing.assert_allclose(z[lu.perm_r], x_ref, rtol=0, atol=1e-12 * np.abs(x_ref).max())
+
+
+def test_native_first_level_matches_oracle_negfd1024():
+    """configs[4]'s matrix family at 1M rows (-FDLaplacian2D 1024^2, FDBratu2D.py:15 sign): the native
+    O(nnz) aggregation, the filtered matrix and the smoothed prolongator of the first coarsening
+    equal the oracle's restatement bit for bit (the GPU suite runs the 8192^2 hierarchy itself)."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear.SmoothedAggregation import SA_coarsen
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 1024)
+    P, agg = SA_coarsen(A, lvl=1)
+    oP, oagg = amg.sa_coarsen(A, lvl=1)
+    assert np.array_equal(agg, oagg)
+    assert _bitwise(P, oP)

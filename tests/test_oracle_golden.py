@@ -11,7 +11,8 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import case_precond, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type, solver_cases
+from conftest import (case_precond, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type, restarted_cases,
+                      solver_cases)
 from oracle import fdlap, krylov, native
 
 
@@ -80,6 +81,31 @@ def test_oracle_solvers_match_reference(case):
     np.testing.assert_allclose(st["hist"], h, rtol=1e-10, atol=0)
     if d["soln"].size:
         np.testing.assert_allclose(st["soln"], d["soln"], rtol=1e-9, atol=1e-12 * np.abs(d["soln"]).max())
+
+
+@pytest.mark.parametrize("case", restarted_cases(), ids=lambda c: c["file"][:-4])
+def test_oracle_restarted_gmres_matches_fixture(case):
+    """GMRES(m) restatement (cycles of GMRESSolver.py:87-160 on the residual system) against the
+    fixtures make_restarted.py pinned cycle by cycle to the reference's own solve."""
+    d = load_golden(case["file"])
+    A = golden_matrix(d)
+    b = d["b"]
+    prec = oracle_prec(A, case["precond"])
+    st = krylov.gmres_restarted(A, b, case["restart"], maxiter=case["maxiter"], tau=case["tau"],
+                                fail_on_maxiter=bool(case["fail_on_maxiter"]), precond=prec)
+    assert st["iters"] == case["iters"] and bool(st["success"]) == case["success"]
+    assert len(st["hist"]) == len(d["hist"])
+    np.testing.assert_allclose(st["hist"], d["hist"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(st["soln"], d["soln"], rtol=1e-9, atol=1e-12 * np.abs(d["soln"]).max())
+
+
+def test_restarted_equals_reference_when_one_cycle_suffices():
+    """restart >= the steps needed: GMRES(m) IS the reference's non-restarted solve (same golden)."""
+    d = load_golden("gmres_dh8_identity.npz")
+    A = golden_matrix(d)
+    st = krylov.gmres_restarted(A, d["b"], 300, maxiter=300, tau=1e-8)
+    assert st["iters"] == int(d["iters"])
+    assert np.array_equal(st["hist"], d["hist"]) and np.array_equal(st["soln"], d["soln"])
 
 
 def test_zero_rhs_convention():

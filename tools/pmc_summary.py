@@ -6,7 +6,10 @@ corrections of MI355X_MICROARCH.md §HBM, verified by tools/pmc_calib.hip:
   write bytes = WRITE_SIZE[KB] * 1024 * (calibrated write factor; 1.0)
 
     python tools/pmc_summary.py gpurun_out/pmc_TAG_FETCH_SIZE gpurun_out/pmc_TAG_WRITE_SIZE \
-        gpurun_out/pmc_TAG_calib_FETCH_SIZE gpurun_out/pmc_TAG_calib_WRITE_SIZE [SIDE "BENCH ARGS"] > profiles/x.json
+        gpurun_out/pmc_TAG_calib_FETCH_SIZE gpurun_out/pmc_TAG_calib_WRITE_SIZE [SIDE "BENCH ARGS" SHA_FILE] > profiles/x.json
+
+SHA_FILE: the `sha256sum` line of the libpsk.so the passes ran with (scripts/gpu_pmc.sh writes it);
+bench.py uses a profile only when it matches the library it loaded.
 """
 import collections
 import csv
@@ -26,7 +29,7 @@ def per_kernel(d):
     return agg
 
 
-def main(fetch_dir, write_dir, cal_fetch, cal_write, side=None, bench_args=None):
+def main(fetch_dir, write_dir, cal_fetch, cal_write, side=None, bench_args=None, sha_file=None):
     cf, cw = per_kernel(cal_fetch), per_kernel(cal_write)
     rfac = {k.split("(")[0]: CALIB_BYTES / (sum(v) / len(v)) for k, v in cf.items() if k.startswith(("void rd", "rd16"))}
     wfac = {k.split("(")[0]: CALIB_BYTES / (sum(v) / len(v)) for k, v in cw.items() if k.startswith("wr8")}
@@ -45,9 +48,11 @@ def main(fetch_dir, write_dir, cal_fetch, cal_write, side=None, bench_args=None)
         out["config"] = {"side": int(side), "bench_args": bench_args,
                          "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (scripts/gpu_pmc.sh), corrected "
                                  "with tools/pmc_calib.hip factors"}
+    if sha_file is not None:
+        out["libpsk_sha256"] = open(sha_file).read().split()[0]
     json.dump(out, sys.stdout, indent=1)
     print()
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:7])
+    main(*sys.argv[1:8])
