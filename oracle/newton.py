@@ -8,6 +8,7 @@ Only tests/ and the golden generator import this module.
   A = -FDLaplacian2D(-1, 1, m)
 """
 import numpy as np
+import scipy.sparse.linalg as spla
 import numpy.linalg as npla
 
 from . import fdlap, krylov
@@ -49,9 +50,11 @@ def simple_backtrack(x0, normF0, p, func, maxsteps=10, low=0.1, alpha=0.0001):
     return False, x_k, F_k, normF_k
 
 
-def newton(func, x0, form_prec, maxiter=10, tau=1e-12, tol_fudge=0.1, min_lin_tol=1e-6, lin_maxiter=100):
+def newton(func, x0, form_prec, maxiter=10, tau=1e-12, tol_fudge=0.1, min_lin_tol=1e-6, lin_maxiter=100,
+           direct=False):
     """Returns dict(success, iters, soln, resid, msg, hist, linear_iters). form_prec(J) -> apply;
-    formed once on the first Jacobian (freezePrec=True)."""
+    formed once on the first Jacobian (freezePrec=True). direct=True: the steps are the default
+    DefaultDirect solves, spla.spsolve(J, -F) (DefaultDirectSolver.py:61-70, Newton.py:13)."""
     x = x0.copy()
     F = func.evalF(x)
     r0 = npla.norm(F)
@@ -63,6 +66,13 @@ def newton(func, x0, form_prec, maxiter=10, tau=1e-12, tol_fudge=0.1, min_lin_to
         if nF <= r0 * tau + tau:
             return dict(success=True, iters=i + 1, soln=x, resid=nF, msg=None, hist=np.array(hist), linear_iters=lin)
         J = func.evalJ(x)
+        if direct:
+            lin.append(None)
+            ok, x, F, nF = simple_backtrack(x, nF, spla.spsolve(J, -F), func)
+            if not ok:
+                return dict(success=False, iters=i, soln=None, resid=None, msg='Line search failed',
+                            hist=np.array(hist), linear_iters=lin)
+            continue
         tl = max(tol_fudge * nF / r0, min_lin_tol)
         if prec is None:
             prec = form_prec(J)

@@ -2,6 +2,7 @@
 from .AMGPreconditioner import AMG, AMGPreconditioner
 from .ClassicSmoothers import GaussSeidelSmoother, JacobiSmoother
 from .DeviceMatrix import DeviceCSR, DeviceVector, spmv
+from .DirectSolver import DefaultDirect, DefaultDirectSolver
 from .Distributed import Communicator, fd_laplacian_2d_sharded, halo_cols, shard_csr
 from .GMRESSolver import GMRES, GMRESSolver
 from .ILUTPreconditioner import (ILUTPreconditioner, LeftILUT, LeftILUTPreconditioner, RightILUT,

@@ -1,24 +1,29 @@
-"""Newton's method with a device Krylov solver for the steps (Newton.py:10-101).
+"""Inexact Newton driver over the device linear solvers (the caller of the hot path, Newton.py:10-101).
 
-The loop is host logic (function and Jacobian evaluation are the caller's numpy code, as in the
-reference); each step's J p = -F solve is one device PCG/GMRES call with the adaptive tolerance
-max(tolFudge ||F||/||F_0||, minLinTol) (:62-73) and, with freezePrec, the preconditioner formed on
-the first Jacobian reused for every later step (:38-39, PreconditionerFreeze).
+Function and Jacobian evaluation are the caller's host code (``func.evalF`` / ``func.evalJ``), as
+in the reference; every Newton step's linear solve J p = -F is one libpsk solve (device PCG/GMRES,
+or the device-applied direct solve of ``DefaultDirect``). Semantics kept from the reference:
+
+* convergence test before each step: ||F_i|| <= tau ||F_0|| + tau (:54);
+* linear tolerance per step: ``minLinTol`` if ``fixLinTol`` else max(tolFudge ||F_i|| / ||F_0||,
+  minLinTol) (:62-73), set only on iterative linear solvers;
+* with ``freezePrec`` the preconditioner formed for the first Jacobian is reused for every later
+  one (PreconditionerFreeze.py:15-21; the reference never unfreezes);
+* a failed linear solve or line search ends the solve through handleBreakdown (:79-82, :95-97);
+  maxiter through handleMaxiter(maxiter, ...) (:101);
+* the unconditional 'freeze prec for solver=' line the reference prints (:38) is printed too.
 """
 from ..IterativeSolver import CommonSolverArgs, IterativeSolver
+from ..Linear.DirectSolver import DefaultDirect
 from ..Linear.IterativeLinearSolver import IterativeLinearSolver
 from .LineSearch import SimpleBacktrack
 from .PreconditionerFreeze import PreconditionerFreeze
 
 
 class NewtonSolver(IterativeSolver):
-    def __init__(self, control=CommonSolverArgs(), solver=None, linesearch=SimpleBacktrack(), fixLinTol=False,
-                 tolFudge=0.1, minLinTol=1.0e-10, freezePrec=True, name='Newton'):
+    def __init__(self, control=CommonSolverArgs(), solver=DefaultDirect(), linesearch=SimpleBacktrack(),
+                 fixLinTol=False, tolFudge=0.1, minLinTol=1.0e-10, freezePrec=True, name='Newton'):
         super().__init__(control, name=name)
-        if solver is None:
-            # the reference's default is DefaultDirect() (a SuperLU wrapper, outside this build's hot path)
-            raise TypeError("NewtonSolver: pass solver=PCG(...) or GMRES(...) (the direct-solver default "
-                            "DefaultDirect is not part of this build)")
         self.solver = solver.makeSolver()
         self.linesearch = linesearch
         self.fixLinTol = fixLinTol
@@ -27,29 +32,44 @@ class NewtonSolver(IterativeSolver):
         self.freezePrec = freezePrec
         self.linear_iters = []          # iterations of each step's linear solve (diagnostics)
 
+    def _linear_tolerance(self, normF, normF0):
+        """Tolerance handed to an iterative step solver (:62-73)."""
+        if self.fixLinTol:
+            return self.minLinTol
+        return max(self.tolFudge * normF / normF0, self.minLinTol)
+
+    def _converged(self, normF, normF0):
+        return normF <= normF0 * self.tau() + self.tau()
+
+    def _step(self, J, F, normF, normF0):
+        """Newton direction p with J p = -F, or (None, message) when the linear solve failed."""
+        if isinstance(self.solver, IterativeLinearSolver):
+            self.solver.setTolerance(self._linear_tolerance(normF, normF0))
+        status = self.solver.solve(J, -F)
+        self.linear_iters.append(status.iters())
+        if status.success():
+            return status.soln(), None
+        return None, 'solve for Newton step failed with msg={}'.format(status.msg())
+
     def solve(self, func, xInit):
-        xCur = xInit.copy()
-        FCur = func.evalF(xCur)
+        x = xInit.copy()
+        F = func.evalF(x)
         print('freeze prec for solver=', self.freezePrec)
         PreconditionerFreeze(self.solver, self.freezePrec)
         self.linesearch.setNorm(self.norm)
-        r0 = self.norm(FCur)
-        normFCur = r0
+        normF0 = self.norm(F)
+        normF = normF0
         self.linear_iters = []
-        for i in range(self.maxiter()):
-            self.reportIter(i, normFCur, r0)
-            if normFCur <= r0 * self.tau() + self.tau():                       # :54
-                return self.handleConvergence(i, xCur, normFCur, r0)
-            J = func.evalJ(xCur)
-            if isinstance(self.solver, IterativeLinearSolver):
-                tau_lin = self.minLinTol if self.fixLinTol else max(self.tolFudge * normFCur / r0, self.minLinTol)
-                self.solver.setTolerance(tau_lin)
-            status = self.solver.solve(J, -FCur)
-            self.linear_iters.append(status.iters())
-            if not status.success():
-                return self.handleBreakdown(i, 'solve for Newton step failed with msg={}'.format(status.msg()))
-            p = status.soln()
-            (success, xCur, FCur, normFCur) = self.linesearch.search(xCur, normFCur, p, func)
-            if not success:
+        i = 0
+        while i < self.maxiter():
+            self.reportIter(i, normF, normF0)
+            if self._converged(normF, normF0):
+                return self.handleConvergence(i, x, normF, normF0)
+            p, why = self._step(func.evalJ(x), F, normF, normF0)
+            if p is None:
+                return self.handleBreakdown(i, why)
+            accepted, x, F, normF = self.linesearch.search(x, normF, p, func)
+            if not accepted:
                 return self.handleBreakdown(i, msg='Line search failed')
-        return self.handleMaxiter(self.maxiter(), xCur, normFCur, r0)
+            i += 1
+        return self.handleMaxiter(self.maxiter(), x, normF, normF0)

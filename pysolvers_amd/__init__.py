@@ -5,11 +5,11 @@ there is no CPU fallback.
 """
 from . import Linear, Nonlinear, io
 from .IterativeSolver import CommonSolverArgs, IterativeSolver, NamedObject, SolveStatus
-from .Linear import (AMG, GMRES, PCG, RightIC, GaussSeidelSmoother, JacobiSmoother, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
+from .Linear import (AMG, DefaultDirect, GMRES, PCG, RightIC, GaussSeidelSmoother, JacobiSmoother, DeviceCSR, DeviceVector, GMRESSolver, IdentityPreconditioner,
                      IdentityPreconditionerType, IterativeLinearSolver, Jacobi, JacobiPreconditioner,
                      JacobiPreconditionerType, LeftILUT, PCGSolver, RightILUT, mvmult)
 
-__all__ = ["Nonlinear", "AMG", "RightIC", "GaussSeidelSmoother", "JacobiSmoother", "Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
+__all__ = ["Nonlinear", "AMG", "DefaultDirect", "RightIC", "GaussSeidelSmoother", "JacobiSmoother", "Linear", "CommonSolverArgs", "IterativeSolver", "NamedObject", "SolveStatus", "GMRES", "PCG",
            "GMRESSolver", "PCGSolver", "DeviceCSR", "DeviceVector", "IdentityPreconditioner",
            "IdentityPreconditionerType", "IterativeLinearSolver", "Jacobi", "JacobiPreconditioner",
            "JacobiPreconditionerType", "LeftILUT", "RightILUT", "mvmult"]

@@ -71,3 +71,9 @@ def restarted_cases():
     own GMRES solve on the residual system)."""
     with open(os.path.join(GOLDEN, "manifest_restarted.json")) as f:
         return json.load(f)["cases"]
+
+
+def direct_manifest():
+    """DefaultDirect / Newton-with-default-solver fixtures (tests/golden/make_direct.py)."""
+    with open(os.path.join(GOLDEN, "manifest_direct.json")) as f:
+        return json.load(f)

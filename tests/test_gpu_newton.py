@@ -36,3 +36,41 @@ def test_newton_bratu_matches_reference(case):
     assert np.max(np.abs(h - d["hist"])) <= 1e-8 * d["hist"][0]
     if d["soln"].size:
         assert np.linalg.norm(st.soln() - d["soln"]) <= 1e-8 * np.linalg.norm(d["soln"])
+
+
+def test_default_direct_matches_reference():
+    """DefaultDirect (DefaultDirectSolver.py:22-74): spsolve's SuperLU factors applied on the device;
+    solution within 1e-10 relative of the reference's spsolve, same status conventions."""
+    import pysolvers_amd as psk
+    from conftest import direct_manifest, golden_matrix
+    for case in direct_manifest()["direct"]:
+        d = load_golden(case["file"])
+        A = golden_matrix(d)
+        st = psk.DefaultDirect().makeSolver().solve(A, d["b"])
+        assert st.success() and st.iters() is None and st.resid() is None and st.msg() == case["msg"]
+        assert np.linalg.norm(st.soln() - d["soln"]) <= 1e-10 * np.linalg.norm(d["soln"])
+        st2 = psk.DefaultDirect().makeSolver().solve(psk.DeviceCSR.from_scipy(A), d["b"])
+        assert np.array_equal(st2.soln(), st.soln())
+    import scipy.sparse as sp
+    bad = psk.DefaultDirect().makeSolver().solve(sp.csr_matrix((3, 3)), np.ones(3))   # singular: exception -> status
+    assert not bad.success() and bad.soln() is None and bad.msg().startswith("Default direct solve failed")
+
+
+def test_newton_default_solver_matches_reference():
+    """NewtonSolver(control) with no solver argument uses DefaultDirect, as the reference (Newton.py:13):
+    same Newton iteration count and success, history within 1e-8 ||F_0||, solution within 1e-8."""
+    import pysolvers_amd as psk
+    from conftest import direct_manifest
+    from pysolvers_amd.Nonlinear import NewtonSolver
+    from oracle import newton
+    for case in direct_manifest()["newton_direct"]:
+        d = load_golden(case["file"])
+        func = newton.Bratu2D(m=case["m"])
+        ns = NewtonSolver(control=psk.CommonSolverArgs(tau=1.0e-12, maxiter=10, showIters=False, showFinal=False))
+        hist = []
+        ns.reportIter = lambda it, nr, n0: hist.append(float(nr))
+        st = ns.solve(func, func.initialU())
+        assert st.iters() == case["iters"] and bool(st.success()) == case["success"]
+        h = np.array(hist)
+        assert len(h) == len(d["hist"]) and np.max(np.abs(h - d["hist"])) <= 1e-8 * d["hist"][0]
+        assert np.linalg.norm(st.soln() - d["soln"]) <= 1e-8 * np.linalg.norm(d["soln"])

@@ -131,3 +131,17 @@ def test_oracle_newton_matches_reference(case):
     assert np.array_equal(st["hist"], d["hist"])
     if d["soln"].size:
         assert np.array_equal(st["soln"], d["soln"])
+
+
+def test_oracle_newton_default_direct_matches_reference():
+    """NewtonSolver with its default linear solver (DefaultDirect: spsolve, Newton.py:13): the oracle
+    reproduces the reference's history, count and solution bit for bit (make_direct.py)."""
+    from conftest import direct_manifest
+    from oracle import newton
+    for case in direct_manifest()["newton_direct"]:
+        d = load_golden(case["file"])
+        m = case["m"]
+        st = newton.newton(newton.Bratu2D(m=m), np.ones(m * m), None, maxiter=10, tau=1e-12, direct=True)
+        assert st["iters"] == case["iters"] and bool(st["success"]) == case["success"]
+        np.testing.assert_allclose(st["hist"], d["hist"], rtol=1e-12, atol=0)
+        np.testing.assert_allclose(st["soln"], d["soln"], rtol=1e-12, atol=0)
