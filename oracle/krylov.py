@@ -72,14 +72,16 @@ def _status(success, iters, soln, resid, msg=None, hist=None):
 # ---------------------------------------------------------------------------
 # PCG  (PCGSolver.py:64-142)
 
-def pcg(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_apply, on_iter=None):
+def pcg(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_apply, on_iter=None,
+        norm=npla.norm):
     """on_iter(k): optional hook called at the top of iteration k (bench.py's cpu_baseline times
-    single iterations with it); it sees no solver state."""
+    single iterations with it); it sees no solver state. norm: CommonSolverArgs.norm, used where the
+    reference calls self.norm (IterativeSolver.py:86-88: PCGSolver.py:86 and :125)."""
     n, nc = A.shape
     assert n == nc                                   # :79-81
     assert n == len(b)                               # :83
     hist = []
-    normB = npla.norm(b)                             # :86 (IterativeSolver.norm -> npla.norm)
+    normB = norm(b)                                  # :86 (IterativeSolver.norm -> npla.norm)
     if normB == 0.0:                                 # :87-88 -> handleConvergence(0,...)
         return _status(True, 1, np.zeros_like(b), 0, hist=hist)
     r = np.copy(b)                                   # :97
@@ -102,7 +104,7 @@ def pcg(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_ap
         x = x + alpha * p                            # :121
         r = r - alpha * Ap                           # :122
         u = precond(r)                               # :123
-        normR = npla.norm(r)                         # :125
+        normR = norm(r)                              # :125
         hist.append(normR)
         if (normR <= tau * normB) or ((not fail_on_maxiter) and k == maxiter - 1):   # :129-131
             return _status(True, k + 1, x, normR, hist=hist)
@@ -139,12 +141,14 @@ def apply_givens_in_place(x, c, s, i):
 # GMRES (GMRESSolver.py:55-180), non-restarted, right preconditioned
 
 def gmres(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_apply,
-          return_internals=False):
+          return_internals=False, norm=npla.norm):
+    """norm: CommonSolverArgs.norm where the reference calls self.norm (GMRESSolver.py:66, :164); the
+    Arnoldi norms are npla.norm in the reference itself (:90, :115, :121)."""
     n, nc = A.shape
     assert n == nc                                       # :61
     assert n == len(b)                                   # :63
     hist = []
-    norm_b = npla.norm(b)                                # :66 (self.norm)
+    norm_b = norm(b)                                     # :66 (self.norm)
     if norm_b == 0.0:                                    # :67-68
         return _status(True, 1, np.zeros_like(b), 0, hist=hist)
     maxiters = maxiter                                   # :75
@@ -182,7 +186,7 @@ def gmres(A, b, maxiter=100, tau=1.0e-8, fail_on_maxiter=True, precond=identity_
             y = npla.solve(HBar[0:k + 1, 0:k + 1], g[0:k + 1])   # :159
             x = precond(np.dot(Q[:, 0:k + 1], y))        # :160
             resid = b - mvmult(A, x)                     # :163
-            norm_r_true = npla.norm(resid)               # :164
+            norm_r_true = norm(resid)                    # :164
             extra = dict(HBar=HBar[:k + 2, :k + 1].copy(), g=g[:k + 2].copy(), y=y) \
                 if return_internals else {}
             if norm_r_true <= tau * norm_b:              # :165-166 -> handleConvergence

@@ -59,6 +59,35 @@ int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
     return PSK_OK;
 }
 
+// The halo exchange on the second stream `cs`, after the work already enqueued on `s` (event ev_a);
+// ev_b marks its completion for the consumer (the next SpMV waits on it).
+int halo_exchange_async(psk_csr *A, double *x, hipStream_t s, hipStream_t cs, hipEvent_t ev_a, hipEvent_t ev_b) {
+    PSK_HIP(hipEventRecord(ev_a, s));
+    PSK_HIP(hipStreamWaitEvent(cs, ev_a, 0));
+    PSK_TRY(halo_exchange(A, x, cs));
+    PSK_HIP(hipEventRecord(ev_b, cs));
+    return PSK_OK;
+}
+
+// Overlap plan: true when every row sent to a peer lies in a prefix [0, lo*tile) or a suffix
+// [hi*tile, n) of the owned rows (contiguous sends: row blocks of banded matrices) and the middle
+// [lo, hi) is at least a quarter of the `nv` tiles, so that K3 can run the send tiles first.
+bool halo_split(const psk_csr *A, int64_t tile, int64_t nv, int64_t &lo, int64_t &hi) {
+    if (!A->comm || A->peers.empty() || A->comm->dry) return false;
+    int64_t pre = 0, suf = A->n;
+    for (const HaloPeer &p : A->peers) {
+        if (p.send_count == 0) continue;
+        if (p.send_idx) return false;
+        const int64_t b = p.send_begin, e = p.send_begin + p.send_count;
+        if (b == 0) pre = std::max(pre, e);
+        else if (e == A->n) suf = std::min(suf, b);
+        else return false;
+    }
+    lo = (pre + tile - 1) / tile;
+    hi = suf / tile;
+    return hi > lo && (hi - lo) * 4 >= nv;
+}
+
 int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipStream_t s) {
     if (!A->comm) return fail(PSK_ERR_ARG, "allgather on an unsharded matrix");
     if (A->comm->dry) return fail(PSK_ERR_UNSUPPORTED, "collective on a dry (RCCL-less) communicator");

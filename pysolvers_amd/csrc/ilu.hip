@@ -31,6 +31,7 @@
 #include "psk_internal.hpp"
 
 #include <algorithm>
+#include <unordered_map>
 #include <cstdlib>
 #include <vector>
 
@@ -701,6 +702,247 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
     }
 }
 
+// Grid: a factor whose dependencies, in solve order q, form a 2-D stencil: with q = y*w + x (w
+// positions per line), every off-diagonal entry of row q refers to q' = q - (yd*w + xd) with
+// 0 <= yd < 64 lines back and, for the skew sigma chosen by the host, ud = xd + sigma*yd >= 1 steps
+// back along u = x + sigma*y (the 5-point Gauss-Seidel factor triu(A): (0,1), (1,0), sigma = 1; an
+// SA coarse operator of a 2-D grid: up to 2 lines back with diagonal neighbours). One wave per band
+// of 64 lines; lane j owns line y0+j and all lanes advance together along u, so step s solves 64
+// rows that do not depend on each other; a dependency on the same band is a read of the LDS ring
+// holding the band's last `ring` steps (ring[(s mod ring)*64 + lane]); only lanes j < yd reach into
+// the band above, through the published values (pre-filled sentinel, agent-scope store / poll as
+// the other schedules), prefetched D steps ahead with everything else a step needs. The critical
+// path is the u range (w + sigma*H steps) plus one hand-off lag per band, instead of one hand-off
+// per dependency level. Per-row arithmetic is the band kernels': fma over the entries in stored
+// order from 0.0, then (b - acc) / diag, so results are bit-identical to the band schedule.
+constexpr int kGridLanes = 64;
+constexpr int kGridMaxRing = 256;   // rows of the LDS ring (<= 256 x 72 doubles)
+#ifdef PSK_GRID_PROF
+// development probe (tools/grid_probe.py): per band start / end s_memtime, waits and cycles waited
+__device__ unsigned long long g_grid_prof[8192 * 4];
+extern "C" int psk_grid_prof_read(unsigned long long *out, int nbands) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_grid_prof), sizeof(unsigned long long) * 4 * (size_t)nbands) ==
+                   hipSuccess ? 0 : -1;
+}
+#endif
+
+// Records of one step of a band: three contiguous 64-lane fields — K 16-bit pattern codes per lane,
+// K values per lane (stored entry order), the diagonal — so each field load is one contiguous access
+// (one 32-B record per lane, loaded as two 16-B halves, touched twice the cache lines and ran the
+// 5-point sweep 1.6x slower).
+template <int K>
+struct GridStep {
+    static constexpr int64_t kCode = 0;                                   // uint16 [64][K]
+    static constexpr int64_t kCoef = kGridLanes * 2 * K;                  // double [64][K]
+    static constexpr int64_t kDiag = kCoef + kGridLanes * 8 * K;          // double [64]
+    static constexpr int64_t kBytes = kDiag + kGridLanes * 8;
+};
+
+template <int K>
+struct GridSlot {
+    uint32_t code[K / 2];   // two 16-bit pattern codes per word
+    double cf[K], d, b;
+};
+
+// Two waves per band. The SOLVER wave (lanes = the band's 64 lines) advances along u. Its records
+// are stored in its access order — slot = (band * S_full + step) * 64 + lane — one 16-B-multiple
+// record per slot, so a step's records are one contiguous 64-lane stream, prefetched D steps ahead;
+// rhs and x stay in natural order (each lane walks its own line). The wave is bound by
+// how many memory operations it can keep in flight (vmcnt saturates at 63), so each step costs
+// about two of them. Dependencies come from ONE LDS ring of `ring` steps x RW = maxyd + 64 columns:
+// columns [0, maxyd) hold the band above's last maxyd lines, written by the POLLER wave as their
+// values get published (64 u-positions polled at a time, the ready prefix announced through an LDS
+// counter after every round trip), columns maxyd + j the solver's own lanes; a dependency (yd lines,
+// ud steps back) of lane j is column j - yd + maxyd of row (s - ud) mod ring whoever produced it. The
+// solver's waits are scalar LDS spins. Padding entries (value 0, code 0 = the lane's own column of
+// the current row: finite) add exactly +-0 to the fma chain. Per-row arithmetic is the band kernels':
+// fma over the entries in stored order from 0.0, then (b - acc) / diag — bit-identical results.
+template <int K, int D>
+__global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
+    int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t S_full, int upper, int pe, int maxyd, int ring_mask,
+    int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
+    GridExt ext) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    const int RW = maxyd + kGridLanes;
+    double *ring = reinterpret_cast<double *>(smem);                  // [ring][RW]
+    int64_t *ctl = reinterpret_cast<int64_t *>(ring + (size_t)(ring_mask + 1) * RW);
+    // ctl[0]: last u of the band above present in the ring (poller -> solver)
+    // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
+    const int tid = threadIdx.x, j = tid & 63;
+    const int64_t y0 = (int64_t)blockIdx.x * kGridLanes;
+    const int64_t ylast = (y0 + kGridLanes - 1 < H - 1) ? y0 + kGridLanes - 1 : H - 1;
+    const int64_t u_lo = sigma * y0, u_hi = (w - 1) + sigma * ylast;
+    const int S = (int)(u_hi - u_lo + 1);
+    int min_ud = 1 << 30, max_ud = 0;
+    for (int e = 0; e < pe; ++e) {
+        const int ud = ext.delta[e] >> 6;
+        min_ud = ud < min_ud ? ud : min_ud;
+        max_ud = ud > max_ud ? ud : max_ud;
+    }
+    const bool has_ext = blockIdx.x > 0 && pe > 0;
+    for (int i = tid; i < (ring_mask + 1) * RW; i += 2 * kGridLanes) ring[i] = 0.0;
+    if (tid == 0) {
+        ctl[0] = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;
+        ctl[1] = u_lo - 1;
+    }
+    __syncthreads();
+#ifdef PSK_GRID_PROF
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long n_wait = 0, c_wait = 0;
+#endif
+    if (tid >= kGridLanes) {
+        // ---------------- poller: u positions [u_lo - max_ud, u_hi - min_ud] of lines y0-maxyd .. y0-1
+        if (!has_ext) return;
+        const int64_t ua = u_lo - max_ud, ub = u_hi - min_ud;
+        for (int64_t base = ua; base <= ub; base += kGridLanes) {
+            const int64_t u = base + j;
+            double *row_slot = ring + (size_t)((u - u_lo) & ring_mask) * RW;
+            // ring capacity: row (u - u_lo) last held u - ring, which the solver reads until it passes
+            // that position + max_ud
+            int64_t spins = 0;
+            while (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                   base + kGridLanes - 1 - (ring_mask + 1) + max_ud) {
+                if (++spins > kMaxSpins) { atomicExch(err, (2 << 24) | (int)blockIdx.x); return; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            uint32_t pending = 0;   // lines of this lane's u still to fetch
+            for (int L = 0; L < maxyd; ++L) {
+                const int64_t yl = y0 - maxyd + L, xl = u - sigma * yl, q = yl * w + xl;
+                const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q < n;
+                if (valid) pending |= 1u << L;
+                else row_slot[L] = 0.0;
+            }
+            spins = 0;
+            while (true) {
+                for (int L = 0; L < maxyd; ++L)
+                    if (pending & (1u << L)) {
+                        const int64_t yl = y0 - maxyd + L, q = yl * w + (u - sigma * yl);
+                        const double v = load_pub(x + (upper ? n - 1 - q : q));
+                        if (!is_sentinel(v)) {
+                            row_slot[L] = v;
+                            pending &= ~(1u << L);
+                        }
+                    }
+                // ready prefix of this chunk: lanes 0..r-1 have every line
+                const uint64_t notready = __ballot(pending != 0);
+                const int r = notready ? __builtin_ctzll(notready) : kGridLanes;
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // ring writes before the announcement
+                if (j == 0 && r > 0)
+                    __hip_atomic_store(&ctl[0], base + r - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (!notready) break;
+                if (++spins > kMaxSpins) { atomicExch(err, (3 << 24) | (int)blockIdx.x); return; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        return;
+    }
+    // ---------------- solver
+    const int64_t y = y0 + j;
+    // lane j's line is active for steps [s_beg, s_end): x = s - sigma*j in [0, w_eff)
+    const int64_t w_eff = y < H ? (n - y * w < w ? n - y * w : w) : 0;
+    const int s_beg = (int)(sigma * j), s_end = (int)(sigma * j + (w_eff > 0 ? w_eff : 0));
+    // row of step s: rbase + rstep * s, q = y*w + s - sigma*j
+    const int64_t qb = y * w - sigma * j;
+    const int64_t rbase = upper ? n - 1 - qb : qb;
+    const int64_t rstep = upper ? -1 : 1;
+    const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
+                                 (int64_t)blockIdx.x * S_full * GridStep<K>::kBytes;
+    int64_t ext_known = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;   // uniform
+    auto fetch = [&](int s, GridSlot<K> &sl) {
+        const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
+        const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
+        const uint32_t *pc = reinterpret_cast<const uint32_t *>(st + GridStep<K>::kCode) + j * (K / 2);
+        if (K == 2) {
+            sl.code[0] = pc[0];
+        } else if (K == 4) {
+            const uint2 c = *reinterpret_cast<const uint2 *>(pc);
+            sl.code[0] = c.x;
+            sl.code[1] = c.y;
+        } else {
+            const uint4 c = *reinterpret_cast<const uint4 *>(pc);
+            sl.code[0] = c.x;
+            sl.code[1] = c.y;
+            sl.code[2] = c.z;
+            sl.code[3] = c.w;
+        }
+        const dv2 *pf = reinterpret_cast<const dv2 *>(st + GridStep<K>::kCoef) + j * (K / 2);
+#pragma unroll
+        for (int k = 0; k < K; k += 2) {
+            const dv2 c = pf[k / 2];
+            sl.cf[k] = c.x;
+            sl.cf[k + 1] = c.y;
+        }
+        sl.d = reinterpret_cast<const double *>(st + GridStep<K>::kDiag)[j];
+        const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);   // clamped into the line
+        sl.b = w_eff > 0 ? rhs[rbase + rstep * sa] : 0.0;
+    };
+    auto solve = [&](int s, const GridSlot<K> &sl) {
+        const int64_t u = u_lo + s;
+        if (has_ext && s < S && ext_known < u - min_ud) {   // uniform: the band above not yet in the ring
+#ifdef PSK_GRID_PROF
+            const unsigned long long tw = __builtin_amdgcn_s_memtime();
+#endif
+            int64_t spins = 0;
+            do {
+                ext_known = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (ext_known >= u - min_ud) break;
+                if (++spins > kMaxSpins) { atomicExch(err, (1 << 24) | (int)blockIdx.x); break; }
+                __builtin_amdgcn_s_sleep(1);
+            } while (true);
+#ifdef PSK_GRID_PROF
+            n_wait += 1;
+            c_wait += __builtin_amdgcn_s_memtime() - tw;
+#endif
+        }
+        double v[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {   // every LDS read first (one round trip)
+            const uint32_t c = (sl.code[k >> 1] >> (16 * (k & 1))) & 0xffff;
+            const int yd = c & 63, ud = c >> 6;
+            v[k] = ring[((s - ud) & ring_mask) * RW + (j + maxyd - yd)];
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc = fma(sl.cf[k], v[k], acc);   // stored order; padding adds +-0
+        double r = sl.b - acc;
+        if (!unit) r = r / sl.d;
+        ring[(s & ring_mask) * RW + maxyd + j] = r;
+        // the lines the band below reads are published; the others are read after the kernel
+        // (agent-scope stores on every lane: 732 -> 561 cycles per step plain, 5-point sweep)
+        if (s >= s_beg && s < s_end) {
+            if (j >= kGridLanes - maxyd) store_pub(x + rbase + rstep * s, r);
+            else x[rbase + rstep * s] = r;
+        }
+    };
+    GridSlot<K> buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) fetch(i, buf[i]);
+    for (int s0 = 0; s0 < S; s0 += D) {
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+            solve(s0 + i, buf[i]);
+            // the ring write of step s0+i precedes the next step's reads (one wave: LDS in order)
+            __asm__ volatile("" ::: "memory");
+            fetch(s0 + i + D, buf[i]);
+        }
+        if (j == 0)   // progress for the poller's ring capacity
+            __hip_atomic_store(&ctl[1], u_lo + s0 + D - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (j == 0) __hip_atomic_store(&ctl[1], INT64_MAX / 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#ifdef PSK_GRID_PROF
+    if (j == 0 && blockIdx.x < 8192) {
+        g_grid_prof[blockIdx.x * 4 + 0] = t_start;
+        g_grid_prof[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memtime();
+        g_grid_prof[blockIdx.x * 4 + 2] = n_wait;
+        g_grid_prof[blockIdx.x * 4 + 3] = c_wait;
+    }
+#endif
+}
+
+static size_t grid_lds_bytes(int ring, int maxyd) {
+    return (size_t)ring * (kGridLanes + maxyd) * sizeof(double) + 2 * sizeof(int64_t);
+}
+
 static size_t narrow_lds_bytes(int ring_words, int K) {
     return (size_t)ring_words * sizeof(double) +
            (size_t)kNarrowBufs * kNarrowChunk * ((2 * K + 2) * sizeof(double) + (K + 2) * sizeof(int32_t)) +
@@ -761,6 +1003,26 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const int32_t *ord = T.order;
         void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
         PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(kLdsThreads), args, (size_t)n * sizeof(double), s));
+        return PSK_OK;
+    }
+    if (T.schedule == kSchedGrid) {
+        if (rhs_idx) return fail(PSK_ERR_ARG, "grid schedule: gathered right-hand side (internal)");
+        const void *k = nullptr;
+#ifndef PSK_GRID_D
+#define PSK_GRID_D 12
+#endif
+        if (T.grid_K == 2) k = reinterpret_cast<const void *>(&sptrsv_grid_kernel<2, PSK_GRID_D>);
+        else if (T.grid_K == 4) k = reinterpret_cast<const void *>(&sptrsv_grid_kernel<4, (PSK_GRID_D > 8 ? 8 : PSK_GRID_D)>);
+        else if (T.grid_K == 8) k = reinterpret_cast<const void *>(&sptrsv_grid_kernel<8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D)>);
+        if (!k) return fail(PSK_ERR_ARG, "grid schedule: bad record width");
+        int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, sfull = T.grid_S;
+        int upper = T.upper ? 1 : 0, pe_ = T.grid_pe, myd = T.grid_maxyd, mask = T.grid_ring - 1;
+        int unit = T.diag ? 0 : 1;
+        const double *gr = T.gd_coef;
+        GridExt ext = T.grid_ext;
+        void *args[] = {&nn, &w, &H, &sg, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr, &ext};
+        const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
+        PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args, grid_lds_bytes(T.grid_ring, T.grid_maxyd), s));
         return PSK_OK;
     }
     if (T.schedule == kSchedBand && T.band_narrow) {
@@ -828,6 +1090,13 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     }
     const double *cur = v;                // current right-hand side
     const int32_t *cur_idx = M->gather_in;
+    const TriFactor &first = M->lo.present ? M->lo : M->up;
+    if (cur_idx && first.present && first.schedule == kSchedGrid) {   // the grid kernel reads rhs[row]
+        hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, cur, cur_idx, M->work + 2 * n);
+        PSK_HIP(hipGetLastError());
+        cur = M->work + 2 * n;
+        cur_idx = nullptr;
+    }
     if (M->lo.present) {
         PSK_TRY(launch_factor(c, n, M->lo, cur, cur_idx, y, M->err, s));
         cur = y;
@@ -853,12 +1122,13 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
     int32_t h = 0;
     PSK_HIP(hipMemcpyAsync(&h, M->err, 4, hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
-    if (h) return fail(PSK_ERR_HIP, "triangular solve: dependency wait exceeded its bound (not co-resident?)");
+    if (h) return fail(PSK_ERR_HIP, "triangular solve: dependency wait exceeded its bound (not co-resident?) code " +
+                                        std::to_string(h));
     return PSK_OK;
 }
 
 void TriFactor::release() {
-    void *ptrs[] = {rowptr, colidx, vals, diag, order, rec_row, rec_end, rec_c, rec_v, rec_d};
+    void *ptrs[] = {rowptr, colidx, vals, diag, order, rec_row, rec_end, rec_c, rec_v, rec_d, gd_code, gd_coef, gd_diag};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -1027,6 +1297,101 @@ void build_band(const HostFactor &F, int64_t B, int num_cus, int per_cu_max, int
     bd.est = tmax;
 }
 
+// Grid schedule plan (sptrsv_grid_kernel): width w = the most frequent solve-order distance >= 2
+// (the line length of a 2-D stencil), every dependency as (yd lines, xd positions) back, the
+// smallest skew sigma making ud = xd + sigma*yd >= 1 for all of them, and the ring depth. Rejected
+// (ok = false) when the factor is not such a stencil: wide rows (> 8 entries), a dependency 64 or
+// more lines back, a skew above 8, more than kGridMaxPE patterns reaching into the band above, a
+// ring deeper than kGridMaxRing, or too few dependencies at distance w to call it a grid.
+// fitted: FD 8192^2 Gauss-Seidel factor (8192 + 8191 steps) 5.0 ms, SA level 3 of it (2731 + 3*4095) 3.9 ms
+constexpr double kGridStepUs = 0.26, kGridLagUs = 2.0;
+constexpr int64_t kGridMaxYd = 8;   // lines of the band above held in the poller's LDS ring
+
+struct GridPlan {
+    bool ok = false;
+    int64_t w = 0, H = 0, sigma = 0;
+    int K = 0, pe = 0, maxyd = 0, ring = 0;
+    GridExt ext{};
+    double est = -1.0;
+};
+
+void plan_grid(const HostFactor &F, GridPlan &g) {
+    const int64_t n = F.n;
+    g = GridPlan();
+    if (n < 4096) return;
+    int32_t kmax = 0;
+    std::unordered_map<int64_t, int64_t> hist;
+    int64_t ndeps = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int32_t len = F.rp[i + 1] - F.rp[i];
+        kmax = std::max(kmax, len);
+        ndeps += len;
+        if (i % 7) continue;   // a sample is enough for the histogram
+        const int64_t p = F.pos(i);
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+            const int64_t d = p - F.pos(F.ci[j]);
+            if (d >= 2) hist[d]++;
+        }
+    }
+    if (kmax == 0 || kmax > 8) return;
+    int64_t w = 0, best = 0;
+    for (const auto &kv : hist)
+        if (kv.second > best || (kv.second == best && kv.first < w)) {
+            w = kv.first;
+            best = kv.second;
+        }
+    if (w < 2 || best * 7 * 8 < n) return;   // at least ~1/8 of the rows hold a distance-w entry
+    // patterns and skew
+    int64_t sigma = 0;
+    int64_t maxyd = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t p = F.pos(i), y = p / w, x = p % w;
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+            const int64_t pd = F.pos(F.ci[j]), yd = y - pd / w, xd = x - pd % w;
+            if (yd > kGridMaxYd) return;
+            maxyd = std::max(maxyd, yd);
+            if (yd >= 1 && xd < 1) sigma = std::max(sigma, (1 - xd + yd - 1) / yd);
+        }
+    }
+    if (sigma > 8) return;
+    int64_t maxud = 0;
+    std::vector<int32_t> ext_codes;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t p = F.pos(i), y = p / w, x = p % w;
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+            const int64_t pd = F.pos(F.ci[j]), yd = y - pd / w, xd = x - pd % w, ud = xd + sigma * yd;
+            if (ud < 1 || ud >= 1023) return;
+            maxud = std::max(maxud, ud);
+            const int32_t code = (int32_t)(ud * 64 + yd);
+            if (yd >= 1 && std::find(ext_codes.begin(), ext_codes.end(), code) == ext_codes.end()) {
+                if ((int)ext_codes.size() == kGridMaxPE) return;
+                ext_codes.push_back(code);
+            }
+        }
+    }
+    // ring rows: the deepest dependency, and room for the poller to stay a 64-position chunk ahead
+    int ring = ext_codes.empty() ? 1 : 2 * kGridLanes;
+    while (ring < maxud + 1 + (ext_codes.empty() ? 0 : kGridLanes)) ring <<= 1;
+    if (ring > kGridMaxRing) return;
+    g.ok = true;
+    g.w = w;
+    g.H = (n + w - 1) / w;
+    g.sigma = sigma;
+    g.K = kmax <= 2 ? 2 : (kmax <= 4 ? 4 : 8);
+    g.pe = (int)ext_codes.size();
+    g.maxyd = (int)maxyd;
+    g.ring = ring;
+    for (int e = 0; e < g.pe; ++e) {
+        const int32_t yd = ext_codes[e] & 63, ud = ext_codes[e] >> 6;
+        g.ext.delta[e] = ext_codes[e];
+        g.ext.yd[e] = yd;
+        g.ext.dq[e] = (int64_t)yd * w + (ud - sigma * yd);
+    }
+    const int64_t nbands = (g.H + kGridLanes - 1) / kGridLanes;
+    g.est = (double)((w - 1) + sigma * (g.H - 1) + 1) * kGridStepUs + (double)nbands * kGridLagUs;
+    (void)ndeps;
+}
+
 }  // namespace
 
 }  // namespace psk
@@ -1142,6 +1507,52 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         const char *le = std::getenv("PSK_TRISOLVE_LDS");
         if (T.est_lds_us < other && !(le && std::atoi(le) == 0)) T.schedule = kSchedLds;
     }
+    // grid schedule (2-D stencil factors): records in solve order
+    GridPlan gp;
+    plan_grid(F, gp);
+    T.est_grid_us = gp.ok ? gp.est : -1.0;
+    std::vector<uint16_t> gcode;
+    std::vector<double> gcoef, gdiag;
+    if (gp.ok) {
+        const char *ge = std::getenv("PSK_TRISOLVE_GRID");
+        const double cur = T.schedule == kSchedBand ? T.est_band_us
+                           : T.schedule == kSchedLds ? T.est_lds_us : T.est_syncfree_us;
+        if (gp.est < cur && !(ge && std::atoi(ge) == 0)) T.schedule = kSchedGrid;
+        T.grid_K = gp.K;
+        T.grid_pe = gp.pe;
+        T.grid_maxyd = gp.maxyd;
+        T.grid_ring = gp.ring;
+        T.grid_w = gp.w;
+        T.grid_H = gp.H;
+        T.grid_sigma = gp.sigma;
+        T.grid_ext = gp.ext;
+        // position p = (y*w + x): band b = y / 64, lane y % 64, step u - sigma*64b with u = x + sigma*y;
+        // one GridStep block per (band, step): codes (ud*64 + yd), values in stored order, diagonal.
+        // Padding: value 0, code 0 (the lane's own column of the current row); empty lanes: diagonal 1
+        // so the wave's unused results stay finite (padding entries read them times 0.0)
+        T.grid_S = (gp.w - 1) + gp.sigma * (kGridLanes - 1) + 1;
+        const int64_t SB = gp.K == 2 ? GridStep<2>::kBytes : gp.K == 4 ? GridStep<4>::kBytes : GridStep<8>::kBytes;
+        const int64_t nb = (gp.H + kGridLanes - 1) / kGridLanes, nsteps = nb * T.grid_S;
+        const int64_t oc = kGridLanes * 2 * gp.K, od = oc + kGridLanes * 8 * gp.K;
+        gcoef.assign((size_t)(nsteps * SB / 8), 0.0);
+        unsigned char *gb = reinterpret_cast<unsigned char *>(gcoef.data());
+        for (int64_t t = 0; t < nsteps; ++t)
+            for (int l = 0; l < kGridLanes; ++l) reinterpret_cast<double *>(gb + t * SB + od)[l] = 1.0;
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t p = F.pos(i), y = p / gp.w, x = p % gp.w, b = y / kGridLanes, l = y % kGridLanes;
+            const int64_t st = x + gp.sigma * y - gp.sigma * kGridLanes * b;
+            unsigned char *blk = gb + (b * T.grid_S + st) * SB;
+            uint16_t *codes = reinterpret_cast<uint16_t *>(blk) + l * gp.K;
+            double *vals = reinterpret_cast<double *>(blk + oc) + l * gp.K;
+            int k = 0;
+            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j, ++k) {
+                const int64_t pd = F.pos(F.ci[j]), yd = y - pd / gp.w, xd = x - pd % gp.w;
+                codes[k] = (uint16_t)((xd + gp.sigma * yd) * 64 + yd);
+                vals[k] = ova[j];
+            }
+            reinterpret_cast<double *>(blk + od)[l] = dg.empty() ? 1.0 : dg[i];
+        }
+    }
     T.present = true;
     T.upper = upper;
     T.nnz = (int64_t)F.ci.size();
@@ -1194,6 +1605,9 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.rec_c, rc_);
     if (rc == PSK_OK) rc = upload(&T.rec_v, rv);
     if (rc == PSK_OK) rc = upload(&T.rec_d, rd);
+    if (rc == PSK_OK) rc = upload(&T.gd_code, gcode);
+    if (rc == PSK_OK) rc = upload(&T.gd_coef, gcoef);
+    if (rc == PSK_OK) rc = upload(&T.gd_diag, gdiag);
     return rc;
 }
 
@@ -1220,7 +1634,7 @@ extern "C" int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, cons
     if (gather_out) gout.assign(gather_out, gather_out + n);
     if (rc == PSK_OK) rc = upload(&M->gather_in, gin);
     if (rc == PSK_OK) rc = upload(&M->gather_out, gout);
-    if (rc == PSK_OK && n > 0 && hipMalloc(&M->work, (size_t)(2 * n) * sizeof(double)) != hipSuccess)
+    if (rc == PSK_OK && n > 0 && hipMalloc(&M->work, (size_t)(3 * n) * sizeof(double)) != hipSuccess)
         rc = fail(PSK_ERR_ALLOC, "trisolve work");
     if (rc == PSK_OK && hipMalloc(&M->err, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_ALLOC, "trisolve err");
     if (rc == PSK_OK && hipMemset(M->err, 0, sizeof(int32_t)) != hipSuccess) rc = fail(PSK_ERR_HIP, "trisolve err");
@@ -1257,8 +1671,10 @@ extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t se
                                          "(more than 8 entries in a row or a level wider than a chunk)");
     if (set == kSchedLds && (M->n > kLdsMaxRows || M->n == 0))
         return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor too large for the LDS schedule");
-    if (set == kSchedSyncFree || set == kSchedBand || set == kSchedLds) T.schedule = set;
-    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1 or 2");
+    if (set == kSchedGrid && T.grid_K == 0)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor is not a 2-D stencil (grid schedule)");
+    if (set == kSchedSyncFree || set == kSchedBand || set == kSchedLds || set == kSchedGrid) T.schedule = set;
+    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1, 2 or 3");
     if (schedule) *schedule = T.schedule;
     if (blocks) *blocks = T.band_nblocks;
     if (ring_words) *ring_words = T.ring_words;

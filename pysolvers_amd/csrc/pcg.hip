@@ -148,14 +148,15 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
                                              double pTAp, double rr, double ur, PcgState *st,
                                              double *__restrict__ udr, double *__restrict__ hist, int64_t k,
-                                             int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta) {
+                                             int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
+                                             int64_t tile) {
     alpha = udr[k] / pTAp;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
-    if (blockIdx.x == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
+    if (tile == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
     if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
-        const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+        const int64_t i = tile * kVecTile + 2 * threadIdx.x;
         for (int64_t j = i; j < i + 2 && j < n; ++j) x[j] = x[j] + alpha * p[j];   // :121
-        if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (tile == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
             st->resid = normR;
             st->done = 1;
@@ -163,7 +164,7 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
         return false;
     }
     beta = ur / udr[k];                                      // :134-135
-    if (blockIdx.x == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
+    if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
     return true;
 }
 
@@ -173,14 +174,17 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ r, double *__restrict__ p,
     const double *__restrict__ dinv, double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts,
     PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter,
-    int fail_on_maxiter) {
+    int fail_on_maxiter, int64_t tile_base) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
+    // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
+    // halo exchange then overlaps the rest); tile 0 alone writes the solver state
+    const int64_t tile = tile_base + blockIdx.x;
     double alpha, beta;
     if (!pcg_direction_scalars(n, x, p, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
                                rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta))
+                               beta, tile))
         return;
-    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
     if (i + 1 < n) {
         const dv2 ro = ld2nt(r + i), po = ld2(p + i), xo = ld2nt(x + i);
@@ -260,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
     if (st->live != k) return;
     double alpha, beta;
     if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta))
+                               beta, blockIdx.x))
         return;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
     for (int64_t j = i; j < i + 2 && j < n; ++j) {
@@ -421,6 +425,20 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         return PSK_OK;
     };
 
+    // halo overlap (sharded, Jacobi/identity): when every row a neighbour needs lies in the first ov_lo
+    // or the last nv - ov_hi K3 tiles (row-block shards of a banded matrix: one grid line each side),
+    // those tiles run first and the exchange of p overlaps the remaining tiles of K3
+    int64_t ov_lo = 0, ov_hi = nv;
+    const bool overlap = sharded && !gen && halo_split(A, kVecTile, nv, ov_lo, ov_hi);
+    hipStream_t cs = nullptr;
+    hipEvent_t ev_k3a = nullptr, ev_halo = nullptr;
+    bool halo_pending = false;
+    if (overlap) {
+        PSK_TRY(comm_stream(c, &cs));
+        PSK_HIP(hipEventCreateWithFlags(&ev_k3a, hipEventDisableTiming));
+        PSK_HIP(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
+    }
+
     int64_t launched = 0;
     int rc = PSK_OK;
     for (int64_t k = 0; k < maxiter && rc == PSK_OK; ++k) {
@@ -437,7 +455,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             }
             if (rc != PSK_OK) break;
         }
-        if (A->comm && (rc = halo_exchange(A, w.p, s)) != PSK_OK) break;
+        if (halo_pending) {   // exchanged during the previous K3
+            if (hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess) { rc = fail(PSK_ERR_HIP, "halo wait"); break; }
+            halo_pending = false;
+        } else if (A->comm && (rc = halo_exchange(A, w.p, s)) != PSK_OK) {
+            break;
+        }
         int slot = (int)(k % TP);
         if (ctl->time_kernels) {
             if ((rc = harvest(slot)) != PSK_OK) break;
@@ -465,22 +488,39 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             hipLaunchKernelGGL(pcg_gen_direction_kernel, gk, dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, w.part2,
                                w.part3, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         } else {
-            if (jac == 2)
-                hipLaunchKernelGGL(pcg_direction_kernel<2>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
-                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
-                                   ctl->fail_on_maxiter);
-            else if (jac == 1)
-                hipLaunchKernelGGL(pcg_direction_kernel<1>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
-                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
-                                   ctl->fail_on_maxiter);
-            else
-                hipLaunchKernelGGL(pcg_direction_kernel<0>, gk, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
-                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
-                                   ctl->fail_on_maxiter);
+            auto k3 = [&](int64_t t0, int64_t t1) {   // K3 over tiles [t0, t1)
+                if (t1 <= t0) return;
+                const dim3 g3((unsigned)(t1 - t0));
+                if (jac == 2)
+                    hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                                       ctl->fail_on_maxiter, t0);
+                else if (jac == 1)
+                    hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                                       ctl->fail_on_maxiter, t0);
+                else
+                    hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                                       ctl->fail_on_maxiter, t0);
+            };
+            if (overlap && k + 1 < maxiter) {
+                // the tiles holding the rows the neighbours need first, then their halo exchange on the
+                // second stream while the other tiles run; the next SpMV waits for it
+                k3(0, ov_lo);
+                k3(ov_hi, nv);
+                if ((rc = halo_exchange_async(A, w.p, s, cs, ev_k3a, ev_halo)) != PSK_OK) break;
+                k3(ov_lo, ov_hi);
+                halo_pending = true;
+            } else {
+                k3(0, nv);
+            }
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
         launched = k + 1;
     }
+    // a halo exchange still in flight (the host stopped enqueueing first) completes before the end
+    if (halo_pending && hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess && rc == PSK_OK) rc = fail(PSK_ERR_HIP, "halo wait");
     if (rc == PSK_OK && hipEventRecord(ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
     PcgState hs{};
     if (rc == PSK_OK && hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess)
@@ -551,5 +591,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     (void)hipHostFree(hflag);
     (void)hipEventDestroy(ev0);
     (void)hipEventDestroy(ev1);
+    if (ev_k3a) (void)hipEventDestroy(ev_k3a);
+    if (ev_halo) (void)hipEventDestroy(ev_halo);
     return rc;
 }

@@ -64,8 +64,10 @@ struct Context {
     uint64_t *gs_gslots = nullptr;   // kMaxGrid * kGridSumMaxW
     std::vector<uint64_t *> gs_retired;
     int32_t *gs_err = nullptr;
+    hipStream_t comm_stream = nullptr;   // halo exchanges overlapped with compute (created lazily)
 };
 int ctx(Context **out);   // current device's context (created lazily)
+int comm_stream(Context *c, hipStream_t *out);
 
 // ---------------------------------------------------------------------------------------------
 // grow-only device buffer
@@ -163,8 +165,20 @@ struct AmgHierarchy;
 //    between levels; dependencies on earlier blocks are waited on through the published values;
 //    an LDS ring of `ring_words` doubles (0 = none) serves the in-block dependencies.
 //  * LDS: small factors (x fits LDS) solved by one workgroup, sync-free inside it with x in LDS.
-// `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds), chosen by host cost models.
-enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2 };
+//  * grid: factors whose dependencies form a 2-D stencil in solve order (grid_w positions per line,
+//    every dependency (lines back, positions back) within 63 lines and skewable by grid_sigma):
+//    one wave per band of 64 lines, all 64 lines advancing together along the skewed coordinate
+//    u = x + sigma y, in-band dependencies through an LDS ring of the last grid_ring steps, only
+//    the band above through published values (sptrsv_grid_kernel).
+// `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds / kSchedGrid), chosen by host
+// cost models.
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3 };
+constexpr int kGridMaxPE = 8;   // distinct dependency patterns reaching into the band above
+struct GridExt {
+    int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
+    int32_t yd[kGridMaxPE];     // lines back
+    int64_t dq[kGridMaxPE];     // solve-order distance yd * w + xd
+};
 struct TriFactor {
     bool present = false, upper = false;
     int64_t nnz = 0;
@@ -180,7 +194,14 @@ struct TriFactor {
     int64_t band_B = 0, band_nblocks = 0, band_levels = 0;
     int32_t ring_words = 0;
     bool band_narrow = false;   // band run by sptrsv_band_narrow_kernel (local levels <= one wave wide)
-    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0;
+    // grid records in solve order q: K pattern codes (uint16, 0xFFFF = padding) and K values per row
+    // (row-major, stored entry order), diagonal (nullptr = unit)
+    uint16_t *gd_code = nullptr;
+    double *gd_coef = nullptr, *gd_diag = nullptr;
+    int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
+    int64_t grid_w = 0, grid_H = 0, grid_sigma = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
+    GridExt grid_ext{};
+    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0;
     void release();
 };
 }  // namespace psk
@@ -505,6 +526,10 @@ inline int grid_for_rows(const Context *c, int64_t rows, int per_tile) {
 int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
 int from_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
 int halo_exchange(psk_csr *A, double *x_local, hipStream_t s);
+// the exchange on stream cs after the work enqueued on s (ev_a), completion recorded in ev_b
+int halo_exchange_async(psk_csr *A, double *x, hipStream_t s, hipStream_t cs, hipEvent_t ev_a, hipEvent_t ev_b);
+// rows sent to peers confined to the first lo / the tiles from hi on (of nv tiles of `tile` rows)
+bool halo_split(const psk_csr *A, int64_t tile, int64_t nv, int64_t &lo, int64_t &hi);
 // recv[q*count + i] = rank q's send[i]: no arithmetic, so every rank holds the same bits and
 // reduces them in rank order itself (RCCL's reduction order is algorithm- and rank-dependent)
 int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipStream_t s);

@@ -19,6 +19,13 @@ int fail(int code, const std::string &msg) {
 static std::mutex g_ctx_mu;
 static Context g_ctx[64];
 
+int comm_stream(Context *c, hipStream_t *out) {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if (c->comm_stream == nullptr) PSK_HIP(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    *out = c->comm_stream;
+    return PSK_OK;
+}
+
 int ctx(Context **out) {
     int dev = 0;
     PSK_HIP(hipGetDevice(&dev));

@@ -231,3 +231,60 @@ def test_lds_schedule_matches_syncfree(psk, n, dens):
     big = TriangularSolveChain(18433, L=sp.eye(18433, format="csr"))
     with pytest.raises(N.PskError):
         big.schedule("L", set="lds")
+
+
+def _grid_available(M, which):
+    from pysolvers_amd import _native as N
+    try:
+        M.schedule(which, set="grid")
+        return True
+    except N.PskError:
+        return False
+
+
+@pytest.mark.parametrize("m,lower", [(64, False), (300, False), (1024, False), (300, True)])
+def test_grid_schedule_fd_factors(psk, m, lower):
+    """The 2-D stencil (grid) schedule on triu(-FD2D) — the Gauss-Seidel smoother's factor
+    (ClassicSmoothers.py:33) — and on tril(-FD2D) (forward solve): eligible, within 1e-12 of
+    spsolve_triangular, and bit-identical to the band schedule (same per-row arithmetic)."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    T = (sp.tril(A) if lower else sp.triu(A)).tocsr()
+    v = np.random.default_rng(m).standard_normal(A.shape[0])
+    ref = spla.spsolve_triangular(T, v, lower=lower)
+    f = "L" if lower else "U"
+    M = TriangularSolveChain(A.shape[0], **({"L": T} if lower else {"U": T}))
+    assert _grid_available(M, f)
+    g = M.apply(v)
+    assert _rel(g, ref) <= 1e-12
+    assert np.array_equal(M.apply(v), g)                 # re-apply (sentinel refill), deterministic
+    M.schedule(f, set="band")
+    assert np.array_equal(M.apply(v), g)
+
+
+def test_grid_schedule_sa_coarse_operator(psk):
+    """An SA coarse operator of a 2-D grid (level 3 of the -FD 1024^2 hierarchy: 342 x 512 aggregate
+    lines, dependencies up to 2 lines back with diagonal neighbours): the grid schedule takes it, and
+    matches the band schedule bit for bit and spsolve_triangular to 1e-12; with a permuted input and
+    output (the pre-gather path) it matches the same solve done by numpy indexing."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear import SmoothedAggregationMLHierarchy, TriangularSolveChain
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 1024)
+    h = SmoothedAggregationMLHierarchy(A, numLevels=5)
+    A3 = h.matrix(3).tocsr()
+    U = sp.triu(A3).tocsr()
+    n = A3.shape[0]
+    v = np.random.default_rng(3).standard_normal(n)
+    ref = spla.spsolve_triangular(U, v, lower=False)
+    M = TriangularSolveChain(n, U=U)
+    assert _grid_available(M, "U")
+    g = M.apply(v)
+    assert _rel(g, ref) <= 1e-12
+    M.schedule("U", set="band")
+    assert np.array_equal(M.apply(v), g)
+    rng = np.random.default_rng(4)
+    pin, pout = rng.permutation(n).astype(np.int32), rng.permutation(n).astype(np.int32)
+    P = TriangularSolveChain(n, U=U, gather_in=pin, gather_out=pout)
+    assert _grid_available(P, "U")
+    assert np.array_equal(P.apply(v), M.apply(v[pin])[pout])

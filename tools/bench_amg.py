@@ -69,8 +69,11 @@ def main():
         info = S.schedule("U")
         out["fine_gs_schedule"] = info
         chosen = info["schedule"]
-        for sched in ("syncfree", "band"):
-            S.schedule("U", set=sched)
+        for sched in ("syncfree", "band", "grid"):
+            try:
+                S.schedule("U", set=sched)
+            except N.PskError:
+                continue
             S.apply(v)
             N.check(N.lib.psk_synchronize(), "sync")
             t3 = time.perf_counter()
@@ -98,6 +101,14 @@ def main():
         e = dict(level=k, n=M.levels()[k], op_ms=timed(op, vk))
         if args.smoother == "gs":
             e.update(op.schedule("U"), dep_levels=op.device_info()["levels_u"])
+            chosen = e["schedule"]
+            for sched in ("syncfree", "band", "grid"):
+                try:
+                    op.schedule("U", set=sched)
+                except N.PskError:
+                    continue
+                e["op_ms_" + sched] = timed(op, vk)
+            op.schedule("U", set=chosen)
         per.append(e)
     v0 = psk.DeviceVector.from_numpy(np.random.default_rng(0).standard_normal(M.levels()[0]))
     co = M._coarse
