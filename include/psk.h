@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PSK_ABI_VERSION 1
+#define PSK_ABI_VERSION 2
 
 /* return codes */
 #define PSK_OK               0
@@ -74,7 +74,7 @@ typedef struct psk_csr  psk_csr;    /* device CSR (int32 rowptr/colidx, f64 vals
 typedef struct psk_prec psk_prec;   /* formed preconditioner, library-owned */
 typedef struct psk_comm psk_comm;   /* RCCL communicator + rank geometry */
 
-/* CommonSolverArgs (IterativeSolver.py:42-57) minus the print/norm knobs. */
+/* CommonSolverArgs (IterativeSolver.py:42-57) minus the print knobs. */
 typedef struct psk_ctl {
     int64_t maxiter;          /* CommonSolverArgs.maxiter */
     double  tau;              /* relative residual tolerance */
@@ -82,6 +82,10 @@ typedef struct psk_ctl {
     int32_t restart;          /* GMRES only: 0 = reference non-restarted (Krylov dim = maxiter) */
     int32_t check_every;      /* host polls the device status every N iterations; 0 = auto */
     int32_t time_kernels;     /* 1 = HIP-event timing of the SpMV launches (psk_result.spmv_ms) */
+    double  norm_b;           /* GMRES: > 0 = ||b|| in the caller's norm (CommonSolverArgs.norm,
+                                 GMRESSolver.py:66) for the threshold tau*||b|| and psk_result.norm_b;
+                                 0 = the device 2-norm. PCG ignores it (a non-2-norm PCG is driven by
+                                 the host, IterativeSolver.py:86-88). Zero-initialise. */
 } psk_ctl;
 
 typedef struct psk_result {

@@ -11,9 +11,11 @@ Newton) are unchanged:
 * ``IterativeSolver``: maxiter/failOnMaxiter/tau/setTolerance/norm and the
   report* printers                                     (IterativeSolver.py:62-155)
 
-The device solvers always measure residuals in the Euclidean norm (the
-reference default, ``npla.norm``); a different ``norm`` callable is rejected
-rather than silently ignored.
+``norm`` may be any callable, as in the reference: the device loops use the
+Euclidean norm (``npla.norm``, the default) in-loop; another norm makes PCG run
+host-driven over the same device kernels (the norm of r is the caller's code,
+PCGSolver.py:86,125) and GMRES apply it to b and to the final true residual
+(GMRESSolver.py:66,164; its Arnoldi norms are npla.norm in the reference too).
 """
 import numpy.linalg as npla
 
@@ -97,11 +99,9 @@ class IterativeSolver(NamedObject):
     def norm(self, x):
         return self._control.norm(x)
 
-    def _check_norm(self):
-        if self._control.norm is not npla.norm:
-            raise NotImplementedError(
-                "%s: the device engine measures residuals in the 2-norm only "
-                "(CommonSolverArgs.norm must be numpy.linalg.norm)" % self.name())
+    def _custom_norm(self):
+        """True when CommonSolverArgs.norm is not numpy.linalg.norm (IterativeSolver.py:86-88)."""
+        return self._control.norm is not npla.norm
 
     # --- printing, same text as the reference ---------------------------------------------
     def reportIter(self, iter, normR, normR0):

@@ -81,10 +81,20 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         if not (isinstance(A, DeviceCSR) and A.comm is not None):
             assert n == nc                                   # PCGSolver.py:79-81
         assert n == len(b)                                   # PCGSolver.py:83
-        self._check_norm()
+        custom = self._custom_norm()
+        normb_caller = 0.0
+        if custom:
+            normb_caller = float(self.norm(_host_copy(b)))     # self.norm(b)  PCGSolver.py:86, GMRESSolver.py:66
+            if normb_caller == 0.0:                            # :87-88 / :67-68
+                x0 = np.zeros(n) if not isinstance(b, DeviceVector) else DeviceVector(n)
+                if isinstance(x0, DeviceVector):
+                    x0.zero()
+                return self.handleConvergence(0, x0, 0, 0)
         dA = self._device_matrix(A)
         if self.precond is None or not self.precFrozen():   # PCGSolver.py:92-94
             self.precond = self.precondType().form(dA)
+        if custom and self._entry == "psk_pcg":
+            return self._host_norm_pcg(dA, b, normb_caller)
         kind = getattr(self.precond, "device_kind", None)
         if kind is None:
             raise TypeError("%s: preconditioner %r has no device implementation; available: "
@@ -94,7 +104,8 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
 
         maxiter = int(self.maxiter())
         ctl = N.PskCtl(maxiter=maxiter, tau=float(self.tau()), fail_on_maxiter=int(bool(self.failOnMaxiter())),
-                       restart=int(self._restart()), check_every=0, time_kernels=int(bool(self.time_kernels)))
+                       restart=int(self._restart()), check_every=0, time_kernels=int(bool(self.time_kernels)),
+                       norm_b=normb_caller)
         res = N.PskResult()
         hist = np.zeros(max(maxiter, 1), dtype=np.float64)
         if isinstance(b, DeviceVector):
@@ -111,7 +122,85 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         fn = getattr(N.lib, self._entry)
         N.check(fn(dA.handle, ph, N.ptr(bp), N.ptr(x), ctypes.byref(ctl), ctypes.byref(res), N.ptr(hist), loc),
                 self._entry)
+        if custom and res.status in (N.PSK_CONVERGED, N.PSK_TRUE_RESID_FAIL) and res.hist_len == res.iters:
+            # GMRES stopped on its recursive residual: the true-residual test in the caller's norm
+            # (GMRESSolver.py:163-174): resid = b - A x on the device, its norm by the caller's code
+            rt = _host_copy(b) - _host_copy(spmv(dA, x))
+            nrt = float(self.norm(rt))
+            ok = nrt <= self.tau() * normb_caller
+            res.resid = nrt
+            res.status = N.PSK_CONVERGED if ok else N.PSK_TRUE_RESID_FAIL
+            res.success = int(ok)
+            res.msg = b"" if ok else (
+                "GMRES failure: true residual %12.5g did not meet tolerance tau=%12.5g. Recursive residual "
+                "was %12.5g." % (nrt, self.tau(), res.resid_recursive)).encode()
         return self._to_status(res, x, hist[:res.hist_len])
+
+    # -----------------------------------------------------------------------------------------
+    def _host_norm_pcg(self, dA, b, normB):
+        """PCG (PCGSolver.py:97-142) with a caller-supplied norm: the loop is driven from the host
+        over the device kernels (SpMV, dot, AXPY-type updates, preconditioner apply), because the
+        reference evaluates self.norm(r) every iteration (:125) and that is the caller's host code;
+        r is copied to the host for it. Same operation order and status conventions as psk_pcg."""
+        n = dA.n
+        dev_out = isinstance(b, DeviceVector)
+        prec = self.precond
+
+        def dot(u, v):
+            out = ctypes.c_double()
+            N.check(N.lib.psk_dot(n, u._p, v._p, N.PSK_DEVICE, ctypes.byref(out)), "psk_dot")
+            return out.value
+
+        def axpy(alpha, v, y):                     # y = y + alpha*v, two roundings (numpy)
+            N.check(N.lib.psk_axpy(n, float(alpha), v._p, y._p, N.PSK_DEVICE), "psk_axpy")
+
+        def copy(v):
+            y = DeviceVector(n)
+            y.zero()
+            axpy(1.0, v, y)
+            return y
+
+        def apply(v):                              # precond.applyRight, never aliasing its input
+            if getattr(prec, "device_kind", None) == N.PSK_PREC_IDENTITY:
+                return copy(v)
+            out = prec.applyRight(v)
+            return copy(out) if out is v else out
+
+        r = DeviceVector.from_numpy(_host_copy(b))                    # r = copy(b)  :97
+        p = apply(r)                                                  # :98
+        u = copy(p)                                                   # :99
+        x = DeviceVector(n)
+        x.zero()                                                      # :100
+        uDotR = dot(u, r)                                             # :102
+        if uDotR == 0.0:                                              # :104-105
+            return self.handleBreakdown(0, 'breakdown dot(u,r)==0')
+        k, normR = -1, None
+        hist = []
+        for k in range(self.maxiter()):                               # :109
+            Ap = spmv(dA, p)                                          # :111
+            pTAp = dot(p, Ap)                                         # :113
+            if pTAp == 0.0:                                           # :114-115
+                return self.handleBreakdown(k, 'breakdown dot(p, Ap)==0')
+            alpha = uDotR / pTAp                                      # :118
+            axpy(alpha, p, x)                                         # x = x + alpha*p  :121
+            axpy(-alpha, Ap, r)                                       # r = r - alpha*Ap  :122
+            u = apply(r)                                              # :123
+            normR = float(self.norm(r.numpy()))                       # :125
+            hist.append(normR)
+            self.reportIter(k, normR, normB)                          # :126
+            if normR <= self.tau() * normB or (not self.failOnMaxiter() and k == self.maxiter() - 1):
+                st = self.handleConvergence(k, x if dev_out else x.numpy(), normR, normB)   # :129-131
+                st.info = dict(status="converged", hist=np.array(hist), norm_b=normB, host_driven=True)
+                return st
+            newUDotR = dot(u, r)                                      # :134
+            beta = newUDotR / uDotR                                   # :135
+            uDotR = newUDotR                                          # :136
+            axpy(beta, p, u)                                          # p = u + beta*p  :138
+            p = u
+        st = self.handleMaxiter(max(k, 0), x if dev_out else x.numpy(), normR, normB)   # :142
+        st.info = dict(status="maxiter", hist=np.array(hist), norm_b=normB, host_driven=True)
+        return st
+
 
     def _to_status(self, res, x, hist):
         normB = res.norm_b
@@ -129,6 +218,15 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
                        loop_ms=res.loop_ms, spmv_ms=res.spmv_ms, spmv_launches=res.spmv_launches,
                        resid_recursive=res.resid_recursive, norm_b=normB)
         return st
+
+
+def _host_copy(v):
+    """A host ndarray of a vector given as ndarray, DeviceVector or CUDA tensor."""
+    if isinstance(v, DeviceVector):
+        return v.numpy()
+    if is_device_vector(v):
+        return v.detach().cpu().numpy()
+    return np.asarray(v, dtype=np.float64)
 
 
 def mvmult(A, x):

@@ -12,6 +12,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"))
 
 PSK_OK = 0
+ABI_VERSION = 2          # include/psk.h PSK_ABI_VERSION (psk_ctl gained norm_b in 2)
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_HOST, PSK_DEVICE = 0, 1
 PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
@@ -25,7 +26,7 @@ STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOW
 class PskCtl(ctypes.Structure):
     _fields_ = [("maxiter", ctypes.c_int64), ("tau", ctypes.c_double),
                 ("fail_on_maxiter", ctypes.c_int32), ("restart", ctypes.c_int32),
-                ("check_every", ctypes.c_int32), ("time_kernels", ctypes.c_int32)]
+                ("check_every", ctypes.c_int32), ("time_kernels", ctypes.c_int32), ("norm_b", ctypes.c_double)]
 
 
 class PskResult(ctypes.Structure):
@@ -150,8 +151,8 @@ def _load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.psk_abi_version() != 1:
-        raise ImportError("libpsk ABI version mismatch")
+    if lib.psk_abi_version() != ABI_VERSION:
+        raise ImportError("libpsk ABI version mismatch (library %d, bindings %d)" % (lib.psk_abi_version(), ABI_VERSION))
     return lib
 
 

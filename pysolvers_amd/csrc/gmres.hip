@@ -49,14 +49,16 @@ __global__ __launch_bounds__(kBlock) void gm_selfdot_kernel(int64_t n, const dou
 __global__ __launch_bounds__(kBlock) void gm_start_kernel(int64_t n, const double *__restrict__ r0,
                                                           double *__restrict__ q0, const double *__restrict__ part,
                                                           int np, double *__restrict__ g, int Kp1, GmresState *st,
-                                                          double tau, int first) {
+                                                          double tau, int first, double normb_caller) {
     __shared__ double sh[kWaves];
     const double bb = reduce_partials(part, np, 1, sh);
     const double beta = sqrt(bb);
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (first) {
-            st->normB = beta;                  // self.norm(b)  :66  (== npla.norm(r0) since r0 = b)
-            st->tauNormB = tau * beta;
+            // self.norm(b)  :66: == npla.norm(r0) since r0 = b, or the caller's norm of b
+            const double nb = normb_caller > 0.0 ? normb_caller : beta;
+            st->normB = nb;
+            st->tauNormB = tau * nb;
             st->zero_b = beta == 0.0;
             if (beta == 0.0) st->done = 1;     // :67-68
         }
@@ -346,12 +348,12 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
         if (first) {
             hipLaunchKernelGGL(gm_selfdot_kernel, dim3(gv), dim3(kBlock), 0, s, n, bv, pa);
             hipLaunchKernelGGL(gm_start_kernel, dim3(gv), dim3(kBlock), 0, s, n, bv, Q, pa, gv, g, ld, st,
-                               ctl->tau, 1);
+                               ctl->tau, 1, ctl->norm_b);
         } else {
             if ((rc = launch_spmv(A, kSpmvResid, x, u, nullptr, bv, pa, nullptr, s)) != PSK_OK) break;
             ++spmv_count;
             hipLaunchKernelGGL(gm_start_kernel, dim3(gv), dim3(kBlock), 0, s, n, u, Q, pa, gs, g, ld, st,
-                               ctl->tau, 0);
+                               ctl->tau, 0, 0.0);
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "gmres start"); break; }
         if (first && n > 0) {

@@ -34,7 +34,7 @@ def test_library_exports_all_symbols():
 
 def test_library_basic_calls_without_gpu():
     from pysolvers_amd import _native as N
-    assert N.lib.psk_abi_version() == 1
+    assert N.lib.psk_abi_version() == 2
     n = N.device_count()
     assert n >= 0
     assert isinstance(N.lib.psk_last_error(), bytes)
@@ -42,8 +42,8 @@ def test_library_basic_calls_without_gpu():
 
 def test_struct_layout_matches_header():
     from pysolvers_amd import _native as N
-    # psk_ctl: int64, double, 4 x int32 ; psk_result: see include/psk.h
-    assert ctypes.sizeof(N.PskCtl) == 32
+    # psk_ctl: int64, double, 4 x int32, double ; psk_result: see include/psk.h
+    assert ctypes.sizeof(N.PskCtl) == 40
     # psk_result: 2 x int32, int64, 5 x double, 2 x int64, char[256]
     assert N.PskResult.msg.offset == 4 + 4 + 8 + 5 * 8 + 2 * 8
     assert ctypes.sizeof(N.PskResult) == 72 + 256

@@ -382,3 +382,60 @@ def test_ilut_apply_large_fd():
     v = np.random.default_rng(9).standard_normal(A.shape[0])
     ref = M.ILU().solve(v)
     assert np.linalg.norm(M.applyRight(v) - ref) <= 1e-12 * np.linalg.norm(ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# CommonSolverArgs.norm other than numpy.linalg.norm (IterativeSolver.py:86-88)
+
+def _inf_norm(v):
+    return np.linalg.norm(v, np.inf)
+
+
+def _one_norm(v):
+    return np.abs(v).sum()
+
+
+@pytest.mark.parametrize("case,norm", [("pcg_dh10_identity.npz", _inf_norm), ("pcg_fd32_identity.npz", _one_norm),
+                                       ("pcg_fd64_jacobi.npz", _inf_norm)])
+def test_pcg_caller_norm_matches_oracle(psk, case, norm):
+    """A caller-supplied norm (PCGSolver.py:86 ||b||, :125 ||r|| every iteration): the host-driven loop
+    over the device kernels takes the oracle's iteration count; residual history within 1e-10 of the
+    norm of b, solution within 1e-10."""
+    from oracle import krylov
+    d = load_golden(case)
+    A = golden_matrix(d)
+    prec = "jacobi" if "jacobi" in case else "identity"
+    ctl = _ctl(maxiter=4000, tau=1e-8, norm=norm)
+    st = psk.PCG(control=ctl, precond=product_prec_type(psk, prec)).makeSolver().solve(A, d["b"])
+    ref = krylov.pcg(A, d["b"], maxiter=4000, tau=1e-8, precond=oracle_prec(A, prec), norm=norm)
+    assert st.iters() == ref["iters"] and bool(st.success()) == bool(ref["success"])
+    nb = norm(d["b"])
+    assert len(st.info["hist"]) == len(ref["hist"])
+    assert np.max(np.abs(st.info["hist"] - ref["hist"])) <= 1e-10 * nb
+    assert np.linalg.norm(st.soln() - ref["soln"]) <= 1e-10 * np.linalg.norm(ref["soln"])
+
+
+@pytest.mark.parametrize("case", ["gmres_dh8_identity.npz", "gmres_fd16_jacobi.npz"])
+def test_gmres_caller_norm_matches_oracle(psk, case):
+    """GMRES with a caller-supplied norm: threshold tau * norm(b) (GMRESSolver.py:66) and the true
+    residual test norm(b - A x) (:164) in that norm; the Arnoldi norms stay npla.norm (:90, :115, :121)."""
+    from oracle import krylov
+    d = load_golden(case)
+    A = golden_matrix(d)
+    prec = "jacobi" if "jacobi" in case else "identity"
+    for norm, tau in ((_inf_norm, 1e-8), (_one_norm, 1e-9)):
+        ctl = _ctl(maxiter=300, tau=tau, norm=norm)
+        st = psk.GMRES(control=ctl, precond=product_prec_type(psk, prec)).makeSolver().solve(A, d["b"])
+        ref = krylov.gmres(A, d["b"], maxiter=300, tau=tau, precond=oracle_prec(A, prec), norm=norm)
+        assert st.iters() == ref["iters"] and bool(st.success()) == bool(ref["success"])
+        assert np.max(np.abs(st.info["hist"] - ref["hist"])) <= 1e-10 * np.linalg.norm(d["b"])
+        assert abs(st.resid() - ref["resid"]) <= 1e-10 * norm(d["b"])
+        assert np.linalg.norm(st.soln() - ref["soln"]) <= 1e-10 * np.linalg.norm(ref["soln"])
+
+
+def test_caller_norm_zero_rhs(psk):
+    d = load_golden("pcg_dh8_identity.npz")
+    A = golden_matrix(d)
+    for f in (psk.PCG, psk.GMRES):
+        st = f(control=_ctl(maxiter=50, norm=_inf_norm)).makeSolver().solve(A, np.zeros(A.shape[0]))
+        assert st.success() and st.iters() == 1 and not np.any(st.soln())
