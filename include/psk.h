@@ -204,8 +204,12 @@ int psk_prec_create_amg(int32_t num_levels, psk_csr *const *A, psk_csr *const *P
 /* Schedule of factor `which` (0 = L, 1 = U) of a triangular-solve chain: 0 = sync-free (one wave per
  * row, global dependency levels), 1 = band (one workgroup per block of the solve order, local levels
  * behind barriers, LDS ring of ring_words doubles), 2 = LDS (factors of at most 18432 rows: one
- * workgroup, sync-free inside it with x in LDS). The library picks the fastest by host cost models
- * (est_*_us); set = 0 / 1 / 2 forces one, -1 only queries. Any out pointer may be NULL. */
+ * workgroup, sync-free inside it with x in LDS), 3 = grid (2-D stencil factors: one wave per band of
+ * 64 lines advancing along a skewed coordinate), 4 = part (rows cut into strips of their natural
+ * index, one workgroup per CU, in-strip dependencies through LDS; its layout is built when chosen or
+ * when PSK_TRISOLVE_PART=1 at creation). The library picks the fastest by host cost models
+ * (est_*_us); set = 0..4 forces one (PSK_ERR_UNSUPPORTED when the factor has no such layout), -1 only
+ * queries. Any out pointer may be NULL. */
 int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t *schedule, int64_t *blocks,
                                int32_t *ring_words, double *est_syncfree_us, double *est_band_us);
 /* kind, size and triangular-solve shape of a preconditioner (any out pointer may be NULL). */

@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <unordered_map>
+#include <cstdio>
 #include <cstdlib>
 #include <vector>
 
@@ -307,6 +308,231 @@ __global__ __launch_bounds__(kLdsThreads) void sptrsv_lds_kernel(int64_t n, cons
     __syncthreads();
     for (int64_t i = tid; i < n; i += kLdsThreads) x[i] = __longlong_as_double((long long)xs[i]);
 }
+
+// Partitioned (sptrsv_part_kernel): the rows are cut into P strips of the NATURAL index (the
+// matrix's own numbering before the factorisation's permutations: for ILU the original equation /
+// unknown of every factor row), one strip per workgroup of 16 waves, one workgroup per CU. A strip of
+// a mesh-like matrix is a band of the mesh, so most dependencies of its rows are rows of the same
+// strip: those hand-offs go through LDS (~0.1 us) instead of a device-scope store seen by a polling
+// load (~1 us). Each workgroup runs its rows in ASAP order (earliest finish under the cost model,
+// host-computed: a topological order), dealt round-robin to its waves; every wave runs the sync-free
+// row pipeline above. Entry codes: c >= 0 = another strip's row, read from x with the sentinel
+// protocol; c < 0 = the strip's own row at local position qd = -c-1, read from an LDS cache of
+// kPartSlots results (slot qd mod kPartSlots) whose tag is the local position it holds. Rows write x
+// (the output) and the cache; the tag goes to kPartWriting while a slot is rewritten, so a reader
+// that sees the same tag before and after reading the value has that row's value, a newer tag means
+// the slot was reused (the value is then read from x), an older one that the row is not done. Same
+// per-row arithmetic as sync-free (same entry order, lane partials, wave_sum), so bit-identical to it.
+// Progress: all P workgroups are co-resident (cooperative launch); the globally ASAP-first unsolved
+// row has all its dependencies solved and every earlier row of its wave is ASAP-earlier.
+constexpr int kPartThreads = 1024;
+constexpr int kPartWaves = kPartThreads / 64;
+constexpr int kPartSlots = 8192;                // 64 KiB of values + 32 KiB of tags
+constexpr int32_t kPartPad = INT32_MIN;         // padding lane
+constexpr int32_t kPartEmpty = -1, kPartWriting = -2;
+constexpr size_t kPartLds = (size_t)kPartSlots * (sizeof(double) + sizeof(int32_t));
+
+// Every load of the row pipeline is unconditional (clamped positions, entry arrays padded by
+// kPartPadEntries on the host, the right-hand side pre-gathered): a load under a divergent branch
+// makes the compiler wait for ALL outstanding loads (vmcnt(0)) at the join, which would serialise
+// the prefetch of the next rows behind this row's dependency polls.
+#ifdef PSK_PART_PROF
+// development probe: [0] wave cycles, [1] local-wait cycles, [2] remote-wait cycles, [3] rows,
+// [4] local waits, [5] remote waits, [6] slot reuses, [7] max wave cycles (summed over the launch)
+__device__ unsigned long long g_part_prof[8];
+extern "C" int psk_part_prof_read(unsigned long long *out) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_part_prof), sizeof(g_part_prof)) != hipSuccess) return -1;
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_part_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#define PART_PROF(...) __VA_ARGS__
+#else
+#define PART_PROF(...)
+#endif
+constexpr int kPtChunks = 2;   // 64-entry chunks of a row held in registers (4 rows in flight per wave)
+constexpr int kPartPadEntries = 64 * kPtChunks;
+struct PtBody {
+    int32_t row, s, e, c[kPtChunks];
+    double v[kPtChunks], b, d;
+};
+
+template <bool UNIT>
+__global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
+    const int64_t *__restrict__ seg, const int32_t *__restrict__ krp, const int32_t *__restrict__ kcode,
+    const double *__restrict__ kva, const double *__restrict__ diag, const double *__restrict__ rhs, double *x,
+    int32_t *err, const int32_t *__restrict__ krow) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    // LDS accesses are workgroup-scope relaxed atomics: ds_read / ds_write in program order, no waits
+    // between them (a wave's LDS operations execute in issue order)
+    uint64_t *sv = reinterpret_cast<uint64_t *>(smem);
+    int32_t *st = reinterpret_cast<int32_t *>(smem + kPartSlots * sizeof(double));
+    auto ld_tag = [&](int32_t s) { return __hip_atomic_load(st + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); };
+    auto ld_val = [&](int32_t s) {
+        return __longlong_as_double((long long)__hip_atomic_load(sv + s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    };
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t wave = tid >> 6;
+    for (int i = tid; i < kPartSlots; i += kPartThreads) st[i] = kPartEmpty;   // before the barrier: plain
+    __syncthreads();
+    const int64_t base = seg[blockIdx.x], R = seg[blockIdx.x + 1] - base;
+    if (wave >= R) return;
+    PART_PROF(const unsigned long long pt0 = clock64(); unsigned long long plw = 0, prw = 0, pnl = 0, pnr = 0, pev = 0;)
+    auto head = [&](int64_t q, SfHead &h) {   // q >= R: a valid position whose row is never used
+        const int64_t k = base + (q < R ? q : R - 1);
+        h.row = krow[k];
+        h.s = krp[k];
+        h.e = krp[k + 1];
+    };
+    auto body = [&](const SfHead &h, PtBody &b) {
+        b.row = h.row;
+        b.s = h.s;
+        b.e = h.e;
+#pragma unroll
+        for (int j = 0; j < kPtChunks; ++j) {
+            const int32_t idx = h.s + 64 * j + lane;   // < nnz + kPartPadEntries
+            const int32_t c = kcode[idx];
+            b.v[j] = kva[idx];
+            b.c[j] = idx < h.e ? c : kPartPad;
+        }
+        b.b = rhs[h.row];
+        b.d = UNIT ? 1.0 : diag[h.row];
+    };
+    // an entry's x value: bits/t1/v/t2 are its first reads (issued together for the whole row)
+    auto resolve = [&](int32_t c, uint64_t bits, int32_t t1, double v, int32_t t2) -> double {
+        if (c >= 0) {
+            const double xv = __longlong_as_double((long long)bits);
+            return is_sentinel(xv) ? wait_pub(x + c, err) : xv;
+        }
+        const int32_t qd = ~c, slot = qd & (kPartSlots - 1);   // ~c == -c-1
+        int64_t spins = 0;
+        PART_PROF(const unsigned long long w0 = clock64(); if (!(t1 == qd && t2 == qd)) pnl++;)
+        while (!(t1 == qd && t2 == qd)) {
+            if (t1 > qd || t1 == qd) {
+                PART_PROF(pev++;)
+                return wait_pub(x + krow[base + qd], err);   // slot reused: x has it
+            }
+            if (++spins > kMaxSpins) {
+                atomicExch(err, 2);
+                return 0.0;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            t1 = ld_tag(slot);
+            v = ld_val(slot);
+            t2 = ld_tag(slot);
+        }
+        PART_PROF(plw += clock64() - w0;)
+        return v;
+    };
+    // Software pipeline over the wave's rows u = 0, 1, ... (position wave + u*W): in iteration u the
+    // wave issues the first x polls of row u+1, the entries of row u+3 and the header of row u+5, then
+    // resolves row u. Every load a step waits for was issued at least one iteration earlier and the
+    // polls go out first, so (loads completing in order) resolving row u waits only for its own polls
+    // and what was issued two iterations before: a wave keeps ~3 rows of loads in flight and a row
+    // whose dependencies are done costs no memory round trip of its own. Rings: bodies and headers 4,
+    // polls 2; the loop is unrolled by 4 so every ring index is a constant.
+    auto poll = [&](const PtBody &b, uint64_t *bits) {   // first polls of the remote entries
+#pragma unroll
+        for (int j = 0; j < kPtChunks; ++j)
+            bits[j] = __hip_atomic_load(reinterpret_cast<const uint64_t *>(x + (b.c[j] >= 0 ? b.c[j] : 0)),
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    constexpr int64_t W = kPartWaves;
+    SfHead H[4];
+    PtBody B[4];
+    uint64_t P[2][kPtChunks];
+    head(wave, H[0]);
+    head(wave + W, H[1]);
+    head(wave + 2 * W, H[2]);
+    body(H[0], B[0]);
+    body(H[1], B[1]);
+    body(H[2], B[2]);
+    head(wave + 3 * W, H[3]);
+    head(wave + 4 * W, H[0]);
+    poll(B[0], P[0]);
+    for (int64_t q0 = wave; q0 < R; q0 += 4 * W) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int64_t q = q0 + t * W;
+            if (q >= R) break;
+            poll(B[(t + 1) & 3], P[(t + 1) & 1]);   // row u+1 (entries issued two iterations ago)
+            body(H[(t + 3) & 3], B[(t + 3) & 3]);   // row u+3 (header issued two iterations ago)
+            head(q + 5 * W, H[(t + 1) & 3]);         // row u+5
+            const PtBody &cur = B[t];
+            const uint64_t *pc = P[t & 1];
+            double acc = 0.0;
+#pragma unroll
+            for (int j = 0; j < kPtChunks; ++j) {
+                const int32_t c = cur.c[j];
+                if (c == kPartPad) continue;
+                double xv;
+                if (c >= 0) {
+                    xv = __longlong_as_double((long long)pc[j]);
+                    if (is_sentinel(xv)) {
+                        PART_PROF(const unsigned long long w0 = clock64(); pnr++;)
+                        xv = wait_pub(x + c, err);
+                        PART_PROF(prw += clock64() - w0;)
+                    }
+                } else {
+                    const int32_t slot = ~c & (kPartSlots - 1);
+                    const int32_t t1 = ld_tag(slot);
+                    const double v = ld_val(slot);
+                    const int32_t t2 = ld_tag(slot);
+                    xv = resolve(c, 0, t1, v, t2);
+                }
+                acc = fma(cur.v[j], xv, acc);
+            }
+            for (int32_t b0 = cur.s + 64 * kPtChunks; b0 < cur.e; b0 += 64 * kSfTail) {   // long rows
+                int32_t tc[kSfTail];
+                double tv[kSfTail];
+#pragma unroll
+                for (int u = 0; u < kSfTail; ++u) {
+                    const int32_t idx = b0 + 64 * u + lane;
+                    tc[u] = idx < cur.e ? kcode[idx] : kPartPad;
+                    tv[u] = idx < cur.e ? kva[idx] : 0.0;
+                }
+#pragma unroll
+                for (int u = 0; u < kSfTail; ++u)
+                    if (tc[u] != kPartPad) {
+                        const int32_t c = tc[u], slot = ~c & (kPartSlots - 1);
+                        const uint64_t bt = c >= 0 ? __hip_atomic_load(reinterpret_cast<const uint64_t *>(x + c),
+                                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                                   : 0;
+                        const int32_t a1 = c < 0 ? ld_tag(slot) : 0;
+                        const double vv = c < 0 ? ld_val(slot) : 0.0;
+                        const int32_t a2 = c < 0 ? ld_tag(slot) : 0;
+                        acc = fma(tv[u], resolve(c, bt, a1, vv, a2), acc);
+                    }
+            }
+            const double sum = wave_sum(acc);
+            if (lane == 0) {
+                double r = cur.b - sum;
+                if (!UNIT) r = r / cur.d;
+                store_pub(x + cur.row, r);
+                const int32_t slot = (int32_t)(q & (kPartSlots - 1));
+                __hip_atomic_store(st + slot, kPartWriting, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(sv + slot, (uint64_t)__double_as_longlong(r), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_store(st + slot, (int32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    }
+#ifdef PSK_PART_PROF
+    unsigned long long vals[6] = {clock64() - pt0, plw, prw, pnl, pnr, pev};
+    for (int i = 0; i < 6; ++i)
+        for (int o = 32; o > 0; o >>= 1) vals[i] = max(vals[i], (unsigned long long)__shfl_xor((long long)vals[i], o));
+    if (lane == 0) {
+        atomicAdd(&g_part_prof[0], vals[0]);
+        atomicAdd(&g_part_prof[1], vals[1]);
+        atomicAdd(&g_part_prof[2], vals[2]);
+        atomicAdd(&g_part_prof[4], vals[3]);
+        atomicAdd(&g_part_prof[5], vals[4]);
+        atomicAdd(&g_part_prof[6], vals[5]);
+        atomicMax(&g_part_prof[7], vals[0]);
+        atomicAdd(&g_part_prof[3], (unsigned long long)((R - wave + kPartWaves - 1) / kPartWaves));
+    }
+#endif
+}
+
 
 // Band: workgroup g takes blocks g, g+G, ... in solve order. Position of row i in solve order: i
 // (lower) or n-1-i (upper); block b = positions [b*B, (b+1)*B). The block's rows come as a RECORD
@@ -1005,6 +1231,17 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(kLdsThreads), args, (size_t)n * sizeof(double), s));
         return PSK_OK;
     }
+    if (T.schedule == kSchedPart) {
+        if (rhs_idx) return fail(PSK_ERR_ARG, "part schedule: gathered right-hand side (internal)");
+        const void *k = dg ? reinterpret_cast<const void *>(&sptrsv_part_kernel<false>)
+                           : reinterpret_cast<const void *>(&sptrsv_part_kernel<true>);
+        const int64_t *sg = T.part_seg;
+        const int32_t *prp = T.part_rp, *pc = T.part_code, *prow = T.part_row;
+        const double *pv = T.part_va;
+        void *args[] = {&sg, &prp, &pc, &pv, &dg, &rhs, &x, &err, &prow};
+        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(T.part_P), dim3(kPartThreads), args, (unsigned)kPartLds, s));
+        return PSK_OK;
+    }
     if (T.schedule == kSchedGrid) {
         if (rhs_idx) return fail(PSK_ERR_ARG, "grid schedule: gathered right-hand side (internal)");
         const void *k = nullptr;
@@ -1091,7 +1328,7 @@ int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     const double *cur = v;                // current right-hand side
     const int32_t *cur_idx = M->gather_in;
     const TriFactor &first = M->lo.present ? M->lo : M->up;
-    if (cur_idx && first.present && first.schedule == kSchedGrid) {   // the grid kernel reads rhs[row]
+    if (cur_idx && first.present && (first.schedule == kSchedGrid || first.schedule == kSchedPart)) {   // rhs[row]
         hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, cur, cur_idx, M->work + 2 * n);
         PSK_HIP(hipGetLastError());
         cur = M->work + 2 * n;
@@ -1128,7 +1365,8 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
 }
 
 void TriFactor::release() {
-    void *ptrs[] = {rowptr, colidx, vals, diag, order, rec_row, rec_end, rec_c, rec_v, rec_d, gd_code, gd_coef, gd_diag};
+    void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,
+                    rec_d,  gd_code, gd_coef, gd_diag, part_seg, part_rp, part_code, part_row, part_va};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -1398,6 +1636,69 @@ void plan_grid(const HostFactor &F, GridPlan &g) {
 
 using namespace psk;
 
+// Partitioned schedule (sptrsv_part_kernel). Strip of row i: its natural index nat[i] cut into P
+// equal ranges; strip s runs on workgroup (s % 8) * (P / 8) + s / 8, so neighbouring strips share an
+// XCD (dispatch deals workgroups round-robin over the 8 XCDs). Cost model (us, provisional until
+// measured): a dependency inside the strip a, across strips b, a row c on its wave.
+constexpr double kPartLocalUs = 0.10, kPartRemoteUs = 1.2, kPartRowUs = 0.15;
+
+struct PartPlan {
+    int P = 0;
+    double est = -1.0;
+    std::vector<int32_t> wg, lpos;   // workgroup and local position of every row
+    std::vector<int64_t> seg;        // P + 1
+};
+
+void plan_part(const HostFactor &F, const std::vector<int32_t> &nat, int P, PartPlan &pp) {
+    const int64_t n = F.n;
+    pp.P = P;
+    pp.wg.assign(n, 0);
+    const int per = std::max(1, P / 8);
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t s = (nat.empty() ? i : nat[i]) * P / n;
+        pp.wg[i] = (P % 8 == 0) ? (int32_t)((s % 8) * per + s / 8) : (int32_t)s;
+    }
+    // ASAP finish times in solve order (a topological order)
+    std::vector<double> fin(n, 0.0);
+    for (int64_t p = 0; p < n; ++p) {
+        const int64_t i = F.row(p);
+        double t = 0.0;
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j)
+            t = std::max(t, fin[F.ci[j]] + (pp.wg[F.ci[j]] == pp.wg[i] ? kPartLocalUs : kPartRemoteUs));
+        fin[i] = t + kPartRowUs;
+    }
+    // every workgroup's rows in ASAP order (ties: solve order)
+    std::vector<int32_t> idx(n);
+    for (int64_t i = 0; i < n; ++i) idx[i] = (int32_t)i;
+    std::sort(idx.begin(), idx.end(), [&](int32_t u, int32_t v) {
+        if (pp.wg[u] != pp.wg[v]) return pp.wg[u] < pp.wg[v];
+        if (fin[u] != fin[v]) return fin[u] < fin[v];
+        return F.pos(u) < F.pos(v);
+    });
+    pp.seg.assign((size_t)P + 1, 0);
+    pp.lpos.assign(n, 0);
+    for (int64_t k = 0; k < n; ++k) pp.seg[(size_t)pp.wg[idx[k]] + 1]++;
+    for (int w = 0; w < P; ++w) pp.seg[w + 1] += pp.seg[w];
+    for (int64_t k = 0; k < n; ++k) pp.lpos[idx[k]] = (int32_t)(k - pp.seg[pp.wg[idx[k]]]);
+    // simulate: rows in global ASAP order, wave lpos % 16 of their workgroup
+    std::sort(idx.begin(), idx.end(), [&](int32_t u, int32_t v) { return fin[u] != fin[v] ? fin[u] < fin[v] : F.pos(u) < F.pos(v); });
+    std::vector<double> done(n, 0.0), wfree((size_t)P * kPartWaves, 0.0);
+    double tmax = 0.0;
+    for (int64_t k = 0; k < n; ++k) {
+        const int32_t i = idx[k];
+        double &wf = wfree[(size_t)pp.wg[i] * kPartWaves + pp.lpos[i] % kPartWaves];
+        double t = wf;
+        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+            const int32_t d = F.ci[j];
+            const bool loc = pp.wg[d] == pp.wg[i] && pp.lpos[i] - pp.lpos[d] < kPartSlots;
+            t = std::max(t, done[d] + (loc ? kPartLocalUs : kPartRemoteUs));
+        }
+        done[i] = wf = t + kPartRowUs;
+        tmax = std::max(tmax, done[i]);
+    }
+    pp.est = tmax;
+}
+
 template <class T>
 static int upload(T **d, const std::vector<T> &h) {
     if (h.empty()) {
@@ -1450,7 +1751,7 @@ static int check_perm(int64_t n, const int32_t *p, const char *what) {
 
 // Build, schedule and upload one factor.
 static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int32_t *ci, const double *va, bool upper,
-                       bool unit, TriFactor &T) {
+                       bool unit, const std::vector<int32_t> &nat, TriFactor &T) {
     HostFactor F;
     F.n = n;
     F.upper = upper;
@@ -1553,6 +1854,55 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
             reinterpret_cast<double *>(blk + od)[l] = dg.empty() ? 1.0 : dg[i];
         }
     }
+    // partitioned schedule: planned for factors too large for one CU and not solved by the grid
+    // schedule (PSK_TRISOLVE_PART=0 disables it, =1 builds it and selects it whatever the estimate)
+    std::vector<int64_t> pseg;
+    std::vector<int32_t> prp, pcode, prow;
+    std::vector<double> pva;
+    {
+        const char *pe = std::getenv("PSK_TRISOLVE_PART");
+        const bool force = pe && std::atoi(pe) == 1, off = pe && std::atoi(pe) == 0;
+        if (!off && n > kLdsMaxRows && (T.schedule != kSchedGrid || force) && n >= (int64_t)c->num_cus * kPartWaves) {
+            PartPlan pp;
+            plan_part(F, nat, c->num_cus, pp);
+            T.est_part_us = pp.est;
+            const double cur = T.schedule == kSchedBand ? T.est_band_us
+                               : T.schedule == kSchedLds  ? T.est_lds_us
+                               : T.schedule == kSchedGrid ? T.est_grid_us
+                                                          : T.est_syncfree_us;
+            if (force || pp.est < cur) {
+                T.schedule = kSchedPart;
+                T.part_P = pp.P;
+                pseg = pp.seg;
+                prow.assign(n, 0);
+                prp.assign((size_t)n + 1, 0);
+                for (int64_t i = 0; i < n; ++i) {
+                    const int64_t k = pp.seg[pp.wg[i]] + pp.lpos[i];
+                    prow[k] = (int32_t)i;
+                    prp[k + 1] = F.rp[i + 1] - F.rp[i];
+                }
+                for (int64_t k = 0; k < n; ++k) prp[k + 1] += prp[k];
+                pcode.assign(F.ci.size() + kPartPadEntries, 0);   // padding: the kernel's unconditional loads
+                pva.assign(F.ci.size() + kPartPadEntries, 0.0);
+                for (int64_t k = 0; k < n; ++k) {
+                    const int32_t i = prow[k];
+                    int32_t o = prp[k];
+                    for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j, ++o) {
+                        const int32_t d = F.ci[j];
+                        const bool loc = pp.wg[d] == pp.wg[i] && pp.lpos[i] - pp.lpos[d] < kPartSlots;
+                        pcode[o] = loc ? ~pp.lpos[d] : d;   // ~q = -q-1 < 0: the strip's q-th row
+                        pva[o] = ova[j];
+                    }
+                }
+            }
+        }
+    }
+    if (const char *ve = std::getenv("PSK_TRISOLVE_VERBOSE"))   // development: the cost model's view
+        if (std::atoi(ve))
+            std::fprintf(stderr, "psk trisolve %s n=%lld levels=%lld est_us syncfree=%.0f band=%.0f lds=%.0f grid=%.0f "
+                                 "part=%.0f -> schedule %d\n",
+                         upper ? "U" : "L", (long long)n, (long long)nlev, T.est_syncfree_us, T.est_band_us,
+                         T.est_lds_us, T.est_grid_us, T.est_part_us, T.schedule);
     T.present = true;
     T.upper = upper;
     T.nnz = (int64_t)F.ci.size();
@@ -1608,6 +1958,11 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.gd_code, gcode);
     if (rc == PSK_OK) rc = upload(&T.gd_coef, gcoef);
     if (rc == PSK_OK) rc = upload(&T.gd_diag, gdiag);
+    if (rc == PSK_OK) rc = upload(&T.part_seg, pseg);
+    if (rc == PSK_OK) rc = upload(&T.part_rp, prp);
+    if (rc == PSK_OK) rc = upload(&T.part_code, pcode);
+    if (rc == PSK_OK) rc = upload(&T.part_row, prow);
+    if (rc == PSK_OK) rc = upload(&T.part_va, pva);
     return rc;
 }
 
@@ -1627,8 +1982,16 @@ extern "C" int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, cons
     M->kind = PSK_PREC_ILU;
     M->n = n;
     int rc = PSK_OK;
-    if (l_rowptr) rc = make_factor(c, n, l_rowptr, l_colidx, l_vals, false, l_unit != 0, M->lo);
-    if (rc == PSK_OK && u_rowptr) rc = make_factor(c, n, u_rowptr, u_colidx, u_vals, true, u_unit != 0, M->up);
+    // natural index of every factor row (the partitioned schedule's strips): L row r solves equation
+    // gather_in[r]; U row gather_out[i] gives unknown i
+    std::vector<int32_t> nat_l, nat_u;
+    if (gather_in) nat_l.assign(gather_in, gather_in + n);
+    if (gather_out) {
+        nat_u.assign(n, 0);
+        for (int64_t i = 0; i < n; ++i) nat_u[gather_out[i]] = (int32_t)i;
+    }
+    if (l_rowptr) rc = make_factor(c, n, l_rowptr, l_colidx, l_vals, false, l_unit != 0, nat_l, M->lo);
+    if (rc == PSK_OK && u_rowptr) rc = make_factor(c, n, u_rowptr, u_colidx, u_vals, true, u_unit != 0, nat_u, M->up);
     std::vector<int32_t> gin, gout;
     if (gather_in) gin.assign(gather_in, gather_in + n);
     if (gather_out) gout.assign(gather_out, gather_out + n);
@@ -1673,8 +2036,11 @@ extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t se
         return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor too large for the LDS schedule");
     if (set == kSchedGrid && T.grid_K == 0)
         return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: factor is not a 2-D stencil (grid schedule)");
-    if (set == kSchedSyncFree || set == kSchedBand || set == kSchedLds || set == kSchedGrid) T.schedule = set;
-    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1, 2 or 3");
+    if (set == kSchedPart && T.part_P == 0)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: partitioned layout not built for this factor "
+                                         "(built when chosen, or with PSK_TRISOLVE_PART=1 at creation)");
+    if (set >= kSchedSyncFree && set <= kSchedPart) T.schedule = set;
+    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1, 2, 3 or 4");
     if (schedule) *schedule = T.schedule;
     if (blocks) *blocks = T.band_nblocks;
     if (ring_words) *ring_words = T.ring_words;

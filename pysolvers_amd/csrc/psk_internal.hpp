@@ -170,9 +170,12 @@ struct AmgHierarchy;
 //    one wave per band of 64 lines, all 64 lines advancing together along the skewed coordinate
 //    u = x + sigma y, in-band dependencies through an LDS ring of the last grid_ring steps, only
 //    the band above through published values (sptrsv_grid_kernel).
-// `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds / kSchedGrid), chosen by host
+//  * part: rows cut into strips of their natural index, one workgroup per strip (per CU), the
+//    strip's own dependencies through an LDS cache, the others through published values
+//    (sptrsv_part_kernel).
+// `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds / kSchedGrid / kSchedPart), chosen by host
 // cost models.
-enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3 };
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4 };
 constexpr int kGridMaxPE = 8;   // distinct dependency patterns reaching into the band above
 struct GridExt {
     int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
@@ -201,7 +204,12 @@ struct TriFactor {
     int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
     int64_t grid_w = 0, grid_H = 0, grid_sigma = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
     GridExt grid_ext{};
-    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0;
+    // part layout: position k = part_seg[w] + q (workgroup w's q-th row); rows, entries (codes) in it
+    int64_t *part_seg = nullptr;
+    int32_t *part_rp = nullptr, *part_code = nullptr, *part_row = nullptr;
+    double *part_va = nullptr;
+    int part_P = 0;
+    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0;
     void release();
 };
 }  // namespace psk
