@@ -92,6 +92,11 @@ struct SfBody {
 
 constexpr int kSfTail = 4;
 
+// Row total of the sync-free family (sync-free, LDS, partitioned kernels: the same function, so the
+// three give identical bits): the DPP wave total (psk_internal.hpp), ~130 cycles on the dependency
+// chain where a butterfly of ds_bpermute shuffles took ~700 (tools/part_micro.py trace, FD chain).
+__device__ __forceinline__ double row_total(double v) { return wave_total(v); }
+
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
                                                         const int32_t *__restrict__ kci, const double *__restrict__ kva,
                                                         const double *__restrict__ diag, const double *__restrict__ rhs,
@@ -173,7 +178,7 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
                     acc = fma(tv[t], xv, acc);
                 }
         }
-        const double sum = wave_sum(acc);
+        const double sum = row_total(acc);
         if (lane == 0) {
             double r = cur.b - sum;
             if (diag) r = r / cur.d;
@@ -296,7 +301,7 @@ __global__ __launch_bounds__(kLdsThreads) void sptrsv_lds_kernel(int64_t n, cons
                         acc = fma(tv[u], tb[u] == kSentinel ? lds_wait(tc[u]) : __longlong_as_double((long long)tb[u]),
                                   acc);
             }
-            const double sum = wave_sum(acc);
+            const double sum = row_total(acc);
             if (lane == 0) {
                 double r = cur.b - sum;
                 if (diag) r = r / cur.d;
@@ -322,7 +327,7 @@ __global__ __launch_bounds__(kLdsThreads) void sptrsv_lds_kernel(int64_t n, cons
 // (the output) and the cache; the tag goes to kPartWriting while a slot is rewritten, so a reader
 // that sees the same tag before and after reading the value has that row's value, a newer tag means
 // the slot was reused (the value is then read from x), an older one that the row is not done. Same
-// per-row arithmetic as sync-free (same entry order, lane partials, wave_sum), so bit-identical to it.
+// per-row arithmetic as sync-free (same entry order, lane partials, row_total), so bit-identical to it.
 // Progress: all P workgroups are co-resident (cooperative launch); the globally ASAP-first unsolved
 // row has all its dependencies solved and every earlier row of its wave is ASAP-earlier.
 constexpr int kPartThreads = 1024;
@@ -344,6 +349,12 @@ extern "C" int psk_part_prof_read(unsigned long long *out) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_part_prof), sizeof(g_part_prof)) != hipSuccess) return -1;
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_part_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+// per-position stamps (s_memtime) of the first 2^17 positions: [2k] dependencies resolved, [2k+1] result stored
+__device__ unsigned long long g_part_trace[2 << 17];
+extern "C" int psk_part_trace_read(unsigned long long *out, int64_t n) {
+    if (n > (1 << 17)) n = 1 << 17;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_part_trace), (size_t)n * 16) == hipSuccess ? 0 : -1;
 }
 #define PART_PROF(...) __VA_ARGS__
 #else
@@ -459,27 +470,63 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
             head(q + 5 * W, H[(t + 1) & 3]);         // row u+5
             const PtBody &cur = B[t];
             const uint64_t *pc = P[t & 1];
+            // x values of the row's register chunks: remote ones from the early polls, local ones from
+            // the LDS cache, polled by the whole wave until every local entry is present (the spin's
+            // control flow is uniform); reused slots and unpublished remote values then wait on x
+            double xv[kPtChunks];
+            bool pend[kPtChunks];
+#pragma unroll
+            for (int j = 0; j < kPtChunks; ++j) {
+                xv[j] = 0.0;   // remote values are read from the polls only below (no wait for them here)
+                pend[j] = cur.c[j] < 0 && cur.c[j] != kPartPad;   // local, not yet read
+            }
+            PART_PROF(const unsigned long long w0 = clock64(); bool waited = false;)
+            for (int64_t spins = 0;; ++spins) {
+                bool left = false;
+#pragma unroll
+                for (int j = 0; j < kPtChunks; ++j)
+                    if (pend[j]) {
+                        const int32_t qd = ~cur.c[j], slot = qd & (kPartSlots - 1);
+                        const int32_t t1 = ld_tag(slot);
+                        const double v = ld_val(slot);
+                        const int32_t t2 = ld_tag(slot);
+                        if (t1 == qd && t2 == qd) {
+                            xv[j] = v;
+                            pend[j] = false;
+                        } else if (t1 >= qd) {   // slot reused (or being rewritten): x holds the value
+                            xv[j] = wait_pub(x + krow[base + qd], err);
+                            pend[j] = false;
+                            PART_PROF(pev++;)
+                        } else {
+                            left = true;
+                        }
+                    }
+                if (!__any(left)) break;
+                if (spins > kMaxSpins) {
+                    if (lane == 0) atomicExch(err, 2);
+                    break;
+                }
+                PART_PROF(waited = true;)
+#ifndef PSK_PART_SLEEP
+#define PSK_PART_SLEEP 1
+#endif
+                __builtin_amdgcn_s_sleep(PSK_PART_SLEEP);
+            }
+            PART_PROF(if (waited) { plw += clock64() - w0; pnl++; })
             double acc = 0.0;
 #pragma unroll
             for (int j = 0; j < kPtChunks; ++j) {
                 const int32_t c = cur.c[j];
                 if (c == kPartPad) continue;
-                double xv;
                 if (c >= 0) {
-                    xv = __longlong_as_double((long long)pc[j]);
-                    if (is_sentinel(xv)) {
-                        PART_PROF(const unsigned long long w0 = clock64(); pnr++;)
-                        xv = wait_pub(x + c, err);
-                        PART_PROF(prw += clock64() - w0;)
+                    xv[j] = __longlong_as_double((long long)pc[j]);
+                    if (is_sentinel(xv[j])) {
+                        PART_PROF(const unsigned long long w1 = clock64(); pnr++;)
+                        xv[j] = wait_pub(x + c, err);
+                        PART_PROF(prw += clock64() - w1;)
                     }
-                } else {
-                    const int32_t slot = ~c & (kPartSlots - 1);
-                    const int32_t t1 = ld_tag(slot);
-                    const double v = ld_val(slot);
-                    const int32_t t2 = ld_tag(slot);
-                    xv = resolve(c, 0, t1, v, t2);
                 }
-                acc = fma(cur.v[j], xv, acc);
+                acc = fma(cur.v[j], xv[j], acc);
             }
             for (int32_t b0 = cur.s + 64 * kPtChunks; b0 < cur.e; b0 += 64 * kSfTail) {   // long rows
                 int32_t tc[kSfTail];
@@ -503,7 +550,8 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
                         acc = fma(tv[u], resolve(c, bt, a1, vv, a2), acc);
                     }
             }
-            const double sum = wave_sum(acc);
+            PART_PROF(const unsigned long long tr0 = clock64();)
+            const double sum = row_total(acc);
             if (lane == 0) {
                 double r = cur.b - sum;
                 if (!UNIT) r = r / cur.d;
@@ -513,6 +561,10 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
                 __hip_atomic_store(sv + slot, (uint64_t)__double_as_longlong(r), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_store(st + slot, (int32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                PART_PROF(if (base + q < (1 << 17)) {
+                    g_part_trace[2 * (base + q)] = tr0;
+                    g_part_trace[2 * (base + q) + 1] = clock64();
+                })
             }
         }
     }

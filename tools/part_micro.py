@@ -31,6 +31,8 @@ def main():
     from pysolvers_amd.Linear import TriangularSolveChain
     cases = [("chain1", 65536, (1,)), ("chain64", 1 << 20, (64,)), ("chain64+1", 1 << 18, (1, 64)),
              ("chain256", 1 << 22, (256,))]
+    if os.environ.get("PART_MICRO_CASES"):
+        cases = [c for c in cases if c[0] in os.environ["PART_MICRO_CASES"].split(",")]
     for name, n, offs in cases:
         L = factor(n, offs)
         os.environ["PSK_TRISOLVE_PART"] = "1"
@@ -53,6 +55,22 @@ def main():
             out[sched + "_ms"] = sorted(ts)[1]
             out[sched + "_us_per_level"] = out[sched + "_ms"] * 1e3 / levels
         out["bit_identical"] = bool(np.array_equal(res["part"], res["syncfree"]))
+        if hasattr(N.lib, "psk_part_trace_read") and n <= (1 << 17):   # -DPSK_PART_PROF build
+            import ctypes
+            M.schedule("L", set="part")
+            M.apply(v)
+            N.check(N.lib.psk_synchronize(), "sync")
+            tr = np.zeros(2 * n, np.uint64)
+            N.lib.psk_part_trace_read(tr.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(n))
+            t0, t1 = tr[0::2].astype(np.int64), tr[1::2].astype(np.int64)
+            # natural order == position order for these factors when strips are not permuted; use rows
+            # inside one strip (positions base..base+R) where consecutive rows are consecutive hops
+            R = n // 256
+            k = np.arange(1, R)
+            wg0 = np.arange(R)   # workgroup 0's positions (strip 0)
+            out["trace_compute_cycles_median"] = float(np.median(t1[wg0] - t0[wg0]))
+            out["trace_handoff_cycles_median"] = float(np.median(t0[k] - t1[k - 1]))
+            out["trace_row_period_cycles_median"] = float(np.median(t1[k] - t1[k - 1]))
         print(json.dumps(out), flush=True)
 
 
