@@ -1429,11 +1429,12 @@ void TriFactor::release() {
 namespace {
 
 // Cost model (us), fitted to measurements on MI355X (tools/bench_amg.py, tools/bench_gmres.py):
-// sync-free: a row costs one agent-scope load round trip (~0.85) on its wave, plus a hand-off (~0.5)
-// after its last dependency was published (FD m=1024 ILU: 1.34 us per level); band: a local level
+// sync-free: a row costs one agent-scope load round trip (~0.61) on its wave, plus a hand-off (~0.36)
+// after its last dependency was published (FD m=1024 ILU with the DPP row total: 0.96 us per level,
+// 12.1 ms for L + U); band: a local level
 // costs ~0.9 us with the ring (it is paced by the one external load of the block's boundary row;
 // FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
-constexpr double kHopUs = 0.5, kRowUs = 0.85, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
+constexpr double kHopUs = 0.36, kRowUs = 0.61, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
 constexpr double kLdsLevelUs = 0.15, kLdsBytesPerUs = 40e3;   // LDS schedule (provisional)
 constexpr double kNarrowLevelUs = 0.8;    // narrow band local level (FD 8192^2 Gauss-Seidel: 12.6 ms / 16128 levels)
 
@@ -1690,9 +1691,17 @@ using namespace psk;
 
 // Partitioned schedule (sptrsv_part_kernel). Strip of row i: its natural index nat[i] cut into P
 // equal ranges; strip s runs on workgroup (s % 8) * (P / 8) + s / 8, so neighbouring strips share an
-// XCD (dispatch deals workgroups round-robin over the 8 XCDs). Cost model (us, provisional until
-// measured): a dependency inside the strip a, across strips b, a row c on its wave.
-constexpr double kPartLocalUs = 0.10, kPartRemoteUs = 1.2, kPartRowUs = 0.15;
+// XCD (dispatch deals workgroups round-robin over the 8 XCDs). Two cost models (us): the PRIORITY
+// model orders each strip's rows (ASAP finish times: a dependency inside the strip a, across strips
+// b, a row c), the ESTIMATE model simulates the resulting schedule with constants fitted to MI355X
+// measurements of the kernel (tools/ilu_probe.py, tools/part_micro.py: a wave's row costs ~0.5 us
+// of issue and memory latency even when its dependencies are done; an LDS hand-off ~0.2 us
+// including the row total and division; a published-value hand-off between CUs ~2 us under load).
+// Strips longer than kPartMaxStrip rows measured slower than sync-free (FD 2896^2 ILUT: 32.8k rows
+// per strip, 31.4 vs ~27 ms) and are not planned.
+constexpr double kPartPrioLocalUs = 0.10, kPartPrioRemoteUs = 1.2, kPartPrioRowUs = 0.15;
+constexpr double kPartEstLocalUs = 0.20, kPartEstRemoteUs = 2.0, kPartEstRowUs = 0.5;
+constexpr int64_t kPartMaxStrip = 16384;
 
 struct PartPlan {
     int P = 0;
@@ -1716,8 +1725,8 @@ void plan_part(const HostFactor &F, const std::vector<int32_t> &nat, int P, Part
         const int64_t i = F.row(p);
         double t = 0.0;
         for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j)
-            t = std::max(t, fin[F.ci[j]] + (pp.wg[F.ci[j]] == pp.wg[i] ? kPartLocalUs : kPartRemoteUs));
-        fin[i] = t + kPartRowUs;
+            t = std::max(t, fin[F.ci[j]] + (pp.wg[F.ci[j]] == pp.wg[i] ? kPartPrioLocalUs : kPartPrioRemoteUs));
+        fin[i] = t + kPartPrioRowUs;
     }
     // every workgroup's rows in ASAP order (ties: solve order)
     std::vector<int32_t> idx(n);
@@ -1743,9 +1752,9 @@ void plan_part(const HostFactor &F, const std::vector<int32_t> &nat, int P, Part
         for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
             const int32_t d = F.ci[j];
             const bool loc = pp.wg[d] == pp.wg[i] && pp.lpos[i] - pp.lpos[d] < kPartSlots;
-            t = std::max(t, done[d] + (loc ? kPartLocalUs : kPartRemoteUs));
+            t = std::max(t, done[d] + (loc ? kPartEstLocalUs : kPartEstRemoteUs));
         }
-        done[i] = wf = t + kPartRowUs;
+        done[i] = wf = t + kPartEstRowUs;
         tmax = std::max(tmax, done[i]);
     }
     pp.est = tmax;
@@ -1914,7 +1923,9 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     {
         const char *pe = std::getenv("PSK_TRISOLVE_PART");
         const bool force = pe && std::atoi(pe) == 1, off = pe && std::atoi(pe) == 0;
-        if (!off && n > kLdsMaxRows && (T.schedule != kSchedGrid || force) && n >= (int64_t)c->num_cus * kPartWaves) {
+        const int64_t strip = (n + c->num_cus - 1) / std::max(1, c->num_cus);
+        if (!off && n > kLdsMaxRows && n >= (int64_t)c->num_cus * kPartWaves &&
+            (force || (T.schedule != kSchedGrid && strip <= kPartMaxStrip))) {
             PartPlan pp;
             plan_part(F, nat, c->num_cus, pp);
             T.est_part_us = pp.est;
