@@ -62,11 +62,15 @@ def _worker(rank, world, port, name, kind, out_dir):
 
 # fd512 x 2: shards of 128 slices whose first/last slices (halo lines) keep 32-bit columns while the
 # rest are packed — the sliced SpMV layout across the halo
-@pytest.mark.parametrize("name,kind,world", [("fd64", "fd", 2), ("fd96", "fd", 3), ("dh12", "general", 3),
-                                             ("fd50", "general", 4), ("fd512", "fd", 2)])
-def test_multirank_pcg_on_one_gpu(tmp_path, name, kind, world):
+# overlap: PSK_HALO_OVERLAP=1, the halo exchange on a second stream overlapping K3 (opt-in)
+@pytest.mark.parametrize("name,kind,world,overlap", [("fd64", "fd", 2, 0), ("fd96", "fd", 3, 0),
+                                                     ("dh12", "general", 3, 0), ("fd50", "general", 4, 0),
+                                                     ("fd512", "fd", 2, 0), ("fd512", "fd", 2, 1),
+                                                     ("fd96", "fd", 3, 1)])
+def test_multirank_pcg_on_one_gpu(tmp_path, monkeypatch, name, kind, world, overlap):
     import torch.multiprocessing as mp
     from oracle import fdlap, krylov
+    monkeypatch.setenv("PSK_HALO_OVERLAP", str(overlap))   # inherited by the spawned ranks
     mp.start_processes(_worker, args=(world, _free_port(), name, kind, str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     parts = [dict(np.load(tmp_path / ("r%d.npz" % r))) for r in range(world)]
