@@ -147,17 +147,23 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
 // K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
 // (K2's expression on the same partials), the convergence test, beta. Returns false when the
 // solve stopped at this iteration; x (which K3 owns) is then still advanced over [i0, i1).
+// pprev != nullptr: iteration k-1 deferred its x update (x += alpha_prev p_{k-1}, applied first).
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
                                              double pTAp, double rr, double ur, PcgState *st,
                                              double *__restrict__ udr, double *__restrict__ hist, int64_t k,
                                              int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
-                                             int64_t tile) {
+                                             int64_t tile, const double *__restrict__ pprev = nullptr,
+                                             double alpha_prev = 0.0) {
     alpha = udr[k] / pTAp;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (tile == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
     if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
         const int64_t i = tile * kVecTile + 2 * threadIdx.x;
-        for (int64_t j = i; j < i + 2 && j < n; ++j) x[j] = x[j] + alpha * p[j];   // :121
+        for (int64_t j = i; j < i + 2 && j < n; ++j) {
+            double xj = x[j];
+            if (pprev) xj = xj + alpha_prev * pprev[j];      // :121 of iteration k-1
+            x[j] = xj + alpha * p[j];                        // :121
+        }
         if (tile == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
             st->resid = normR;
@@ -171,25 +177,34 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
 }
 
 // ---- K3: x += alpha p, convergence test, beta, p = u + beta p (one-shot, as K2) -------------
+// x += alpha p is deferred on even iterations: x is read and written every other iteration only
+// (x = (x + alpha_{k-1} p_{k-1}) + alpha_k p_k on odd k and on the last, the reference's two
+// roundings in its order), with p double-buffered so p_{k-1} is still there: K3 reads p_k from
+// pcur and p_{k-1} (odd k) from pnext, where it writes p_{k+1} (each element read before it is
+// written). A breakdown after an even iteration leaves one update pending (pcg_flush_kernel).
 template <int JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
-    int64_t n, double *__restrict__ x, const double *__restrict__ r, double *__restrict__ p,
-    const double *__restrict__ dinv, double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts,
-    PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter,
-    int fail_on_maxiter, int64_t tile_base) {
+    int64_t n, double *__restrict__ x, const double *__restrict__ r, const double *__restrict__ pcur,
+    double *__restrict__ pnext, const double *__restrict__ dinv, double ds, const double *__restrict__ pap,
+    const double *__restrict__ rrur, int nparts, PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
+    double *__restrict__ alphas, int64_t k, int64_t maxiter, int fail_on_maxiter, int64_t tile_base) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
     // halo exchange then overlaps the rest); tile 0 alone writes the solver state
     const int64_t tile = tile_base + blockIdx.x;
+    const bool pend = (k & 1) != 0;                          // iteration k-1 deferred its x update
+    const double alpha_prev = pend ? alphas[k - 1] : 0.0;
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, p, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
+    if (!pcg_direction_scalars(n, x, pcur, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
                                rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta, tile))
+                               beta, tile, pend ? pnext : nullptr, alpha_prev))
         return;
+    if (tile == 0 && threadIdx.x == 0) alphas[k] = alpha;
+    const bool flush = pend || k == maxiter - 1;
     const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
     if (i + 1 < n) {
-        const dv2 ro = ld2nt(r + i), po = ld2(p + i), xo = ld2nt(x + i);
+        const dv2 ro = ld2nt(r + i), po = ld2(pcur + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2nt(dinv + i);
         double u0 = ro.x, u1 = ro.y;
@@ -197,19 +212,39 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
             u0 = d.x * ro.x;
             u1 = d.y * ro.y;
         }
-        dv2 pn, xn;
-        xn.x = xo.x + alpha * po.x;                          // x = x + alpha*p  :121
-        xn.y = xo.y + alpha * po.y;
+        if (flush) {
+            dv2 xo = ld2nt(x + i);
+            if (pend) {
+                const dv2 pp = ld2nt(pnext + i);
+                xo.x = xo.x + alpha_prev * pp.x;             // x = x + alpha*p  :121 (iteration k-1)
+                xo.y = xo.y + alpha_prev * pp.y;
+            }
+            dv2 xn;
+            xn.x = xo.x + alpha * po.x;                      // :121
+            xn.y = xo.y + alpha * po.y;
+            st2nt(x + i, xn);
+        }
+        dv2 pn;
         pn.x = u0 + beta * po.x;                             // p = u + beta*p  :138
         pn.y = u1 + beta * po.y;
-        st2nt(x + i, xn);
-        st2(p + i, pn);
+        st2(pnext + i, pn);
     } else if (i < n) {
         const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
-        const double pi = p[i];
-        x[i] = x[i] + alpha * pi;
-        p[i] = u0 + beta * pi;
+        const double pi = pcur[i];
+        if (flush) {
+            double xi = x[i];
+            if (pend) xi = xi + alpha_prev * pnext[i];
+            x[i] = xi + alpha * pi;
+        }
+        pnext[i] = u0 + beta * pi;
     }
+}
+
+// the x update a breakdown left pending: x += alpha p_{k-1} (after an even iteration k-1)
+__global__ void pcg_flush_kernel(int64_t n, double *__restrict__ x, const double *__restrict__ pprev,
+                                 const double *__restrict__ alpha) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i < n) x[i] = x[i] + *alpha * pprev[i];
 }
 
 // ---- general preconditioner (ILU, ...): u = M^-1 r is materialised by the preconditioner's own
@@ -283,6 +318,7 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 
 struct PcgWork {
     double *x, *r, *p, *Ap, *u, *part1, *part2, *part3, *udr, *hist;
+    double *p2, *alphas;   // Jacobi/identity K3: the second p buffer, alpha_k (deferred x updates)
     // sharded (P ranks): the ranks' gathered scalars, [P] p.Ap and [P][2] (r.r, u.r), and the
     // gathered init partials [P][kMaxGrid][2]; unsharded: part1g/part2g alias part1/part2
     double *part1g, *part2g, *initg;
@@ -291,7 +327,7 @@ struct PcgWork {
 
 static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &w) {
     const size_t vec = align_up((size_t)A->n * 8, 256), vecc = align_up((size_t)A->ncols * 8, 256);
-    const size_t big = (gen ? 4 : 3) * vec + vecc;
+    const size_t big = (gen ? 4 : 3) * vec + (gen ? 1 : 2) * vecc;
     PSK_TRY(A->ws.ensure(big > 0 ? big : 256));
     char *b = A->ws.as<char>();
     w.x = reinterpret_cast<double *>(b);
@@ -299,9 +335,10 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &
     w.Ap = reinterpret_cast<double *>(b + 2 * vec);
     w.p = reinterpret_cast<double *>(b + 3 * vec);
     w.u = gen ? reinterpret_cast<double *>(b + 3 * vec + vecc) : nullptr;
+    w.p2 = gen ? nullptr : reinterpret_cast<double *>(b + 3 * vec + vecc);
     const size_t small = align_up(sizeof(PcgState), 256) + 2 * align_up(kMaxGrid * 8, 256) +
                          align_up(2 * kMaxGrid * 8, 256) + align_up((size_t)(maxiter + 2) * 8, 256) +
-                         align_up((size_t)(maxiter + 1) * 8, 256);
+                         align_up((size_t)(maxiter + 1) * 8, 256) + align_up((size_t)(maxiter + 1) * 8, 256);
     const size_t gath = P > 1 ? align_up((size_t)P * 8, 256) + align_up((size_t)P * 16, 256) +
                                     align_up((size_t)P * 2 * kMaxGrid * 8, 256)
                               : 0;
@@ -318,6 +355,8 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &
     w.udr = reinterpret_cast<double *>(s);
     s += align_up((size_t)(maxiter + 2) * 8, 256);
     w.hist = reinterpret_cast<double *>(s);
+    s += align_up((size_t)(maxiter + 1) * 8, 256);
+    w.alphas = reinterpret_cast<double *>(s);
     s += align_up((size_t)(maxiter + 1) * 8, 256);
     if (P > 1) {
         w.part1g = reinterpret_cast<double *>(s);
@@ -467,10 +506,13 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             }
             if (rc != PSK_OK) break;
         }
+        // p_k and the buffer K3 writes p_{k+1} into (Jacobi/identity: alternating; general: in place)
+        double *pk = (gen || !(k & 1)) ? w.p : w.p2;
+        double *pn = gen ? w.p : ((k & 1) ? w.p : w.p2);
         if (halo_pending) {   // exchanged during the previous K3
             if (hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess) { rc = fail(PSK_ERR_HIP, "halo wait"); break; }
             halo_pending = false;
-        } else if (A->comm && (rc = halo_exchange(A, w.p, s)) != PSK_OK) {
+        } else if (A->comm && (rc = halo_exchange(A, pk, s)) != PSK_OK) {
             break;
         }
         int slot = (int)(k % TP);
@@ -479,7 +521,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
             if (hipEventRecord(ta[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         }
-        if ((rc = launch_spmv(A, kSpmvDot, w.p, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s)) != PSK_OK)
+        if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s)) != PSK_OK)
             break;
         if (ctl->time_kernels && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
@@ -504,16 +546,16 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
                 if (t1 <= t0) return;
                 const dim3 g3((unsigned)(t1 - t0));
                 if (jac == 2)
-                    hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
-                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                    hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, pk, pn, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
                                        ctl->fail_on_maxiter, t0);
                 else if (jac == 1)
-                    hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
-                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                    hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, pk, pn, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
                                        ctl->fail_on_maxiter, t0);
                 else
-                    hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.p, dinv, ds,
-                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, k, maxiter,
+                    hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, pk, pn, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
                                        ctl->fail_on_maxiter, t0);
             };
             if (overlap && k + 1 < maxiter) {
@@ -521,7 +563,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
                 // second stream while the other tiles run; the next SpMV waits for it
                 k3(0, ov_lo);
                 k3(ov_hi, nv);
-                if ((rc = halo_exchange_async(A, w.p, s, cs, ev_k3a, ev_halo)) != PSK_OK) break;
+                if ((rc = halo_exchange_async(A, pn, s, cs, ev_k3a, ev_halo)) != PSK_OK) break;
                 k3(ov_lo, ov_hi);
                 halo_pending = true;
             } else {
@@ -583,7 +625,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             res->hist_len = nh;
             res->resid_recursive = nh > 0 ? hh[(size_t)nh - 1] : hs.normB;
             if (res->status == PSK_MAXITER) res->resid = maxiter > 0 ? res->resid_recursive : hs.normB;
-            rc = from_device_vec(w.x, loc, n, xout, s);
+            // a dot(p,Ap) breakdown at odd k: iteration k-1 (even) deferred its x update
+            if (!gen && hs.done == 2 && hs.brk_kind != 1 && (hs.iters & 1) && n > 0) {
+                const int64_t kp = hs.iters - 1;
+                hipLaunchKernelGGL(pcg_flush_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,
+                                   w.x, (kp & 1) ? w.p2 : w.p, w.alphas + kp);
+                if (hipGetLastError() != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg flush");
+            }
+            if (rc == PSK_OK) rc = from_device_vec(w.x, loc, n, xout, s);
             if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x copy");
         }
         if (ctl->time_kernels) {

@@ -201,6 +201,46 @@ def test_pcg_breakdown_later_history(psk):
     np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=1e-14)
 
 
+@pytest.mark.parametrize("maxiter", [5, 6, 7])
+@pytest.mark.parametrize("fail", [True, False])
+@pytest.mark.parametrize("jac", ["identity", "jacobi"])
+def test_pcg_solution_at_maxiter_odd_even(psk, maxiter, fail, jac):
+    """K3 defers x += alpha p on even iterations (x read and written every other iteration, p double
+    buffered): the solution the loop stops with — at maxiter (odd and even) with and without
+    failOnMaxiter — is the oracle's (to rounding: the device's dot products sum in another order
+    than numpy's), and so is the history; a missing or doubled update would be O(1) off."""
+    from oracle import fdlap, krylov
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, 24)
+    b, _ = fdlap.manufactured_rhs(A, 12345)
+    pre = psk.Jacobi() if jac == "jacobi" else psk.IdentityPreconditionerType()
+    ref = krylov.pcg(A, b, maxiter=maxiter, tau=1e-14, fail_on_maxiter=fail,
+                     precond=krylov.jacobi_form(A) if jac == "jacobi" else krylov.identity_apply)
+    ctl = psk.CommonSolverArgs(maxiter=maxiter, tau=1e-14, failOnMaxiter=fail, showIters=False, showFinal=False)
+    st = psk.PCG(control=ctl, precond=pre).makeSolver().solve(A, b)
+    assert st.iters() == ref["iters"] and bool(st.success()) == bool(ref["success"])
+    np.testing.assert_allclose(st.soln(), ref["soln"], rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=1e-12)
+
+
+def test_pcg_breakdown_after_even_iteration_flushes_x(psk):
+    """A dot(p, Ap) == 0 breakdown at k = 1 leaves iteration 0's deferred x update pending; the C ABI
+    still returns x with it applied (x1 = x0 + alpha0 p0, as the reference's loop holds it)."""
+    import ctypes
+    from pysolvers_amd import _native as N
+    A = sp.csr_matrix(np.array([[2.0, 0.0, 0.0], [0.0, 0.0, 0.0], [0.0, 0.0, 0.0]]))
+    b = np.array([1.0, 1.0, 0.0])
+    dA = psk.DeviceCSR.from_scipy(A)
+    ctl = N.PskCtl(maxiter=10, tau=1e-8, fail_on_maxiter=1, restart=0, check_every=0, time_kernels=0)
+    res = N.PskResult()
+    x = np.full(3, np.nan)
+    N.check(N.lib.psk_pcg(dA.handle, None, N.ptr(b), N.ptr(x), ctypes.byref(ctl), ctypes.byref(res), None,
+                          N.PSK_HOST), "psk_pcg")
+    assert res.status == 2 and res.iters == 1                 # PSK_BREAKDOWN at k = 1
+    r0 = b.copy()
+    alpha0 = (r0 @ r0) / (r0 @ (A @ r0))                      # p0 = r0, x0 = 0
+    assert np.array_equal(x, 0.0 + alpha0 * r0)
+
+
 def test_torch_tensors_ordered_after_torch_stream(psk):
     """b, x and SpMV/preconditioner operands as torch tensors written by still-queued torch kernels:
     libpsk waits for torch's stream first (same answers as the numpy path)."""
