@@ -48,19 +48,21 @@ def spmv_bytes(n, nnz):
     return 12 * nnz + 4 * (n + 1) + 16 * n
 
 
-PCG_VEC_BYTES_PER_ROW = 80   # K2 (r, Ap, dinv in; r out) + K3 (r, p, x, dinv in; x, p out), Jacobi
+PCG_VEC_BYTES_PER_ROW = 76   # K2 (r, Ap, dinv in; r out) + K3 (r, p, dinv in; p out; x and p_{k-1} every other iteration), Jacobi
 LAYOUT_NAMES = {0: "csr", 1: "sliced", 2: "sliced_wide", 3: "sliced_dict"}   # PSK_LAYOUT_*
 
 
 def pcg_iter_bytes(n, nnz, jacobi=True):
     """Compulsory bytes of one PCG iteration in libpsk's 3-launch schedule with a CSR SpMV
     (SURVEY.md §8d)."""
-    return spmv_bytes(n, nnz) + (PCG_VEC_BYTES_PER_ROW if jacobi else 64) * n
+    return spmv_bytes(n, nnz) + (PCG_VEC_BYTES_PER_ROW if jacobi else 60) * n
 
 
 def vec_bytes_per_row(N, M):
-    """K2 + K3 bytes per row: 80 with a streamed DInv, 64 when the Jacobi diagonal is one scalar
-    (psk_prec_jacobi_uniform)."""
+    """K2 + K3 bytes per row, averaged over iterations: K2 24 (r, Ap read, r written); K3 reads r and
+    p_k and writes p_{k+1} every iteration, and x (read + write) with p_{k-1} on odd iterations only
+    (the deferred x update, pcg.hip) = 24 + 24/2; + 16 for a streamed DInv (K2 and K3 read it).
+    60 when the Jacobi diagonal is one scalar (psk_prec_jacobi_uniform), 76 otherwise."""
     u = N.I32()
     N.check(N.lib.psk_prec_jacobi_uniform(M, ctypes.byref(u), None), "psk_prec_jacobi_uniform")
     return PCG_VEC_BYTES_PER_ROW - (16 if u.value else 0)
