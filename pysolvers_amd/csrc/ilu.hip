@@ -26,8 +26,13 @@
 // between levels, so a dependency inside the block costs a barrier and an LDS-ring read instead of
 // a hand-off; only dependencies on earlier blocks go through the published values. For the
 // Gauss-Seidel factor triu(A) of a 5-point grid (2m-1 levels, each up to m rows wide) this is what
-// makes the smoother usable at m = 8192. The host simulates both schedules with measured per-level
-// costs and keeps the faster (TriFactor::schedule).
+// makes the smoother usable at m = 8192.
+//
+// Also below: the single-workgroup LDS schedule (small factors, x in LDS), the grid schedule (2-D
+// stencil factors: one wave per band of 64 lines along a skewed coordinate) and the partitioned
+// schedule (strips of the natural index, one workgroup per CU, in-strip hand-offs through LDS). The
+// host simulates the schedules with measured per-level / per-row costs and keeps the fastest
+// (TriFactor::schedule; psk_prec_trisolve_schedule reports and overrides it).
 #include "psk_internal.hpp"
 
 #include <algorithm>
