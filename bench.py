@@ -1,25 +1,28 @@
 #!/usr/bin/env python3
-"""Benchmark: PCG + Jacobi iterations/s on the 5-point FDLaplacian2D, CSR SpMV vs the HBM roofline.
+"""Benchmark: PCG + Jacobi iterations/s on the 5-point FDLaplacian2D, SpMV vs the HBM roofline.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--side M]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
 One "step" = one PCG iteration (PCGSolver.py:109-138: SpMV, 2 dots + norm, 3 updates, Jacobi
-apply) over the whole matrix. The workload is fixed for every N (strong scaling): A =
-FDLaplacian2D(-1, 1, m) generated on the device (bit-identical to examples/FDLaplacian2D.py),
-b = A @ default_rng(12345).random(n), control = CommonSolverArgs(maxiter=K, tau=0,
-failOnMaxiter=False) so exactly K iterations run (PCGSolver.py:129-131). With N > 1 the rows are
-split on whole grid lines across ranks (one process per GPU), halo lines are exchanged with
-ncclSend/Recv and the dot partials all-reduced with RCCL over xGMI, all inside libpsk.
+apply) over the whole matrix. The headline workload is the metric's own (BASELINE.json: "5-pt
+Laplacian N=10M"): A = FDLaplacian2D(-1, 1, 3163) (n = 10,004,569) generated on the device
+(bit-identical to examples/FDLaplacian2D.py), b = A @ default_rng(12345).random(n),
+control = CommonSolverArgs(maxiter=K, tau=0, failOnMaxiter=False) so exactly K iterations run
+(PCGSolver.py:129-131). It is fixed for every N (strong scaling): with N > 1 the rows are split on
+whole grid lines across ranks (one process per GPU), halo lines are exchanged with ncclSend/Recv
+and the dot partials all-gathered with RCCL over xGMI, all inside libpsk. configs[3]'s 16384^2
+system is timed the same way at the same N (`strong_scaling_16384`: the series the north star's
+>= 6x 1 -> 8 GPU target is quoted on).
 
 Timed region: barrier + device sync, ONE psk_pcg call of K iterations, device sync + barrier;
-max over ranks; --repeats such regions, value = the median one. `roofline` prices the SpMV kernel
+max over ranks; --repeats such regions, value = the median one. `roofline` prices the in-loop SpMV
 (the metric's kernel) from HIP events recorded by libpsk on its own stream around every SpMV launch
 of the median region; `traffic` comes from a rocprofv3 PMC profile of the SAME libpsk.so build
 (sha256-checked) or is null. On rank 0 at N = 1 the extra keys time the general-matrix path,
-N = 10M (`roofline_N10M`), configs[1] (4096^2), configs[2] (GMRES(30)+ILUT, 2896^2), configs[4]
-(PCG+AMG, 8192^2) and the CPU oracle (`cpu_baseline`), after the 16384^2 operands are freed.
+configs[1] (4096^2), GMRES(30) Arnoldi steps (4096^2), configs[2] (GMRES(30)+ILUT, 2896^2),
+configs[4] (PCG+AMG, 8192^2) and the CPU oracle at N = 10M (`cpu_baseline`).
 """
 import argparse
 import ctypes
@@ -34,6 +37,7 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "CG iterations/sec + SpMV GB/s vs HBM roofline, 5-pt Laplacian N=10M"
+METRIC_SIDE = 3163              # FDLaplacian2D side of the metric's N = 10M: n = 10,004,569
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
 
@@ -79,22 +83,24 @@ def layout_bytes(N, A, n):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--side", type=int, default=16384, help="grid side m of FDLaplacian2D (n = m^2 rows)")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--side", type=int, default=METRIC_SIDE,
+                    help="grid side m of FDLaplacian2D for the headline (n = m^2 rows; 3163 = the metric's N=10M)")
+    ap.add_argument("--scaling-side", type=int, default=16384,
+                    help="also time configs[3]'s 16384^2 system at this N (the strong-scaling series; 0 = skip)")
+    ap.add_argument("--scaling-steps", type=int, default=50)
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed regions of --steps iterations each; value = the median (SURVEY.md §8d)")
-    ap.add_argument("--cpu-iters", type=int, default=5, help="timed oracle iterations for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-iters", type=int, default=20, help="timed oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--general", type=int, default=1,
                     help="also time the general-matrix path (double values, streamed DInv) on rank 0")
     ap.add_argument("--config2", type=int, default=1, help="also time configs[2] (GMRES(30)+ILUT, FD 2896^2) on rank 0")
     ap.add_argument("--config4", type=int, default=1, help="also time configs[4] (PCG+AMG, -FD 8192^2) on rank 0")
-    ap.add_argument("--spmv10m", type=int, default=1, help="also time SpMV at N=10M (m=3163) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r2_pmc_traffic_16384.json"),
-                    help="PMC traffic summary (tools/pmc_summary.py) of the same build, kernel and side")
-    ap.add_argument("--traffic-json-10m", default=os.path.join(REPO, "profiles", "r2_pmc_traffic_3163.json"),
-                    help="PMC traffic summary of the same build at m = 3163 (N = 10M)")
+    ap.add_argument("--gmres", type=int, default=1, help="also time GMRES(30)+Jacobi Arnoldi steps at 4096^2 on rank 0")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r3_pmc_traffic_%d.json"),
+                    help="PMC traffic summary (tools/pmc_summary.py) of the same build; %%d = the side")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,12 +137,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    m = args.side
-    n, nnz = fd_sizes(m)
-    t_setup = time.time()
-    # ---- operator, preconditioner, right-hand side (all resident in HBM before timing) -----------
     comm = ctypes.c_void_p()
-    A = ctypes.c_void_p()
     # PSK_BENCH_TRANSPORT=host: rehearsal of the N>1 path with all ranks on ONE GPU (collectives over
     # host shared memory, psk_comm_init_host); never a measurement
     transport = os.environ.get("PSK_BENCH_TRANSPORT", "rccl")
@@ -152,83 +153,27 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
         N.check(N.lib.psk_comm_init(world, rank, uid, ctypes.byref(comm)), "psk_comm_init")
-    if world > 1:
-        rb, re_ = ctypes.c_int64(), ctypes.c_int64()
-        N.check(N.lib.psk_csr_create_fd2d_dist(-1.0, 1.0, m, comm, ctypes.byref(A), ctypes.byref(rb),
-                                               ctypes.byref(re_)), "psk_csr_create_fd2d_dist")
-        row_begin, row_end = rb.value, re_.value
-    else:
-        N.check(N.lib.psk_csr_create_fd2d(-1.0, 1.0, m, ctypes.byref(A)), "psk_csr_create_fd2d")
-        row_begin, row_end = 0, n
-    nloc = row_end - row_begin
-    ncols = nloc + (m if row_begin > 0 else 0) + (m if row_end < n else 0)
-    M = ctypes.c_void_p()
-    N.check(N.lib.psk_prec_create(A, N.PSK_PREC_JACOBI, ctypes.byref(M)), "psk_prec_create")
-    # x_exact rows of this rank: default_rng(12345).random(n)[row_begin:row_end] (one u64 per double)
-    rng = np.random.default_rng(12345)
-    rng.bit_generator.advance(row_begin)
-    xe = rng.random(nloc)
-    dx = ctypes.c_void_p()
-    db = ctypes.c_void_p()
-    dsol = ctypes.c_void_p()
-    N.check(N.lib.psk_dmalloc(ncols * 8, ctypes.byref(dx)), "alloc")
-    N.check(N.lib.psk_dmalloc(nloc * 8, ctypes.byref(db)), "alloc")
-    N.check(N.lib.psk_dmalloc(nloc * 8, ctypes.byref(dsol)), "alloc")
-    N.check(N.lib.psk_h2d(dx, N.ptr(xe), nloc * 8), "h2d")
-    del xe
-    N.check(N.lib.psk_spmv(A, dx, db, N.PSK_DEVICE), "psk_spmv")      # b = A @ x_exact (halo inside)
-    N.check(N.lib.psk_synchronize(), "sync")
-    setup_s = time.time() - t_setup
 
-    def run(iters, time_kernels):
-        ctl = N.PskCtl(maxiter=iters, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0,
-                       time_kernels=int(time_kernels))
-        res = N.PskResult()
-        N.check(N.lib.psk_pcg(A, M, db, dsol, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "psk_pcg")
-        return res
+    # ---- the headline: the metric's N = 10M system on `world` GPUs ----------------------------------
+    m = args.side
+    n, nnz = fd_sizes(m)
+    sys_ = PcgSystem(N, m, comm if world > 1 else None, world)
+    regions = sys_.regions(args.steps, args.warmup, args.repeats, barrier, dist)
+    dt, spmv_ms_med, spmv_launches = regions[sorted(range(len(regions)), key=lambda i: regions[i][0])[len(regions) // 2]]
 
-    if args.warmup > 0:
-        r = run(args.warmup, False)
-        assert r.iters == args.warmup, r.iters
-    # R timed regions of exactly K iterations, each bracketed by barrier + device sync; per region
-    # the max over ranks; value = the median region (warm median of >= 5 runs)
-    regions = []
-    for _ in range(max(1, args.repeats)):
-        barrier()
-        N.check(N.lib.psk_synchronize(), "sync")
-        t0 = time.perf_counter()
-        res = run(args.steps, True)
-        N.check(N.lib.psk_synchronize(), "sync")
-        barrier()
-        dt = time.perf_counter() - t0
-        assert res.iters == args.steps and res.success == 1, (res.iters, res.success)
-        spmv_ms = res.spmv_ms
-        if dist is not None:
-            import torch
-            t = torch.tensor([dt, spmv_ms], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt, spmv_ms = float(t[0]), float(t[1])
-        regions.append((dt, spmv_ms, res.spmv_launches))
-    order = sorted(range(len(regions)), key=lambda i: regions[i][0])
-    dt, spmv_ms_med, spmv_launches = regions[order[len(order) // 2]]
-
+    out = None
     if rank == 0:
         it_s = args.steps / dt
-        nloc_r0 = nloc
-        nnz_loc = ctypes.c_int64()
-        N.check(N.lib.psk_csr_info(A, None, ctypes.byref(nnz_loc)), "info")
-        bspmv = spmv_bytes(nloc_r0, nnz_loc.value)
-        lay, slots, packed, stream = N.I32(), N.I64(), N.I64(), N.I64()
-        N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), ctypes.byref(slots), ctypes.byref(packed),
-                                     ctypes.byref(stream)), "psk_csr_layout")
+        nloc_r0 = sys_.nloc
+        bspmv = spmv_bytes(nloc_r0, sys_.nnz_loc)
+        blay, lname, lay = sys_.layout()
         # the bytes this launch must move in its storage layout (matrix stream + x read + y written;
         # DESIGN.md §5); with a value dictionary far fewer than CSR's 12 B/entry
-        blay = stream.value + 16 * nloc_r0
         ach = blay / (spmv_ms_med * 1e-3) / 1e9 if spmv_ms_med > 0 else None
         csr_eq = bspmv / (spmv_ms_med * 1e-3) / 1e9 if spmv_ms_med > 0 else None
-        vb = vec_bytes_per_row(N, M)
+        vb = vec_bytes_per_row(N, sys_.M)
         biter = blay * world + vb * n
-        pmc = pmc_traffic(args.traffic_json, m, world, mode=1, sliced=lay.value != N.PSK_LAYOUT_CSR)
+        pmc = pmc_traffic(args.traffic_json % m, m, world, mode=1, sliced=lay != N.PSK_LAYOUT_CSR)
         out = {
             "metric": METRIC,
             "value": it_s,
@@ -243,19 +188,19 @@ def main():
             "dtype": "f64",
             "data": "synthetic: FDLaplacian2D(-1,1,m) built on device (bit-identical to the reference "
                     "generator), b = A @ default_rng(12345).random(n)",
-            "config": {"workload": "PCG+Jacobi, FDLaplacian2D %dx%d (n=%d, nnz=%d), tau=0 fixed-iteration"
-                                   % (m, m, n, nnz),
+            "config": {"workload": "PCG+Jacobi, FDLaplacian2D %dx%d (n=%d, nnz=%d; the metric's N=10M), tau=0 "
+                                   "fixed-iteration" % (m, m, n, nnz),
                        "m": m, "precond": "jacobi", "parallelism": "row-block x%d (%s)" % (world, "RCCL" if transport == "rccl" else "host-shm rehearsal")
                        if world > 1 else "single GPU"},
             "repeats": {"regions": len(regions), "value_is": "median region",
                         "it_s": [args.steps / r[0] for r in regions],
                         "spmv_avg_launch_ms": [r[1] for r in regions]},
-            "roofline": {"bound": "hbm", "kernel": pmc.pop("kernel", None) or spmv_kernel_label(lay.value, 1),
+            "roofline": {"bound": "hbm", "kernel": pmc.pop("kernel", None) or spmv_kernel_label(lay, 1),
                          "achieved": ach, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": (ach / HBM_PEAK_GBPS) if ach else None,
                          **pmc,
                          "algorithmic_bytes_per_launch": blay, "avg_launch_ms": spmv_ms_med,
-                         "launches": spmv_launches, "layout": LAYOUT_NAMES[lay.value],
+                         "launches": spmv_launches, "layout": lname,
                          "timing": "HIP events libpsk records on its own stream around every SpMV launch of the "
                                    "median timed region (rank 0's events; max over ranks at N > 1)",
                          "csr_bytes_per_launch": bspmv,
@@ -265,33 +210,51 @@ def main():
             "pcg_iteration_roofline": {"bytes_per_iteration": biter, "vector_bytes_per_row": vb,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
-            "setup_s": setup_s,
+            "setup_s": sys_.setup_s,
         }
         if world == 1:
             # the same matrix, plain y = A x launches back to back (no dot epilogue, no solver kernels
             # in between): how much of the in-loop SpMV time is the PCG context
             bms = ctypes.c_double()
-            N.check(N.lib.psk_spmv_timed(A, db, dsol, 20, ctypes.byref(bms)), "psk_spmv_timed")
-            out["spmv_plain_batch20"] = {"avg_launch_ms": bms.value,
+            N.check(N.lib.psk_spmv_timed(sys_.A, sys_.db, sys_.dsol, 50, ctypes.byref(bms)), "psk_spmv_timed")
+            pbb = pmc_traffic(args.traffic_json % m, m, 1, mode=0, sliced=lay != N.PSK_LAYOUT_CSR)
+            out["spmv_plain_batch50"] = {"avg_launch_ms": bms.value,
                                          "achieved_GBps": blay / (bms.value * 1e-3) / 1e9,
-                                         "frac": blay / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+                                         "frac": blay / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS, **pbb}
             if args.general:
-                out["general_path"] = general_path(N, A, db, dsol, m, args.steps)
-            out["spmv_csr_layout_batch20"] = csr_layout_batch(N, A, db, dsol, bspmv)
+                out["general_path"] = general_path(N, sys_.A, sys_.db, sys_.dsol, m, args.steps)
+            out["spmv_csr_layout_batch50"] = csr_layout_batch(N, sys_.A, sys_.db, sys_.dsol, bspmv, reps=50)
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
-    # the 16384^2 operands are no longer needed: free them before the other configs
-    N.lib.psk_dfree(dx)
-    N.lib.psk_dfree(db)
-    N.lib.psk_dfree(dsol)
-    N.lib.psk_prec_destroy(M)
-    N.lib.psk_csr_destroy(A)
+    sys_.free()
+
+    # ---- configs[3]'s 16384^2 system at the same N: the strong-scaling series of the >= 6x target ----
+    if args.scaling_side and args.scaling_side != m:
+        ms_ = args.scaling_side
+        big = PcgSystem(N, ms_, comm if world > 1 else None, world)
+        reg = big.regions(args.scaling_steps, 5, 3, barrier, dist)
+        if rank == 0:
+            dtb, smsb, _ = reg[sorted(range(len(reg)), key=lambda i: reg[i][0])[len(reg) // 2]]
+            bl, lname, lay = big.layout()
+            pm = pmc_traffic(args.traffic_json % ms_, ms_, world, mode=1, sliced=lay != N.PSK_LAYOUT_CSR)
+            nb_, _ = fd_sizes(ms_)
+            vbb = vec_bytes_per_row(N, big.M)
+            out["strong_scaling_%d" % ms_] = {
+                "workload": "PCG+Jacobi, FDLaplacian2D %dx%d (configs[3]), tau=0, %d iterations per region, "
+                            "median of %d regions, same N as the headline" % (ms_, ms_, args.scaling_steps, len(reg)),
+                "n_gpus": world, "pcg_it_per_s": args.scaling_steps / dtb, "ms_per_step": dtb * 1e3 / args.scaling_steps,
+                "regions_it_s": [args.scaling_steps / r[0] for r in reg],
+                "spmv_avg_launch_ms": smsb, "spmv_algorithmic_bytes_per_launch": bl, "layout": lname,
+                "spmv_frac": bl / (smsb * 1e-3) / 1e9 / HBM_PEAK_GBPS, **pm,
+                "pcg_iteration_frac_of_aggregate_peak":
+                    (bl * world + vbb * nb_) * args.scaling_steps / dtb / 1e9 / (HBM_PEAK_GBPS * world)}
+        big.free()
+
     if rank == 0:
-        if world == 1 and args.spmv10m and m != 3163:
-            out["spmv_N10M"] = spmv_10m(N, args.traffic_json_10m)
-            out["roofline_N10M"] = out["spmv_N10M"].pop("roofline")
         if world == 1 and args.config1 and m != 4096:
             out["configs1_pcg_jacobi_4096"] = pcg_4096(N)
+        if world == 1 and args.gmres:
+            out["gmres30_jacobi_4096"] = gmres_arnoldi(N)
         if world == 1 and args.config2:
             out["configs2_gmres30_ilut"] = gmres_ilut(N)
         if world == 1 and args.config4:
@@ -306,6 +269,94 @@ def main():
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
+
+
+class PcgSystem:
+    """FDLaplacian2D(-1, 1, m) (row-block shard of this rank when comm is set), its Jacobi
+    preconditioner and b = A @ default_rng(12345).random(n), all resident in HBM."""
+
+    def __init__(self, N, m, comm, world):
+        self.N = N
+        t0 = time.time()
+        n, _ = fd_sizes(m)
+        self.A = ctypes.c_void_p()
+        if comm is not None:
+            rb, re_ = ctypes.c_int64(), ctypes.c_int64()
+            N.check(N.lib.psk_csr_create_fd2d_dist(-1.0, 1.0, m, comm, ctypes.byref(self.A), ctypes.byref(rb),
+                                                   ctypes.byref(re_)), "psk_csr_create_fd2d_dist")
+            row_begin, row_end = rb.value, re_.value
+        else:
+            N.check(N.lib.psk_csr_create_fd2d(-1.0, 1.0, m, ctypes.byref(self.A)), "psk_csr_create_fd2d")
+            row_begin, row_end = 0, n
+        self.nloc = row_end - row_begin
+        ncols = self.nloc + (m if row_begin > 0 else 0) + (m if row_end < n else 0)
+        self.M = ctypes.c_void_p()
+        N.check(N.lib.psk_prec_create(self.A, N.PSK_PREC_JACOBI, ctypes.byref(self.M)), "psk_prec_create")
+        # x_exact rows of this rank: default_rng(12345).random(n)[row_begin:row_end] (one u64 per double)
+        rng = np.random.default_rng(12345)
+        rng.bit_generator.advance(row_begin)
+        xe = rng.random(self.nloc)
+        self.dx, self.db, self.dsol = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+        N.check(N.lib.psk_dmalloc(ncols * 8, ctypes.byref(self.dx)), "alloc")
+        N.check(N.lib.psk_dmalloc(self.nloc * 8, ctypes.byref(self.db)), "alloc")
+        N.check(N.lib.psk_dmalloc(self.nloc * 8, ctypes.byref(self.dsol)), "alloc")
+        N.check(N.lib.psk_h2d(self.dx, N.ptr(xe), self.nloc * 8), "h2d")
+        del xe
+        N.check(N.lib.psk_spmv(self.A, self.dx, self.db, N.PSK_DEVICE), "psk_spmv")   # b = A @ x_exact (halo inside)
+        N.check(N.lib.psk_synchronize(), "sync")
+        nnz = ctypes.c_int64()
+        N.check(N.lib.psk_csr_info(self.A, None, ctypes.byref(nnz)), "info")
+        self.nnz_loc = nnz.value
+        self.setup_s = time.time() - t0
+
+    def run(self, iters, time_kernels):
+        N = self.N
+        ctl = N.PskCtl(maxiter=iters, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0,
+                       time_kernels=int(time_kernels))
+        res = N.PskResult()
+        N.check(N.lib.psk_pcg(self.A, self.M, self.db, self.dsol, ctypes.byref(ctl), ctypes.byref(res), None,
+                              N.PSK_DEVICE), "psk_pcg")
+        return res
+
+    def regions(self, steps, warmup, repeats, barrier, dist):
+        """`repeats` timed regions of exactly `steps` iterations, each bracketed by barrier + device
+        sync; per region the max over ranks of (wall time, mean SpMV launch time)."""
+        N = self.N
+        if warmup > 0:
+            r = self.run(warmup, False)
+            assert r.iters == warmup, r.iters
+        out = []
+        for _ in range(max(1, repeats)):
+            barrier()
+            N.check(N.lib.psk_synchronize(), "sync")
+            t0 = time.perf_counter()
+            res = self.run(steps, True)
+            N.check(N.lib.psk_synchronize(), "sync")
+            barrier()
+            dt = time.perf_counter() - t0
+            assert res.iters == steps and res.success == 1, (res.iters, res.success)
+            spmv_ms = res.spmv_ms
+            if dist is not None:
+                import torch
+                t = torch.tensor([dt, spmv_ms], dtype=torch.float64)
+                dist.all_reduce(t, op=dist.ReduceOp.MAX)
+                dt, spmv_ms = float(t[0]), float(t[1])
+            out.append((dt, spmv_ms, res.spmv_launches))
+        return out
+
+    def layout(self):
+        N = self.N
+        lay, stream = N.I32(), N.I64()
+        N.check(N.lib.psk_csr_layout(self.A, -1, ctypes.byref(lay), None, None, ctypes.byref(stream)),
+                "psk_csr_layout")
+        return stream.value + 16 * self.nloc, LAYOUT_NAMES[lay.value], lay.value
+
+    def free(self):
+        N = self.N
+        for p in (self.dx, self.db, self.dsol):
+            N.lib.psk_dfree(p)
+        N.lib.psk_prec_destroy(self.M)
+        N.lib.psk_csr_destroy(self.A)
 
 
 def median(v):
@@ -454,62 +505,6 @@ def pmc_traffic(path, m, world, mode, sliced):
                               "%d launches)" % (src, v["launches"])}
 
 
-def spmv_10m(N, traffic_json, iters=30):
-    """SpMV at the metric's N=10M (m=3163): mean launch time of the PCG SpMV over `iters` iterations
-    (in the loop) and of 50 plain launches back to back, each priced on the layout's bytes."""
-    m = 3163
-    n, nnz = fd_sizes(m)
-    A, M, db, dx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
-    N.check(N.lib.psk_csr_create_fd2d(-1.0, 1.0, m, ctypes.byref(A)), "fd2d")
-    N.check(N.lib.psk_prec_create(A, N.PSK_PREC_JACOBI, ctypes.byref(M)), "prec")
-    N.check(N.lib.psk_dmalloc(n * 8, ctypes.byref(db)), "alloc")
-    N.check(N.lib.psk_dmalloc(n * 8, ctypes.byref(dx)), "alloc")
-    xe = np.random.default_rng(12345).random(n)
-    N.check(N.lib.psk_h2d(dx, N.ptr(xe), n * 8), "h2d")
-    N.check(N.lib.psk_spmv(A, dx, db, N.PSK_DEVICE), "spmv")
-    ctl = N.PskCtl(maxiter=10, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=0)
-    res = N.PskResult()
-    N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
-    regs = []
-    for _ in range(5):
-        ctl = N.PskCtl(maxiter=iters, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0, time_kernels=1)
-        res = N.PskResult()
-        N.check(N.lib.psk_pcg(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "pcg")
-        regs.append((res.spmv_ms, res.loop_ms))
-    regs.sort()
-    spmv_ms, loop_ms = regs[len(regs) // 2]
-    b = spmv_bytes(n, nnz)
-    bl, lname = layout_bytes(N, A, n)
-    lay = N.I32()
-    N.check(N.lib.psk_csr_layout(A, -1, ctypes.byref(lay), None, None, None), "psk_csr_layout")
-    gbps = bl / (spmv_ms * 1e-3) / 1e9
-    # back-to-back launches between two events (no per-launch event in between)
-    bms = ctypes.c_double()
-    N.check(N.lib.psk_spmv_timed(A, dx, db, 50, ctypes.byref(bms)), "psk_spmv_timed")
-    bb = bl / (bms.value * 1e-3) / 1e9
-    sl = lay.value != N.PSK_LAYOUT_CSR
-    pin, pbb = pmc_traffic(traffic_json, m, 1, mode=1, sliced=sl), pmc_traffic(traffic_json, m, 1, mode=0, sliced=sl)
-    roof = {
-        "in_loop": {"bound": "hbm", "kernel": pin.pop("kernel", None) or spmv_kernel_label(lay.value, 1),
-                    "achieved": gbps, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": gbps / HBM_PEAK_GBPS, **pin,
-                    "algorithmic_bytes_per_launch": bl, "avg_launch_ms": spmv_ms, "layout": lname,
-                    "how": "HIP events around each SpMV launch of a %d-iteration PCG+Jacobi solve; median of 5" % iters},
-        "back_to_back": {"bound": "hbm", "kernel": pbb.pop("kernel", None) or spmv_kernel_label(lay.value, 0),
-                         "achieved": bb, "peak": HBM_PEAK_GBPS, "unit": "GB/s", "frac": bb / HBM_PEAK_GBPS, **pbb,
-                         "algorithmic_bytes_per_launch": bl, "avg_launch_ms": bms.value, "layout": lname,
-                         "how": "50 plain y = A x launches between two HIP events on the library stream"},
-    }
-    csr = csr_layout_batch(N, A, dx, db, b, reps=50)
-    out = {"n": n, "nnz": nnz, "layout": lname, "pcg_it_per_s": iters / (loop_ms * 1e-3),
-           "csr_bytes_per_launch": b, "csr_count_over_time_GBps_in_loop": b / (spmv_ms * 1e-3) / 1e9,
-           "batch50_csr_layout": csr, "roofline": roof}
-    for p in (db, dx):
-        N.lib.psk_dfree(p)
-    N.lib.psk_prec_destroy(M)
-    N.lib.psk_csr_destroy(A)
-    return out
-
-
 def pcg_4096(N, iters=300):
     """configs[1]: PCG+Jacobi on FDLaplacian2D 4096^2, one GPU, `iters` fixed iterations (median of 5)."""
     m = 4096
@@ -543,6 +538,62 @@ def pcg_4096(N, iters=300):
            "regions_it_s": [iters / r for r in regs],
            "pcg_iteration_frac_of_peak": (bl + vec_bytes_per_row(N, M) * n) * iters / dt / 1e9 / HBM_PEAK_GBPS,
            "spmv_avg_launch_ms": res.spmv_ms, "spmv_frac": bl / (res.spmv_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    for p in (db, dx):
+        N.lib.psk_dfree(p)
+    N.lib.psk_prec_destroy(M)
+    N.lib.psk_csr_destroy(A)
+    return out
+
+
+def gmres_arnoldi(N, m=4096, restart=30, cycles=2, repeats=3):
+    """GMRES(30) + Jacobi on FDLaplacian2D 4096^2, one GPU: Arnoldi steps/s over exactly `cycles`
+    restart cycles per timed solve (tau = 0), priced on two byte models per step k (k = 0..29):
+      * reference op list (SURVEY.md §8d): B_spmv(CSR) + (k+1) 40n + 24n, + 24n for the Jacobi apply;
+      * libpsk's fused schedule: the SpMV layout's stream + x and DInv gathers + y written + q_0 read
+        (layout bytes + 16n; Jacobi fused into the gather), MGS j < k 32n (u read + written, q_j and
+        q_{j+1} read), j = k 24n, normalisation 16n (u read, q_{k+1} written): layout + (56 + 32k) n.
+    The restart (host least-squares solve, x update, residual SpMV) is inside the timed region."""
+    n, nnz = fd_sizes(m)
+    A, M, db, dx = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_void_p()
+    N.check(N.lib.psk_csr_create_fd2d(-1.0, 1.0, m, ctypes.byref(A)), "fd2d")
+    os.environ["PSK_JACOBI_UNIFORM"] = "0"
+    try:
+        N.check(N.lib.psk_prec_create(A, N.PSK_PREC_JACOBI, ctypes.byref(M)), "prec")
+    finally:
+        del os.environ["PSK_JACOBI_UNIFORM"]
+    N.check(N.lib.psk_dmalloc(n * 8, ctypes.byref(db)), "alloc")
+    N.check(N.lib.psk_dmalloc(n * 8, ctypes.byref(dx)), "alloc")
+    xe = np.random.default_rng(12345).random(n)
+    N.check(N.lib.psk_h2d(dx, N.ptr(xe), n * 8), "h2d")
+    N.check(N.lib.psk_spmv(A, dx, db, N.PSK_DEVICE), "spmv")
+    steps = restart * cycles
+
+    def run(k):
+        ctl = N.PskCtl(maxiter=k, tau=0.0, fail_on_maxiter=0, restart=restart, check_every=0, time_kernels=0)
+        res = N.PskResult()
+        N.check(N.lib.psk_gmres(A, M, db, dx, ctypes.byref(ctl), ctypes.byref(res), None, N.PSK_DEVICE), "psk_gmres")
+        return res
+    run(restart)
+    regs = []
+    for _ in range(repeats):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        run(steps)
+        N.check(N.lib.psk_synchronize(), "sync")
+        regs.append(time.perf_counter() - t0)
+    dt = median(regs)
+    bl, lname = layout_bytes(N, A, n)
+    ks = range(restart)
+    b_ref = sum(spmv_bytes(n, nnz) + (k + 1) * 40 * n + 24 * n + 24 * n for k in ks) / restart
+    b_fused = sum(bl + 16 * n + (56 + 32 * k) * n for k in ks) / restart
+    sps = steps / dt
+    out = {"workload": "GMRES(%d) + Jacobi, FDLaplacian2D %dx%d, tau=0, %d Arnoldi steps (%d cycles) per solve, "
+                       "median of %d" % (restart, m, m, steps, cycles, repeats),
+           "n": n, "layout": lname, "steps_per_s": sps, "ms_per_step": dt * 1e3 / steps,
+           "regions_steps_per_s": [steps / r for r in regs],
+           "bytes_per_step_reference_ops": b_ref, "bytes_per_step_fused": b_fused,
+           "frac_reference_ops": b_ref * sps / 1e9 / HBM_PEAK_GBPS,
+           "frac_fused": b_fused * sps / 1e9 / HBM_PEAK_GBPS}
     for p in (db, dx):
         N.lib.psk_dfree(p)
     N.lib.psk_prec_destroy(M)

@@ -76,3 +76,36 @@ def manufactured_rhs(A, seed=12345):
     x = np.random.default_rng(seed).random(n)
     b = A @ x
     return b, x
+
+
+class FDStencil:
+    """FDLaplacian2D(a, b, m) as a matrix-free operator whose ``@`` is bit-identical to scipy
+    csr_matvec on the CSR that ``fd_laplacian_2d`` (= the reference generator) builds: every row is
+    summed from 0.0 in stored order [diag, -m, +m, -1, +1] with rounded products, absent neighbours
+    skipped (IterativeLinearSolver.py:104 -> csr_matvec; FDLaplacian2D.py:13-21). Vectorised over
+    rows in that slot order, so configs[3]'s m = 16384 (1.34e9 entries) needs no 16 GB CSR on the
+    host: only a few n-vectors. Has what oracle/krylov.py reads from a matrix: shape, diagonal(),
+    ``@``. tests/test_oracle_golden.py pins it to the CSR product."""
+
+    def __init__(self, a, b, m):
+        self.m = int(m)
+        n = self.m * self.m
+        self.shape = (n, n)
+        h = np.abs(b - a) / np.double(m + 1)          # FDLaplacian2D.py:6
+        self.dval = -4.0 / h / h                      # :13
+        self.oval = 1.0 / h / h                       # :15-21
+
+    def diagonal(self):
+        return np.full(self.shape[0], self.dval)
+
+    def __matmul__(self, x):
+        m = self.m
+        x = np.asarray(x, dtype=np.float64)
+        y = np.add(0.0, self.dval * x)                # sum = 0; sum += diag * x_k (0.0 + -0.0 = +0.0 as in C)
+        if m > 1:
+            y[m:] += self.oval * x[:-m]               # -m neighbour: rows with iy > 0
+            y[:-m] += self.oval * x[m:]               # +m: iy < m-1
+            Y, X = y.reshape(m, m), x.reshape(m, m)
+            Y[:, 1:] += self.oval * X[:, :-1]         # -1: ix > 0
+            Y[:, :-1] += self.oval * X[:, 1:]         # +1: ix < m-1
+        return y

@@ -114,12 +114,14 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     // own done flag, which its first workgroup may set while later ones are still starting
     if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
     // cache policy: Ap is dead after this kernel (non-temporal); r and dinv are re-read by K3
     if (i + 1 < n) {
         const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2(dinv + i);
+        ticket = gridsum_ticket(gs);
         dv2 rn;
         rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
         rn.y = ro.y - alpha * a.y;
@@ -134,6 +136,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
+        ticket = gridsum_ticket(gs);
         const double rn = r[i] - alpha * Ap[i];
         const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
@@ -141,7 +144,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = u0 * rn;
     }
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
-    gridsum_publish<2>(gs, v, sh);
+    gridsum_publish<2>(gs, v, sh, ticket);
 }
 
 // K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
@@ -287,11 +290,12 @@ __global__ __launch_bounds__(kBlock) void pcg_dot_kernel(int64_t n, const double
     if (st->done) return;
     __shared__ double sh[kWaves];
     const int64_t i = (int64_t)blockIdx.x * kVecTile + threadIdx.x;
+    const uint32_t ticket = gridsum_ticket(gs);
     double acc = 0.0;
     if (i < n) acc = a[i] * c[i];                                               // np.dot(u, r) :134
     if (i + kBlock < n) acc = fma(a[i + kBlock], c[i + kBlock], acc);
     const double v = block_sum(acc, sh);
-    gridsum_publish<1>(gs, &v, sh);
+    gridsum_publish<1>(gs, &v, sh, ticket);
 }
 
 __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(

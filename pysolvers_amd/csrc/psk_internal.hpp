@@ -62,6 +62,7 @@ struct Context {
     uint64_t *gs_slots = nullptr;
     int64_t gs_cap = 0;
     uint64_t *gs_gslots = nullptr;   // kMaxGrid * kGridSumMaxW
+    uint32_t *gs_cnt = nullptr;      // gridsum ticket counters (zero between launches)
     std::vector<uint64_t *> gs_retired;
     int32_t *gs_err = nullptr;
     hipStream_t comm_stream = nullptr;   // halo exchanges overlapped with compute (created lazily)
@@ -296,58 +297,107 @@ __device__ __forceinline__ double reduce_partials(const double *part, int np, in
 // ---------------------------------------------------------------------------------------------
 // One-shot launches and their deterministic grid reduction ("gridsum").
 //
-// The streaming kernels (SpMV, PCG K2/K3) run ONE TILE PER WORKGROUP, grid = tiles: workgroups are
-// dispatched in id order, so the chip sweeps a compact window of every stream and no workgroup
-// carries loop state (tools/spmv_lab.hip / tools/stream_lab.hip at n = 268M: SpMV +5%, the K2
-// access shape +7% over persistent grids; SpMV +7-10% at n = 10-17M).
-// Their dot products are finished inside the same launch, deterministically, without data atomics
-// and without making the consumers re-reduce per-workgroup partials (at 5*10^5 workgroups that
-// re-reduction alone would cost more than the stream):
-//  1. workgroup b publishes its W partials with agent-scope 8-byte stores into slots armed with a
-//     signalling-NaN sentinel (value-is-flag);
-//  2. the partials of group g (grp ~ sqrt(nwg) consecutive workgroups) are summed in a
-//     fixed order by ONE reducer workgroup — the one kGridSumLag ids after the group's last member,
-//     or that last member itself when the lagged id is past the grid — and published the same way;
-//  3. the grid's last workgroup sums the group sums in a fixed order into out[0..W).
-// Every reader re-arms what it read. A workgroup only waits for LOWER ids, which were dispatched
-// before it and only wait for lower ids themselves, so every wait ends; with the lag above the
-// resident capacity (2048 workgroups) step 2 almost never waits. grp == 1 skips step 2.
-constexpr int64_t kGridSumLag = 4096;
+// The streaming kernels (SpMV, PCG K2/K3) run ONE TILE PER WORKGROUP, grid = tiles: no workgroup
+// carries loop state and the chip sweeps a compact window of every stream (tools/spmv_lab.hip /
+// tools/stream_lab.hip at n = 268M: SpMV +5%, the K2 access shape +7% over persistent grids; SpMV
+// +7-10% at n = 10-17M). Their dot products are finished inside the same launch, deterministically,
+// without data atomics, and no workgroup ever waits for one that has not started — so the protocol
+// holds whatever the dispatch order, the workgroup->XCD placement or the co-resident kernels (HIP
+// promises none of them, MI355X_MICROARCH.md "Contract [G]"):
+//  1. a tile's workgroup draws a TICKET when it starts: one returning agent-scope atomic add by
+//     lane 0 of wave 0 on its group's counter, issued once the tile's stream loads are in flight
+//     (the return hides behind them; it is read at the end). Groups interleave tiles — group l of
+//     a superblock holds tiles l, l+256, l+512, ... — so the tickets drawn at any moment spread
+//     over 256 counters, each on its own 256-B line (one word takes ~88 atomics/us; the SpMV at
+//     16384^2 starts ~580 tiles/us).
+//  2. at its end every SLOT of the tile — the workgroup, or each of its waves for the *_wave
+//     variant (no workgroup barrier) — publishes its W partials with agent-scope (sc1) 8-byte
+//     stores into slots armed with a signalling-NaN sentinel (value-is-flag; MI355X_MICROARCH.md
+//     handoff granule).
+//  3. the tile holding its group's LAST ticket (its wave 0) sums the group's slots in order: every
+//     other member tile drew its ticket earlier, so all its waves are resident (a workgroup's waves
+//     are created together) and running, and producers never wait, so every slot it polls is
+//     written by a store that will land. It re-arms the slots, resets the counter, publishes the
+//     group sum the same way, then draws a ticket on the final counter.
+//  4. the group reducer holding the final counter's last ticket sums the group sums in group order
+//     into out[0..W) (again only already-issued stores are awaited) and resets that counter.
+// Launches of at most kBlock tiles skip the group stage: every slot publishes into the group-sum
+// slots and draws the final ticket at its end. The summation order depends on the tile and slot
+// indices only: sums are bitwise reproducible run to run, and equal across kernels that publish
+// over the same tiles and slots (the SpMV layouts).
+constexpr int kGridSumLLog = 8;
+constexpr int64_t kGridSumL = (int64_t)1 << kGridSumLLog;   // groups interleaved per superblock
+// counters one per 256-B line: atomics to one line serialise at its memory channel (64 counters
+// packed in 256 B, one ticket per wave, put the SpMV at ~800 tickets/us: in-loop SpMV 1.8 -> 6.8 ms
+// at 16384^2)
+constexpr int kGridSumCntStride = 64;
 constexpr uint64_t kGridSumSentinel = 0x7FF0000000000001ull;   // sNaN: arithmetic never produces it
 constexpr int kGridSumMaxW = 4;
+static_assert(kWaves == 4, "gridsum_prepare encodes kWaves slots per tile as spw_log2 = 2");
+constexpr int64_t kGridSumMaxGroups = kMaxGrid;
+// a wait on an already-issued store that has not landed after ~1.3 s (s_memrealtime, 100 MHz) is
+// reported (gridsum_check) instead of hanging the launch: never expected
+constexpr uint64_t kGridSumWaitTicks = (uint64_t)1 << 27;
 
 struct GridSum {
-    uint64_t *slots;    // nwg*W workgroup partials (grp > 1)
-    uint64_t *gslots;   // ngroups*W group sums
+    uint64_t *slots;    // nt*spw*W slot partials (two-level launches)
+    uint64_t *gslots;   // ngroups*W group sums (one-level: the slots themselves)
+    uint32_t *cnt;      // counter g at cnt[g * kGridSumCntStride] (g < kGridSumMaxGroups), the final one at
+                        // g = kGridSumMaxGroups; zero between launches
     double *out;        // the W grid sums
-    int64_t grp;        // units (workgroups / waves) per group: a power of two
-    int32_t grp_log2;   // log2(grp): every producer finds its roles with shifts and masks
-    int32_t *err;       // set when a bounded wait expires (reported by gridsum_check)
+    int64_t nt;         // tiles (workgroups) of the launch
+    int64_t ngroups;    // groups of tiles (one-level: nt * spw)
+    int32_t grp_log2;   // tiles of a full group = 2^grp_log2; -1 = one level (nt <= kBlock)
+    int32_t spw_log2;   // slots per tile: 1 (workgroup sums) or kWaves (wave sums)
+    int32_t *err;       // set when a wait expires (reported by gridsum_check)
 };
 
-// grp ~ sqrt(nwg), a power of two: the launch's tail waits for one group reduction (grp/256 loads
-// per lane) and the final one (ngroups/256), so both are kept short; ngroups <= kMaxGrid. A power
-// of two because every producer tests its roles: 64-bit (or even 32-bit) division and modulo are
-// long SALU sequences at the end of every wave (the SpMV's dot epilogue).
-inline int32_t gridsum_grp_log2(int64_t nwg) {
-    if (nwg <= kBlock) return 0;
+// tiles of a full group ~ sqrt(nt) (both reductions stay short), and ngroups <= kGridSumMaxGroups
+inline int32_t gridsum_grp_log2(int64_t nt) {
+    if (nt <= kBlock) return -1;
     int32_t l = 0;
-    while (((int64_t)1 << (2 * l)) < nwg) ++l;   // (2^l)^2 >= nwg
-    while (((int64_t)kMaxGrid << l) < nwg) ++l;  // ngroups <= kMaxGrid
+    while (((int64_t)1 << (2 * l)) < nt) ++l;
+    auto ng = [&](int32_t g) { return ((nt + (kGridSumL << g) - 1) >> (kGridSumLLog + g)) * kGridSumL; };
+    while (ng(l) > kGridSumMaxGroups) ++l;
     return l;
+}
+inline int64_t gridsum_ngroups(int64_t nt, int32_t gl, int32_t spw_log2) {
+    if (gl < 0) return nt << spw_log2;
+    const int64_t S = kGridSumL << gl, full = nt / S, tail = nt - full * S;
+    return full * kGridSumL + (tail < kGridSumL ? tail : kGridSumL);
+}
+
+__device__ __forceinline__ int64_t gridsum_group_of(int64_t t, int32_t gl) {
+    return ((t >> (kGridSumLLog + gl)) << kGridSumLLog) | (t & (kGridSumL - 1));
+}
+// member tiles of group g (base, base + 256, ...): count
+__device__ __forceinline__ int64_t gridsum_members(const GridSum &gs, int64_t g, int64_t &base) {
+    const int32_t gl = gs.grp_log2;
+    const int64_t sb = g >> kGridSumLLog, l = g & (kGridSumL - 1), S = kGridSumL << gl;
+    base = sb * S + l;
+    const int64_t t = gs.nt - sb * S;
+    return t >= S ? ((int64_t)1 << gl) : (t - l + kGridSumL - 1) >> kGridSumLLog;
 }
 
 __device__ __forceinline__ void gridsum_put(uint64_t *sl, double v) {
     __hip_atomic_store(sl, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// waits for a published value (bounded: ~10 ms, never expected; reported by gridsum_check, result
-// poisoned; once the flag is up no later wait spins, so a broken launch still drains quickly)
+__device__ __forceinline__ uint32_t gridsum_draw(uint32_t *c) {
+    return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gridsum_reset(uint32_t *c) {
+    __hip_atomic_store(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t *gridsum_counter(const GridSum &gs, int64_t g) {
+    return gs.cnt + g * kGridSumCntStride;
+}
+// a published value whose store has been issued (see above); poisoned and reported if it never lands
 __device__ __forceinline__ uint64_t gridsum_wait(const uint64_t *sl, int32_t *err) {
-    if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return 0x7FF8000000000000ull;
-    uint64_t bits;
-    int spins = 0;
+    uint64_t bits = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (bits != kGridSumSentinel) return bits;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while ((bits = __hip_atomic_load(sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == kGridSumSentinel) {
-        if (++spins > (1 << 18)) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kGridSumWaitTicks) {
             atomicOr(err, 1);
             return 0x7FF8000000000000ull;
         }
@@ -356,156 +406,188 @@ __device__ __forceinline__ uint64_t gridsum_wait(const uint64_t *sl, int32_t *er
     return bits;
 }
 
-// sum of src[j*W + c] for j in [j0, j1): lane-strided (lane t sums j0+t, j0+t+256, ... in order),
-// then block_sum — a fixed order for fixed bounds. The loads of a lane are issued together and
-// only the (rare) ones still holding the sentinel are waited on; every slot is re-armed.
-template <int W>
-__device__ __forceinline__ void gridsum_take_range(uint64_t *src, int64_t j0, int64_t j1, int32_t *err,
-                                                   double *sh, double *res) {
+// sum over members m in [0, cnt) of src[slot(m)*W + c], slot(m) = (base + (m >> sl) * stride) << sl
+// | (m & (2^sl - 1)) — member tiles in order, each tile's 2^sl slots in order — lane-strided over
+// NT lanes (lane t sums m = t, t + NT, ... in order), then the lanes' fixed-order total; every slot
+// is re-armed. NT = kBlock: whole workgroup (block_sum); NT = 64: one wave (wave_total).
+template <int W, int NT>
+__device__ __forceinline__ void gridsum_take(uint64_t *src, int64_t base, int64_t stride, int32_t sl, int64_t cnt,
+                                             int32_t *err, double *sh, double *res) {
+    const int lane = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+    const int64_t lo = ((int64_t)1 << sl) - 1;
+    auto slot = [&](int64_t m) { return ((base + (m >> sl) * stride) << sl) | (m & lo); };
 #pragma unroll
     for (int c = 0; c < W; ++c) {
-        // optimistic pass: independent loads (the compiler overlaps them), summed in order; a
-        // sentinel seen anywhere (rare) redoes the lane's sum in the same order with waits
+        // optimistic pass: independent loads (overlapped), summed in order; a sentinel seen anywhere
+        // (rare) redoes the lane's sum in the same order with waits
         double a = 0.0;
         bool ok = true;
 #pragma unroll 4
-        for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
-            const uint64_t v = __hip_atomic_load(src + j * W + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        for (int64_t m = lane; m < cnt; m += NT) {
+            const uint64_t v = __hip_atomic_load(src + slot(m) * W + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             ok = ok && v != kGridSumSentinel;
             a += __longlong_as_double((long long)v);
         }
         if (!ok) {
             a = 0.0;
-            for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock)
-                a += __longlong_as_double((long long)gridsum_wait(src + j * W + c, err));
+            for (int64_t m = lane; m < cnt; m += NT)
+                a += __longlong_as_double((long long)gridsum_wait(src + slot(m) * W + c, err));
         }
-        for (int64_t j = j0 + threadIdx.x; j < j1; j += kBlock)
-            src[j * W + c] = kGridSumSentinel;   // re-arm; ordered before the next launch by the boundary
-        res[c] = block_sum(a, sh);
+        for (int64_t m = lane; m < cnt; m += NT)
+            src[slot(m) * W + c] = kGridSumSentinel;   // re-arm; ordered before the next launch by the boundary
+        res[c] = NT == 64 ? wave_total(a) : block_sum(a, sh);
     }
 }
 
-// Called by every thread of every workgroup of a one-shot launch with the workgroup's W sums
-// (identical in all threads, e.g. from block_sum). Kernel-uniform control flow (barriers inside).
+// ---- workgroup slots (every thread of every workgroup calls these; barriers inside) ---------
+// The ticket (meaningful in thread 0 only; read at publish time). Call once the workgroup is known
+// to publish (after any launch-uniform early exit), best after its first stream loads are issued.
+__device__ __forceinline__ uint32_t gridsum_ticket(const GridSum &gs) {
+    uint32_t t = 0;
+    if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(blockIdx.x, gs.grp_log2)));
+    return t;
+}
+
+// final stage: after this workgroup's group sum (or one-level partial) was stored
 template <int W>
-__device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double *v, double *sh) {
-    const int64_t b = blockIdx.x, nwg = gridDim.x, grp = gs.grp;
-    const int sh2 = gs.grp_log2;
-    const int64_t ngroups = (nwg + grp - 1) >> sh2;
+__device__ __forceinline__ void gridsum_final(const GridSum &gs, double *sh) {
+    __shared__ uint32_t tk;
+    if (threadIdx.x == 0) tk = gridsum_draw(gridsum_counter(gs, kGridSumMaxGroups));
+    __syncthreads();
+    const bool last = tk == (uint32_t)(gs.ngroups - 1);
+    __syncthreads();
+    if (!last) return;
     double r[W];
-    if (grp == 1) {
+    gridsum_take<W, kBlock>(gs.gslots, 0, 1, 0, gs.ngroups, gs.err, sh, r);
+    if (threadIdx.x == 0) {
+        gridsum_reset(gridsum_counter(gs, kGridSumMaxGroups));
+#pragma unroll
+        for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+    }
+}
+
+// Called with the workgroup's W sums (identical in all threads, e.g. from block_sum) and the raw
+// ticket from gridsum_ticket. Kernel-uniform control flow.
+template <int W>
+__device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double *v, double *sh, uint32_t ticket) {
+    const int64_t b = blockIdx.x;
+    if (gs.grp_log2 < 0) {
         if (threadIdx.x == 0)
 #pragma unroll
             for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + b * W + c, v[c]);
-    } else {
-        if (threadIdx.x == 0)
-#pragma unroll
-            for (int c = 0; c < W; ++c) gridsum_put(gs.slots + b * W + c, v[c]);
-        const int64_t t = b - (grp - 1) - kGridSumLag;   // lagged role: group t/grp
-        if (t >= 0 && (t & (grp - 1)) == 0) {
-            const int64_t g = t >> sh2;
-            gridsum_take_range<W>(gs.slots, g * grp, g * grp + grp, gs.err, sh, r);
-            if (threadIdx.x == 0)
-#pragma unroll
-                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
-        }
-        const int64_t g = b >> sh2, lastm = (g * grp + grp - 1 < nwg) ? g * grp + grp - 1 : nwg - 1;
-        if (b == lastm && g * grp + grp - 1 + kGridSumLag >= nwg) {   // own-group role
-            gridsum_take_range<W>(gs.slots, g * grp, lastm + 1, gs.err, sh, r);
-            if (threadIdx.x == 0)
-#pragma unroll
-                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
-        }
+        gridsum_final<W>(gs, sh);
+        return;
     }
-    if (b == nwg - 1) {   // final role
-        gridsum_take_range<W>(gs.gslots, 0, ngroups, gs.err, sh, r);
-        if (threadIdx.x == 0)
+    __shared__ uint32_t tk;
+    if (threadIdx.x == 0) {
 #pragma unroll
-            for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+        for (int c = 0; c < W; ++c) gridsum_put(gs.slots + b * W + c, v[c]);
+        tk = ticket;
     }
-}
-
-// Wave-level gridsum: every WAVE of the launch is a unit (u = blockIdx * kWaves + wave) and
-// publishes its own wave sum, so a producer needs no workgroup barrier at all (the SpMV's dot
-// epilogue: one butterfly, one store by lane 0, and the wave is gone). The roles are those of
-// gridsum_publish over units instead of workgroups (a reducer is one wave: lane-strided by 64, then
-// the butterfly); a unit still only waits for lower units — earlier workgroups, or lower waves of its
-// own workgroup, which are resident beside it and never wait for it. The host prepares it with
-// nwg * kWaves units (gridsum_prepare). Every kernel that must give bit-identical sums to another
-// (the SpMV layouts) uses the same variant over the same rows per wave.
-template <int W>
-__device__ __forceinline__ void gridsum_take_range_wave(uint64_t *src, int64_t j0, int64_t j1, int32_t *err,
-                                                        double *res) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int c = 0; c < W; ++c) {
-        double a = 0.0;
-        bool ok = true;
-#pragma unroll 4
-        for (int64_t j = j0 + lane; j < j1; j += 64) {
-            const uint64_t v = __hip_atomic_load(src + j * W + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = ok && v != kGridSumSentinel;
-            a += __longlong_as_double((long long)v);
-        }
-        if (!ok) {
-            a = 0.0;
-            for (int64_t j = j0 + lane; j < j1; j += 64)
-                a += __longlong_as_double((long long)gridsum_wait(src + j * W + c, err));
-        }
-        for (int64_t j = j0 + lane; j < j1; j += 64) src[j * W + c] = kGridSumSentinel;
-        res[c] = wave_total(a);
-    }
-}
-
-// Called by every lane of every wave with the wave's W sums (identical in all lanes, e.g. from
-// wave_sum). No barrier; control flow is uniform per wave.
-template <int W>
-__device__ __forceinline__ void gridsum_publish_wave(const GridSum &gs, const double *v) {
-    const bool lane0 = (threadIdx.x & 63) == 0;
-    const int64_t u = (int64_t)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t nu = (int64_t)gridDim.x * kWaves, grp = gs.grp;
-    const int sh2 = gs.grp_log2;
-    const int64_t ngroups = (nu + grp - 1) >> sh2;
-    constexpr int64_t lag = kGridSumLag * kWaves;
+    __syncthreads();
+    const int64_t g = gridsum_group_of(b, gs.grp_log2);
+    int64_t base;
+    const int64_t cnt = gridsum_members(gs, g, base);
+    const bool last = tk == (uint32_t)(cnt - 1);
+    __syncthreads();
+    if (!last) return;
     double r[W];
-    if (grp == 1) {
+    gridsum_take<W, kBlock>(gs.slots, base, kGridSumL, 0, cnt, gs.err, sh, r);
+    if (threadIdx.x == 0) {
+        gridsum_reset(gridsum_counter(gs, g));
+#pragma unroll
+        for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
+    }
+    gridsum_final<W>(gs, sh);
+}
+
+// ---- wave slots (slot = tile * kWaves + wave; tile = the launch's logical tile index): no
+// workgroup barrier at all (the SpMV's dot epilogue: a DPP wave total, one store by lane 0, and
+// the wave is gone unless it reduces). Only wave 0 of a tile draws and holds the ticket. --------
+// the tile's ticket, in lane 0 of wave 0 (read at publish time, so its return is not waited on here)
+__device__ __forceinline__ uint32_t gridsum_ticket_wave(const GridSum &gs, int64_t tile) {
+    uint32_t t = 0;
+    if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tile, gs.grp_log2)));
+    return t;
+}
+
+template <int W>
+__device__ __forceinline__ void gridsum_final_wave(const GridSum &gs) {
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    uint32_t f = 0;
+    if (lane0) f = gridsum_draw(gridsum_counter(gs, kGridSumMaxGroups));
+    f = __builtin_amdgcn_readfirstlane(f);
+    if (f != (uint32_t)(gs.ngroups - 1)) return;
+    double r[W];
+    gridsum_take<W, 64>(gs.gslots, 0, 1, 0, gs.ngroups, gs.err, nullptr, r);
+    if (lane0) {
+        gridsum_reset(gridsum_counter(gs, kGridSumMaxGroups));
+#pragma unroll
+        for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+    }
+}
+
+// Called by every lane of every wave with the wave's W sums (identical in all lanes) and the raw
+// ticket from gridsum_ticket_wave. Control flow is uniform per wave.
+template <int W>
+__device__ __forceinline__ void gridsum_publish_wave(const GridSum &gs, const double *v, uint32_t ticket, int64_t tile) {
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t u = tile * kWaves + wave;
+    if (gs.grp_log2 < 0) {
         if (lane0)
 #pragma unroll
             for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + u * W + c, v[c]);
-    } else {
-        if (lane0)
-#pragma unroll
-            for (int c = 0; c < W; ++c) gridsum_put(gs.slots + u * W + c, v[c]);
-        const int64_t t = u - (grp - 1) - lag;   // lagged role: group t/grp
-        if (t >= 0 && (t & (grp - 1)) == 0) {
-            const int64_t g = t >> sh2;
-            gridsum_take_range_wave<W>(gs.slots, g * grp, g * grp + grp, gs.err, r);
-            if (lane0)
-#pragma unroll
-                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
-        }
-        const int64_t g = u >> sh2;
-        const int64_t lastm = (g * grp + grp - 1 < nu) ? g * grp + grp - 1 : nu - 1;
-        if (u == lastm && g * grp + grp - 1 + lag >= nu) {   // own-group role
-            gridsum_take_range_wave<W>(gs.slots, g * grp, lastm + 1, gs.err, r);
-            if (lane0)
-#pragma unroll
-                for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
-        }
+        gridsum_final_wave<W>(gs);
+        return;
     }
-    if (u == nu - 1) {   // final role
-        gridsum_take_range_wave<W>(gs.gslots, 0, ngroups, gs.err, r);
-        if (lane0)
+    if (lane0)
 #pragma unroll
-            for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+        for (int c = 0; c < W; ++c) gridsum_put(gs.slots + u * W + c, v[c]);
+    if (wave != 0) return;
+    const int64_t g = gridsum_group_of(tile, gs.grp_log2);
+    int64_t base;
+    const int64_t cnt = gridsum_members(gs, g, base);
+    // the asm pins the ticket's read here (its return hides behind the whole tile; a hoisted
+    // readfirstlane would wait for it before the gathers)
+    __asm__ volatile("" : "+v"(ticket));
+    if (__builtin_amdgcn_readfirstlane(ticket) != (uint32_t)(cnt - 1)) return;
+    double r[W];
+    gridsum_take<W, 64>(gs.slots, base, kGridSumL, gs.spw_log2, cnt << gs.spw_log2, gs.err, nullptr, r);
+    if (lane0) {
+        gridsum_reset(gridsum_counter(gs, g));
+#pragma unroll
+        for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
     }
+    gridsum_final_wave<W>(gs);
 }
 
-// host: a GridSum for a one-shot launch of nwg workgroups (or, for gridsum_publish_wave, nwg *
-// kWaves waves) with W (<= kGridSumMaxW) sums, written to out[0..W)
-int gridsum_prepare(Context *c, int64_t nwg, int W, double *out, GridSum *gs);
+// host: a GridSum for a one-shot launch of nt tiles (workgroups) with W (<= kGridSumMaxW) sums
+// written to out[0..W); spw = slots per tile: 1 (gridsum_publish) or kWaves (gridsum_publish_wave)
+int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs, int spw = 1);
 // reports (and clears) an expired gridsum wait; syncs the stream
 int gridsum_check(Context *c);
+
+// ---------------------------------------------------------------------------------------------
+// XCD-banded tile order (speed only, never correctness): workgroups are dealt round-robin over the
+// 8 XCDs (observed; MI355X_MICROARCH.md), so blocks b and b + 8 share an XCD and its L2. Tile
+// (slice) t = s_k + b/8 for block b, k = b mod 8, hands XCD k the CONTIGUOUS tiles [s_k, s_k + c_k):
+// a stencil row's x neighbours one grid line away (m rows = m/256 tiles: 12.4 at N = 10M, where
+// round-robin puts them on other XCDs and x is fetched ~3 times) are then read through the same L2.
+// TileMap{0, 0} is the identity. Bijective for any tile count.
+struct TileMap {
+    int64_t a;   // tiles / 8 (0 = identity)
+    int32_t r;   // tiles mod 8: classes k < r hold one more tile
+};
+inline TileMap tile_map_for(int64_t ntiles, bool banded) {
+    return banded && ntiles >= 64 ? TileMap{ntiles >> 3, (int32_t)(ntiles & 7)} : TileMap{0, 0};
+}
+__device__ __forceinline__ int64_t tile_of_block(TileMap tm) {
+    const int64_t b = blockIdx.x;
+    if (tm.a == 0) return b;
+    const int64_t k = b & 7, j = b >> 3;
+    return k * tm.a + (k < tm.r ? k : tm.r) + j;
+}
 
 // 16-byte vector accesses; *_nt = non-temporal (streamed data that is not re-read soon)
 typedef double dv2 __attribute__((ext_vector_type(2)));

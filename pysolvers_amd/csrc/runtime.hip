@@ -87,21 +87,29 @@ static int gridsum_arm(uint64_t **p, int64_t count, hipStream_t s) {
     return PSK_OK;
 }
 
-int gridsum_prepare(Context *c, int64_t nwg, int W, double *out, GridSum *gs) {
-    if (W < 1 || W > kGridSumMaxW || nwg < 1) return fail(PSK_ERR_ARG, "gridsum_prepare: bad geometry");
+int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs, int spw) {
+    if (W < 1 || W > kGridSumMaxW || nt < 1 || (spw != 1 && spw != kWaves))
+        return fail(PSK_ERR_ARG, "gridsum_prepare: bad geometry");
     if (!c->gs_err) {
         PSK_HIP(hipMalloc(&c->gs_err, sizeof(int32_t)));
         PSK_HIP(hipMemsetAsync(c->gs_err, 0, sizeof(int32_t), c->stream));
-        PSK_TRY(gridsum_arm(&c->gs_gslots, (int64_t)kMaxGrid * kGridSumMaxW, c->stream));
+        const size_t cb = (size_t)(kGridSumMaxGroups + 1) * kGridSumCntStride * sizeof(uint32_t);
+        PSK_HIP(hipMalloc(&c->gs_cnt, cb));
+        PSK_HIP(hipMemsetAsync(c->gs_cnt, 0, cb, c->stream));
+        PSK_TRY(gridsum_arm(&c->gs_gslots, (int64_t)kGridSumMaxGroups * kGridSumMaxW, c->stream));
     }
     gs->out = out;
-    gs->grp_log2 = gridsum_grp_log2(nwg);
-    gs->grp = (int64_t)1 << gs->grp_log2;
+    gs->nt = nt;
+    gs->spw_log2 = spw == 1 ? 0 : 2;
+    gs->grp_log2 = gridsum_grp_log2(nt);
+    gs->ngroups = gridsum_ngroups(nt, gs->grp_log2, gs->spw_log2);
+    if (gs->ngroups > kGridSumMaxGroups) return fail(PSK_ERR_ARG, "gridsum_prepare: too many groups");
     gs->err = c->gs_err;
     gs->gslots = c->gs_gslots;
+    gs->cnt = c->gs_cnt;
     gs->slots = nullptr;
-    if (gs->grp == 1) return PSK_OK;
-    const int64_t need = nwg * W;
+    if (gs->grp_log2 < 0) return PSK_OK;
+    const int64_t need = nt * spw * W;
     if (need > c->gs_cap) {
         int64_t cap = c->gs_cap > 0 ? c->gs_cap : (int64_t)1 << 20;
         while (cap < need) cap *= 2;
@@ -122,7 +130,7 @@ int gridsum_check(Context *c) {
     PSK_HIP(hipStreamSynchronize(c->stream));
     if (h == 0) return PSK_OK;
     PSK_HIP(hipMemsetAsync(c->gs_err, 0, sizeof(int32_t), c->stream));
-    return fail(PSK_ERR_HIP, "grid reduction: a partial sum was never published (bounded wait expired)");
+    return fail(PSK_ERR_HIP, "grid reduction: an issued partial-sum store never landed (1.3 s wait expired)");
 }
 
 int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s) {

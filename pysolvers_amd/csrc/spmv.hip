@@ -30,34 +30,33 @@ __device__ __forceinline__ double ld_stream(const double *p) { return __builtin_
 
 // The dot epilogue of every SpMV kernel (p.Ap, q_0.u, ||b-Ax||^2): one partial per WAVE, published
 // by gridsum_publish_wave — no workgroup barrier at the end of a slice. Both layouts sum 64 rows per
-// wave in the same lanes (256-row tiles / slices), so their grid sums are bit-identical.
-// (PSK_SPMV_BLOCK_PARTIALS: the previous per-workgroup epilogue, kept for same-box A/B runs.)
-#ifdef PSK_SPMV_BLOCK_PARTIALS
-constexpr int kSpmvUnitsPerWg = 1;
-__device__ __forceinline__ void spmv_publish(const GridSum &gs, double acc, double *sh) {
-    const double bs = block_sum(acc, sh);
-    gridsum_publish<1>(gs, &bs, sh);
+// wave in the same lanes (256-row tiles / slices), so their grid sums are bit-identical. The wave's
+// gridsum ticket is drawn once its stream loads are in flight (spmv_ticket).
+template <int MODE>
+__device__ __forceinline__ bool spmv_publishes(const GridSum &gs) {
+    return MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr);
 }
-#else
-constexpr int kSpmvUnitsPerWg = kWaves;
-__device__ __forceinline__ void spmv_publish(const GridSum &gs, double acc, double *) {
+template <int MODE>
+__device__ __forceinline__ uint32_t spmv_ticket(const GridSum &gs, int64_t t) {
+    return spmv_publishes<MODE>(gs) ? gridsum_ticket_wave(gs, t) : 0u;
+}
+__device__ __forceinline__ void spmv_publish(const GridSum &gs, double acc, uint32_t ticket, int64_t t) {
     const double ws = wave_total(acc);
-    gridsum_publish_wave<1>(gs, &ws);
+    gridsum_publish_wave<1>(gs, &ws, ticket, t);
 }
-#endif
 
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(
     int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
     const double *__restrict__ vals, const double *__restrict__ x, double *__restrict__ y,
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs,
-    const int32_t *__restrict__ done, int32_t nnz) {
+    const int32_t *__restrict__ done, int32_t nnz, TileMap tm) {
     if (done != nullptr && *done != 0) return;
     constexpr int KU = kChunk / kBlock;   // staged entries per lane per chunk
     __shared__ double prod[kChunk + kBlock];   // + a dump row for lanes past the chunk's end
-    __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
-    const int64_t r0 = (int64_t)blockIdx.x * trows;
+    const int64_t t = tile_of_block(tm);
+    const int64_t r0 = t * trows;
     const int64_t r1 = (r0 + trows < n) ? r0 + trows : n;
     const int32_t last = nnz > 0 ? nnz - 1 : 0;   // colidx/vals hold at least one (dummy) entry
     const int32_t e0 = rowptr[r0], e1 = rowptr[r1];
@@ -76,6 +75,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             vv[k] = ld_stream(vals + ee);
         }
     }
+    const uint32_t ticket = spmv_ticket<MODE>(gs, t);
     const int64_t row = r0 + tid;
     const bool has = tid < trows && row < r1;
     const int64_t rowc = has ? row : r0;   // a valid row for the unconditional epilogue loads
@@ -145,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
         }
     }
     // only the residual mode may be called without partials (AMG smoothing); kernel-uniform test
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) spmv_publish(gs, acc, sh);
+    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, acc, ticket, t);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -286,13 +286,12 @@ template <int MODE, int DK, int UW>
 __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
     int64_t n, const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ sdict,
     const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
-    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
+    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done, TileMap tm) {
     constexpr int NP = (UW + 1) / 2;                 // packed column words per lane
     constexpr int NI = DK > 0 ? (UW + 3) / 4 : 0;    // dictionary index words per lane
-    __shared__ double sh[kWaves];
     const int32_t dn = *(done ? done : &g_spmv_never_done);   // tested once the stream is in flight
     const int tid = threadIdx.x;
-    const int64_t t = blockIdx.x, row = t * kSlice + tid;
+    const int64_t t = tile_of_block(tm), row = t * kSlice + tid;
     const bool has = row < n;
     const int32_t *pword = spcol + t * (int64_t)((NP + NI) * kSlice) + tid;
     uint32_t cw[NP], iw[NI > 0 ? NI : 1];
@@ -331,6 +330,7 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
         }
         return;
     }
+    const uint32_t ticket = spmv_ticket<MODE>(gs, t);
     const int32_t row32 = (int32_t)row;
     int32_t cc[UW];
     double xv[UW];
@@ -351,7 +351,7 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
         if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
     if (MODE == kSpmvDot) eq = diag_x<UW>(cc, xv, row32, x, has);
     const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) spmv_publish(gs, acc, sh);
+    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, acc, ticket, t);
 }
 
 // General sliced layout (per-slice widths, offsets and formats loaded from the slice header).
@@ -362,11 +362,10 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const int32_t *__restrict__ scol, const int32_t *__restrict__ spcol, const double *__restrict__ sval,
     const double *__restrict__ sdict,
     const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
-    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done) {
+    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done, TileMap tm) {
     if (done != nullptr && *done != 0) return;
-    __shared__ double sh[kWaves];
     const int tid = threadIdx.x;
-    const int64_t t = blockIdx.x, row = t * kSlice + tid;
+    const int64_t t = tile_of_block(tm), row = t * kSlice + tid;
     const bool has = row < n;
     const int64_t o = soff[t];
     const int w = (int)((soff[t + 1] - o) / kSlice);
@@ -375,6 +374,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const int32_t *pword = spcol + wo;                                         // packed column words
     const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
     const DictRegs dv = load_dict<DK>(sdict);
+    const uint32_t ticket = spmv_ticket<MODE>(gs, t);
     const int32_t row32 = (int32_t)row;
     double eq = 0.0;
     if (has) {
@@ -460,7 +460,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
         }
     }
     const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr)) spmv_publish(gs, acc, sh);
+    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, acc, ticket, t);
 }
 
 // per slice: widest row, and the largest |column - row| of its entries (saturated to int32)
@@ -752,6 +752,15 @@ int tile_rows_for(int64_t n, int64_t nnz) {
     return r;
 }
 
+// PSK_SPMV_XCD_BANDS=0: tiles in block order (A/B runs); default: XCD-banded (psk_internal.hpp)
+static bool spmv_xcd_bands() {
+    static const bool on = [] {
+        const char *e = std::getenv("PSK_SPMV_XCD_BANDS");
+        return !(e && std::atoi(e) == 0);
+    }();
+    return on;
+}
+
 static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) / A->tile_rows; }
 
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
@@ -761,22 +770,23 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     PSK_TRY(ctx(&c));
     const bool sliced = A->sl_off != nullptr;
     const int64_t nwg = sliced ? (A->n + kSlice - 1) / kSlice : spmv_tiles(A);
-    GridSum gs{nullptr, nullptr, nullptr, 1, 0, nullptr};
-    if (partial) PSK_TRY(gridsum_prepare(c, nwg * kSpmvUnitsPerWg, 1, partial, &gs));
+    GridSum gs{nullptr, nullptr, nullptr, nullptr, 0, 0, -1, 0, nullptr};
+    if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs, kWaves));
     dim3 gd((unsigned)nwg), bd(kBlock);
+    const TileMap tm = tile_map_for(nwg, spmv_xcd_bands());
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
 #define PSK_UNI_LAUNCH(M, DK, UW)                                                                              \
     hipLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, A->n, A->sl_pcol, A->sl_val, A->sl_dict, \
-                       x, y, aux_d, aux_q, gs, done_flag)
+                       x, y, aux_d, aux_q, gs, done_flag, tm)
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
     do {                                                                                                       \
         switch (uw) {                                                                                          \
         case 0:                                                                                                \
             hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff,         \
                                A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, \
-                               done_flag);                                                                     \
+                               done_flag, tm);                                                                     \
             break;                                                                                             \
         case 1: PSK_UNI_LAUNCH(M, DK, 1); break;                                                               \
         case 2: PSK_UNI_LAUNCH(M, DK, 2); break;                                                               \
@@ -815,7 +825,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     const int32_t nz = (int32_t)A->nnz;
 #define PSK_SPMV_LAUNCH(M)                                                                                  \
     hipLaunchKernelGGL(spmv_kernel<M>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals, x, y, aux_d, \
-                       aux_q, gs, done_flag, nz)
+                       aux_q, gs, done_flag, nz, tm)
     switch (mode) {
     case kSpmvPlain: PSK_SPMV_LAUNCH(kSpmvPlain); break;
     case kSpmvDot: PSK_SPMV_LAUNCH(kSpmvDot); break;

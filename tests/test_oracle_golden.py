@@ -50,6 +50,23 @@ def test_spmv_exact(tag):
     assert np.array_equal(native.csr_matvec(A, d[tag + "_x"]), y_ref)     # plain-C restatement
 
 
+@pytest.mark.parametrize("m", [1, 2, 3, 5, 64, 300])
+def test_fd_stencil_matches_csr_matvec(m):
+    """oracle.fdlap.FDStencil (the matrix-free restatement the 16384^2 GPU tests use) against scipy
+    csr_matvec on the reference generator's CSR: bit for bit, including signed zeros."""
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    S = fdlap.FDStencil(-1.0, 1.0, m)
+    assert S.shape == A.shape
+    assert np.array_equal(S.diagonal(), A.diagonal())
+    rng = np.random.default_rng(m)
+    for x in (rng.random(m * m), rng.standard_normal(m * m), np.where(rng.random(m * m) < 0.5, -0.0, 0.0)):
+        y, yr = S @ x, A @ x
+        assert np.array_equal(y.view(np.int64), yr.view(np.int64))
+    if m == 64:
+        d = load_golden("spmv.npz")
+        assert np.array_equal(S @ d["fd64_x"], d["fd64_y"])
+
+
 def test_csr_diagonal_exact():
     d = load_golden("spmv.npz")
     for tag in ("fd64", "dh8"):
