@@ -37,6 +37,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 METRIC = "CG iterations/sec + SpMV GB/s vs HBM roofline, 5-pt Laplacian N=10M"
+# libpsk times every EVENT_STRIDE-th SpMV launch of a timed region between two HIP events (an event
+# pair around every launch cost ~5% of the iteration rate at N = 10M)
+EVENT_STRIDE = 8
 METRIC_SIDE = 3163              # FDLaplacian2D side of the metric's N = 10M: n = 10,004,569
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 
@@ -201,8 +204,8 @@ def main():
                          **pmc,
                          "algorithmic_bytes_per_launch": blay, "avg_launch_ms": spmv_ms_med,
                          "launches": spmv_launches, "layout": lname,
-                         "timing": "HIP events libpsk records on its own stream around every SpMV launch of the "
-                                   "median timed region (rank 0's events; max over ranks at N > 1)",
+                         "timing": "HIP events libpsk records on its own stream around every %d-th SpMV launch "
+                                   "of the median timed region (rank 0's events; max over ranks at N > 1)" % EVENT_STRIDE,
                          "csr_bytes_per_launch": bspmv,
                          "csr_count_over_time_GBps": csr_eq,
                          "csr_count_note": "SURVEY §8d's CSR byte count (12 nnz + 4(n+1) + 16n) over the same time: "
@@ -213,6 +216,10 @@ def main():
             "setup_s": sys_.setup_s,
         }
         if world == 1:
+            # what the sampled per-launch HIP events of the timed regions cost: the same regions without them
+            ne = sys_.regions(args.steps, 0, 3, barrier, dist, events=False)
+            out["regions_without_kernel_events"] = {"it_s": [args.steps / r[0] for r in ne],
+                                                    "median_it_s": args.steps / median([r[0] for r in ne])}
             # the same matrix, plain y = A x launches back to back (no dot epilogue, no solver kernels
             # in between): how much of the in-loop SpMV time is the PCG context
             bms = ctypes.c_double()
@@ -312,15 +319,16 @@ class PcgSystem:
     def run(self, iters, time_kernels):
         N = self.N
         ctl = N.PskCtl(maxiter=iters, tau=0.0, fail_on_maxiter=0, restart=0, check_every=0,
-                       time_kernels=int(time_kernels))
+                       time_kernels=EVENT_STRIDE if time_kernels else 0)
         res = N.PskResult()
         N.check(N.lib.psk_pcg(self.A, self.M, self.db, self.dsol, ctypes.byref(ctl), ctypes.byref(res), None,
                               N.PSK_DEVICE), "psk_pcg")
         return res
 
-    def regions(self, steps, warmup, repeats, barrier, dist):
+    def regions(self, steps, warmup, repeats, barrier, dist, events=True):
         """`repeats` timed regions of exactly `steps` iterations, each bracketed by barrier + device
-        sync; per region the max over ranks of (wall time, mean SpMV launch time)."""
+        sync; per region the max over ranks of (wall time, mean SpMV launch time). events: libpsk
+        records HIP events around every SpMV launch (the roofline's kernel time)."""
         N = self.N
         if warmup > 0:
             r = self.run(warmup, False)
@@ -330,7 +338,7 @@ class PcgSystem:
             barrier()
             N.check(N.lib.psk_synchronize(), "sync")
             t0 = time.perf_counter()
-            res = self.run(steps, True)
+            res = self.run(steps, events)
             N.check(N.lib.psk_synchronize(), "sync")
             barrier()
             dt = time.perf_counter() - t0

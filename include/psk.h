@@ -81,7 +81,8 @@ typedef struct psk_ctl {
     int32_t fail_on_maxiter;  /* CommonSolverArgs.failOnMaxiter */
     int32_t restart;          /* GMRES only: 0 = reference non-restarted (Krylov dim = maxiter) */
     int32_t check_every;      /* host polls the device status every N iterations; 0 = auto */
-    int32_t time_kernels;     /* 1 = HIP-event timing of the SpMV launches (psk_result.spmv_ms) */
+    int32_t time_kernels;     /* S > 0: HIP-event timing of every S-th SpMV launch (iterations k with
+                                 k % S == 0; psk_result.spmv_ms); 0 = off */
     double  norm_b;           /* GMRES: > 0 = ||b|| in the caller's norm (CommonSolverArgs.norm,
                                  GMRESSolver.py:66) for the threshold tau*||b|| and psk_result.norm_b;
                                  0 = the device 2-norm. PCG ignores it (a non-2-norm PCG is driven by
@@ -96,8 +97,8 @@ typedef struct psk_result {
     double  resid_recursive;  /* last recursive residual estimate */
     double  norm_b;           /* ||b|| */
     double  loop_ms;          /* device wall time of the solve (HIP events) */
-    double  spmv_ms;          /* mean SpMV launch duration when ctl.time_kernels */
-    int64_t spmv_launches;    /* number of SpMV launches (timed ones when ctl.time_kernels) */
+    double  spmv_ms;          /* mean duration of the timed SpMV launches when ctl.time_kernels */
+    int64_t spmv_launches;    /* number of SpMV launches (the timed ones when ctl.time_kernels) */
     int64_t hist_len;         /* valid entries written to hist */
     char    msg[256];         /* SolveStatus.msg() */
 } psk_result;

@@ -333,22 +333,20 @@ constexpr int64_t kGridSumL = (int64_t)1 << kGridSumLLog;   // groups interleave
 constexpr int kGridSumCntStride = 64;
 constexpr uint64_t kGridSumSentinel = 0x7FF0000000000001ull;   // sNaN: arithmetic never produces it
 constexpr int kGridSumMaxW = 4;
-static_assert(kWaves == 4, "gridsum_prepare encodes kWaves slots per tile as spw_log2 = 2");
 constexpr int64_t kGridSumMaxGroups = kMaxGrid;
 // a wait on an already-issued store that has not landed after ~1.3 s (s_memrealtime, 100 MHz) is
 // reported (gridsum_check) instead of hanging the launch: never expected
 constexpr uint64_t kGridSumWaitTicks = (uint64_t)1 << 27;
 
 struct GridSum {
-    uint64_t *slots;    // nt*spw*W slot partials (two-level launches)
+    uint64_t *slots;    // W partials per tile, group-major (two-level launches)
     uint64_t *gslots;   // ngroups*W group sums (one-level: the slots themselves)
     uint32_t *cnt;      // counter g at cnt[g * kGridSumCntStride] (g < kGridSumMaxGroups), the final one at
                         // g = kGridSumMaxGroups; zero between launches
     double *out;        // the W grid sums
     int64_t nt;         // tiles (workgroups) of the launch
-    int64_t ngroups;    // groups of tiles (one-level: nt * spw)
+    int64_t ngroups;    // groups of tiles (one-level: nt)
     int32_t grp_log2;   // tiles of a full group = 2^grp_log2; -1 = one level (nt <= kBlock)
-    int32_t spw_log2;   // slots per tile: 1 (workgroup sums) or kWaves (wave sums)
     int32_t *err;       // set when a wait expires (reported by gridsum_check)
 };
 
@@ -361,8 +359,8 @@ inline int32_t gridsum_grp_log2(int64_t nt) {
     while (ng(l) > kGridSumMaxGroups) ++l;
     return l;
 }
-inline int64_t gridsum_ngroups(int64_t nt, int32_t gl, int32_t spw_log2) {
-    if (gl < 0) return nt << spw_log2;
+inline int64_t gridsum_ngroups(int64_t nt, int32_t gl) {
+    if (gl < 0) return nt;
     const int64_t S = kGridSumL << gl, full = nt / S, tail = nt - full * S;
     return full * kGridSumL + (tail < kGridSumL ? tail : kGridSumL);
 }
@@ -406,37 +404,59 @@ __device__ __forceinline__ uint64_t gridsum_wait(const uint64_t *sl, int32_t *er
     return bits;
 }
 
-// sum over members m in [0, cnt) of src[slot(m)*W + c], slot(m) = (base + (m >> sl) * stride) << sl
-// | (m & (2^sl - 1)) — member tiles in order, each tile's 2^sl slots in order — lane-strided over
-// NT lanes (lane t sums m = t, t + NT, ... in order), then the lanes' fixed-order total; every slot
-// is re-armed. NT = kBlock: whole workgroup (block_sum); NT = 64: one wave (wave_total).
+// sum of src[(start + m)*W + c] over m in [0, cnt), lane-strided over NT lanes (lane t sums m = t,
+// t + NT, ... in order), then the lanes' fixed-order total; every slot is re-armed. NT = kBlock:
+// whole workgroup (block_sum); NT = 64: one wave (wave_total). A group's slots are contiguous
+// (gridsum_slot), so is the group-sum array.
 template <int W, int NT>
-__device__ __forceinline__ void gridsum_take(uint64_t *src, int64_t base, int64_t stride, int32_t sl, int64_t cnt,
-                                             int32_t *err, double *sh, double *res) {
-    const int lane = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
-    const int64_t lo = ((int64_t)1 << sl) - 1;
-    auto slot = [&](int64_t m) { return ((base + (m >> sl) * stride) << sl) | (m & lo); };
+__device__ __forceinline__ void gridsum_take(uint64_t *src, int64_t start, int64_t cnt, int32_t *err, double *sh,
+                                             double *res) {
+    // B loads per lane in flight at once: the reductions of the launch's last tiles are its tail
+    // (every group reducer and then the final one), one memory round trip per batch. 32-bit
+    // offsets from one base (a group holds < 2^26 slots) keep the batch in few registers.
+    constexpr int B = NT == 64 ? 8 : 4;
+    const uint32_t lane = NT == 64 ? (threadIdx.x & 63) : threadIdx.x;
+    const uint32_t n = (uint32_t)cnt;
+    uint64_t *p = src + start * W;
 #pragma unroll
     for (int c = 0; c < W; ++c) {
-        // optimistic pass: independent loads (overlapped), summed in order; a sentinel seen anywhere
-        // (rare) redoes the lane's sum in the same order with waits
+        // optimistic pass: a batch of independent loads, summed in member order; a sentinel seen
+        // anywhere (rare: a store still in flight) redoes the lane's sum in the same order with waits
         double a = 0.0;
         bool ok = true;
-#pragma unroll 4
-        for (int64_t m = lane; m < cnt; m += NT) {
-            const uint64_t v = __hip_atomic_load(src + slot(m) * W + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            ok = ok && v != kGridSumSentinel;
-            a += __longlong_as_double((long long)v);
+        for (uint32_t m0 = lane; m0 < n; m0 += NT * B) {
+            // unpredicated loads (index clamped with a min); members past the end then add -0.0,
+            // which leaves every sum (+0.0 included) unchanged
+            uint64_t v[B];
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                const uint32_t m = __builtin_elementwise_min(m0 + (uint32_t)(i * NT), n - 1);
+                v[i] = __hip_atomic_load(p + (m * W + c), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int i = 0; i < B; ++i) {
+                const uint64_t x = m0 + (uint32_t)(i * NT) < n ? v[i] : 0x8000000000000000ull;
+                ok = ok && x != kGridSumSentinel;
+                a += __longlong_as_double((long long)x);
+            }
         }
         if (!ok) {
             a = 0.0;
-            for (int64_t m = lane; m < cnt; m += NT)
-                a += __longlong_as_double((long long)gridsum_wait(src + slot(m) * W + c, err));
+            for (uint32_t m = lane; m < n; m += NT)
+                a += __longlong_as_double((long long)gridsum_wait(p + (m * W + c), err));
         }
-        for (int64_t m = lane; m < cnt; m += NT)
-            src[slot(m) * W + c] = kGridSumSentinel;   // re-arm; ordered before the next launch by the boundary
+        for (uint32_t m = lane; m < n; m += NT)
+            p[m * W + c] = kGridSumSentinel;   // re-arm; ordered before the next launch by the boundary
         res[c] = NT == 64 ? wave_total(a) : block_sum(a, sh);
     }
+}
+
+// slot of tile t in the two-level layout: group-major, so a group's slots (member tiles in order)
+// are contiguous
+__device__ __forceinline__ int64_t gridsum_slot(const GridSum &gs, int64_t t) {
+    const int32_t gl = gs.grp_log2;
+    const int64_t g = gridsum_group_of(t, gl), j = (t & ((kGridSumL << gl) - 1)) >> kGridSumLLog;
+    return (g << gl) + j;
 }
 
 // ---- workgroup slots (every thread of every workgroup calls these; barriers inside) ---------
@@ -458,7 +478,7 @@ __device__ __forceinline__ void gridsum_final(const GridSum &gs, double *sh) {
     __syncthreads();
     if (!last) return;
     double r[W];
-    gridsum_take<W, kBlock>(gs.gslots, 0, 1, 0, gs.ngroups, gs.err, sh, r);
+    gridsum_take<W, kBlock>(gs.gslots, 0, gs.ngroups, gs.err, sh, r);
     if (threadIdx.x == 0) {
         gridsum_reset(gridsum_counter(gs, kGridSumMaxGroups));
 #pragma unroll
@@ -481,7 +501,7 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
     __shared__ uint32_t tk;
     if (threadIdx.x == 0) {
 #pragma unroll
-        for (int c = 0; c < W; ++c) gridsum_put(gs.slots + b * W + c, v[c]);
+        for (int c = 0; c < W; ++c) gridsum_put(gs.slots + gridsum_slot(gs, b) * W + c, v[c]);
         tk = ticket;
     }
     __syncthreads();
@@ -492,7 +512,7 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
     __syncthreads();
     if (!last) return;
     double r[W];
-    gridsum_take<W, kBlock>(gs.slots, base, kGridSumL, 0, cnt, gs.err, sh, r);
+    gridsum_take<W, kBlock>(gs.slots, g << gs.grp_log2, cnt, gs.err, sh, r);
     if (threadIdx.x == 0) {
         gridsum_reset(gridsum_counter(gs, g));
 #pragma unroll
@@ -501,11 +521,26 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
     gridsum_final<W>(gs, sh);
 }
 
-// ---- wave slots (slot = tile * kWaves + wave; tile = the launch's logical tile index): no
-// workgroup barrier at all (the SpMV's dot epilogue: a DPP wave total, one store by lane 0, and
-// the wave is gone unless it reduces). Only wave 0 of a tile draws and holds the ticket. --------
-// the tile's ticket, in lane 0 of wave 0 (read at publish time, so its return is not waited on here)
-__device__ __forceinline__ uint32_t gridsum_ticket_wave(const GridSum &gs, int64_t tile) {
+// ---- per-wave partials combined in LDS (the SpMV's dot epilogue) ------------------------------
+// Each wave of a tile writes its wave total (DPP, no shuffle traffic) to LDS and counts itself in
+// with an LDS atomic; the wave that counts last adds the kWaves totals in wave order and publishes
+// the tile's ONE slot, then plays the tile's part in the ticket protocol. One write-through store
+// per tile instead of one per wave: an 8-B sc1 store is a fabric write of its own, and 4 per tile
+// cost ~7 us of a 57-us SpMV at N = 10M (probe builds -DPSK_LAB_GS_*, profiles/r3_gridsum_lab.txt).
+// No workgroup barrier at the end; the one barrier (arming the LDS counter) sits where every wave
+// waits for its stream loads anyway.
+template <int W>
+struct GridSumTile {
+    uint32_t cnt;
+    uint32_t ticket;
+    double part[kWaves * W];
+};
+// every thread, once the tile's stream loads are issued and it is known to publish (after any
+// launch-uniform early exit); returns the raw ticket (thread 0), read at publish time
+template <int W>
+__device__ __forceinline__ uint32_t gridsum_tile_begin(const GridSum &gs, GridSumTile<W> &L, int64_t tile) {
+    if (threadIdx.x == 0) L.cnt = 0;
+    __syncthreads();
     uint32_t t = 0;
     if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tile, gs.grp_log2)));
     return t;
@@ -519,7 +554,7 @@ __device__ __forceinline__ void gridsum_final_wave(const GridSum &gs) {
     f = __builtin_amdgcn_readfirstlane(f);
     if (f != (uint32_t)(gs.ngroups - 1)) return;
     double r[W];
-    gridsum_take<W, 64>(gs.gslots, 0, 1, 0, gs.ngroups, gs.err, nullptr, r);
+    gridsum_take<W, 64>(gs.gslots, 0, gs.ngroups, gs.err, nullptr, r);
     if (lane0) {
         gridsum_reset(gridsum_counter(gs, kGridSumMaxGroups));
 #pragma unroll
@@ -527,33 +562,47 @@ __device__ __forceinline__ void gridsum_final_wave(const GridSum &gs) {
     }
 }
 
-// Called by every lane of every wave with the wave's W sums (identical in all lanes) and the raw
-// ticket from gridsum_ticket_wave. Control flow is uniform per wave.
+// every lane of every wave, with the wave's W totals (uniform) and the raw ticket; no barrier
 template <int W>
-__device__ __forceinline__ void gridsum_publish_wave(const GridSum &gs, const double *v, uint32_t ticket, int64_t tile) {
+__device__ __forceinline__ void gridsum_tile_publish(const GridSum &gs, GridSumTile<W> &L, const double *v,
+                                                     uint32_t ticket, int64_t tile) {
     const bool lane0 = (threadIdx.x & 63) == 0;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t u = tile * kWaves + wave;
+    uint32_t old = 0;
+    if (lane0) {
+#pragma unroll
+        for (int c = 0; c < W; ++c) L.part[wave * W + c] = v[c];
+        if (threadIdx.x == 0) L.ticket = ticket;
+        // this wave's LDS writes land before its count (release, LDS only)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        old = atomicAdd(&L.cnt, 1u);
+    }
+    if (__builtin_amdgcn_readfirstlane(old) != kWaves - 1) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    double s[W];
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+        s[c] = L.part[c];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) s[c] += L.part[w * W + c];   // wave order
+    }
+    const uint32_t tk = L.ticket;
     if (gs.grp_log2 < 0) {
         if (lane0)
 #pragma unroll
-            for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + u * W + c, v[c]);
+            for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + tile * W + c, s[c]);
         gridsum_final_wave<W>(gs);
         return;
     }
     if (lane0)
 #pragma unroll
-        for (int c = 0; c < W; ++c) gridsum_put(gs.slots + u * W + c, v[c]);
-    if (wave != 0) return;
+        for (int c = 0; c < W; ++c) gridsum_put(gs.slots + gridsum_slot(gs, tile) * W + c, s[c]);
     const int64_t g = gridsum_group_of(tile, gs.grp_log2);
     int64_t base;
     const int64_t cnt = gridsum_members(gs, g, base);
-    // the asm pins the ticket's read here (its return hides behind the whole tile; a hoisted
-    // readfirstlane would wait for it before the gathers)
-    __asm__ volatile("" : "+v"(ticket));
-    if (__builtin_amdgcn_readfirstlane(ticket) != (uint32_t)(cnt - 1)) return;
+    if (tk != (uint32_t)(cnt - 1)) return;
     double r[W];
-    gridsum_take<W, 64>(gs.slots, base, kGridSumL, gs.spw_log2, cnt << gs.spw_log2, gs.err, nullptr, r);
+    gridsum_take<W, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
     if (lane0) {
         gridsum_reset(gridsum_counter(gs, g));
 #pragma unroll
@@ -563,8 +612,8 @@ __device__ __forceinline__ void gridsum_publish_wave(const GridSum &gs, const do
 }
 
 // host: a GridSum for a one-shot launch of nt tiles (workgroups) with W (<= kGridSumMaxW) sums
-// written to out[0..W); spw = slots per tile: 1 (gridsum_publish) or kWaves (gridsum_publish_wave)
-int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs, int spw = 1);
+// written to out[0..W)
+int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs);
 // reports (and clears) an expired gridsum wait; syncs the stream
 int gridsum_check(Context *c);
 

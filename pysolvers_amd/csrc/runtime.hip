@@ -87,8 +87,8 @@ static int gridsum_arm(uint64_t **p, int64_t count, hipStream_t s) {
     return PSK_OK;
 }
 
-int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs, int spw) {
-    if (W < 1 || W > kGridSumMaxW || nt < 1 || (spw != 1 && spw != kWaves))
+int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs) {
+    if (W < 1 || W > kGridSumMaxW || nt < 1)
         return fail(PSK_ERR_ARG, "gridsum_prepare: bad geometry");
     if (!c->gs_err) {
         PSK_HIP(hipMalloc(&c->gs_err, sizeof(int32_t)));
@@ -100,16 +100,15 @@ int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs, int
     }
     gs->out = out;
     gs->nt = nt;
-    gs->spw_log2 = spw == 1 ? 0 : 2;
     gs->grp_log2 = gridsum_grp_log2(nt);
-    gs->ngroups = gridsum_ngroups(nt, gs->grp_log2, gs->spw_log2);
+    gs->ngroups = gridsum_ngroups(nt, gs->grp_log2);
     if (gs->ngroups > kGridSumMaxGroups) return fail(PSK_ERR_ARG, "gridsum_prepare: too many groups");
     gs->err = c->gs_err;
     gs->gslots = c->gs_gslots;
     gs->cnt = c->gs_cnt;
     gs->slots = nullptr;
     if (gs->grp_log2 < 0) return PSK_OK;
-    const int64_t need = nt * spw * W;
+    const int64_t need = (gs->ngroups << gs->grp_log2) * W;   // group-major slots (gridsum_slot)
     if (need > c->gs_cap) {
         int64_t cap = c->gs_cap > 0 ? c->gs_cap : (int64_t)1 << 20;
         while (cap < need) cap *= 2;

@@ -28,21 +28,23 @@ namespace psk {
 __device__ __forceinline__ int32_t ld_stream(const int32_t *p) { return __builtin_nontemporal_load(p); }
 __device__ __forceinline__ double ld_stream(const double *p) { return __builtin_nontemporal_load(p); }
 
-// The dot epilogue of every SpMV kernel (p.Ap, q_0.u, ||b-Ax||^2): one partial per WAVE, published
-// by gridsum_publish_wave — no workgroup barrier at the end of a slice. Both layouts sum 64 rows per
-// wave in the same lanes (256-row tiles / slices), so their grid sums are bit-identical. The wave's
-// gridsum ticket is drawn once its stream loads are in flight (spmv_ticket).
+// The dot epilogue of every SpMV kernel (p.Ap, q_0.u, ||b-Ax||^2): one DPP total per WAVE, the
+// tile's wave totals added in LDS in wave order and published as one gridsum slot per tile
+// (gridsum_tile_*, psk_internal.hpp) — no workgroup barrier at the end of a slice. Both layouts sum
+// 64 rows per wave in the same lanes over the same 256-row tiles, so their grid sums are
+// bit-identical.
 template <int MODE>
 __device__ __forceinline__ bool spmv_publishes(const GridSum &gs) {
     return MODE != kSpmvPlain && MODE != kSpmvAdd && (MODE != kSpmvResid || gs.out != nullptr);
 }
 template <int MODE>
-__device__ __forceinline__ uint32_t spmv_ticket(const GridSum &gs, int64_t t) {
-    return spmv_publishes<MODE>(gs) ? gridsum_ticket_wave(gs, t) : 0u;
+__device__ __forceinline__ uint32_t spmv_begin(const GridSum &gs, GridSumTile<1> &L, int64_t t) {
+    return spmv_publishes<MODE>(gs) ? gridsum_tile_begin<1>(gs, L, t) : 0u;
 }
-__device__ __forceinline__ void spmv_publish(const GridSum &gs, double acc, uint32_t ticket, int64_t t) {
+__device__ __forceinline__ void spmv_publish(const GridSum &gs, GridSumTile<1> &L, double acc, uint32_t ticket,
+                                             int64_t t) {
     const double ws = wave_total(acc);
-    gridsum_publish_wave<1>(gs, &ws, ticket, t);
+    gridsum_tile_publish<1>(gs, L, &ws, ticket, t);
 }
 
 template <int MODE>
@@ -75,7 +77,8 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             vv[k] = ld_stream(vals + ee);
         }
     }
-    const uint32_t ticket = spmv_ticket<MODE>(gs, t);
+    __shared__ GridSumTile<1> gsl;
+    const uint32_t ticket = spmv_begin<MODE>(gs, gsl, t);
     const int64_t row = r0 + tid;
     const bool has = tid < trows && row < r1;
     const int64_t rowc = has ? row : r0;   // a valid row for the unconditional epilogue loads
@@ -145,7 +148,7 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
         }
     }
     // only the residual mode may be called without partials (AMG smoothing); kernel-uniform test
-    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, acc, ticket, t);
+    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -330,7 +333,8 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
         }
         return;
     }
-    const uint32_t ticket = spmv_ticket<MODE>(gs, t);
+    __shared__ GridSumTile<1> gsl;
+    const uint32_t ticket = spmv_begin<MODE>(gs, gsl, t);
     const int32_t row32 = (int32_t)row;
     int32_t cc[UW];
     double xv[UW];
@@ -351,7 +355,7 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
         if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
     if (MODE == kSpmvDot) eq = diag_x<UW>(cc, xv, row32, x, has);
     const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
-    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, acc, ticket, t);
+    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
 }
 
 // General sliced layout (per-slice widths, offsets and formats loaded from the slice header).
@@ -374,7 +378,8 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
     const int32_t *pword = spcol + wo;                                         // packed column words
     const int32_t *vword = pword + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);   // dictionary indices
     const DictRegs dv = load_dict<DK>(sdict);
-    const uint32_t ticket = spmv_ticket<MODE>(gs, t);
+    __shared__ GridSumTile<1> gsl;
+    const uint32_t ticket = spmv_begin<MODE>(gs, gsl, t);
     const int32_t row32 = (int32_t)row;
     double eq = 0.0;
     if (has) {
@@ -460,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
         }
     }
     const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
-    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, acc, ticket, t);
+    if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
 }
 
 // per slice: widest row, and the largest |column - row| of its entries (saturated to int32)
@@ -770,10 +775,13 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     PSK_TRY(ctx(&c));
     const bool sliced = A->sl_off != nullptr;
     const int64_t nwg = sliced ? (A->n + kSlice - 1) / kSlice : spmv_tiles(A);
-    GridSum gs{nullptr, nullptr, nullptr, nullptr, 0, 0, -1, 0, nullptr};
-    if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs, kWaves));
+    GridSum gs{nullptr, nullptr, nullptr, nullptr, 0, 0, -1, nullptr};
+    if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
     dim3 gd((unsigned)nwg), bd(kBlock);
-    const TileMap tm = tile_map_for(nwg, spmv_xcd_bands());
+    // XCD bands for the sliced layouts (N = 10M in the loop 0.078 -> 0.072 ms, back to back 0.067 ->
+    // 0.057 ms); the CSR tile kernel measured 2-3% slower with them (3163^2 and 16384^2), so it keeps
+    // block order
+    const TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands());
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
@@ -1177,16 +1185,27 @@ int psk_spmv_timed(const psk_csr *A, const double *x, double *y, int32_t reps, d
     hipEvent_t e0, e1;
     PSK_HIP(hipEventCreate(&e0));
     PSK_HIP(hipEventCreate(&e1));
-    int rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, c->stream);   // warm
+    // PSK_SPMV_TIMED_MODE=1: the PCG loop's kSpmvDot launch (dot epilogue + gridsum) instead of a
+    // plain y = A x (lab switch: separates the epilogue from the loop context)
+    static const int mode = [] {
+        const char *e = std::getenv("PSK_SPMV_TIMED_MODE");
+        return e && std::atoi(e) == 1 ? (int)kSpmvDot : (int)kSpmvPlain;
+    }();
+    DevBuf part;
+    if (mode == kSpmvDot) PSK_TRY(part.ensure(64));
+    double *pp = mode == kSpmvDot ? part.as<double>() : nullptr;
+    int rc = launch_spmv(A, mode, x, y, nullptr, nullptr, pp, nullptr, c->stream);   // warm
     if (rc == PSK_OK && hipEventRecord(e0, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
     for (int r = 0; r < reps && rc == PSK_OK; ++r)
-        rc = launch_spmv(A, kSpmvPlain, x, y, nullptr, nullptr, nullptr, nullptr, c->stream);
+        rc = launch_spmv(A, mode, x, y, nullptr, nullptr, pp, nullptr, c->stream);
     if (rc == PSK_OK && hipEventRecord(e1, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
     float ms = 0.f;
     if (rc == PSK_OK && hipEventSynchronize(e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
     if (rc == PSK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event time");
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    if (mode == kSpmvDot) (void)hipStreamSynchronize(c->stream);   // before `part` is freed
+    part.release();
     if (rc == PSK_OK) *avg_ms = (double)ms / reps;
     return rc;
 }
