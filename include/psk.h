@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PSK_ABI_VERSION 2
+#define PSK_ABI_VERSION 3
 
 /* return codes */
 #define PSK_OK               0
@@ -58,6 +58,15 @@ extern "C" {
 #define PSK_MAXITER          1   /* handleMaxiter                IterativeSolver.py:115-129 */
 #define PSK_BREAKDOWN        2   /* handleBreakdown              IterativeSolver.py:109-113 */
 #define PSK_TRUE_RESID_FAIL  3   /* GMRES true residual missed   GMRESSolver.py:167-174 */
+
+/* psk_result.exit: why the iteration loop stopped (gates the host-side checks a caller-supplied
+   norm needs, e.g. the GMRES true-residual test GMRESSolver.py:163-174, without inferring it from
+   the history length) */
+#define PSK_EXIT_NONE             0   /* no loop ran (b = 0: IterativeSolver.py:86-88 / GMRESSolver.py:67-68) */
+#define PSK_EXIT_TOLERANCE        1   /* recursive residual <= tau*||b||  PCGSolver.py:129, GMRESSolver.py:158 */
+#define PSK_EXIT_ARNOLDI_BREAKDOWN 2  /* GMRES: h_{k+1,k} <= 1e-16 ||h_k|| (counts as convergence, :122,:158) */
+#define PSK_EXIT_MAXITER          3   /* maxiter reached (k == maxiter-1 with !failOnMaxiter for PCG, :130) */
+#define PSK_EXIT_DOT_BREAKDOWN    4   /* PCG dot(u,r) == 0 or dot(p,Ap) == 0  :104-105, :114-115 */
 
 /* where the vector pointers of a call live */
 #define PSK_HOST   0
@@ -101,6 +110,8 @@ typedef struct psk_result {
     int64_t spmv_launches;    /* number of SpMV launches (the timed ones when ctl.time_kernels) */
     int64_t hist_len;         /* valid entries written to hist */
     char    msg[256];         /* SolveStatus.msg() */
+    int32_t exit;             /* PSK_EXIT_* (ABI 3) */
+    int32_t reserved;
 } psk_result;
 
 /* ---- library / device ---------------------------------------------------------------- */

@@ -86,10 +86,10 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         if custom:
             normb_caller = float(self.norm(_host_copy(b)))     # self.norm(b)  PCGSolver.py:86, GMRESSolver.py:66
             if normb_caller == 0.0:                            # :87-88 / :67-68
-                x0 = np.zeros(n) if not isinstance(b, DeviceVector) else DeviceVector(n)
+                x0 = DeviceVector(n) if isinstance(b, DeviceVector) else np.zeros(n)
                 if isinstance(x0, DeviceVector):
                     x0.zero()
-                return self.handleConvergence(0, x0, 0, 0)
+                return self.handleConvergence(0, _like(b, x0), 0, 0)
         dA = self._device_matrix(A)
         if self.precond is None or not self.precFrozen():   # PCGSolver.py:92-94
             self.precond = self.precondType().form(dA)
@@ -122,7 +122,7 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         fn = getattr(N.lib, self._entry)
         N.check(fn(dA.handle, ph, N.ptr(bp), N.ptr(x), ctypes.byref(ctl), ctypes.byref(res), N.ptr(hist), loc),
                 self._entry)
-        if custom and res.status in (N.PSK_CONVERGED, N.PSK_TRUE_RESID_FAIL) and res.hist_len == res.iters:
+        if custom and res.exit in (N.PSK_EXIT_TOLERANCE, N.PSK_EXIT_ARNOLDI_BREAKDOWN):
             # GMRES stopped on its recursive residual: the true-residual test in the caller's norm
             # (GMRESSolver.py:163-174): resid = b - A x on the device, its norm by the caller's code
             rt = _host_copy(b) - _host_copy(spmv(dA, x))
@@ -143,8 +143,10 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         reference evaluates self.norm(r) every iteration (:125) and that is the caller's host code;
         r is copied to the host for it. Same operation order and status conventions as psk_pcg."""
         n = dA.n
-        dev_out = isinstance(b, DeviceVector)
         prec = self.precond
+
+        def result(x):                             # the kind of vector the caller passed (as psk_pcg)
+            return x if isinstance(b, DeviceVector) else _like(b, x.numpy())
 
         def dot(u, v):
             out = ctypes.c_double()
@@ -189,7 +191,7 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
             hist.append(normR)
             self.reportIter(k, normR, normB)                          # :126
             if normR <= self.tau() * normB or (not self.failOnMaxiter() and k == self.maxiter() - 1):
-                st = self.handleConvergence(k, x if dev_out else x.numpy(), normR, normB)   # :129-131
+                st = self.handleConvergence(k, result(x), normR, normB)   # :129-131
                 st.info = dict(status="converged", hist=np.array(hist), norm_b=normB, host_driven=True)
                 return st
             newUDotR = dot(u, r)                                      # :134
@@ -197,7 +199,7 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
             uDotR = newUDotR                                          # :136
             axpy(beta, p, u)                                          # p = u + beta*p  :138
             p = u
-        st = self.handleMaxiter(max(k, 0), x if dev_out else x.numpy(), normR, normB)   # :142
+        st = self.handleMaxiter(max(k, 0), result(x), normR, normB)   # :142
         st.info = dict(status="maxiter", hist=np.array(hist), norm_b=normB, host_driven=True)
         return st
 
@@ -218,6 +220,15 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
                        loop_ms=res.loop_ms, spmv_ms=res.spmv_ms, spmv_launches=res.spmv_launches,
                        resid_recursive=res.resid_recursive, norm_b=normB)
         return st
+
+
+def _like(b, x):
+    """x (a host ndarray, or a DeviceVector when b is one) as the kind of vector b is: a CUDA tensor
+    on b's device for a tensor b, else unchanged."""
+    if is_device_vector(b) and not isinstance(x, DeviceVector):
+        import torch
+        return torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64, device=b.device)
+    return x
 
 
 def _host_copy(v):

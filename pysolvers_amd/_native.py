@@ -12,8 +12,9 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"))
 
 PSK_OK = 0
-ABI_VERSION = 2          # include/psk.h PSK_ABI_VERSION (psk_ctl gained norm_b in 2)
+ABI_VERSION = 3          # include/psk.h PSK_ABI_VERSION (psk_ctl gained norm_b in 2, psk_result.exit in 3)
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
+PSK_EXIT_NONE, PSK_EXIT_TOLERANCE, PSK_EXIT_ARNOLDI_BREAKDOWN, PSK_EXIT_MAXITER, PSK_EXIT_DOT_BREAKDOWN = 0, 1, 2, 3, 4
 PSK_HOST, PSK_DEVICE = 0, 1
 PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
 PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE, PSK_LAYOUT_SLICED_DICT = 0, 1, 2, 3
@@ -33,7 +34,8 @@ class PskResult(ctypes.Structure):
     _fields_ = [("status", ctypes.c_int32), ("success", ctypes.c_int32), ("iters", ctypes.c_int64),
                 ("resid", ctypes.c_double), ("resid_recursive", ctypes.c_double),
                 ("norm_b", ctypes.c_double), ("loop_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double),
-                ("spmv_launches", ctypes.c_int64), ("hist_len", ctypes.c_int64), ("msg", ctypes.c_char * 256)]
+                ("spmv_launches", ctypes.c_int64), ("hist_len", ctypes.c_int64), ("msg", ctypes.c_char * 256),
+                ("exit", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 # name -> (restype, argtypes); this is the full list of symbols include/psk.h declares

@@ -421,6 +421,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             if (hipMemcpyAsync(&hs, st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipStreamSynchronize(s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "gmres state"); break; }
             res->iters = it + kc + 1;
+            res->exit = hs.brk ? PSK_EXIT_ARNOLDI_BREAKDOWN : PSK_EXIT_TOLERANCE;
             res->resid = hs.true_resid;
             res->resid_recursive = hs.rec;
             if (hs.true_resid <= hs.tauNormB) {
@@ -441,6 +442,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             if (it >= maxiter) {
                 // maxiter reached (reference: NameError at :180) -> handleMaxiter(k, x, |g|, ...)
                 hit_maxiter = true;
+                res->exit = PSK_EXIT_MAXITER;
                 res->iters = maxiter > 0 ? maxiter - 1 : 0;
                 res->resid = hs.rec;
                 res->resid_recursive = hs.rec;
@@ -470,6 +472,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             res->success = 1;
             res->iters = 1;
             res->resid = 0.0;
+            res->exit = PSK_EXIT_NONE;
         }
         // every step reported one residual (reportIter, :155): iters + 1 entries at maxiter (k = maxiter - 1)
         const int64_t nh = res->iters + (hit_maxiter ? 1 : 0);

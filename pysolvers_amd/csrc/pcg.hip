@@ -605,9 +605,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             res->success = 1;
             res->iters = hs.iters;
             res->resid = hs.resid;
+            res->exit = hs.normB == 0.0 ? PSK_EXIT_NONE
+                        : hs.resid <= hs.tauNormB ? PSK_EXIT_TOLERANCE : PSK_EXIT_MAXITER;
             nk = nhist = hs.normB == 0.0 ? 0 : hs.iters;
         } else if (hs.done == 2) {
             res->status = PSK_BREAKDOWN;
+            res->exit = PSK_EXIT_DOT_BREAKDOWN;
             res->success = 0;
             res->iters = hs.iters;
             res->resid = NAN;
@@ -617,6 +620,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         } else {
             // handleMaxiter(k=maxiter-1, ...) (IterativeSolver.py:115-129); maxiter==0 -> k unset
             res->status = PSK_MAXITER;
+            res->exit = PSK_EXIT_MAXITER;
             res->success = 0;
             res->iters = maxiter > 0 ? maxiter - 1 : 0;
             set_msg(res, "failure to converge");

@@ -34,19 +34,33 @@ def test_library_exports_all_symbols():
 
 def test_library_basic_calls_without_gpu():
     from pysolvers_amd import _native as N
-    assert N.lib.psk_abi_version() == 2
+    assert N.lib.psk_abi_version() == N.ABI_VERSION == 3
     n = N.device_count()
     assert n >= 0
     assert isinstance(N.lib.psk_last_error(), bytes)
 
 
-def test_struct_layout_matches_header():
+def test_struct_layout_matches_header(tmp_path):
+    """The ctypes structs against the C compiler's layout of include/psk.h (gcc, plain C)."""
+    import subprocess
     from pysolvers_amd import _native as N
-    # psk_ctl: int64, double, 4 x int32, double ; psk_result: see include/psk.h
-    assert ctypes.sizeof(N.PskCtl) == 40
-    # psk_result: 2 x int32, int64, 5 x double, 2 x int64, char[256]
-    assert N.PskResult.msg.offset == 4 + 4 + 8 + 5 * 8 + 2 * 8
-    assert ctypes.sizeof(N.PskResult) == 72 + 256
+    prog = tmp_path / "layout.c"
+    fields = {"psk_ctl": [f for f, _ in N.PskCtl._fields_], "psk_result": [f for f, _ in N.PskResult._fields_]}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "psk.h"', 'int main(void) {']
+    for st, fs in fields.items():
+        lines.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (st, st))
+        for f in fs:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (st, f, st, f))
+    lines.append('return 0; }')
+    prog.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), str(prog), "-o", str(exe)], check=True)
+    got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                       check=True).stdout.splitlines())
+    for st, cls in (("psk_ctl", N.PskCtl), ("psk_result", N.PskResult)):
+        assert int(got["%s sizeof" % st]) == ctypes.sizeof(cls), st
+        for f in fields[st]:
+            assert int(got["%s %s" % (st, f)]) == getattr(cls, f).offset, (st, f)
 
 
 def test_no_cpu_fallback_when_library_missing(tmp_path):

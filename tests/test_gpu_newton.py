@@ -51,9 +51,33 @@ def test_default_direct_matches_reference():
         assert np.linalg.norm(st.soln() - d["soln"]) <= 1e-10 * np.linalg.norm(d["soln"])
         st2 = psk.DefaultDirect().makeSolver().solve(psk.DeviceCSR.from_scipy(A), d["b"])
         assert np.array_equal(st2.soln(), st.soln())
+    import warnings
     import scipy.sparse as sp
-    bad = psk.DefaultDirect().makeSolver().solve(sp.csr_matrix((3, 3)), np.ones(3))   # singular: exception -> status
-    assert not bad.success() and bad.soln() is None and bad.msg().startswith("Default direct solve failed")
+    from scipy.sparse.linalg import MatrixRankWarning
+    for case in direct_manifest()["singular"]:   # the reference's spsolve: warning, NaNs, SUCCESS (make_direct.py)
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            st = psk.DefaultDirect().makeSolver().solve(sp.csr_matrix(np.array(case["dense"])), np.array(case["b"]))
+        assert bool(st.success()) == case["success"] and st.msg() == case["msg"]
+        assert bool(np.all(np.isnan(st.soln()))) == case["soln_all_nan"]
+        assert sorted({type(i.message).__name__ for i in w}) == case["warnings"] == [MatrixRankWarning.__name__]
+
+
+def test_default_direct_refactors_a_matrix_updated_in_place():
+    """The cached factors are tied to the matrix CONTENTS: an evalJ that updates J.data
+    in place must get the new Jacobian's solution, as the reference's spsolve-per-call does."""
+    import pysolvers_amd as psk
+    import scipy.sparse as sp
+    from oracle import fdlap
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, 16)
+    b = np.ones(A.shape[0])
+    solver = psk.DefaultDirect().makeSolver()
+    x1 = solver.solve(A, b).soln()
+    A.data *= 2.0                                   # same object, new values
+    x2 = solver.solve(A, b).soln()
+    assert np.linalg.norm(2.0 * x2 - x1) <= 1e-12 * np.linalg.norm(x1)
+    x3 = solver.solve(A, b).soln()                  # unchanged contents: cached factors, same bits
+    assert np.array_equal(x3, x2)
 
 
 def test_newton_default_solver_matches_reference():

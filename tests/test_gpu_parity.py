@@ -347,6 +347,27 @@ def test_fd1024_pcg_jacobi_iterations(psk):
     assert np.linalg.norm(x[:4096] - d["soln_head"]) <= tx * float(d["soln_norm"])
 
 
+def test_fd4096_pcg_jacobi_iterations(psk):
+    """configs[1] (PCG + Jacobi, FD 4096^2) to convergence at tau = 1e-8: the iteration count the
+    reference path takes (5813, tests/golden/make_large_oracle.py: the oracle, bit-identical to the
+    reference on every fixture; its 1-ulp dot perturbations keep 5813 and move the history by
+    8.6e-17 ||b||) must be identical; history within 1e-10 ||b||; solution within 1e-10."""
+    d = load_golden("large_fd4096.npz")
+    m = int(d["m"])
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    b = psk.mvmult(dA, np.random.default_rng(12345).random(m * m))
+    assert np.array_equal(b[:4096], d["b_head"])
+    assert hashlib.sha256(b.tobytes()).hexdigest() == str(d["b_sha256"])
+    st = psk.PCG(control=_ctl(maxiter=40000), precond=psk.Jacobi()).makeSolver().solve(dA, b)
+    assert st.success() and st.iters() == int(d["iters"]) == 5813
+    nb = np.linalg.norm(b)
+    th = max(RTOL_RESID, 10 * float(d["sens_hist"]))
+    assert np.max(np.abs(st.info["hist"] - d["hist"])) / nb <= th
+    assert abs(st.resid() - float(d["resid"])) / nb <= th
+    tx = max(1e-10, 10 * float(d["sens_x"]))
+    assert np.linalg.norm(st.soln()[:4096] - d["soln_head"]) <= tx * float(d["soln_norm"])
+
+
 def test_fd4096_spmv_and_first_iterations(psk):
     """configs[1] size (n = 16.7M): SpMV bit-exact vs the C oracle, 12 PCG+Jacobi steps vs the numpy oracle."""
     from oracle import fdlap, krylov, native
@@ -479,3 +500,41 @@ def test_caller_norm_zero_rhs(psk):
     for f in (psk.PCG, psk.GMRES):
         st = f(control=_ctl(maxiter=50, norm=_inf_norm)).makeSolver().solve(A, np.zeros(A.shape[0]))
         assert st.success() and st.iters() == 1 and not np.any(st.soln())
+
+
+def test_caller_norm_keeps_the_vector_kind(psk):
+    """A CUDA-tensor right-hand side gets a CUDA tensor back on every path — the device loop, the
+    host-driven caller-norm PCG and its b = 0 early return — and the same numbers."""
+    import torch
+    d = load_golden("pcg_dh8_identity.npz")
+    A = golden_matrix(d)
+    bt = torch.as_tensor(d["b"], dtype=torch.float64, device="cuda")
+    for ctl in (_ctl(maxiter=4000, tau=1e-8), _ctl(maxiter=4000, tau=1e-8, norm=_inf_norm)):
+        st = psk.PCG(control=ctl).makeSolver().solve(A, bt)
+        sh = psk.PCG(control=ctl).makeSolver().solve(A, d["b"])
+        assert torch.is_tensor(st.soln()) and st.soln().is_cuda and isinstance(sh.soln(), np.ndarray)
+        assert np.array_equal(st.soln().cpu().numpy(), sh.soln()) and st.iters() == sh.iters()
+    z = psk.PCG(control=_ctl(maxiter=50, norm=_inf_norm)).makeSolver().solve(A, torch.zeros_like(bt))
+    assert torch.is_tensor(z.soln()) and z.soln().is_cuda and not bool(torch.any(z.soln() != 0))
+
+
+def test_gmres_exit_reason(psk):
+    """psk_result.exit (ABI 3) says why the loop stopped; the caller-norm true-residual re-test is
+    gated on it, not on the history length."""
+    import ctypes
+    from pysolvers_amd import _native as N
+    d = load_golden("gmres_dh8_identity.npz")
+    dA = psk.DeviceCSR.from_scipy(golden_matrix(d))
+    b = np.ascontiguousarray(d["b"])
+    for maxiter, fom, want in ((300, 1, N.PSK_EXIT_TOLERANCE), (10, 1, N.PSK_EXIT_MAXITER),
+                               (10, 0, N.PSK_EXIT_MAXITER)):
+        ctl = N.PskCtl(maxiter=maxiter, tau=1e-8, fail_on_maxiter=fom, restart=0, check_every=0, time_kernels=0)
+        res, x = N.PskResult(), np.empty_like(b)
+        N.check(N.lib.psk_gmres(dA.handle, None, N.ptr(b), N.ptr(x), ctypes.byref(ctl), ctypes.byref(res), None,
+                                N.PSK_HOST), "psk_gmres")
+        assert res.exit == want, (maxiter, fom, res.exit)
+    res, x, z = N.PskResult(), np.empty_like(b), np.zeros_like(b)
+    ctl = N.PskCtl(maxiter=10, tau=1e-8, fail_on_maxiter=1, restart=0, check_every=0, time_kernels=0)
+    N.check(N.lib.psk_gmres(dA.handle, None, N.ptr(z), N.ptr(x), ctypes.byref(ctl), ctypes.byref(res), None,
+                            N.PSK_HOST), "psk_gmres")
+    assert res.exit == N.PSK_EXIT_NONE and res.success == 1

@@ -162,3 +162,18 @@ def test_oracle_newton_default_direct_matches_reference():
         assert st["iters"] == case["iters"] and bool(st["success"]) == case["success"]
         np.testing.assert_allclose(st["hist"], d["hist"], rtol=1e-12, atol=0)
         np.testing.assert_allclose(st["soln"], d["soln"], rtol=1e-12, atol=0)
+
+
+def test_direct_singular_fixture_is_spsolve():
+    """The singular-input fixtures make_direct.py took from the reference's DefaultDirect are what
+    scipy's spsolve (the reference's call, DefaultDirectSolver.py:65) does: warn, return NaNs."""
+    import warnings
+    import scipy.sparse as sp
+    import scipy.sparse.linalg as spla
+    from conftest import direct_manifest
+    for case in direct_manifest()["singular"]:
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            x = spla.spsolve(sp.csr_matrix(np.array(case["dense"])), np.array(case["b"]))
+        assert case["success"] and bool(np.all(np.isnan(x))) == case["soln_all_nan"]
+        assert sorted({type(i.message).__name__ for i in w}) == case["warnings"]
