@@ -1002,9 +1002,12 @@ constexpr int kGridLanes = 64;
 constexpr int kGridMaxRing = 256;   // rows of the LDS ring (<= 256 x 72 doubles)
 #ifdef PSK_GRID_PROF
 // development probe (tools/grid_probe.py): per band start / end s_memtime, waits and cycles waited
-__device__ unsigned long long g_grid_prof[8192 * 4];
+// 8 words per band: start, end, waits on the band above, cycles waited, then the solver's cycles per
+// step phase summed over the band: records + rhs ready, LDS ring reads, arithmetic (fma chain and
+// division), ring write + x store issued
+__device__ unsigned long long g_grid_prof[8192 * 8];
 extern "C" int psk_grid_prof_read(unsigned long long *out, int nbands) {
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_grid_prof), sizeof(unsigned long long) * 4 * (size_t)nbands) ==
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_grid_prof), sizeof(unsigned long long) * 8 * (size_t)nbands) ==
                    hipSuccess ? 0 : -1;
 }
 #endif
@@ -1071,7 +1074,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     __syncthreads();
 #ifdef PSK_GRID_PROF
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long n_wait = 0, c_wait = 0;
+    unsigned long long n_wait = 0, c_wait = 0, c_fetch = 0, c_lds = 0, c_arith = 0, c_store = 0;
 #endif
     if (tid >= kGridLanes) {
         // ---------------- poller: u positions [u_lo - max_ud, u_hi - min_ud] of lines y0-maxyd .. y0-1
@@ -1177,6 +1180,17 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             c_wait += __builtin_amdgcn_s_memtime() - tw;
 #endif
         }
+#ifdef PSK_GRID_PROF
+        // phase stamps: each asm consumes the values of the phase before, so the compiler's wait for
+        // them lands in front of the stamp
+        const unsigned long long p0 = __builtin_amdgcn_s_memtime();
+#pragma unroll
+        for (int k = 0; k < K / 2; ++k) __asm__ volatile("" ::"v"(sl.code[k]));
+#pragma unroll
+        for (int k = 0; k < K; ++k) __asm__ volatile("" ::"v"(sl.cf[k]));
+        __asm__ volatile("" ::"v"(sl.d), "v"(sl.b));
+        const unsigned long long p1 = __builtin_amdgcn_s_memtime();
+#endif
         double v[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) {   // every LDS read first (one round trip)
@@ -1184,11 +1198,20 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             const int yd = c & 63, ud = c >> 6;
             v[k] = ring[((s - ud) & ring_mask) * RW + (j + maxyd - yd)];
         }
+#ifdef PSK_GRID_PROF
+#pragma unroll
+        for (int k = 0; k < K; ++k) __asm__ volatile("" ::"v"(v[k]));
+        const unsigned long long p2 = __builtin_amdgcn_s_memtime();
+#endif
         double acc = 0.0;
 #pragma unroll
         for (int k = 0; k < K; ++k) acc = fma(sl.cf[k], v[k], acc);   // stored order; padding adds +-0
         double r = sl.b - acc;
         if (!unit) r = r / sl.d;
+#ifdef PSK_GRID_PROF
+        __asm__ volatile("" ::"v"(r));
+        const unsigned long long p3 = __builtin_amdgcn_s_memtime();
+#endif
         ring[(s & ring_mask) * RW + maxyd + j] = r;
         // the lines the band below reads are published; the others are read after the kernel
         // (agent-scope stores on every lane: 732 -> 561 cycles per step plain, 5-point sweep)
@@ -1196,6 +1219,13 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             if (j >= kGridLanes - maxyd) store_pub(x + rbase + rstep * s, r);
             else x[rbase + rstep * s] = r;
         }
+#ifdef PSK_GRID_PROF
+        const unsigned long long p4 = __builtin_amdgcn_s_memtime();
+        c_fetch += p1 - p0;
+        c_lds += p2 - p1;
+        c_arith += p3 - p2;
+        c_store += p4 - p3;
+#endif
     };
     GridSlot<K> buf[D];
 #pragma unroll
@@ -1214,10 +1244,14 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     if (j == 0) __hip_atomic_store(&ctl[1], INT64_MAX / 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 #ifdef PSK_GRID_PROF
     if (j == 0 && blockIdx.x < 8192) {
-        g_grid_prof[blockIdx.x * 4 + 0] = t_start;
-        g_grid_prof[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memtime();
-        g_grid_prof[blockIdx.x * 4 + 2] = n_wait;
-        g_grid_prof[blockIdx.x * 4 + 3] = c_wait;
+        g_grid_prof[blockIdx.x * 8 + 0] = t_start;
+        g_grid_prof[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
+        g_grid_prof[blockIdx.x * 8 + 2] = n_wait;
+        g_grid_prof[blockIdx.x * 8 + 3] = c_wait;
+        g_grid_prof[blockIdx.x * 8 + 4] = c_fetch;
+        g_grid_prof[blockIdx.x * 8 + 5] = c_lds;
+        g_grid_prof[blockIdx.x * 8 + 6] = c_arith;
+        g_grid_prof[blockIdx.x * 8 + 7] = c_store;
     }
 #endif
 }

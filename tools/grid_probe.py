@@ -47,19 +47,27 @@ def main():
         out[sched + "_ms"] = (time.perf_counter() - t) * 1e3 / 3
     if hasattr(N.lib, "psk_grid_prof_read"):
         nb = 8192
-        buf = (ctypes.c_ulonglong * (4 * nb))()
+        buf = (ctypes.c_ulonglong * (8 * nb))()
         N.lib.psk_grid_prof_read(buf, nb)
-        a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 4).astype(np.int64)
+        a = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
         used = a[:, 1] > 0
         a = a[used]
         t0 = a[:, 0].min()
-        # s_memtime runs at 100 MHz on gfx9 parts (10 ns ticks)
         out["bands"] = int(len(a))
         out["probe"] = [{"band": int(b), "start": int(a[b, 0] - t0), "end": int(a[b, 1] - t0),
                          "dur": int(a[b, 1] - a[b, 0]), "waits": int(a[b, 2]), "wait_ticks": int(a[b, 3])}
                         for b in sorted(set([0, 1, 2, len(a) // 2, len(a) - 2, len(a) - 1]))]
         out["total_ticks"] = int(a[:, 1].max() - t0)
         out["waits_total"] = int(a[:, 2].sum())
+        # per-step phases (s_memtime ticks summed over every step of every band; the last apply's)
+        steps = 0.0 if args.level3 else float(m + 63) * len(a)   # FD: w = m, sigma = 1: S = w + 63 per band
+        ph = {"records_rhs_ready": a[:, 4].sum(), "lds_ring_reads": a[:, 5].sum(), "fma_div": a[:, 6].sum(),
+              "ring_write_store_issue": a[:, 7].sum(), "ext_wait": a[:, 3].sum()}
+        tot = float(sum(ph.values()))
+        out["phase_share"] = {k: float(v) / tot for k, v in ph.items()}
+        out["phase_ticks_total"] = {k: int(v) for k, v in ph.items()}
+        if steps:
+            out["ticks_per_step"] = {k: float(v) / steps for k, v in ph.items()}
     print(json.dumps(out), flush=True)
 
 
