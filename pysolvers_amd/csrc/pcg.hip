@@ -474,15 +474,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // or the last nv - ov_hi K3 tiles (row-block shards of a banded matrix: one grid line each side),
     // those tiles run first and the exchange of p overlaps the remaining tiles of K3
     int64_t ov_lo = 0, ov_hi = nv;
-    // Opt-in (PSK_HALO_OVERLAP=1). Bit-identical in tests/test_gpu_multirank.py, but the N = 2
-    // rehearsal of bench.py with both ranks on one GPU (host transport) stops with an expired
-    // grid-reduction wait at FD 2048^2 and larger with the overlap on, and runs without it
-    // (profiles/r2_multirank_rehearsal.txt); until that is explained on real multi-GPU hardware the
-    // exchange runs before the SpMV on the compute stream. At P = 8 the exchange is ~2% of an
-    // iteration.
+    // Default since round 3 (PSK_HALO_OVERLAP=0 turns it off). In round 2 the N = 2 rehearsal of bench.py
+    // with both ranks on one GPU stopped with an expired grid-reduction wait with the overlap on: the
+    // round-2 gridsum waited for lower workgroup ids, i.e. assumed a dispatch order, which a second
+    // process's / stream's kernels occupying an XCD can break. The ticket gridsum (psk_internal.hpp)
+    // waits only for work that has started, and the same rehearsal runs with the overlap
+    // (profiles/r3_multirank_rehearsal.txt).
     static const bool overlap_on = [] {
         const char *e = std::getenv("PSK_HALO_OVERLAP");
-        return e && std::atoi(e) == 1;
+        return !(e && std::atoi(e) == 0);
     }();
     const bool overlap = overlap_on && sharded && !gen && halo_split(A, kVecTile, nv, ov_lo, ov_hi);
     hipStream_t cs = nullptr;
