@@ -2,12 +2,14 @@
 //
 // Krylov basis Q lives in HBM column-major (each q_j contiguous, n x (K+1)); the Hessenberg
 // column, the Givens table and g live in HBM too and are advanced by one lane of workgroup 0.
-// Per Arnoldi step k (launches, no host sync):
-//   G1      u = A M^-1 q_k, fused partials of q_0.u                     (:107, first MGS dot)
-//   G2_j    h_jk = sum(partials); u -= h_jk q_j; partials of q_{j+1}.u   (:110-112, MGS, j=0..k)
-//           (for j==k the partials are u.u for the norm)
+// Per Arnoldi step k (one-shot launches, one 512-element tile per workgroup; no host sync):
+//   G1      u = A M^-1 q_k, with q_0.u finished in-launch (gridsum)      (:107, first MGS dot)
+//   G2_j    h_jk (G1's or G2_{j-1}'s grid sum); u -= h_jk q_j; q_{j+1}.u (:110-112, MGS, j=0..k)
+//           finished in-launch (for j==k u.u, the norm)
 //   G3      h_{k+1,k} = ||u||; breakdown test; q_{k+1} = u / h_{k+1,k};  (:115-125)
 //           workgroup 0: old rotations, new rotation, g update, |g_{k+1}|, convergence (:133-158)
+// Bytes per step (algorithmic): the SpMV's, then 32n per G2_j (u read + written, q_j, q_{j+1}),
+// 24n for G2_k, 16n for G3.
 // On convergence the (k+1)^2 triangular-ish least-squares system is solved on the host (it is
 // 31x31 at config 3; LU with partial pivoting as LAPACK dgesv, :159), then
 //   x = M^-1 (Q[:, :k+1] y) on the device (:160) and the true residual ||b - A x|| (:163-164).
@@ -71,44 +73,42 @@ __global__ __launch_bounds__(kBlock) void gm_start_kernel(int64_t n, const doubl
     for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) q0[i] = r0[i] / beta;   // :91
 }
 
-// MGS step j of Arnoldi column k
+// MGS step j of Arnoldi column k, one-shot (one 512-element tile per workgroup, 16-B accesses):
+// h = HBar[j,k] (the previous launch's grid sum), u -= h q_j, and the next dot — q_{j+1}.u, or u.u
+// for j == k (the norm of :115) — finished in-launch by gridsum into hout.
 __global__ __launch_bounds__(kBlock) void gm_mgs_kernel(int64_t n, double *__restrict__ u,
                                                         const double *__restrict__ qj,
                                                         const double *__restrict__ qnext,
-                                                        const double *__restrict__ pin, int npin,
-                                                        double *__restrict__ pout, double *__restrict__ hcol,
-                                                        int j, const GmresState *st) {
+                                                        const double *__restrict__ hin, double *__restrict__ hcol,
+                                                        int j, GridSum gs, const GmresState *st) {
     if (st->done) return;
     __shared__ double sh[kWaves];
-    const double h = reduce_partials(pin, npin, 1, sh);   // HBar[j,k] = np.dot(Q[:,j], u)  :111
+    const double h = *hin;                                  // HBar[j,k] = np.dot(Q[:,j], u)  :111
     if (blockIdx.x == 0 && threadIdx.x == 0) hcol[j] = h;
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    uint32_t ticket = 0;
     double acc = 0.0;
-    int64_t i = i0 + 2 * threadIdx.x;
-    for (; i + 1 < i1; i += kVecTile) {
-        double2 uv = *reinterpret_cast<const double2 *>(u + i);
-        const double2 qv = *reinterpret_cast<const double2 *>(qj + i);
-        uv.x = uv.x - h * qv.x;                           // u -= HBar[j,k]*Q[:,j]  :112
+    if (i + 1 < n) {
+        // q_j is not read again this step (non-temporal); u and q_{j+1} are read by the next launch
+        dv2 uv = ld2(u + i);
+        const dv2 qv = ld2nt(qj + i);
+        dv2 nv = uv;
+        if (qnext) nv = ld2(qnext + i);
+        ticket = gridsum_ticket(gs);
+        uv.x = uv.x - h * qv.x;                             // u -= HBar[j,k]*Q[:,j]  :112
         uv.y = uv.y - h * qv.y;
-        *reinterpret_cast<double2 *>(u + i) = uv;
-        if (qnext) {
-            const double2 nv = *reinterpret_cast<const double2 *>(qnext + i);
-            acc = fma(nv.x, uv.x, acc);
-            acc = fma(nv.y, uv.y, acc);
-        } else {
-            acc = fma(uv.x, uv.x, acc);
-            acc = fma(uv.y, uv.y, acc);
-        }
-    }
-    if (i < i1) {
+        st2(u + i, uv);
+        if (!qnext) nv = uv;
+        acc = fma(nv.x, uv.x, acc);
+        acc = fma(nv.y, uv.y, acc);
+    } else if (i < n) {
+        ticket = gridsum_ticket(gs);
         const double ui = u[i] - h * qj[i];
         u[i] = ui;
-        acc = fma(qnext ? qnext[i] : ui, ui, acc);
+        acc = (qnext ? qnext[i] : ui) * ui;
     }
-    const double s = block_sum(acc, sh);
-    if (threadIdx.x == 0) pout[blockIdx.x] = s;
+    const double v = block_sum(acc, sh);
+    gridsum_publish<1>(gs, &v, sh, ticket);
 }
 
 __device__ __forceinline__ void givens_apply(double *x, double c, double s, int i) {
@@ -117,24 +117,30 @@ __device__ __forceinline__ void givens_apply(double *x, double c, double s, int 
     x[i + 1] = -s * xi + c * xi1;
 }
 
-// h_{k+1,k}, breakdown, q_{k+1}, Givens, convergence
+// h_{k+1,k}, breakdown, q_{k+1}, Givens, convergence; one-shot like gm_mgs_kernel (hsq: the grid
+// sum u.u of the last MGS launch)
 __global__ __launch_bounds__(kBlock) void gm_normalize_kernel(
-    int64_t n, const double *__restrict__ u, double *__restrict__ qnext, const double *__restrict__ pin, int npin,
+    int64_t n, const double *__restrict__ u, double *__restrict__ qnext, const double *__restrict__ hsq,
     double *__restrict__ H, double *__restrict__ R, double *__restrict__ CS, double *__restrict__ g, int ld, int k,
     int64_t it, GmresState *st, double *__restrict__ hist) {
     if (st->done) return;
-    __shared__ double sh[kWaves];
-    const double hk = sqrt(reduce_partials(pin, npin, 1, sh));   // npla.norm(u)  :115
+    const double hk = sqrt(*hsq);                                   // npla.norm(u)  :115
     const double *hcol = H + (int64_t)k * ld;
     double hh = 0.0;
     for (int j = 0; j <= k; ++j) hh += hcol[j] * hcol[j];
-    const double hlast = sqrt(hh);                                // npla.norm(HBar[0:k+1,k])  :121
-    const bool brk = fabs(hk) <= 1.0e-16 * hlast;                  // :122
-    if (!brk) {
-        int64_t t0, t1;
-        block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-        const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
-        for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) qnext[i] = u[i] / hk;   // :125
+    const double hlast = sqrt(hh);                                  // npla.norm(HBar[0:k+1,k])  :121
+    const bool brk = fabs(hk) <= 1.0e-16 * hlast;                    // :122
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    if (!brk) {                                                     // Q[:,k+1] = u / HBar[k+1,k]  :125
+        if (i + 1 < n) {
+            const dv2 uv = ld2nt(u + i);
+            dv2 q;
+            q.x = uv.x / hk;
+            q.y = uv.y / hk;
+            st2(qnext + i, q);
+        } else if (i < n) {
+            qnext[i] = u[i] / hk;
+        }
     }
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         H[(int64_t)k * ld + k + 1] = hk;
@@ -250,6 +256,8 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
     const int gs = 1;   // partials of a dot-mode SpMV: it finishes its sum in-launch (gridsum)
     const int gv = grid_for_rows(c, n, kVecTile);
+    const int64_t nv = n > 0 ? (n + kVecTile - 1) / kVecTile : 1;   // one-shot grid of the MGS kernels
+    if (nv > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_gmres: vector too long for a one-shot grid");
     const size_t vec = aup((size_t)n * 8);
     const size_t qbytes = vec * (size_t)(K + 1);
     {
@@ -270,7 +278,8 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     double *tt = gen ? reinterpret_cast<double *>(wb + qbytes + 4 * vec) : nullptr;
     const size_t hb = aup((size_t)ld * K * 8);
     const size_t small = aup(sizeof(GmresState)) + 2 * hb + aup((size_t)2 * K * 8) + aup((size_t)ld * 8) +
-                         2 * aup((size_t)kMaxGrid * 8) + aup((size_t)(maxiter + 1) * 8) + aup((size_t)ld * 8);
+                         aup((size_t)kMaxGrid * 8) + aup((size_t)(maxiter + 1) * 8) + aup((size_t)ld * 8) +
+                         aup((size_t)(K + 2) * 8);
     PSK_TRY(A->ws_small.ensure(small));
     char *sb = A->ws_small.as<char>();
     GmresState *st = reinterpret_cast<GmresState *>(sb);
@@ -283,13 +292,13 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     sb += aup((size_t)2 * K * 8);
     double *g = reinterpret_cast<double *>(sb);
     sb += aup((size_t)ld * 8);
-    double *pa = reinterpret_cast<double *>(sb);
-    sb += aup((size_t)kMaxGrid * 8);
-    double *pb = reinterpret_cast<double *>(sb);
+    double *pa = reinterpret_cast<double *>(sb);   // partials of the cycle-start norm / the residual's sum
     sb += aup((size_t)kMaxGrid * 8);
     double *dhist = reinterpret_cast<double *>(sb);
     sb += aup((size_t)(maxiter + 1) * 8);
     double *dy = reinterpret_cast<double *>(sb);
+    sb += aup((size_t)ld * 8);
+    double *hv = reinterpret_cast<double *>(sb);   // K + 2 grid sums of a step (gm_mgs_kernel)
 
     hipEvent_t ev0, ev1;
     PSK_HIP(hipEventCreate(&ev0));
@@ -387,24 +396,24 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
             const double *q0 = Q;
             if (gen) {   // u = A (M^-1 q_k): materialise M^-1 q_k (GMRESSolver.py:107)
                 if ((rc = prec_apply_dev(M, n, qk, w, s)) != PSK_OK) break;
-                if ((rc = launch_spmv(A, kSpmvPlainDot, w, u, nullptr, q0, pa, &st->done, s)) != PSK_OK) break;
-            } else if ((rc = launch_spmv(A, dinv ? kSpmvJacobiDot : kSpmvPlainDot, qk, u, dinv, q0, pa, &st->done,
+                if ((rc = launch_spmv(A, kSpmvPlainDot, w, u, nullptr, q0, hv, &st->done, s)) != PSK_OK) break;
+            } else if ((rc = launch_spmv(A, dinv ? kSpmvJacobiDot : kSpmvPlainDot, qk, u, dinv, q0, hv, &st->done,
                                          s)) != PSK_OK)
                 break;
             ++spmv_count;
-            double *pin = pa, *pout = pb;
-            int npin = gs;
+            // hv[0] = q_0.u (the SpMV's grid sum), hv[j+1] = the dot MGS step j finishes
             double *hcol = H + (size_t)k * ld;
             for (int64_t j = 0; j <= k; ++j) {
                 const double *qj = Q + (size_t)j * (vec / 8);
                 const double *qn = j < k ? Q + (size_t)(j + 1) * (vec / 8) : nullptr;
-                hipLaunchKernelGGL(gm_mgs_kernel, dim3(gv), dim3(kBlock), 0, s, n, u, qj, qn, pin, npin, pout, hcol,
-                                   (int)j, st);
-                std::swap(pin, pout);
-                npin = gv;
+                GridSum gsj;
+                if ((rc = gridsum_prepare(c, nv, 1, hv + j + 1, &gsj)) != PSK_OK) break;
+                hipLaunchKernelGGL(gm_mgs_kernel, dim3((unsigned)nv), dim3(kBlock), 0, s, n, u, qj, qn, hv + j, hcol,
+                                   (int)j, gsj, st);
             }
-            hipLaunchKernelGGL(gm_normalize_kernel, dim3(gv), dim3(kBlock), 0, s, n, u,
-                               Q + (size_t)(k + 1) * (vec / 8), pin, npin, H, R, CS, g, ld, (int)k, it + k, st,
+            if (rc != PSK_OK) break;
+            hipLaunchKernelGGL(gm_normalize_kernel, dim3((unsigned)nv), dim3(kBlock), 0, s, n, u,
+                               Q + (size_t)(k + 1) * (vec / 8), hv + k + 1, H, R, CS, g, ld, (int)k, it + k, st,
                                dhist);
             if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "gmres step launch"); break; }
         }

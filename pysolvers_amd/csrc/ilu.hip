@@ -38,6 +38,7 @@
 #include <algorithm>
 #include <unordered_map>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -1043,15 +1044,30 @@ struct GridSlot {
 // solver's waits are scalar LDS spins. Padding entries (value 0, code 0 = the lane's own column of
 // the current row: finite) add exactly +-0 to the fma chain. Per-row arithmetic is the band kernels':
 // fma over the entries in stored order from 0.0, then (b - acc) / diag — bit-identical results.
-template <int K, int D>
+// DICT: the records come from a dictionary (TriFactor::grid_dict_n): per lane-step ONE 32-bit index
+// load instead of the three record loads (codes, values, diagonal), the dictionary in LDS, the next
+// step's record looked up while the current step's ring reads are in flight. The grid phase probe
+// (profiles/r3_grid_phase_probe.txt) put the step's cost in its memory instructions.
+template <int K>
+struct GridRec {
+    uint32_t code[K / 2];
+    double cf[K], d;
+};
+template <int K, int D, bool DICT>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t S_full, int upper, int pe, int maxyd, int ring_mask,
     int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
-    GridExt ext) {
+    GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int RW = maxyd + kGridLanes;
     double *ring = reinterpret_cast<double *>(smem);                  // [ring][RW]
     int64_t *ctl = reinterpret_cast<int64_t *>(ring + (size_t)(ring_mask + 1) * RW);
+    // dictionary (DICT): [ndict][K] values, [ndict] diagonals, [ndict][K/2] code words
+    double *dcf = reinterpret_cast<double *>(ctl + 2);
+    double *ddg = dcf + (DICT ? ndict * K : 0);
+    uint32_t *dcode = reinterpret_cast<uint32_t *>(ddg + (DICT ? ndict : 0));
+    if (DICT)
+        for (int i = threadIdx.x; i < ndict * (K + 1) + (ndict * K / 2 + 1) / 2; i += 2 * kGridLanes) dcf[i] = gdict[i];
     // ctl[0]: last u of the band above present in the ring (poller -> solver)
     // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
     const int tid = threadIdx.x, j = tid & 63;
@@ -1134,8 +1150,15 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
                                  (int64_t)blockIdx.x * S_full * GridStep<K>::kBytes;
     int64_t ext_known = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;   // uniform
+    const uint32_t *pidx = gidx + (int64_t)blockIdx.x * S_full * kGridLanes + j;
     auto fetch = [&](int s, GridSlot<K> &sl) {
         const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
+        if (DICT) {
+            sl.code[0] = pidx[(int64_t)sc * kGridLanes];   // the record index
+            const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);
+            sl.b = w_eff > 0 ? rhs[rbase + rstep * sa] : 0.0;
+            return;
+        }
         const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
         const uint32_t *pc = reinterpret_cast<const uint32_t *>(st + GridStep<K>::kCode) + j * (K / 2);
         if (K == 2) {
@@ -1162,7 +1185,23 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);   // clamped into the line
         sl.b = w_eff > 0 ? rhs[rbase + rstep * sa] : 0.0;
     };
-    auto solve = [&](int s, const GridSlot<K> &sl) {
+    auto lookup = [&](uint32_t idx, GridRec<K> &rc) {   // DICT: the record of a step, from LDS
+#pragma unroll
+        for (int k = 0; k < K / 2; ++k) rc.code[k] = dcode[idx * (K / 2) + k];
+#pragma unroll
+        for (int k = 0; k < K; ++k) rc.cf[k] = dcf[idx * K + k];
+        rc.d = ddg[idx];
+    };
+    auto solve = [&](int s, const GridSlot<K> &slr, const GridRec<K> &rec) {
+        // the step's record: from the slot (records streamed) or the dictionary lookup (DICT)
+        GridSlot<K> sl = slr;
+        if (DICT) {
+#pragma unroll
+            for (int k = 0; k < K / 2; ++k) sl.code[k] = rec.code[k];
+#pragma unroll
+            for (int k = 0; k < K; ++k) sl.cf[k] = rec.cf[k];
+            sl.d = rec.d;
+        }
         const int64_t u = u_lo + s;
         if (has_ext && s < S && ext_known < u - min_ud) {   // uniform: the band above not yet in the ring
 #ifdef PSK_GRID_PROF
@@ -1230,10 +1269,16 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     GridSlot<K> buf[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) fetch(i, buf[i]);
+    GridRec<K> rcur{}, rnext{};
+    if (DICT) lookup(buf[0].code[0], rcur);
     for (int s0 = 0; s0 < S; s0 += D) {
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            solve(s0 + i, buf[i]);
+            // DICT: the next step's record is looked up now (its index arrived steps ago), so its LDS
+            // round trip overlaps this step's ring reads
+            if (DICT) lookup(buf[i + 1 < D ? i + 1 : 0].code[0], rnext);
+            solve(s0 + i, buf[i], rcur);
+            if (DICT) rcur = rnext;
             // the ring write of step s0+i precedes the next step's reads (one wave: LDS in order)
             __asm__ volatile("" ::: "memory");
             fetch(s0 + i + D, buf[i]);
@@ -1256,8 +1301,9 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
 #endif
 }
 
-static size_t grid_lds_bytes(int ring, int maxyd) {
-    return (size_t)ring * (kGridLanes + maxyd) * sizeof(double) + 2 * sizeof(int64_t);
+static size_t grid_lds_bytes(int ring, int maxyd, int K = 0, int ndict = 0) {
+    return (size_t)ring * (kGridLanes + maxyd) * sizeof(double) + 2 * sizeof(int64_t) +
+           (ndict > 0 ? (size_t)ndict * (K + 1) * sizeof(double) + ((size_t)ndict * K / 2 + 1) / 2 * sizeof(double) : 0);
 }
 
 static size_t narrow_lds_bytes(int ring_words, int K) {
@@ -1339,18 +1385,28 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
 #ifndef PSK_GRID_D
 #define PSK_GRID_D 12
 #endif
-        if (T.grid_K == 2) k = reinterpret_cast<const void *>(&sptrsv_grid_kernel<2, PSK_GRID_D>);
-        else if (T.grid_K == 4) k = reinterpret_cast<const void *>(&sptrsv_grid_kernel<4, (PSK_GRID_D > 8 ? 8 : PSK_GRID_D)>);
-        else if (T.grid_K == 8) k = reinterpret_cast<const void *>(&sptrsv_grid_kernel<8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D)>);
+        const bool dict = T.grid_dict_n > 0;
+#define PSK_GRID_K(KK, DD)                                                                                    \
+    k = dict ? reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DD, true>)                               \
+             : reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DD, false>)
+        if (T.grid_K == 2) PSK_GRID_K(2, PSK_GRID_D);
+        else if (T.grid_K == 4) PSK_GRID_K(4, (PSK_GRID_D > 8 ? 8 : PSK_GRID_D));
+        else if (T.grid_K == 8) PSK_GRID_K(8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D));
+#undef PSK_GRID_K
         if (!k) return fail(PSK_ERR_ARG, "grid schedule: bad record width");
         int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, sfull = T.grid_S;
         int upper = T.upper ? 1 : 0, pe_ = T.grid_pe, myd = T.grid_maxyd, mask = T.grid_ring - 1;
         int unit = T.diag ? 0 : 1;
         const double *gr = T.gd_coef;
         GridExt ext = T.grid_ext;
-        void *args[] = {&nn, &w, &H, &sg, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr, &ext};
+        const uint32_t *gi = T.gd_idx;
+        const double *gdd = T.gd_dict;
+        int nd = T.grid_dict_n;
+        void *args[] = {&nn, &w, &H, &sg, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr, &ext,
+                        &gi, &gdd, &nd};
         const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
-        PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args, grid_lds_bytes(T.grid_ring, T.grid_maxyd), s));
+        PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args,
+                                grid_lds_bytes(T.grid_ring, T.grid_maxyd, T.grid_K, T.grid_dict_n), s));
         return PSK_OK;
     }
     if (T.schedule == kSchedBand && T.band_narrow) {
@@ -1456,8 +1512,8 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
 }
 
 void TriFactor::release() {
-    void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,
-                    rec_d,  gd_code, gd_coef, gd_diag, part_seg, part_rp, part_code, part_row, part_va};
+    void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,   rec_d,
+                    gd_code, gd_coef, gd_diag, gd_idx, gd_dict, part_seg, part_rp, part_code, part_row, part_va};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -1466,6 +1522,57 @@ void TriFactor::release() {
 // ---------------------------------------------------------------------------------------------
 // host: schedules and their cost model
 namespace {
+
+constexpr int kGridDictMax = 64;
+
+// Distinct records of the grid schedule's record blob (nsteps blocks of SB bytes: [64][K] codes at 0,
+// [64][K] values at oc, [64] diagonals at od). With at most kGridDictMax of them: idx = each
+// lane-step's record number in the kernel's access order (block-major, lane-minor), dict = [n][K]
+// values, [n] diagonals, [n][K/2] code words packed two uint32 per double; ndict = n. Else ndict = 0.
+void build_grid_dict(const unsigned char *gb, int64_t nsteps, int64_t SB, int K, int64_t oc, int64_t od,
+                     std::vector<uint32_t> &idx, std::vector<double> &dict, int &ndict) {
+    ndict = 0;
+    const size_t rb = (size_t)K * 2 + (size_t)K * 8 + 8;   // key bytes: codes, values, diagonal
+    std::vector<unsigned char> keys;                       // distinct records, rb bytes each
+    std::unordered_map<uint64_t, std::vector<int>> by_hash;
+    idx.assign((size_t)(nsteps * kGridLanes), 0);
+    unsigned char key[2 * 8 + 8 * 8 + 8];
+    for (int64_t t = 0; t < nsteps; ++t) {
+        const unsigned char *blk = gb + t * SB;
+        for (int l = 0; l < kGridLanes; ++l) {
+            std::memcpy(key, blk + (size_t)l * K * 2, (size_t)K * 2);
+            std::memcpy(key + K * 2, blk + oc + (size_t)l * K * 8, (size_t)K * 8);
+            std::memcpy(key + K * 10, blk + od + (size_t)l * 8, 8);
+            uint64_t h = 1469598103934665603ull;   // FNV-1a
+            for (size_t i = 0; i < rb; ++i) h = (h ^ key[i]) * 1099511628211ull;
+            int found = -1;
+            auto &cand = by_hash[h];
+            for (int c : cand)
+                if (std::memcmp(keys.data() + (size_t)c * rb, key, rb) == 0) { found = c; break; }
+            if (found < 0) {
+                found = (int)(keys.size() / rb);
+                if (found == kGridDictMax) {
+                    idx.clear();
+                    return;
+                }
+                keys.insert(keys.end(), key, key + rb);
+                cand.push_back(found);
+            }
+            idx[(size_t)(t * kGridLanes + l)] = (uint32_t)found;
+        }
+    }
+    const int nd = (int)(keys.size() / rb);
+    const size_t ncw = (size_t)nd * K / 2;                  // code words
+    dict.assign((size_t)nd * (K + 1) + (ncw + 1) / 2, 0.0);
+    uint32_t *cw = reinterpret_cast<uint32_t *>(dict.data() + (size_t)nd * (K + 1));
+    for (int r = 0; r < nd; ++r) {
+        const unsigned char *k = keys.data() + (size_t)r * rb;
+        std::memcpy(dict.data() + (size_t)r * K, k + K * 2, (size_t)K * 8);
+        std::memcpy(dict.data() + (size_t)nd * K + r, k + K * 10, 8);
+        std::memcpy(cw + (size_t)r * (K / 2), k, (size_t)K * 2);   // K uint16 codes = K/2 words, as in a record
+    }
+    ndict = nd;
+}
 
 // Cost model (us), fitted to measurements on MI355X (tools/bench_amg.py, tools/bench_gmres.py):
 // sync-free: a row costs one agent-scope load round trip (~0.61) on its wave, plus a hand-off (~0.36)
@@ -1913,7 +2020,8 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     plan_grid(F, gp);
     T.est_grid_us = gp.ok ? gp.est : -1.0;
     std::vector<uint16_t> gcode;
-    std::vector<double> gcoef, gdiag;
+    std::vector<double> gcoef, gdiag, gdict;
+    std::vector<uint32_t> gidx;
     if (gp.ok) {
         const char *ge = std::getenv("PSK_TRISOLVE_GRID");
         const double cur = T.schedule == kSchedBand ? T.est_band_us
@@ -1953,6 +2061,13 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
             }
             reinterpret_cast<double *>(blk + od)[l] = dg.empty() ? 1.0 : dg[i];
         }
+        // record dictionary: when the lane-steps hold at most kGridDictMax distinct records (stencil
+        // factors: the interior record, the boundary variants, the empty lanes), the kernel loads one
+        // 32-bit index per lane-step instead of the record (PSK_TRISOLVE_GRID_DICT=0: never)
+        const char *gde = std::getenv("PSK_TRISOLVE_GRID_DICT");
+        if (!(gde && std::atoi(gde) == 0))
+            build_grid_dict(gb, nsteps, SB, gp.K, oc, od, gidx, gdict, T.grid_dict_n);
+        if (T.grid_dict_n > 0) std::vector<double>().swap(gcoef);   // the records are not uploaded
     }
     // partitioned schedule: planned for factors too large for one CU and not solved by the grid
     // schedule (PSK_TRISOLVE_PART=0 disables it, =1 builds it and selects it whatever the estimate)
@@ -2060,6 +2175,8 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.gd_code, gcode);
     if (rc == PSK_OK) rc = upload(&T.gd_coef, gcoef);
     if (rc == PSK_OK) rc = upload(&T.gd_diag, gdiag);
+    if (rc == PSK_OK) rc = upload(&T.gd_idx, gidx);
+    if (rc == PSK_OK) rc = upload(&T.gd_dict, gdict);
     if (rc == PSK_OK) rc = upload(&T.part_seg, pseg);
     if (rc == PSK_OK) rc = upload(&T.part_rp, prp);
     if (rc == PSK_OK) rc = upload(&T.part_code, pcode);

@@ -61,7 +61,7 @@ struct Context {
     // exit because queued launches may still use them
     uint64_t *gs_slots = nullptr;
     int64_t gs_cap = 0;
-    uint64_t *gs_gslots = nullptr;   // kMaxGrid * kGridSumMaxW
+    uint64_t *gs_gslots = nullptr;   // kGridSumMaxGroups * kGridSumMaxW
     uint32_t *gs_cnt = nullptr;      // gridsum ticket counters (zero between launches)
     std::vector<uint64_t *> gs_retired;
     int32_t *gs_err = nullptr;
@@ -202,6 +202,12 @@ struct TriFactor {
     // (row-major, stored entry order), diagonal (nullptr = unit)
     uint16_t *gd_code = nullptr;
     double *gd_coef = nullptr, *gd_diag = nullptr;
+    // record dictionary (grid_dict_n > 0): every lane-step's record is one of grid_dict_n distinct
+    // (codes, values, diagonal) records, gd_dict = [n][K] values, [n] diagonals, then [n][K/2] code
+    // words; gd_idx = the record index of each lane-step in the solver's access order
+    uint32_t *gd_idx = nullptr;
+    double *gd_dict = nullptr;
+    int grid_dict_n = 0;
     int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
     int64_t grid_w = 0, grid_H = 0, grid_sigma = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
     GridExt grid_ext{};
@@ -378,7 +384,11 @@ __device__ __forceinline__ int64_t gridsum_members(const GridSum &gs, int64_t g,
 }
 
 __device__ __forceinline__ void gridsum_put(uint64_t *sl, double v) {
+#ifdef PSK_LAB_GS_XCHG
+    (void)__hip_atomic_exchange(sl, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
     __hip_atomic_store(sl, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
 }
 __device__ __forceinline__ uint32_t gridsum_draw(uint32_t *c) {
     return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -542,6 +552,9 @@ __device__ __forceinline__ uint32_t gridsum_tile_begin(const GridSum &gs, GridSu
     if (threadIdx.x == 0) L.cnt = 0;
     __syncthreads();
     uint32_t t = 0;
+#if defined(PSK_LAB_GS_NOTICKET) || defined(PSK_LAB_GS_NOSTORE)
+    return t;   // development probes (scripts/build_variant.sh): no ticket, no reduction — wrong sums
+#endif
     if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tile, gs.grp_log2)));
     return t;
 }
@@ -587,6 +600,10 @@ __device__ __forceinline__ void gridsum_tile_publish(const GridSum &gs, GridSumT
         for (int w = 1; w < kWaves; ++w) s[c] += L.part[w * W + c];   // wave order
     }
     const uint32_t tk = L.ticket;
+#ifdef PSK_LAB_GS_NOSTORE
+    if (s[0] == 1.2345e-300 && lane0) gs.out[0] = s[0];   // keeps the sums live; probe only
+    return;
+#endif
     if (gs.grp_log2 < 0) {
         if (lane0)
 #pragma unroll
@@ -597,6 +614,9 @@ __device__ __forceinline__ void gridsum_tile_publish(const GridSum &gs, GridSumT
     if (lane0)
 #pragma unroll
         for (int c = 0; c < W; ++c) gridsum_put(gs.slots + gridsum_slot(gs, tile) * W + c, s[c]);
+#ifdef PSK_LAB_GS_NOTICKET
+    return;
+#endif
     const int64_t g = gridsum_group_of(tile, gs.grp_log2);
     int64_t base;
     const int64_t cnt = gridsum_members(gs, g, base);

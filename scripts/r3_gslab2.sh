@@ -1,0 +1,9 @@
+#!/bin/bash
+# dot-epilogue lab 2 (tile slots): plain vs dot-mode back-to-back SpMV, in-tree build and probes
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+for L in pysolvers_amd/_lib/libpsk.so tools/bin/ab_noticket/libpsk.so tools/bin/ab_nostore/libpsk.so; do
+  for MODE in 0 1; do
+    PSK_LIBRARY=$L PSK_SPMV_TIMED_MODE=$MODE timeout -k 10 120 python tools/spmv_batch.py 3163 200 || exit $?
+  done
+done

@@ -288,3 +288,24 @@ def test_grid_schedule_sa_coarse_operator(psk):
     P = TriangularSolveChain(n, U=U, gather_in=pin, gather_out=pout)
     assert _grid_available(P, "U")
     assert np.array_equal(P.apply(v), M.apply(v[pin])[pout])
+
+
+@pytest.mark.parametrize("m,lower", [(300, False), (300, True), (1024, False)])
+def test_grid_record_dictionary_bitwise(psk, monkeypatch, m, lower):
+    """The grid schedule's record dictionary (one index per lane-step into an LDS table of the
+    distinct records; FD factors have a handful) gives the same bits as streaming the records."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    T = (sp.tril(A) if lower else sp.triu(A)).tocsr()
+    v = np.random.default_rng(m + 7).standard_normal(A.shape[0])
+    f = "L" if lower else "U"
+    outs = []
+    for dict_on in ("1", "0"):
+        monkeypatch.setenv("PSK_TRISOLVE_GRID_DICT", dict_on)
+        M = TriangularSolveChain(A.shape[0], **({"L": T} if lower else {"U": T}))
+        assert _grid_available(M, f)
+        outs.append(M.apply(v))
+    assert np.array_equal(outs[0], outs[1])
+    ref = spla.spsolve_triangular(T, v, lower=lower)
+    assert _rel(outs[0], ref) <= 1e-12
