@@ -526,11 +526,11 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if (timed) {
             if ((rc = harvest(slot)) != PSK_OK) break;
             tk[slot] = k;
-            if (hipEventRecord(ta[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         }
-        if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s)) != PSK_OK)
+        // a timed launch records its events in its own dispatch (kernel start / end)
+        if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s,
+                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr)) != PSK_OK)
             break;
-        if (timed && hipEventRecord(tb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
         if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
         const dim3 gk((unsigned)nv);
         if (jac == 2)

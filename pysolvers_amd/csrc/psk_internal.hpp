@@ -384,11 +384,7 @@ __device__ __forceinline__ int64_t gridsum_members(const GridSum &gs, int64_t g,
 }
 
 __device__ __forceinline__ void gridsum_put(uint64_t *sl, double v) {
-#ifdef PSK_LAB_GS_XCHG
-    (void)__hip_atomic_exchange(sl, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
     __hip_atomic_store(sl, (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 __device__ __forceinline__ uint32_t gridsum_draw(uint32_t *c) {
     return __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -722,8 +718,11 @@ int tile_rows_for(int64_t n, int64_t nnz);
 // CSR arrays (PSK_SPMV_LAYOUT=csr|sliced overrides); called at the end of every creation path
 int csr_choose_layout(psk_csr *A, hipStream_t s);
 void sliced_free(psk_csr *A);
-// one-shot SpMV (grid = tiles of A->tile_rows rows); dot modes write their grid sum to partial[0]
+// one-shot SpMV (grid = tiles of A->tile_rows rows); dot modes write their grid sum to partial[0].
+// ev0/ev1 (optional): HIP events the dispatch itself records at the kernel's start and end
+// (hipExtLaunchKernel), so their interval is the kernel alone, without the launch gaps around it
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
-                const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s);
+                const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s,
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 }  // namespace psk

@@ -15,6 +15,8 @@
 // PCG, q_0.u for GMRES, ||b-Ax||^2 for the true residual), reduced deterministically by gridsum.
 #include "psk_internal.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <climits>
 #include <cstdlib>
@@ -769,7 +771,8 @@ static bool spmv_xcd_bands() {
 static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) / A->tile_rows; }
 
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
-                const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s) {
+                const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s, hipEvent_t ev0,
+                hipEvent_t ev1) {
     if (A->n == 0) return PSK_OK;
     Context *c;
     PSK_TRY(ctx(&c));
@@ -786,13 +789,13 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
 #define PSK_UNI_LAUNCH(M, DK, UW)                                                                              \
-    hipLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, A->n, A->sl_pcol, A->sl_val, A->sl_dict, \
+    hipExtLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol, A->sl_val, A->sl_dict, \
                        x, y, aux_d, aux_q, gs, done_flag, tm)
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
     do {                                                                                                       \
         switch (uw) {                                                                                          \
         case 0:                                                                                                \
-            hipLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, A->n, A->sl_off, A->sl_woff,         \
+            hipExtLaunchKernelGGL((spmv_sliced_kernel<M, DK>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_off, A->sl_woff,         \
                                A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, \
                                done_flag, tm);                                                                     \
             break;                                                                                             \
@@ -832,7 +835,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     const int tr = A->tile_rows;
     const int32_t nz = (int32_t)A->nnz;
 #define PSK_SPMV_LAUNCH(M)                                                                                  \
-    hipLaunchKernelGGL(spmv_kernel<M>, gd, bd, 0, s, A->n, tr, A->rowptr, A->colidx, A->vals, x, y, aux_d, \
+    hipExtLaunchKernelGGL(spmv_kernel<M>, gd, bd, 0, s, ev0, ev1, 0, A->n, tr, A->rowptr, A->colidx, A->vals, x, y, aux_d, \
                        aux_q, gs, done_flag, nz, tm)
     switch (mode) {
     case kSpmvPlain: PSK_SPMV_LAUNCH(kSpmvPlain); break;
