@@ -530,11 +530,11 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
 // ---- per-wave partials combined in LDS (the SpMV's dot epilogue) ------------------------------
 // Each wave of a tile writes its wave total (DPP, no shuffle traffic) to LDS and counts itself in
 // with an LDS atomic; the wave that counts last adds the kWaves totals in wave order and publishes
-// the tile's ONE slot, then plays the tile's part in the ticket protocol. One write-through store
-// per tile instead of one per wave: an 8-B sc1 store is a fabric write of its own, and 4 per tile
-// cost ~7 us of a 57-us SpMV at N = 10M (probe builds -DPSK_LAB_GS_*, profiles/r3_gridsum_lab.txt).
-// No workgroup barrier at the end; the one barrier (arming the LDS counter) sits where every wave
-// waits for its stream loads anyway.
+// the tile's ONE slot, then plays the tile's part in the ticket protocol: one write-through store
+// per tile instead of one per wave (~2 us less at N = 10M; what the remaining ~6 us of the dot
+// epilogue is — it is not per store — is recorded in profiles/r3_gridsum_lab.txt, probe builds
+// -DPSK_LAB_GS_NOTICKET / NOSTORE). No workgroup barrier at the end; the one barrier (arming the
+// LDS counter) sits where every wave waits for its stream loads anyway.
 template <int W>
 struct GridSumTile {
     uint32_t cnt;
