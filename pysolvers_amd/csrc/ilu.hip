@@ -1156,7 +1156,11 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         if (DICT) {
             sl.code[0] = pidx[(int64_t)sc * kGridLanes];   // the record index
             const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);
+#ifdef PSK_LAB_GRID_NORHS
+            sl.b = rhs[(int64_t)blockIdx.x * 64 + j + (sa & 1023) * 8192];   // probe: coalesced, wrong values
+#else
             sl.b = w_eff > 0 ? rhs[rbase + rstep * sa] : 0.0;
+#endif
             return;
         }
         const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
@@ -1256,7 +1260,9 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         // (agent-scope stores on every lane: 732 -> 561 cycles per step plain, 5-point sweep)
         if (s >= s_beg && s < s_end) {
             if (j >= kGridLanes - maxyd) store_pub(x + rbase + rstep * s, r);
+#ifndef PSK_LAB_GRID_NOXSTORE
             else x[rbase + rstep * s] = r;
+#endif
         }
 #ifdef PSK_GRID_PROF
         const unsigned long long p4 = __builtin_amdgcn_s_memtime();
