@@ -95,7 +95,7 @@ def main():
     ap.add_argument("--scaling-steps", type=int, default=50)
     ap.add_argument("--repeats", type=int, default=5,
                     help="timed regions of --steps iterations each; value = the median (SURVEY.md §8d)")
-    ap.add_argument("--cpu-iters", type=int, default=20, help="timed oracle iterations for cpu_baseline (0 = skip)")
+    ap.add_argument("--cpu-iters", type=int, default=50, help="timed oracle iterations for cpu_baseline (0 = skip)")
     ap.add_argument("--general", type=int, default=1,
                     help="also time the general-matrix path (double values, streamed DInv) on rank 0")
     ap.add_argument("--config2", type=int, default=1, help="also time configs[2] (GMRES(30)+ILUT, FD 2896^2) on rank 0")
