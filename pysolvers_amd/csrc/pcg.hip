@@ -147,16 +147,41 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     gridsum_publish<2>(gs, v, sh, ticket);
 }
 
+// Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
+// p_j lives in ring buffer j mod kPcgDefer; K3 of iteration k reads p_k and writes p_{k+1} over
+// p_{k+1-kPcgDefer}, which the last flush consumed (or, on a flush, which this K3 reads first, element
+// by element). A flush applies the pending updates in iteration order, x = ((x + a_{k-q} p_{k-q}) + ...)
+// + a_k p_k, the reference's two roundings per update in its order (PCGSolver.py:121), so x is
+// bit-identical to updating every iteration. x traffic per iteration: 16 B/row updated every
+// iteration, 8 (kPcgDefer + 1) / kPcgDefer deferred (12 at 2, 10 at 4).
+#ifndef PSK_PCG_DEFER
+#define PSK_PCG_DEFER 4
+#endif
+constexpr int kPcgDefer = PSK_PCG_DEFER;
+static_assert(kPcgDefer >= 1 && kPcgDefer <= 8, "kPcgDefer");
+struct PRing {
+    double *b[kPcgDefer];
+};
+// iterations whose x update is still pending when K3 of iteration k runs: k - q .. k - 1
+__host__ __device__ inline int pcg_pending(int64_t k) { return (int)(k % kPcgDefer); }
+
+// x[j] with the pending updates of iterations k - q .. k - 1 applied (ring: their p; alphas[i] = a_i)
+__device__ __forceinline__ double pcg_catch_up(double xj, const PRing *pr, int q, int64_t k,
+                                               const double *__restrict__ alphas, int64_t j) {
+    for (int t = q; t >= 1; --t) xj = xj + alphas[k - t] * pr->b[(k - t) % kPcgDefer][j];   // :121
+    return xj;
+}
+
 // K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
 // (K2's expression on the same partials), the convergence test, beta. Returns false when the
-// solve stopped at this iteration; x (which K3 owns) is then still advanced over [i0, i1).
-// pprev != nullptr: iteration k-1 deferred its x update (x += alpha_prev p_{k-1}, applied first).
+// solve stopped at this iteration; x (which K3 owns) is then still advanced over the tile.
+// pr != nullptr: the q = pcg_pending(k) deferred x updates are applied first.
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
                                              double pTAp, double rr, double ur, PcgState *st,
                                              double *__restrict__ udr, double *__restrict__ hist, int64_t k,
                                              int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
-                                             int64_t tile, const double *__restrict__ pprev = nullptr,
-                                             double alpha_prev = 0.0) {
+                                             int64_t tile, const PRing *pr = nullptr,
+                                             const double *__restrict__ alphas = nullptr) {
     alpha = udr[k] / pTAp;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (tile == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
@@ -164,7 +189,7 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
         const int64_t i = tile * kVecTile + 2 * threadIdx.x;
         for (int64_t j = i; j < i + 2 && j < n; ++j) {
             double xj = x[j];
-            if (pprev) xj = xj + alpha_prev * pprev[j];      // :121 of iteration k-1
+            if (pr) xj = pcg_catch_up(xj, pr, pcg_pending(k), k, alphas, j);
             x[j] = xj + alpha * p[j];                        // :121
         }
         if (tile == 0 && threadIdx.x == 0) {
@@ -179,31 +204,28 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
     return true;
 }
 
-// ---- K3: x += alpha p, convergence test, beta, p = u + beta p (one-shot, as K2) -------------
-// x += alpha p is deferred on even iterations: x is read and written every other iteration only
-// (x = (x + alpha_{k-1} p_{k-1}) + alpha_k p_k on odd k and on the last, the reference's two
-// roundings in its order), with p double-buffered so p_{k-1} is still there: K3 reads p_k from
-// pcur and p_{k-1} (odd k) from pnext, where it writes p_{k+1} (each element read before it is
-// written). A breakdown after an even iteration leaves one update pending (pcg_flush_kernel).
+// ---- K3: x += alpha p (deferred, above), convergence test, beta, p = u + beta p (one-shot, as K2) --
+// A breakdown leaves the updates of the iterations since the last flush pending (pcg_flush_kernel).
 template <int JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
-    int64_t n, double *__restrict__ x, const double *__restrict__ r, const double *__restrict__ pcur,
-    double *__restrict__ pnext, const double *__restrict__ dinv, double ds, const double *__restrict__ pap,
-    const double *__restrict__ rrur, int nparts, PcgState *st, double *__restrict__ udr, double *__restrict__ hist,
-    double *__restrict__ alphas, int64_t k, int64_t maxiter, int fail_on_maxiter, int64_t tile_base) {
+    int64_t n, double *__restrict__ x, const double *__restrict__ r, PRing pr, const double *__restrict__ dinv,
+    double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts, PcgState *st,
+    double *__restrict__ udr, double *__restrict__ hist, double *__restrict__ alphas, int64_t k, int64_t maxiter,
+    int fail_on_maxiter, int64_t tile_base) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
     // halo exchange then overlaps the rest); tile 0 alone writes the solver state
     const int64_t tile = tile_base + blockIdx.x;
-    const bool pend = (k & 1) != 0;                          // iteration k-1 deferred its x update
-    const double alpha_prev = pend ? alphas[k - 1] : 0.0;
+    const double *__restrict__ pcur = pr.b[k % kPcgDefer];
+    double *__restrict__ pnext = pr.b[(k + 1) % kPcgDefer];
+    const int q = pcg_pending(k);
     double alpha, beta;
     if (!pcg_direction_scalars(n, x, pcur, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
                                rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta, tile, pend ? pnext : nullptr, alpha_prev))
+                               beta, tile, &pr, alphas))
         return;
     if (tile == 0 && threadIdx.x == 0) alphas[k] = alpha;
-    const bool flush = pend || k == maxiter - 1;
+    const bool flush = q == kPcgDefer - 1 || k == maxiter - 1;
     const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
     if (i + 1 < n) {
@@ -217,11 +239,17 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
         }
         if (flush) {
             dv2 xo = ld2nt(x + i);
-            if (pend) {
-                const dv2 pp = ld2nt(pnext + i);
-                xo.x = xo.x + alpha_prev * pp.x;             // x = x + alpha*p  :121 (iteration k-1)
-                xo.y = xo.y + alpha_prev * pp.y;
-            }
+            dv2 pp[kPcgDefer > 1 ? kPcgDefer - 1 : 1];
+#pragma unroll
+            for (int t = 1; t < kPcgDefer; ++t)
+                if (t <= q) pp[t - 1] = ld2nt(pr.b[(k - t) % kPcgDefer] + i);
+#pragma unroll
+            for (int t = kPcgDefer - 1; t >= 1; --t)
+                if (t <= q) {
+                    const double a = alphas[k - t];
+                    xo.x = xo.x + a * pp[t - 1].x;           // x = x + alpha*p  :121 (iteration k-t)
+                    xo.y = xo.y + a * pp[t - 1].y;
+                }
             dv2 xn;
             xn.x = xo.x + alpha * po.x;                      // :121
             xn.y = xo.y + alpha * po.y;
@@ -234,20 +262,16 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     } else if (i < n) {
         const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
         const double pi = pcur[i];
-        if (flush) {
-            double xi = x[i];
-            if (pend) xi = xi + alpha_prev * pnext[i];
-            x[i] = xi + alpha * pi;
-        }
+        if (flush) x[i] = pcg_catch_up(x[i], &pr, q, k, alphas, i) + alpha * pi;
         pnext[i] = u0 + beta * pi;
     }
 }
 
-// the x update a breakdown left pending: x += alpha p_{k-1} (after an even iteration k-1)
-__global__ void pcg_flush_kernel(int64_t n, double *__restrict__ x, const double *__restrict__ pprev,
-                                 const double *__restrict__ alpha) {
+// the x updates a breakdown at iteration k left pending: iterations k - q .. k - 1, q = pcg_pending(k)
+__global__ void pcg_flush_kernel(int64_t n, double *__restrict__ x, PRing pr, const double *__restrict__ alphas,
+                                 int64_t k) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) x[i] = x[i] + *alpha * pprev[i];
+    if (i < n) x[i] = pcg_catch_up(x[i], &pr, pcg_pending(k), k, alphas, i);
 }
 
 // ---- general preconditioner (ILU, ...): u = M^-1 r is materialised by the preconditioner's own
@@ -322,7 +346,8 @@ static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; 
 
 struct PcgWork {
     double *x, *r, *p, *Ap, *u, *part1, *part2, *part3, *udr, *hist;
-    double *p2, *alphas;   // Jacobi/identity K3: the second p buffer, alpha_k (deferred x updates)
+    PRing pr;              // Jacobi/identity K3: p_j in pr.b[j % kPcgDefer] (pr.b[0] = p)
+    double *alphas;        // alpha_k (deferred x updates)
     // sharded (P ranks): the ranks' gathered scalars, [P] p.Ap and [P][2] (r.r, u.r), and the
     // gathered init partials [P][kMaxGrid][2]; unsharded: part1g/part2g alias part1/part2
     double *part1g, *part2g, *initg;
@@ -331,7 +356,7 @@ struct PcgWork {
 
 static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &w) {
     const size_t vec = align_up((size_t)A->n * 8, 256), vecc = align_up((size_t)A->ncols * 8, 256);
-    const size_t big = (gen ? 4 : 3) * vec + (gen ? 1 : 2) * vecc;
+    const size_t big = (gen ? 4 : 3) * vec + (gen ? 1 : kPcgDefer) * vecc;
     PSK_TRY(A->ws.ensure(big > 0 ? big : 256));
     char *b = A->ws.as<char>();
     w.x = reinterpret_cast<double *>(b);
@@ -339,7 +364,8 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &
     w.Ap = reinterpret_cast<double *>(b + 2 * vec);
     w.p = reinterpret_cast<double *>(b + 3 * vec);
     w.u = gen ? reinterpret_cast<double *>(b + 3 * vec + vecc) : nullptr;
-    w.p2 = gen ? nullptr : reinterpret_cast<double *>(b + 3 * vec + vecc);
+    for (int t = 0; t < kPcgDefer; ++t)
+        w.pr.b[t] = gen ? (t == 0 ? w.p : nullptr) : reinterpret_cast<double *>(b + 3 * vec + t * vecc);
     const size_t small = align_up(sizeof(PcgState), 256) + 2 * align_up(kMaxGrid * 8, 256) +
                          align_up(2 * kMaxGrid * 8, 256) + align_up((size_t)(maxiter + 2) * 8, 256) +
                          align_up((size_t)(maxiter + 1) * 8, 256) + align_up((size_t)(maxiter + 1) * 8, 256);
@@ -511,8 +537,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             if (rc != PSK_OK) break;
         }
         // p_k and the buffer K3 writes p_{k+1} into (Jacobi/identity: alternating; general: in place)
-        double *pk = (gen || !(k & 1)) ? w.p : w.p2;
-        double *pn = gen ? w.p : ((k & 1) ? w.p : w.p2);
+        double *pk = gen ? w.p : w.pr.b[k % kPcgDefer];
+        double *pn = gen ? w.p : w.pr.b[(k + 1) % kPcgDefer];
         if (halo_pending) {   // exchanged during the previous K3
             if (hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess) { rc = fail(PSK_ERR_HIP, "halo wait"); break; }
             halo_pending = false;
@@ -553,15 +579,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
                 if (t1 <= t0) return;
                 const dim3 g3((unsigned)(t1 - t0));
                 if (jac == 2)
-                    hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, pk, pn, dinv, ds,
+                    hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
                                        ctl->fail_on_maxiter, t0);
                 else if (jac == 1)
-                    hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, pk, pn, dinv, ds,
+                    hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
                                        ctl->fail_on_maxiter, t0);
                 else
-                    hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, pk, pn, dinv, ds,
+                    hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
                                        ctl->fail_on_maxiter, t0);
             };
@@ -636,11 +662,10 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             res->hist_len = nh;
             res->resid_recursive = nh > 0 ? hh[(size_t)nh - 1] : hs.normB;
             if (res->status == PSK_MAXITER) res->resid = maxiter > 0 ? res->resid_recursive : hs.normB;
-            // a dot(p,Ap) breakdown at odd k: iteration k-1 (even) deferred its x update
-            if (!gen && hs.done == 2 && hs.brk_kind != 1 && (hs.iters & 1) && n > 0) {
-                const int64_t kp = hs.iters - 1;
+            // a dot(p,Ap) breakdown at k: the iterations since the last flush deferred their x updates
+            if (!gen && hs.done == 2 && hs.brk_kind != 1 && pcg_pending(hs.iters) > 0 && n > 0) {
                 hipLaunchKernelGGL(pcg_flush_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,
-                                   w.x, (kp & 1) ? w.p2 : w.p, w.alphas + kp);
+                                   w.x, w.pr, w.alphas, (int64_t)hs.iters);
                 if (hipGetLastError() != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg flush");
             }
             if (rc == PSK_OK) rc = from_device_vec(w.x, loc, n, xout, s);

@@ -201,14 +201,15 @@ def test_pcg_breakdown_later_history(psk):
     np.testing.assert_allclose(st.info["hist"], ref["hist"], rtol=1e-14)
 
 
-@pytest.mark.parametrize("maxiter", [5, 6, 7])
+@pytest.mark.parametrize("maxiter", [5, 6, 7, 8, 9])
 @pytest.mark.parametrize("fail", [True, False])
 @pytest.mark.parametrize("jac", ["identity", "jacobi"])
 def test_pcg_solution_at_maxiter_odd_even(psk, maxiter, fail, jac):
-    """K3 defers x += alpha p on even iterations (x read and written every other iteration, p double
-    buffered): the solution the loop stops with — at maxiter (odd and even) with and without
-    failOnMaxiter — is the oracle's (to rounding: the device's dot products sum in another order
-    than numpy's), and so is the history; a missing or doubled update would be O(1) off."""
+    """K3 defers x += alpha p (x read and written every kPcgDefer = 4 iterations, p in a ring of 4
+    buffers): the solution the loop stops with — at maxiter 5..9, i.e. 0..3 updates pending, with
+    and without failOnMaxiter — is the oracle's (to rounding: the device's dot products sum in
+    another order than numpy's), and so is the history; a missing or doubled update would be O(1)
+    off."""
     from oracle import fdlap, krylov
     A = fdlap.fd_laplacian_2d(-1.0, 1.0, 24)
     b, _ = fdlap.manufactured_rhs(A, 12345)
