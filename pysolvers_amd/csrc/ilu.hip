@@ -1051,8 +1051,24 @@ struct GridSlot {
 template <int K>
 struct GridRec {
     uint32_t code[K / 2];
-    double cf[K], d;
+    double cf[K], d, rd;   // rd = RN(1 / d), DICT only
 };
+// (b - acc) / d on the solver's dependency chain without the IEEE division sequence (two
+// dependent scale steps, the reciprocal, five fmas and the fix-up): q0 = RN(r * rd) from the
+// correctly rounded reciprocal rd = RN(1/d) (computed once per dictionary entry, off the chain), then
+// two Markstein corrections q <- RN(q + RN(r - q d) rd) with the remainder exact in an fma. With rd
+// correctly rounded, a correction from any q within one ulp of r/d returns RN(r/d), and q0 is within
+// 1.5 ulp, so the second correction returns the IEEE quotient; r = +-0 keeps q0 (the signed zero).
+// tools/markstein_check.c: 0 mismatches against r / d in 2e8 random pairs after ONE correction.
+#ifndef PSK_GRID_MARKSTEIN
+#define PSK_GRID_MARKSTEIN 1
+#endif
+__device__ __forceinline__ double div_markstein(double r, double d, double rd) {
+    const double q0 = r * rd;
+    const double q1 = fma(fma(-q0, d, r), rd, q0);
+    const double q2 = fma(fma(-q1, d, r), rd, q1);
+    return r == 0.0 ? q0 : q2;
+}
 template <int K, int D, bool DICT>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t S_full, int upper, int pe, int maxyd, int ring_mask,
@@ -1062,12 +1078,17 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const int RW = maxyd + kGridLanes;
     double *ring = reinterpret_cast<double *>(smem);                  // [ring][RW]
     int64_t *ctl = reinterpret_cast<int64_t *>(ring + (size_t)(ring_mask + 1) * RW);
-    // dictionary (DICT): [ndict][K] values, [ndict] diagonals, [ndict][K/2] code words
+    // dictionary (DICT): [ndict][K] values, [ndict] diagonals, [ndict][K/2] code words (gdict's
+    // layout), then [ndict] reciprocals of the diagonals (computed here)
     double *dcf = reinterpret_cast<double *>(ctl + 2);
     double *ddg = dcf + (DICT ? ndict * K : 0);
     uint32_t *dcode = reinterpret_cast<uint32_t *>(ddg + (DICT ? ndict : 0));
-    if (DICT)
-        for (int i = threadIdx.x; i < ndict * (K + 1) + (ndict * K / 2 + 1) / 2; i += 2 * kGridLanes) dcf[i] = gdict[i];
+    const int dwords = DICT ? ndict * (K + 1) + (ndict * K / 2 + 1) / 2 : 0;   // doubles of gdict
+    double *drd = dcf + dwords;
+    if (DICT) {
+        for (int i = threadIdx.x; i < dwords; i += 2 * kGridLanes) dcf[i] = gdict[i];
+        for (int i = threadIdx.x; i < ndict; i += 2 * kGridLanes) drd[i] = 1.0 / gdict[ndict * K + i];
+    }
     // ctl[0]: last u of the band above present in the ring (poller -> solver)
     // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
     const int tid = threadIdx.x, j = tid & 63;
@@ -1195,11 +1216,14 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
 #pragma unroll
         for (int k = 0; k < K; ++k) rc.cf[k] = dcf[idx * K + k];
         rc.d = ddg[idx];
+        rc.rd = drd[idx];
     };
     auto solve = [&](int s, const GridSlot<K> &slr, const GridRec<K> &rec) {
         // the step's record: from the slot (records streamed) or the dictionary lookup (DICT)
         GridSlot<K> sl = slr;
+        double rd = 0.0;
         if (DICT) {
+            rd = rec.rd;
 #pragma unroll
             for (int k = 0; k < K / 2; ++k) sl.code[k] = rec.code[k];
 #pragma unroll
@@ -1250,7 +1274,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
 #pragma unroll
         for (int k = 0; k < K; ++k) acc = fma(sl.cf[k], v[k], acc);   // stored order; padding adds +-0
         double r = sl.b - acc;
-        if (!unit) r = r / sl.d;
+        if (!unit) r = (DICT && PSK_GRID_MARKSTEIN) ? div_markstein(r, sl.d, rd) : r / sl.d;
 #ifdef PSK_GRID_PROF
         __asm__ volatile("" ::"v"(r));
         const unsigned long long p3 = __builtin_amdgcn_s_memtime();
@@ -1309,7 +1333,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
 
 static size_t grid_lds_bytes(int ring, int maxyd, int K = 0, int ndict = 0) {
     return (size_t)ring * (kGridLanes + maxyd) * sizeof(double) + 2 * sizeof(int64_t) +
-           (ndict > 0 ? (size_t)ndict * (K + 1) * sizeof(double) + ((size_t)ndict * K / 2 + 1) / 2 * sizeof(double) : 0);
+           (ndict > 0 ? (size_t)ndict * (K + 2) * sizeof(double) + ((size_t)ndict * K / 2 + 1) / 2 * sizeof(double) : 0);
 }
 
 static size_t narrow_lds_bytes(int ring_words, int K) {
