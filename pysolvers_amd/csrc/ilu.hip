@@ -1069,6 +1069,27 @@ __device__ __forceinline__ double div_markstein(double r, double d, double rd) {
     const double q2 = fma(fma(-q1, d, r), rd, q1);
     return r == 0.0 ? q0 : q2;
 }
+// Buffer (bounds-checked) access for the solver wave's rhs loads and x stores: an out-of-range
+// offset loads 0 / drops the store in hardware, so every lane issues every load and store with no
+// branch around it. The compiler's vmcnt waits count only memory operations it knows were issued:
+// with the rhs load and the two x stores under divergent branches it assumed one operation per step
+// (the record index) and waited with vmcnt(10) — i.e. for stores and loads issued ~3 steps before,
+// write-through stores included — where the prefetch runs D steps ahead. Byte offsets are 32-bit:
+// the grid schedule takes factors of at most kGridMaxRows rows (host check).
+constexpr uint32_t kBufOOB = 0xFFFFFFFFu;
+constexpr int64_t kGridMaxRows = (int64_t)1 << 29;
+typedef unsigned int grid_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t grid_rsrc(const double *p, int64_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), (short)0, (int)(uint32_t)(n * 8), 0x00020000);
+}
+__device__ __forceinline__ double grid_bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+template <int CPOL>   // 0x10: sc1 (agent-scope write-through, the publication store), 0: plain
+__device__ __forceinline__ void grid_bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(grid_u2, v), r, off, 0, CPOL);
+}
+
 template <int K, int D, bool DICT>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t S_full, int upper, int pe, int maxyd, int ring_mask,
@@ -1172,16 +1193,13 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
                                  (int64_t)blockIdx.x * S_full * GridStep<K>::kBytes;
     int64_t ext_known = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;   // uniform
     const uint32_t *pidx = gidx + (int64_t)blockIdx.x * S_full * kGridLanes + j;
+    const __amdgpu_buffer_rsrc_t rrhs = grid_rsrc(rhs, n), rx = grid_rsrc(x, n);
     auto fetch = [&](int s, GridSlot<K> &sl) {
         const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
         if (DICT) {
             sl.code[0] = pidx[(int64_t)sc * kGridLanes];   // the record index
             const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);
-#ifdef PSK_LAB_GRID_NORHS
-            sl.b = rhs[(int64_t)blockIdx.x * 64 + j + (sa & 1023) * 8192];   // probe: coalesced, wrong values
-#else
-            sl.b = w_eff > 0 ? rhs[rbase + rstep * sa] : 0.0;
-#endif
+            sl.b = grid_bload(rrhs, w_eff > 0 ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
             return;
         }
         const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
@@ -1208,7 +1226,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         }
         sl.d = reinterpret_cast<const double *>(st + GridStep<K>::kDiag)[j];
         const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);   // clamped into the line
-        sl.b = w_eff > 0 ? rhs[rbase + rstep * sa] : 0.0;
+        sl.b = grid_bload(rrhs, w_eff > 0 ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
     };
     auto lookup = [&](uint32_t idx, GridRec<K> &rc) {   // DICT: the record of a step, from LDS
 #pragma unroll
@@ -1282,11 +1300,11 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         ring[(s & ring_mask) * RW + maxyd + j] = r;
         // the lines the band below reads are published; the others are read after the kernel
         // (agent-scope stores on every lane: 732 -> 561 cycles per step plain, 5-point sweep)
-        if (s >= s_beg && s < s_end) {
-            if (j >= kGridLanes - maxyd) store_pub(x + rbase + rstep * s, r);
-#ifndef PSK_LAB_GRID_NOXSTORE
-            else x[rbase + rstep * s] = r;
-#endif
+        {
+            const bool act = s >= s_beg && s < s_end, pub = j >= kGridLanes - maxyd;
+            const uint32_t o = act ? (uint32_t)((rbase + rstep * s) * 8) : kBufOOB;
+            grid_bstore<0x10>(rx, pub ? o : kBufOOB, r);
+            grid_bstore<0>(rx, pub ? kBufOOB : o, r);
         }
 #ifdef PSK_GRID_PROF
         const unsigned long long p4 = __builtin_amdgcn_s_memtime();
@@ -2048,6 +2066,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     // grid schedule (2-D stencil factors): records in solve order
     GridPlan gp;
     plan_grid(F, gp);
+    if (n > kGridMaxRows) gp.ok = false;   // the grid kernel's 32-bit buffer offsets
     T.est_grid_us = gp.ok ? gp.est : -1.0;
     std::vector<uint16_t> gcode;
     std::vector<double> gcoef, gdiag, gdict;
