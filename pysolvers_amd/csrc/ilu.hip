@@ -80,20 +80,28 @@ __global__ void fill_sentinel_kernel(int64_t n, double *x) {
     if (i < n) reinterpret_cast<uint64_t *>(x)[i] = kSentinel;
 }
 
-// Sync-free: x_i = (rhs_i - sum_j T_ij x_j) / diag_i  (diag == nullptr: unit), rhs_i = rhs[rhs_idx[i]]
-// when rhs_idx is given. The factor is stored in SOLVE ORDER (host-built): position k holds row
-// krow[k] with entries [krp[k], krp[k+1]) of kci/kva, so a wave's rows stream. Wave w takes positions
-// w, w+W, ... and software-pipelines them: while it waits on the dependencies of position k it already
-// has position k+W's row, entries, right-hand side and diagonal in flight (stage B) and position
-// k+2W's row header (stage A), so a row costs one hand-off round trip instead of a chain of dependent
-// HBM loads (order -> rowptr -> entries -> rhs index -> rhs).
+// Branch-free row pipeline (the LDS kernel's, SfSrc below). The compiler's vmcnt waits count only
+// the memory operations it knows were issued; a load under a divergent branch (a lane test, a row
+// past the end) is not counted, so the wait for a row's first dependency became vmcnt(0) — it also
+// waited for the prefetch of the rows D ahead issued after it, which is what the pipeline exists to
+// hide. Every load of SfSrc is issued by every lane at a clamped, valid address (the value selected
+// afterwards), the row header is loaded per lane (VMEM, counted in order, not SMEM), and the rare
+// slow path (a row longer than the register chunks) ends with an explicit vmcnt(0), so the fast
+// path's counts survive its join.
+__device__ __forceinline__ void drain_vm() { __builtin_amdgcn_s_waitcnt(0x0F70); }   // vmcnt(0) only
+__device__ __forceinline__ int32_t opaque_zero() {
+    int32_t z;
+    __asm__ volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
 struct SfHead {
     int32_t row, s, e;
 };
 constexpr int kSfChunks = 3;   // 64-entry chunks of a row held in registers (longer rows loop)
 struct SfBody {
-    int32_t row, s, e, c[kSfChunks];
-    double v[kSfChunks], b, d;
+    int32_t row, s, e, ri, c[kSfChunks];
+    double v[kSfChunks], d;
 };
 
 constexpr int kSfTail = 4;
@@ -102,6 +110,58 @@ constexpr int kSfTail = 4;
 // three give identical bits): the DPP wave total (psk_internal.hpp), ~130 cycles on the dependency
 // chain where a butterfly of ds_bpermute shuffles took ~700 (tools/part_micro.py trace, FD chain).
 __device__ __forceinline__ double row_total(double v) { return wave_total(v); }
+
+// the loads of a row (positions clamped into [0, n), entries into [0, nnz); callers select)
+struct SfSrc {
+    int64_t n;
+    int32_t last;   // nnz - 1 (>= 0)
+    const int32_t *krp, *kci, *krow, *ridx;   // ridx: rhs_idx, or krow (any valid int array of n)
+    const double *kva, *dg;                   // dg: diag, or rhs (any valid double array of n)
+    bool has_ri, has_d;
+    int32_t zv;                               // opaque zero: per-lane header loads
+    __device__ void head(int64_t k, SfHead &h) const {
+        const int64_t kk = (k < n ? k : n - 1) + zv;
+        h.row = krow[kk];
+        h.s = krp[kk];
+        h.e = krp[kk + 1];
+    }
+    __device__ void body(const SfHead &h, SfBody &b, int lane) const {
+        b.row = h.row;
+        b.s = h.s;
+        b.e = h.e;
+        // lanes past the row's end re-read its first entry (the line lane 0 reads; an empty row: the
+        // entry before it), never one shared address (a hot line every wave would hit)
+        const int32_t fb = h.s < h.e ? h.s : (h.e > 0 ? h.e - 1 : 0);
+#pragma unroll
+        for (int j = 0; j < kSfChunks; ++j) {
+            const int32_t idx = h.s + 64 * j + lane;
+            const bool ok = idx < h.e;
+            const int32_t ic = ok ? idx : fb;
+            const int32_t c = kci[ic];
+            const double v = kva[ic];
+            b.c[j] = ok ? c : -1;
+            b.v[j] = ok ? v : 0.0;
+        }
+        const int32_t ri = ridx[h.row];
+        const double d = dg[h.row];
+        b.ri = has_ri ? ri : h.row;
+        b.d = has_d ? d : 1.0;
+    }
+};
+
+// Sync-free: x_i = (rhs_i - sum_j T_ij x_j) / diag_i  (diag == nullptr: unit), rhs_i = rhs[rhs_idx[i]]
+// when rhs_idx is given. The factor is stored in SOLVE ORDER (host-built): position k holds row
+// krow[k] with entries [krp[k], krp[k+1]) of kci/kva, so a wave's rows stream. Wave w takes positions
+// w, w+W, ... and software-pipelines them: while it waits on the dependencies of position k it already
+// has position k+W's row, entries, right-hand side and diagonal in flight (stage B) and position
+// k+2W's row header (stage A), so a row costs one hand-off round trip instead of a chain of dependent
+// HBM loads (order -> rowptr -> entries -> rhs index -> rhs). Its loads stay under lane tests: the
+// branch-free form of the LDS kernel below (SfSrc) measured 27.0 -> 27.9-28.9 ms on configs[2]'s ILU
+// apply (profiles/r3_grid_phase_probe.txt), where the hand-off, not the compiler's waits, bounds a row.
+struct SfRow {
+    int32_t row, s, e, c[kSfChunks];
+    double v[kSfChunks], b, d;
+};
 
 __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
                                                         const int32_t *__restrict__ kci, const double *__restrict__ kva,
@@ -119,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
             h.e = krp[k + 1];
         }
     };
-    auto body = [&](int64_t k, const SfHead &h, SfBody &b) {
+    auto body = [&](int64_t k, const SfHead &h, SfRow &b) {
         if (k < n) {
             b.row = h.row;
             b.s = h.s;
@@ -137,7 +197,7 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
         }
     };
     SfHead ha, hb;
-    SfBody cur, nxt;
+    SfRow cur, nxt;
     head(wave, ha);
     body(wave, ha, cur);
     head(wave + W, hb);
@@ -231,89 +291,80 @@ __global__ __launch_bounds__(kLdsThreads) void sptrsv_lds_kernel(int64_t n, cons
         }
         return __longlong_as_double((long long)b);
     };
-    auto head = [&](int64_t k, SfHead &h) {
-        if (k < n) {
-            h.row = krow[k];
-            h.s = krp[k];
-            h.e = krp[k + 1];
+    const int32_t nnz = krp[n];
+    if (nnz == 0) {   // diagonal factor: no dependencies
+        for (int64_t k = wave; k < n; k += W) {
+            const int32_t row = krow[k];
+            double r = rhs[rhs_idx ? rhs_idx[row] : row];
+            if (diag) r = r / diag[row];
+            if (lane == 0) x[row] = r;
         }
-    };
-    auto body = [&](int64_t k, const SfHead &h, SfBody &b) {
-        if (k < n) {
-            b.row = h.row;
-            b.s = h.s;
-            b.e = h.e;
-#pragma unroll
-            for (int j = 0; j < kSfChunks; ++j) {
-                const int32_t idx = h.s + 64 * j + lane;
-                b.c[j] = idx < h.e ? kci[idx] : -1;
-                b.v[j] = idx < h.e ? kva[idx] : 0.0;
-            }
-            if (lane == 0) {
-                b.b = rhs[rhs_idx ? rhs_idx[h.row] : h.row];
-                b.d = diag ? diag[h.row] : 1.0;
-            }
-        }
-    };
+        return;
+    }
+    const SfSrc src{n, nnz - 1, krp, kci, krow, rhs_idx ? rhs_idx : krow, kva, diag ? diag : rhs,
+                    rhs_idx != nullptr, diag != nullptr, opaque_zero()};
     // register ring of D rows per wave: row k's entries are loaded D rows (D*W positions) before
     // it is solved and its header 2D rows before, so a wave keeps D rows of HBM loads in flight
-    // while it waits on LDS hand-offs (one row in flight cost one HBM round trip per row)
+    // while it waits on LDS hand-offs (one row in flight cost one HBM round trip per row); all of
+    // them branch-free (see SfSrc), so the compiler's vmcnt waits leave them in flight
     SfHead hq[D];
     SfBody bq[D];
 #pragma unroll
-    for (int t = 0; t < D; ++t) head(wave + t * W, hq[t]);
+    for (int t = 0; t < D; ++t) src.head(wave + t * W, hq[t]);
 #pragma unroll
-    for (int t = 0; t < D; ++t) body(wave + t * W, hq[t], bq[t]);
+    for (int t = 0; t < D; ++t) src.body(hq[t], bq[t], lane);
 #pragma unroll
-    for (int t = 0; t < D; ++t) head(wave + (D + t) * W, hq[t]);
+    for (int t = 0; t < D; ++t) src.head(wave + (D + t) * W, hq[t]);
     for (int64_t k0 = wave; k0 < n; k0 += D * W) {
 #pragma unroll
         for (int t = 0; t < D; ++t) {
             const int64_t k = k0 + t * W;
             if (k >= n) break;
             const SfBody cur = bq[t];
-            body(k + D * W, hq[t], bq[t]);
-            head(k + 2 * D * W, hq[t]);
+            const double bv = rhs[cur.ri];   // goes out before the prefetches (loads complete in order)
+            src.body(hq[t], bq[t], lane);
+            src.head(k + 2 * D * W, hq[t]);
             // all of this row's first LDS reads go out together; only a sentinel among them waits
             uint64_t bits[kSfChunks];
 #pragma unroll
             for (int j = 0; j < kSfChunks; ++j)
-                bits[j] = cur.c[j] >= 0
-                              ? __hip_atomic_load(xs + cur.c[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)
-                              : 0;
+                bits[j] = __hip_atomic_load(xs + (cur.c[j] >= 0 ? cur.c[j] : 0), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
             double acc = 0.0;
 #pragma unroll
             for (int j = 0; j < kSfChunks; ++j)   // lane's entries in stored order: lane, lane+64, ...
                 if (cur.c[j] >= 0)
                     acc = fma(cur.v[j],
                               bits[j] == kSentinel ? lds_wait(cur.c[j]) : __longlong_as_double((long long)bits[j]), acc);
-            // longer rows (the dense tail of an LU factor): kLdsTail chunks of entries in flight at once
-            for (int32_t base = cur.s + 64 * kSfChunks; base < cur.e; base += 64 * kLdsTail) {
-                int32_t tc[kLdsTail];
-                double tv[kLdsTail];
-                uint64_t tb[kLdsTail];
+            // longer rows (the dense tail of an LU factor, uniform): kLdsTail chunks of entries in flight at once
+            if (cur.e - cur.s > 64 * kSfChunks) {
+                for (int32_t base = cur.s + 64 * kSfChunks; base < cur.e; base += 64 * kLdsTail) {
+                    int32_t tc[kLdsTail];
+                    double tv[kLdsTail];
+                    uint64_t tb[kLdsTail];
 #pragma unroll
-                for (int u = 0; u < kLdsTail; ++u) {
-                    const int32_t idx = base + 64 * u + lane;
-                    tc[u] = idx < cur.e ? kci[idx] : -1;
-                    tv[u] = idx < cur.e ? kva[idx] : 0.0;
+                    for (int u = 0; u < kLdsTail; ++u) {
+                        const int32_t idx = base + 64 * u + lane;
+                        tc[u] = idx < cur.e ? kci[idx] : -1;
+                        tv[u] = idx < cur.e ? kva[idx] : 0.0;
+                    }
+#pragma unroll
+                    for (int u = 0; u < kLdsTail; ++u)
+                        tb[u] = tc[u] >= 0 ? __hip_atomic_load(xs + tc[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+#pragma unroll
+                    for (int u = 0; u < kLdsTail; ++u)
+                        if (tc[u] >= 0)
+                            acc = fma(tv[u], tb[u] == kSentinel ? lds_wait(tc[u]) : __longlong_as_double((long long)tb[u]),
+                                      acc);
                 }
-#pragma unroll
-                for (int u = 0; u < kLdsTail; ++u)
-                    tb[u] = tc[u] >= 0 ? __hip_atomic_load(xs + tc[u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
-#pragma unroll
-                for (int u = 0; u < kLdsTail; ++u)
-                    if (tc[u] >= 0)
-                        acc = fma(tv[u], tb[u] == kSentinel ? lds_wait(tc[u]) : __longlong_as_double((long long)tb[u]),
-                                  acc);
+                drain_vm();
             }
             const double sum = row_total(acc);
-            if (lane == 0) {
-                double r = cur.b - sum;
-                if (diag) r = r / cur.d;
-                __hip_atomic_store(xs + cur.row, (uint64_t)__double_as_longlong(r), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
+            double r = bv - sum;
+            if (diag) r = r / cur.d;
+            // every lane: the same value to the same LDS word
+            __hip_atomic_store(xs + cur.row, (uint64_t)__double_as_longlong(r), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     }
     __syncthreads();
