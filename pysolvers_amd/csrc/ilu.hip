@@ -1484,10 +1484,13 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
 #ifndef PSK_GRID_D
 #define PSK_GRID_D 12
 #endif
+#ifndef PSK_GRID_DD   // prefetch depth with the record dictionary (a step's slot: index + rhs)
+#define PSK_GRID_DD PSK_GRID_D
+#endif
         const bool dict = T.grid_dict_n > 0;
-#define PSK_GRID_K(KK, DD)                                                                                    \
-    k = dict ? reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DD, true>)                               \
-             : reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DD, false>)
+#define PSK_GRID_K(KK, DN)                                                                                    \
+    k = dict ? reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, PSK_GRID_DD, true>)                      \
+             : reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DN, false>)
         if (T.grid_K == 2) PSK_GRID_K(2, PSK_GRID_D);
         else if (T.grid_K == 4) PSK_GRID_K(4, (PSK_GRID_D > 8 ? 8 : PSK_GRID_D));
         else if (T.grid_K == 8) PSK_GRID_K(8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D));
