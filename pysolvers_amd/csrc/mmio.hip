@@ -79,6 +79,13 @@ int mm_open(const char *path, MMFile &f) {
         f.ncols = c;
         f.entries = e;
         f.body = pos;
+        // an entry takes at least 4 bytes ("r c\n"; 3 on an unterminated last line): a size line
+        // claiming more entries than the body can hold is refused here, before anything is sized
+        // from it (scripts/asan_host.sh: a 9e18-entry header made the reserve below throw through
+        // the C ABI)
+        if (e > (long long)((pos < f.text.size() ? f.text.size() - pos : 0) / 3 + 1))
+            return fail(PSK_ERR_ARG, "MatrixMarket: fewer entries than the size line says");
+        if (r >= INT32_MAX || c >= INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "MatrixMarket: int32 CSR required");
         return PSK_OK;
     }
     return fail(PSK_ERR_ARG, "MatrixMarket: missing size line");

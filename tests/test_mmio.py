@@ -62,6 +62,11 @@ def test_header_variants(tmp_path, name):
     "%%MatrixMarket matrix coordinate real general\n2 2 2\n1 1 1\n3 1 1\n",     # index out of range
     "%%MatrixMarket matrix coordinate real general\n2 2 3\n1 1 1\n",            # too few entries
     "not a matrix market file\n",
+    # size lines claiming more than the file can hold / more than int32 CSR (found by the ASan run,
+    # scripts/asan_host.sh: the first one made the reader's reserve throw through the C ABI)
+    "%%MatrixMarket matrix coordinate real general\n3 3 9000000000000000000\n1 1 1\n",
+    "%%MatrixMarket matrix coordinate real symmetric\n3 3 4611686018427387904\n1 1 1\n",
+    "%%MatrixMarket matrix coordinate real general\n99999999999 3 1\n1 1 1\n",
 ])
 def test_rejects(tmp_path, text):
     from pysolvers_amd import _native as N
