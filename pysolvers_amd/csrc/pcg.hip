@@ -32,8 +32,23 @@ struct PcgState {
     double normB;
     double tauNormB;
     int64_t live;      // k of the last K2 that ran to completion (no breakdown); -1 before the loop
-    double pad[2];
+    int64_t *hdone;    // host-mapped stamp of the iteration that set `done` (nullptr: none), see set_done
+    double pad;
 };
+
+// done = v != 0, and the host-mapped stamp the solve loop polls: k + 2 for a kernel of iteration k, 1
+// for the init (0 = running) — a system-scope store drained before the kernel ends, so once an event
+// recorded after this kernel has completed the host reads the word directly, with no per-chunk
+// device-to-host copy (a blit kernel) on the solver's stream. The stamp lets the host act on the state
+// as of the chunk it waited for, not a later one its GPU has already run: every rank of a sharded
+// solve then stops after the same chunk and enqueues the same collectives.
+__device__ __forceinline__ void set_done(PcgState *st, int32_t v, int64_t stamp) {
+    st->done = v;
+    if (st->hdone) {
+        __hip_atomic_store(st->hdone, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
+}
 
 // ---- K0: r = b; p = M r; x = 0; partials [b.b, u.r] ----------------------------------------
 __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const double *__restrict__ b,
@@ -63,7 +78,7 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const doubl
 }
 
 __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *part, int np, double tau,
-                                                                 PcgState *st, double *udr) {
+                                                                 PcgState *st, double *udr, int64_t *hdone) {
     __shared__ double sh[kWaves];
     const double bb = reduce_partials(part, np, 2, sh);
     const double ur = reduce_partials(part + 1, np, 2, sh);
@@ -75,14 +90,15 @@ __global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *p
         st->resid = 0.0;
         st->brk_kind = 0;
         st->live = -1;
+        st->hdone = hdone;
         udr[0] = ur;
         if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
-            st->done = 1;
             st->iters = 1;
+            set_done(st, 1, 1);
         } else if (ur == 0.0) {                        // :104-105
-            st->done = 2;
             st->brk_kind = 1;
             st->iters = 0;
+            set_done(st, 2, 1);
         } else {
             st->done = 0;
         }
@@ -105,7 +121,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
             st->iters = k;
-            st->done = 2;
+            set_done(st, 2, k + 2);
         }
         return;
     }
@@ -195,7 +211,7 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
         if (tile == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
             st->resid = normR;
-            st->done = 1;
+            set_done(st, 1, k + 2);
         }
         return false;
     }
@@ -462,15 +478,23 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     }
     PSK_HIP(hipGetLastError());
     if (sharded) PSK_TRY(allgather(A, w.part2, w.initg, 2 * npi, s));
+    // polling: every C iterations an event; the host waits on the event L chunks back and then reads the
+    // host-mapped done word the kernels set (set_done). PSK_PCG_FLAG_COPY=1: the round-2/3 scheme, a
+    // 4-byte device-to-host copy of st->done per chunk (a blit kernel on the stream)
+    static const bool flag_copy = [] {
+        const char *e = std::getenv("PSK_PCG_FLAG_COPY");
+        return e && std::atoi(e) == 1;
+    }();
+    const int L = 2, NS = L + 2;
+    int32_t *hflag = nullptr;   // [0, NS): per-chunk copies (flag_copy); then the mapped int64 stamp
+    PSK_HIP(hipHostMalloc(&hflag, (NS + 2) * sizeof(int64_t), hipHostMallocCoherent));
+    volatile int64_t *hdone = reinterpret_cast<int64_t *>(hflag) + NS;
+    *hdone = 0;
     hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.initg, P * npi, ctl->tau, w.st,
-                       w.udr);
+                       w.udr, flag_copy ? nullptr : const_cast<int64_t *>(hdone));
     PSK_HIP(hipGetLastError());
 
-    // polling ring: flag copies every C iterations, host waits on the copy L chunks back
     int C = ctl->check_every > 0 ? ctl->check_every : (n >= (1 << 20) ? 2 : 16);
-    const int L = 2, NS = L + 2;
-    int32_t *hflag = nullptr;
-    PSK_HIP(hipHostMalloc(&hflag, NS * sizeof(int32_t), hipHostMallocDefault));
     hipEvent_t fev[NS];
     for (int i = 0; i < NS; ++i) PSK_HIP(hipEventCreateWithFlags(&fev[i], hipEventDisableTiming));
     // optional SpMV timing ring
@@ -526,13 +550,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if (k > 0 && k % C == 0) {
             const int64_t chunk = k / C;   // chunks fully launched
             const int slot = (int)((chunk - 1) % NS);
-            rc = hipMemcpyAsync(&hflag[slot], &w.st->done, 4, hipMemcpyDeviceToHost, s) == hipSuccess
-                     ? PSK_OK : fail(PSK_ERR_HIP, "flag copy");
+            if (flag_copy)
+                rc = hipMemcpyAsync(&hflag[slot], &w.st->done, 4, hipMemcpyDeviceToHost, s) == hipSuccess
+                         ? PSK_OK : fail(PSK_ERR_HIP, "flag copy");
             if (rc == PSK_OK && hipEventRecord(fev[slot], s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
             if (rc == PSK_OK && chunk - 1 - L >= 0) {
                 const int os = (int)((chunk - 1 - L) % NS);
                 if (hipEventSynchronize(fev[os]) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
-                else if (hflag[os] != 0) break;
+                else if (flag_copy ? hflag[os] != 0 : (*hdone != 0 && *hdone <= (chunk - L) * (int64_t)C + 1)) break;
             }
             if (rc != PSK_OK) break;
         }
