@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 namespace psk {
@@ -50,15 +51,21 @@ __global__ void amg_add_kernel(int64_t n, double *__restrict__ x, const double *
     if (i < n) x[i] = x[i] + d[i];   // x + dx (ClassicSmoothers.py:14, :34)
 }
 
+// ||v||^2 partials, and x = copy(v) (VCycleSolver.py:69) in the same pass
 __global__ __launch_bounds__(kBlock) void amg_sqnorm_partial_kernel(int64_t n, const double *__restrict__ v,
-                                                                    double *__restrict__ part) {
+                                                                    double *__restrict__ part,
+                                                                    double *__restrict__ x) {
     __shared__ double sh[kWaves];
     int64_t t0, t1;
     const int64_t ntiles = (n + kVecTile - 1) / kVecTile;
     block_range(ntiles, t0, t1);
     const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
     double acc = 0.0;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) acc = fma(v[i], v[i], acc);
+    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
+        const double vi = v[i];
+        x[i] = vi;
+        acc = fma(vi, vi, acc);
+    }
     const double s = block_sum(acc, sh);
     if (threadIdx.x == 0) part[blockIdx.x] = s;
 }
@@ -104,6 +111,14 @@ static int amg_smooth(const AmgHierarchy *h, const Context *c, int lev, const do
     double *r = h->r[lev].as<double>(), *t = h->t[lev].as<double>();
     for (int it = 0; it < nu; ++it) {
         PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, s));
+        static const bool fuse = [] {   // PSK_AMG_FUSE=0: separate gather and add (A/B only)
+            const char *e = std::getenv("PSK_AMG_FUSE");
+            return !(e && std::atoi(e) == 0);
+        }();
+        if (fuse && h->S[lev] && h->S[lev]->kind == PSK_PREC_ILU) {   // Gauss-Seidel: x += U^-1 r in the last gather
+            PSK_TRY(ilu_apply_add(h->S[lev], r, x, s));
+            continue;
+        }
         PSK_TRY(prec_apply_dev(h->S[lev], n, r, t, s));
         hipLaunchKernelGGL(amg_add_kernel, vgrid(n), dim3(kBlock), 0, s, n, x, t);
         PSK_HIP(hipGetLastError());
@@ -142,11 +157,10 @@ int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     int64_t *flag = reinterpret_cast<int64_t *>(scal + 1);
     double *part = scal + 2;
     const int gv = grid_for_rows(c, n, kVecTile), ga = 1;   // the residual SpMV's sum: in-launch
-    hipLaunchKernelGGL(amg_sqnorm_partial_kernel, dim3(gv), dim3(kBlock), 0, s, n, v, part);
+    hipLaunchKernelGGL(amg_sqnorm_partial_kernel, dim3(gv), dim3(kBlock), 0, s, n, v, part, x);   // + x = copy(b) (:69)
     PSK_HIP(hipGetLastError());
     hipLaunchKernelGGL(amg_init_kernel, dim3(1), dim3(kBlock), 0, s, part, gv, scal, flag);
     PSK_HIP(hipGetLastError());
-    PSK_HIP(hipMemcpyAsync(x, v, (size_t)n * sizeof(double), hipMemcpyDeviceToDevice, s));   // x = copy(b) (:69)
     for (int k = 0; k < h->num_iters; ++k) {
         PSK_TRY(amg_level(h, c, top, v, x, s));                                            // runCycle (:79)
         if (k + 1 < h->num_iters) {

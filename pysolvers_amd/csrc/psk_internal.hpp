@@ -703,6 +703,7 @@ int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int6
 // generic preconditioner apply (device pointers, out must not alias v): identity copy, Jacobi, ILU
 int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, hipStream_t s);
 int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
+int ilu_apply_add(const psk_prec *M, const double *v, double *x, hipStream_t s);   // x += M^-1 v
 int ilu_check_error(const psk_prec *M, hipStream_t s);
 int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
 void amg_free(AmgHierarchy *h);
