@@ -95,6 +95,14 @@ def test_configs4_amg_hierarchy_and_pcg_fd8192(psk):
     assert st1.iters() == st2.iters() == 3 and st1.success()
     assert np.array_equal(st1.info["hist"], st2.info["hist"]) and np.array_equal(st1.soln(), st2.soln())
     assert np.all(np.isfinite(st1.info["hist"])) and st1.info["hist"][-1] < np.linalg.norm(b)
+    # size-independent property at full size: the V-cycle apply (x = copy(v), VCycleSolver.py:69, then
+    # cycles of smoothing / restriction / prolongation, no convergence snapshot for random v) is
+    # linear in v, so M(u + 2 v) = M(u) + 2 M(v) up to rounding
+    rng = np.random.default_rng(8192)
+    u, v = rng.standard_normal(A.shape[0]), rng.standard_normal(A.shape[0])
+    yu, yv, yuv = M.applyRight(u), M.applyRight(v), M.applyRight(u + 2.0 * v)
+    assert np.all(np.isfinite(yuv))
+    assert np.linalg.norm(yuv - (yu + 2.0 * yv)) <= 1e-10 * np.linalg.norm(yuv)
 
 
 def test_configs4_amg_apply_and_pcg_vs_oracle_fd2048(psk):
