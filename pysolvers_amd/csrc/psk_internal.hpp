@@ -140,6 +140,8 @@ struct psk_csr {
     double *sl_dict = nullptr;   // value dictionary (<= 8 distinct values, padded to 8), nullptr = none
     int32_t sl_dict_n = 0;
     int32_t sl_uniform_w = 0;    // > 0: every slice this wide and packed (offsets computed, not loaded)
+    int32_t sl_compact = 0;      // uniform, odd width, <= 2 dictionary values: the value-index bits sit in
+                                 // the last delta word's free half (no index words; spmv_uniform_kernel CMP)
     int64_t sl_slots = 0, sl_packed_slots = 0, sl_stream_bytes = 0;
     // distributed
     psk_comm *comm = nullptr;

@@ -286,14 +286,17 @@ __device__ __forceinline__ double diag_x(const int32_t *cc, const double *xv, in
 // then waited on each one: four memory round trips per slice instead of two), the offsets are
 // computed from the slice index, and every slot's gather is issued unconditionally (padding slots
 // gather x[0], and their product is skipped). DK: dictionary size class (0 = double values in slot
-// pairs, 2 / 4 / 8 entries).
-template <int MODE, int DK, int UW>
+// pairs, 2 / 4 / 8 entries). CMP (odd UW, DK = 2): entry j's 1-bit value index is bit j of the last
+// column word's upper half — the half an odd width leaves unused — so no index words are streamed
+// (FD: 12 instead of 20 B/row of stream).
+template <int MODE, int DK, int UW, bool CMP = false>
 __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
     int64_t n, const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ sdict,
     const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
     const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done, TileMap tm) {
     constexpr int NP = (UW + 1) / 2;                 // packed column words per lane
-    constexpr int NI = DK > 0 ? (UW + 3) / 4 : 0;    // dictionary index words per lane
+    static_assert(!CMP || (DK == 2 && (UW & 1)), "compact stream: odd width, 2-entry dictionary");
+    constexpr int NI = DK > 0 && !CMP ? (UW + 3) / 4 : 0;   // dictionary index words per lane
     const int32_t dn = *(done ? done : &g_spmv_never_done);   // tested once the stream is in flight
     const int tid = threadIdx.x;
     const int64_t t = tile_of_block(tm), row = t * kSlice + tid;
@@ -306,6 +309,7 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
     if (DK > 0) {
 #pragma unroll
         for (int q = 0; q < NI; ++q) iw[q] = (uint32_t)ld_stream(pword + (NP + q) * kSlice);
+        if (CMP) iw[0] = 0;
     } else {
         const double *v0 = sval + t * (int64_t)(UW * kSlice);
 #pragma unroll
@@ -349,7 +353,8 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
     }
     if (DK > 0) {
 #pragma unroll
-        for (int j = 0; j < UW; ++j) vv[j] = dict_pick<DK>(dv, (iw[j >> 2] >> (8 * (j & 3))) & 0xff);
+        for (int j = 0; j < UW; ++j)
+            vv[j] = dict_pick<DK>(dv, CMP ? (cw[NP - 1] >> (16 + j)) & 1u : (iw[j >> 2] >> (8 * (j & 3))) & 0xff);
     }
     double sum = 0.0;
 #pragma unroll
@@ -545,7 +550,8 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
                                                              const int64_t *__restrict__ swoff,
                                                              const int8_t *__restrict__ sfmt, int32_t *__restrict__ scol,
                                                              int32_t *__restrict__ spcol, double *__restrict__ sval,
-                                                             const double *__restrict__ sdict, int nd) {
+                                                             const double *__restrict__ sdict, int nd,
+                                                             int compact) {
     const int tid = threadIdx.x;
     const int64_t t = blockIdx.x, row = t * kSlice + tid;
     const int64_t o = soff[t];
@@ -557,7 +563,7 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
         if (!sdict) sval[sliced_vpos(o, j, w, tid)] = j < len ? vals[a + j] : 0.0;
         if (!packed) scol[o + (int64_t)j * kSlice + tid] = j < len ? colidx[a + j] : -1;
     }
-    if (sdict) {   // index words; padding slots index entry 0 (never read: their column is padding)
+    if (sdict && !compact) {   // index words; padding slots index entry 0 (never read: their column is padding)
         int32_t *vword = spcol + swoff[t] + (packed ? (int64_t)((w + 1) / 2) * kSlice : 0);
         for (int q = 0; 4 * q < w; ++q) {
             uint32_t word = 0;
@@ -576,7 +582,13 @@ __global__ __launch_bounds__(kBlock) void sliced_fill_kernel(int64_t n, const in
             const int j0 = 2 * p, j1 = 2 * p + 1;
             const int16_t d0 = j0 < len ? (int16_t)(colidx[a + j0] - row) : kPad16;
             const int16_t d1 = j1 < len ? (int16_t)(colidx[a + j1] - row) : kPad16;
-            spcol[swoff[t] + (int64_t)p * kSlice + tid] = (int32_t)(uint16_t)d0 | ((int32_t)d1 * 65536);
+            uint32_t hi = (uint16_t)d1;
+            if (compact && j1 == w) {   // the free half: bit j = entry j's dictionary index (nd <= 2)
+                hi = 0;
+                for (int j = 0; j < w && j < len; ++j)
+                    if (nd > 1 && !same_bits(sdict[0], vals[a + j])) hi |= 1u << j;   // the index word's k
+            }
+            spcol[swoff[t] + (int64_t)p * kSlice + tid] = (int32_t)((uint32_t)(uint16_t)d0 | (hi << 16));
         }
 }
 
@@ -593,6 +605,7 @@ void sliced_free(psk_csr *A) {
     A->sl_dict = nullptr;
     A->sl_dict_n = 0;
     A->sl_uniform_w = 0;
+    A->sl_compact = 0;
     A->sl_slots = 0;
     A->sl_packed_slots = 0;
     A->sl_stream_bytes = 0;
@@ -681,6 +694,10 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
         all_pack && wmax > 0 && wmax <= kSliceRegs && wmax * nt * 100 <= wsum * 101 && !(ue && std::atoi(ue) == 0);
     if (uniform)
         for (int64_t t = 0; t < nt; ++t) wd[(size_t)t] = (int32_t)wmax;
+    // compact stream (PSK_SPMV_COMPACT=0: never): uniform, odd width, a 1-bit value index
+    const char *ce = std::getenv("PSK_SPMV_COMPACT");
+    const bool compact = uniform && !dict.empty() && dict.size() <= 2 && (wmax & 1) && wmax <= 15 &&
+                         !(ce && std::atoi(ce) == 0);
     std::vector<int64_t> off((size_t)nt + 1), woff((size_t)nt + 1);
     std::vector<int8_t> fmt((size_t)nt);
     off[0] = 0;
@@ -692,9 +709,9 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
         fmt[(size_t)t] = (pack && wd[(size_t)(nt + t)] <= kMaxDelta16) ? 1 : 0;
         if (fmt[(size_t)t]) packed_slots += w * kSlice;
         col_bytes += (fmt[(size_t)t] ? 4 * ((w + 1) / 2) : 4 * w) * kSlice;
-        val_bytes += (dict.empty() ? 8 * w : 4 * ((w + 3) / 4)) * kSlice;
+        val_bytes += (dict.empty() ? 8 * w : compact ? 0 : 4 * ((w + 3) / 4)) * kSlice;
         // the word stream: packed column words, then dictionary index words
-        const int64_t words = (fmt[(size_t)t] ? (w + 1) / 2 : 0) + (dict.empty() ? 0 : (w + 3) / 4);
+        const int64_t words = (fmt[(size_t)t] ? (w + 1) / 2 : 0) + (dict.empty() || compact ? 0 : (w + 3) / 4);
         woff[(size_t)t + 1] = woff[(size_t)t] + words * kSlice;
     }
     const int64_t slots = off[(size_t)nt], nwords = woff[(size_t)nt];
@@ -727,9 +744,10 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
     }
     A->sl_dict_n = (int32_t)dict.size();
     A->sl_uniform_w = uniform ? (int32_t)wmax : 0;
+    A->sl_compact = compact ? 1 : 0;
     hipLaunchKernelGGL(sliced_fill_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, A->n, A->rowptr, A->colidx, A->vals,
                        A->sl_off, A->sl_woff, A->sl_fmt, A->sl_col, A->sl_pcol, A->sl_val, A->sl_dict,
-                       A->sl_dict_n);
+                       A->sl_dict_n, compact ? 1 : 0);
     PSK_HIP(hipGetLastError());
     PSK_HIP(hipStreamSynchronize(s));
     A->sl_slots = slots;
@@ -809,9 +827,17 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         default: PSK_UNI_LAUNCH(M, DK, 8); break;                                                              \
         }                                                                                                      \
     } while (0)
+#define PSK_UNI_LAUNCH_C(M, UW)                                                                                \
+    hipExtLaunchKernelGGL((spmv_uniform_kernel<M, 2, UW, true>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol, A->sl_val, \
+                          A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm)
 #define PSK_SLICED_LAUNCH(M)                                                                                   \
     do {                                                                                                       \
-        if (dk == 0) PSK_SLICED_LAUNCH_DK(M, 0);                                                               \
+        if (A->sl_compact) {   /* uniform, odd width, 2-entry dictionary */                                    \
+            if (uw == 1) PSK_UNI_LAUNCH_C(M, 1);                                                               \
+            else if (uw == 3) PSK_UNI_LAUNCH_C(M, 3);                                                          \
+            else if (uw == 5) PSK_UNI_LAUNCH_C(M, 5);                                                          \
+            else PSK_UNI_LAUNCH_C(M, 7);                                                                       \
+        } else if (dk == 0) PSK_SLICED_LAUNCH_DK(M, 0);                                                        \
         else if (dk == 2) PSK_SLICED_LAUNCH_DK(M, 2);                                                          \
         else if (dk == 4) PSK_SLICED_LAUNCH_DK(M, 4);                                                          \
         else PSK_SLICED_LAUNCH_DK(M, 8);                                                                       \
@@ -829,6 +855,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
 #undef PSK_SLICED_LAUNCH
 #undef PSK_SLICED_LAUNCH_DK
 #undef PSK_UNI_LAUNCH
+#undef PSK_UNI_LAUNCH_C
         PSK_HIP(hipGetLastError());
         return PSK_OK;
     }
