@@ -107,11 +107,21 @@ def main():
                     help="PMC traffic summary (tools/pmc_summary.py) of the same build; %%d = the side")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # launched as `python bench.py --gpus N` (no torchrun): start the N ranks ourselves. Nothing in
+        # this process has touched the GPU (libpsk is imported by the ranks only).
+        sys.exit(spawn_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    maps_out = os.environ.get("PSK_DUMP_MAPS")
+    if maps_out:
+        # registered before libpsk's own atexit hook, so it runs after it (LIFO): the process's
+        # mappings as exit() starts tearing libraries down, to resolve a fault PC to library + offset
+        import atexit
+        atexit.register(_dump_maps, maps_out)
 
     from pysolvers_amd import _native as N
     # one GPU per rank: LOCAL_RANK when every GPU is visible to every rank; a launcher that narrows
@@ -231,7 +241,10 @@ def main():
                                          "frac": blay / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS, **pbb}
             if args.general:
                 out["general_path"] = general_path(N, sys_.A, sys_.db, sys_.dsol, m, args.steps)
+            out["fixed_overhead"] = fixed_overhead(sys_, args.steps)
             out["spmv_csr_layout_batch50"] = csr_layout_batch(N, sys_.A, sys_.db, sys_.dsol, bspmv, reps=50)
+            # the north star's "CSR SpMV" inside the PCG loop: the same solve with the CSR layout
+            out["csr_layout_in_loop"] = csr_in_loop(sys_, bspmv, args.steps)
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
     sys_.free()
@@ -277,6 +290,84 @@ def main():
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
+
+
+def _dump_maps(path):
+    try:
+        with open("/proc/self/maps") as f, open(path, "w") as g:
+            g.write(f.read())
+    except OSError:
+        pass
+
+
+def spawn_ranks(nranks):
+    """One process per GPU without an external launcher: RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set
+    for each child (rendezvous on 127.0.0.1), rank 0's JSON line forwarded to stdout, non-zero exit if
+    any rank fails. The torchrun path (WORLD_SIZE already set) does not come here."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks), LOCAL_WORLD_SIZE=str(nranks),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = procs[0].communicate()[0]
+    codes = [p.wait() for p in procs]
+    sys.stdout.write(out0.decode())
+    sys.stdout.flush()
+    bad = [(r, c) for r, c in enumerate(codes) if c != 0]
+    if bad:
+        sys.stderr.write("bench.py: ranks failed (rank, exit code): %s\n" % bad)
+        return 1
+    return 0
+
+
+def fixed_overhead(sys_, steps, short=20, reps=5):
+    """The per-solve cost outside the iterations: median wall time of psk_pcg calls of `short` and of
+    `steps` iterations (no timing events), fitted as T(K) = a + b K; a is what a caller pays once per
+    solve (setup launches, final synchronisation, result copies)."""
+    N = sys_.N
+
+    def t(k):
+        ts = []
+        for _ in range(reps):
+            N.check(N.lib.psk_synchronize(), "sync")
+            t0 = time.perf_counter()
+            sys_.run(k, False)
+            N.check(N.lib.psk_synchronize(), "sync")
+            ts.append(time.perf_counter() - t0)
+        return median(ts)
+    t_short, t_long = t(short), t(steps)
+    b = (t_long - t_short) / (steps - short) if steps > short else float("nan")
+    return {"short_iters": short, "long_iters": steps, "short_ms": t_short * 1e3, "long_ms": t_long * 1e3,
+            "per_iteration_ms": b * 1e3, "fixed_overhead_ms": (t_short - short * b) * 1e3,
+            "short_it_s": short / t_short, "long_it_s": steps / t_long}
+
+
+def csr_in_loop(sys_, bspmv, steps, repeats=3):
+    """The headline solve with the matrix in the CSR layout (PSK_LAYOUT_CSR: the tile kernel with
+    LDS-staged products, 80 B/row of SURVEY §8d's CSR bytes): iterations/s and the in-loop CSR SpMV
+    priced on the CSR bytes. Leaves the matrix in the CSR layout (call after the other keys)."""
+    N = sys_.N
+    N.check(N.lib.psk_csr_layout(sys_.A, N.PSK_LAYOUT_CSR, None, None, None, None), "psk_csr_layout")
+    sys_.run(5, False)
+    regs = []
+    for _ in range(repeats):
+        N.check(N.lib.psk_synchronize(), "sync")
+        t0 = time.perf_counter()
+        res = sys_.run(steps, True)
+        N.check(N.lib.psk_synchronize(), "sync")
+        regs.append((time.perf_counter() - t0, res.spmv_ms))
+    regs.sort()
+    dt, sms = regs[len(regs) // 2]
+    ach = bspmv / (sms * 1e-3) / 1e9
+    return {"kernel": "spmv_kernel<kSpmvDot> (CSR layout, in the PCG loop)", "pcg_it_per_s": steps / dt,
+            "spmv_avg_launch_ms": sms, "csr_bytes_per_launch": bspmv, "achieved_GBps": ach,
+            "frac": ach / HBM_PEAK_GBPS, "regions_it_s": [steps / r[0] for r in regs]}
 
 
 class PcgSystem:

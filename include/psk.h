@@ -120,6 +120,12 @@ const char *psk_last_error(void);
 int         psk_device_count(int32_t *n);
 int         psk_set_device(int32_t dev);
 int         psk_synchronize(void);
+/* Drain every device stream and release the library's process-lifetime resources (streams, events,
+ * host-mapped words, reduction arrays) while the HIP runtime is alive; call once at process exit
+ * (the Python binding registers it with atexit). Afterwards entry points that need a device return
+ * PSK_ERR_ARG and psk_csr_destroy / psk_prec_destroy / psk_dfree are no-ops. No reference
+ * counterpart (process teardown). */
+int         psk_shutdown(void);
 /* device memory helpers (so a host binding can keep vectors resident in HBM) */
 int psk_dmalloc(int64_t bytes, void **dptr);
 int psk_dfree(void *dptr);
@@ -255,7 +261,8 @@ int psk_sa_aggregate(int64_t n, const int32_t *rowptr, const int32_t *colidx, co
                      int32_t *agg, int64_t *count, double *af_vals);
 
 /* ---- solvers ------------------------------------------------------------------------------ */
-/* M == NULL means identity. b, x: length n (local length for a distributed A). hist: nullable
+/* M == NULL means identity. b, x: length n (local length for a distributed A); with loc ==
+ * PSK_DEVICE b is read in place and x written in place during the solve (x must not alias b). hist: nullable
  * HOST array of ctl->maxiter doubles receiving the per-iteration residual norms reportIter
  * sees (PCG ||r_k||, GMRES |g[k+1]|); entries past res->iters+1 are left untouched.
  * x is overwritten with the solution (SolveStatus.soln()). */

@@ -12,7 +12,12 @@ frozen Newton Jacobian factors once and a Jacobian updated in place is refactore
 Status conventions as the reference: SolveStatus(True, x, None, None, '<name> solve succeeded') or
 SolveStatus(False, None, None, None, '<name> solve failed: <error>'). An exactly singular sparse
 matrix behaves as spsolve does there: a MatrixRankWarning and an all-NaN solution with a SUCCESS
-status (spsolve does not raise; the reference only fails on an exception).
+status (spsolve does not raise; the reference only fails on an exception). A DENSE ndarray goes to
+npla.solve in the reference, whose LinAlgError on an exactly singular matrix becomes
+SolveStatus(False, None, None, None, '<name> solve failed: Singular matrix'); here the same status is
+returned when the SuperLU factorisation of that matrix finds it exactly singular (make_direct.py pins
+both conventions; LAPACK's partial pivoting and SuperLU's ordering could disagree on a matrix that
+is singular only in one of the two pivot orders — no fixture has one).
 """
 import warnings
 
@@ -67,8 +72,11 @@ class DefaultDirectSolver(LinearSolver):
         assert n == len(b)
         if not (sp.issparse(A) or isinstance(A, (np.ndarray, DeviceCSR))):
             return SolveStatus(False, None, None, None, 'Input to solver [%s] not numpy or scipy' % self.name())
+        dense = isinstance(A, np.ndarray)
         try:
             op, singular = self._operator(A)
+            if singular and dense:                   # npla.solve (:64-65) raises LinAlgError -> failure
+                return SolveStatus(False, None, None, None, '%s solve failed: Singular matrix' % self.name())
             if singular:                             # spsolve: warning + NaN solution, no exception
                 warnings.warn("Matrix is exactly singular", MatrixRankWarning, stacklevel=2)
                 x = np.full(n, np.nan)

@@ -3,6 +3,7 @@
 There is no CPU fallback: if the library is missing or cannot be loaded this
 module raises ImportError, and every solve goes through the HIP kernels.
 """
+import atexit
 import ctypes
 import os
 
@@ -48,6 +49,7 @@ SIGNATURES = {
     "psk_device_count": (ctypes.c_int, [ctypes.POINTER(I32)]),
     "psk_set_device": (ctypes.c_int, [I32]),
     "psk_synchronize": (ctypes.c_int, []),
+    "psk_shutdown": (ctypes.c_int, []),
     "psk_dmalloc": (ctypes.c_int, [I64, PP]),
     "psk_dfree": (ctypes.c_int, [P]),
     "psk_h2d": (ctypes.c_int, [P, P, I64]),
@@ -159,6 +161,21 @@ def _load():
 
 
 lib = _load()
+shut_down = False
+
+
+def _shutdown():
+    """atexit: release libpsk's streams, events and host-mapped memory while the HIP runtime is still
+    alive (psk_shutdown). Registered at import, so it runs after every atexit handler registered
+    later (a caller's own cleanup still has the library); objects collected afterwards find their
+    destroy entry points turned into no-ops."""
+    global shut_down
+    if not shut_down:
+        shut_down = True
+        lib.psk_shutdown()
+
+
+atexit.register(_shutdown)
 
 
 def check(rc, where):

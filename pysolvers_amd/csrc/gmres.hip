@@ -246,6 +246,7 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
         return fail(PSK_ERR_UNSUPPORTED, "psk_gmres: sharded GMRES not built (replicas only)");
     Context *c;
     PSK_TRY(ctx(&c));
+    std::lock_guard<std::mutex> solve_lock(c->solve_mu);
     hipStream_t s = c->stream;
     std::memset(res, 0, sizeof(*res));
     const int64_t n = A->n, maxiter = ctl->maxiter;
@@ -300,9 +301,10 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     sb += aup((size_t)ld * 8);
     double *hv = reinterpret_cast<double *>(sb);   // K + 2 grid sums of a step (gm_mgs_kernel)
 
-    hipEvent_t ev0, ev1;
-    PSK_HIP(hipEventCreate(&ev0));
-    PSK_HIP(hipEventCreate(&ev1));
+    // events and the poll words come from the device's SolveKit (allocated once, round 4)
+    SolveKit *kit;
+    PSK_TRY(solve_kit(c, false, &kit));
+    hipEvent_t ev0 = kit->ev0, ev1 = kit->ev1;
     PSK_HIP(hipMemsetAsync(st, 0, sizeof(GmresState), s));
     // Hessenberg and rotated copies start at zero: entries below the subdiagonal are never written
     // and the least-squares solve reads them (HBar = np.zeros, GMRESSolver.py:80)
@@ -312,11 +314,10 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     PSK_HIP(hipMemsetAsync(x, 0, (size_t)n * 8, s));
     PSK_HIP(hipEventRecord(ev0, s));
 
-    int32_t *hflag = nullptr;
-    const int L = 2, NS = L + 2;
-    PSK_HIP(hipHostMalloc(&hflag, NS * sizeof(int32_t), hipHostMallocDefault));
-    hipEvent_t fev[NS];
-    for (int i = 0; i < NS; ++i) PSK_HIP(hipEventCreateWithFlags(&fev[i], hipEventDisableTiming));
+    const int L = 2, NS = kPollSlots;
+    static_assert(kPollSlots >= L + 2, "poll slots");
+    int32_t *hflag = reinterpret_cast<int32_t *>(static_cast<char *>(kit->hstage) + 1024);   // pinned, NS words
+    hipEvent_t *fev = kit->fev;
 
     int rc = PSK_OK;
     int64_t it = 0;          // global iterations completed before this cycle
@@ -469,6 +470,9 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
     }
     if (rc == PSK_OK && hipEventRecord(ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "gmres sync");
+    // an expired in-launch reduction wait (MGS / normalisation / SpMV dots) poisons h with NaN; report it
+    // as the error it is rather than as a numerical non-convergence (and never to a later solve)
+    if (rc == PSK_OK) rc = gridsum_check(c);
     if (rc == PSK_OK && gen) rc = prec_check_error(M, s);
     if (rc == PSK_OK) {
         float ms = 0.f;
@@ -493,9 +497,5 @@ extern "C" int psk_gmres(const psk_csr *Ac, const psk_prec *M, const double *b, 
         if (rc == PSK_OK) rc = from_device_vec(x, loc, n, xout, s);
         if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x copy");
     }
-    for (int i = 0; i < NS; ++i) (void)hipEventDestroy(fev[i]);
-    (void)hipHostFree(hflag);
-    (void)hipEventDestroy(ev0);
-    (void)hipEventDestroy(ev1);
     return rc;
 }

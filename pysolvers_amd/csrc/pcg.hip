@@ -33,7 +33,9 @@ struct PcgState {
     double tauNormB;
     int64_t live;      // k of the last K2 that ran to completion (no breakdown); -1 before the loop
     int64_t *hdone;    // host-mapped stamp of the iteration that set `done` (nullptr: none), see set_done
-    double pad;
+    double last_hist;  // the latest reported ||r_k|| (resid_recursive without copying the history back)
+    int32_t x_written; // 1 once x has been stored (Jacobi/identity: x0 = 0 is implicit until the first flush)
+    int32_t pad;
 };
 
 // done = v != 0, and the host-mapped stamp the solve loop polls: k + 2 for a kernel of iteration k, 1
@@ -50,59 +52,95 @@ __device__ __forceinline__ void set_done(PcgState *st, int32_t v, int64_t stamp)
     }
 }
 
-// ---- K0: r = b; p = M r; x = 0; partials [b.b, u.r] ----------------------------------------
-__global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const double *__restrict__ b,
-                                                          const double *__restrict__ dinv,
-                                                          double *__restrict__ x, double *__restrict__ r,
-                                                          double *__restrict__ p, double *__restrict__ part) {
-    __shared__ double sh[kWaves];
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
-    double bb = 0.0, ur = 0.0;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
-        const double bi = b[i];
-        const double ui = dinv ? dinv[i] * bi : bi;   // p = precond.applyRight(r)  :98
-        r[i] = bi;                                     // r = np.copy(b)             :97
-        p[i] = ui;
-        x[i] = 0.0;                                    // x = np.zeros_like(b)       :100
-        bb = fma(bi, bi, bb);
-        ur = fma(ui, bi, ur);                          // uDotR = np.dot(u, r)       :102
-    }
-    const double s0 = block_sum(bb, sh);
-    const double s1 = block_sum(ur, sh);
-    if (threadIdx.x == 0) {
-        part[2 * blockIdx.x] = s0;
-        part[2 * blockIdx.x + 1] = s1;
+// the solver state after the init sums bb = b.b and ur = u.r (PCGSolver.py:86-105)
+__device__ __forceinline__ void pcg_init_state(double bb, double ur, double tau, PcgState *st, double *udr,
+                                               int64_t *hdone, int32_t x_written) {
+    const double normB = sqrt(bb);                 // self.norm(b)   :86
+    st->normB = normB;
+    st->tauNormB = tau * normB;
+    st->iters = 0;
+    st->resid = 0.0;
+    st->brk_kind = 0;
+    st->live = -1;
+    st->hdone = hdone;
+    st->last_hist = normB;
+    st->x_written = x_written;
+    udr[0] = ur;
+    if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
+        st->iters = 1;
+        set_done(st, 1, 1);
+    } else if (ur == 0.0) {                        // :104-105
+        st->brk_kind = 1;
+        st->iters = 0;
+        set_done(st, 2, 1);
+    } else {
+        st->done = 0;
     }
 }
 
-__global__ __launch_bounds__(kBlock) void pcg_init_finish_kernel(const double *part, int np, double tau,
-                                                                 PcgState *st, double *udr, int64_t *hdone) {
+// fused init finish: runs once, in thread 0 of the workgroup that completes the init's grid sums
+struct PcgInitFin {
+    double tau;
+    PcgState *st;
+    double *udr;
+    int64_t *hdone;
+    int32_t x_written;
+    __device__ void operator()(const double *r) const { pcg_init_state(r[0], r[1], tau, st, udr, hdone, x_written); }
+};
+
+// ---- K0 (Jacobi/identity): r = b; p_0 = M r; [b.b, u.r] -----------------------------------
+// One-shot like K2 (one 512-element tile per workgroup), the two sums finished in the same launch by
+// gridsum and, unsharded, the solver state set by the workgroup that completes them (PcgInitFin; a
+// sharded solve all-gathers the per-rank sums and runs pcg_init_finish_kernel). x0 = 0 is not stored:
+// K3's first flush of the deferred x updates starts from the literal 0.0 (x = np.zeros_like(b) :100,
+// then x + alpha*p :121: the same roundings), so the init streams 24 B/row instead of 32.
+template <int JAC, bool FUSED>
+__global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const double *__restrict__ b,
+                                                          const double *__restrict__ dinv, double ds,
+                                                          double *__restrict__ r, double *__restrict__ p, GridSum gs,
+                                                          PcgInitFin fin) {
     __shared__ double sh[kWaves];
-    const double bb = reduce_partials(part, np, 2, sh);
-    const double ur = reduce_partials(part + 1, np, 2, sh);
-    if (threadIdx.x == 0) {
-        const double normB = sqrt(bb);                 // self.norm(b)   :86
-        st->normB = normB;
-        st->tauNormB = tau * normB;
-        st->iters = 0;
-        st->resid = 0.0;
-        st->brk_kind = 0;
-        st->live = -1;
-        st->hdone = hdone;
-        udr[0] = ur;
-        if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
-            st->iters = 1;
-            set_done(st, 1, 1);
-        } else if (ur == 0.0) {                        // :104-105
-            st->brk_kind = 1;
-            st->iters = 0;
-            set_done(st, 2, 1);
-        } else {
-            st->done = 0;
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    uint32_t ticket = 0;
+    double bb = 0.0, ur = 0.0;
+    if (i + 1 < n) {
+        const dv2 bi = ld2nt(b + i);
+        dv2 d{ds, ds};
+        if (JAC == 1) d = ld2nt(dinv + i);
+        ticket = gridsum_ticket(gs);
+        dv2 u = bi;
+        if (JAC) {
+            u.x = d.x * bi.x;                          // p = precond.applyRight(r)  :98
+            u.y = d.y * bi.y;
+        }
+        st2(r + i, bi);                                // r = np.copy(b)             :97
+        st2(p + i, u);
+        bb = fma(bi.x, bi.x, bb);
+        bb = fma(bi.y, bi.y, bb);
+        ur = fma(u.x, bi.x, ur);                       // uDotR = np.dot(u, r)       :102
+        ur = fma(u.y, bi.y, ur);
+    } else {
+        ticket = gridsum_ticket(gs);
+        if (i < n) {   // odd tail element
+            const double bi = b[i];
+            const double u0 = JAC == 2 ? ds * bi : JAC ? dinv[i] * bi : bi;
+            r[i] = bi;
+            p[i] = u0;
+            bb = bi * bi;
+            ur = u0 * bi;
         }
     }
+    const double v[2] = {block_sum(bb, sh), block_sum(ur, sh)};
+    if (FUSED)
+        gridsum_publish<2>(gs, v, sh, ticket, fin);
+    else
+        gridsum_publish<2>(gs, v, sh, ticket);
+}
+
+// sharded init: the per-rank sums all-gathered, added in rank order (bit-identical on every rank)
+__global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgState *st, double *udr,
+                                       int64_t *hdone) {
+    if (threadIdx.x == 0) pcg_init_state(rank_sum(g, P, 2, 0), rank_sum(g, P, 2, 1), tau, st, udr, hdone, 0);
 }
 
 // ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
@@ -200,17 +238,23 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
                                              const double *__restrict__ alphas = nullptr) {
     alpha = udr[k] / pTAp;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
-    if (tile == 0 && threadIdx.x == 0) hist[k] = normR;   // reportIter  :126
+    if (tile == 0 && threadIdx.x == 0) {
+        hist[k] = normR;                                     // reportIter  :126
+        st->last_hist = normR;
+    }
     if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
         const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+        // deferred updates (pr): before the first flush (k < kPcgDefer) x is still the implicit x0 = 0
+        const bool x0 = pr && k < kPcgDefer;
         for (int64_t j = i; j < i + 2 && j < n; ++j) {
-            double xj = x[j];
+            double xj = x0 ? 0.0 : x[j];
             if (pr) xj = pcg_catch_up(xj, pr, pcg_pending(k), k, alphas, j);
             x[j] = xj + alpha * p[j];                        // :121
         }
         if (tile == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
             st->resid = normR;
+            st->x_written = 1;
             set_done(st, 1, k + 2);
         }
         return false;
@@ -232,16 +276,22 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
     // halo exchange then overlaps the rest); tile 0 alone writes the solver state
     const int64_t tile = tile_base + blockIdx.x;
-    const double *__restrict__ pcur = pr.b[k % kPcgDefer];
-    double *__restrict__ pnext = pr.b[(k + 1) % kPcgDefer];
+    const double *pcur = pr.b[k % kPcgDefer];
+    // NOT __restrict__: on a flush iteration pnext is p_{k+1-kPcgDefer}'s buffer, which the x catch-up
+    // below reads through pr.b first; the store to pnext must stay after those loads
+    double *pnext = pr.b[(k + 1) % kPcgDefer];
     const int q = pcg_pending(k);
     double alpha, beta;
     if (!pcg_direction_scalars(n, x, pcur, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
                                rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
                                beta, tile, &pr, alphas))
         return;
-    if (tile == 0 && threadIdx.x == 0) alphas[k] = alpha;
     const bool flush = q == kPcgDefer - 1 || k == maxiter - 1;
+    const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0 (never loaded)
+    if (tile == 0 && threadIdx.x == 0) {
+        alphas[k] = alpha;
+        if (flush) st->x_written = 1;
+    }
     const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
     if (i + 1 < n) {
@@ -254,7 +304,8 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
             u1 = d.y * ro.y;
         }
         if (flush) {
-            dv2 xo = ld2nt(x + i);
+            dv2 xo{0.0, 0.0};
+            if (!x0) xo = ld2nt(x + i);
             dv2 pp[kPcgDefer > 1 ? kPcgDefer - 1 : 1];
 #pragma unroll
             for (int t = 1; t < kPcgDefer; ++t)
@@ -274,11 +325,15 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
         dv2 pn;
         pn.x = u0 + beta * po.x;                             // p = u + beta*p  :138
         pn.y = u1 + beta * po.y;
+#ifdef PSK_LAB_K3_PNT
+        st2nt(pnext + i, pn);   // lab: p stored non-temporally (the K3 -> SpMV boundary's dirty bytes)
+#else
         st2(pnext + i, pn);
+#endif
     } else if (i < n) {
         const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
         const double pi = pcur[i];
-        if (flush) x[i] = pcg_catch_up(x[i], &pr, q, k, alphas, i) + alpha * pi;
+        if (flush) x[i] = pcg_catch_up(x0 ? 0.0 : x[i], &pr, q, k, alphas, i) + alpha * pi;
         pnext[i] = u0 + beta * pi;
     }
 }
@@ -287,7 +342,7 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
 __global__ void pcg_flush_kernel(int64_t n, double *__restrict__ x, PRing pr, const double *__restrict__ alphas,
                                  int64_t k) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i < n) x[i] = pcg_catch_up(x[i], &pr, pcg_pending(k), k, alphas, i);
+    if (i < n) x[i] = pcg_catch_up(k < kPcgDefer ? 0.0 : x[i], &pr, pcg_pending(k), k, alphas, i);
 }
 
 // ---- general preconditioner (ILU, ...): u = M^-1 r is materialised by the preconditioner's own
@@ -301,27 +356,22 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_init_kernel(int64_t n, const d
     }
 }
 
-// p = u (copy of M^-1 r, :98-99); partials [b.b, u.r]
+// p = u (copy of M^-1 r, :98-99); [b.b, u.r] finished in-launch and the state set (one-shot, as K0)
 __global__ __launch_bounds__(kBlock) void pcg_gen_init2_kernel(int64_t n, const double *__restrict__ r,
                                                                const double *__restrict__ u, double *__restrict__ p,
-                                                               double *__restrict__ part) {
+                                                               GridSum gs, PcgInitFin fin) {
     __shared__ double sh[kWaves];
-    int64_t t0, t1;
-    block_range((n + kVecTile - 1) / kVecTile, t0, t1);
-    const int64_t i0 = t0 * kVecTile, i1 = (t1 * kVecTile < n) ? t1 * kVecTile : n;
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    const uint32_t ticket = gridsum_ticket(gs);
     double bb = 0.0, ur = 0.0;
-    for (int64_t i = i0 + threadIdx.x; i < i1; i += kBlock) {
-        const double ri = r[i], ui = u[i];
-        p[i] = ui;
-        bb = fma(ri, ri, bb);
-        ur = fma(ui, ri, ur);
+    for (int64_t j = i; j < i + 2 && j < n; ++j) {
+        const double rj = r[j], uj = u[j];
+        p[j] = uj;
+        bb = fma(rj, rj, bb);
+        ur = fma(uj, rj, ur);
     }
-    const double s0 = block_sum(bb, sh);
-    const double s1 = block_sum(ur, sh);
-    if (threadIdx.x == 0) {
-        part[2 * blockIdx.x] = s0;
-        part[2 * blockIdx.x + 1] = s1;
-    }
+    const double v[2] = {block_sum(bb, sh), block_sum(ur, sh)};
+    gridsum_publish<2>(gs, v, sh, ticket, fin);
 }
 
 __global__ __launch_bounds__(kBlock) void pcg_dot_kernel(int64_t n, const double *__restrict__ a,
@@ -364,30 +414,32 @@ struct PcgWork {
     double *x, *r, *p, *Ap, *u, *part1, *part2, *part3, *udr, *hist;
     PRing pr;              // Jacobi/identity K3: p_j in pr.b[j % kPcgDefer] (pr.b[0] = p)
     double *alphas;        // alpha_k (deferred x updates)
-    // sharded (P ranks): the ranks' gathered scalars, [P] p.Ap and [P][2] (r.r, u.r), and the
-    // gathered init partials [P][kMaxGrid][2]; unsharded: part1g/part2g alias part1/part2
+    double *pinit;         // the init's two grid sums [b.b, u.r] (this rank's, sharded)
+    // sharded (P ranks): the ranks' gathered scalars, [P] p.Ap, [P][2] (r.r, u.r) and [P][2] init sums;
+    // unsharded: part1g/part2g alias part1/part2
     double *part1g, *part2g, *initg;
     PcgState *st;
 };
 
-static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &w) {
+static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, bool own_x, int P, PcgWork &w) {
     const size_t vec = align_up((size_t)A->n * 8, 256), vecc = align_up((size_t)A->ncols * 8, 256);
-    const size_t big = (gen ? 4 : 3) * vec + (gen ? 1 : kPcgDefer) * vecc;
+    // x lives in the caller's device vector when the solve writes there directly (own_x false)
+    const size_t nx = own_x ? 1 : 0;
+    const size_t big = (2 + nx + (gen ? 1 : 0)) * vec + (gen ? 1 : kPcgDefer) * vecc;
     PSK_TRY(A->ws.ensure(big > 0 ? big : 256));
     char *b = A->ws.as<char>();
-    w.x = reinterpret_cast<double *>(b);
-    w.r = reinterpret_cast<double *>(b + vec);
-    w.Ap = reinterpret_cast<double *>(b + 2 * vec);
-    w.p = reinterpret_cast<double *>(b + 3 * vec);
-    w.u = gen ? reinterpret_cast<double *>(b + 3 * vec + vecc) : nullptr;
+    w.r = reinterpret_cast<double *>(b);
+    w.Ap = reinterpret_cast<double *>(b + vec);
+    w.x = own_x ? reinterpret_cast<double *>(b + 2 * vec) : nullptr;
+    char *pb = b + (2 + nx) * vec;
+    w.p = reinterpret_cast<double *>(pb);
+    w.u = gen ? reinterpret_cast<double *>(pb + vecc) : nullptr;
     for (int t = 0; t < kPcgDefer; ++t)
-        w.pr.b[t] = gen ? (t == 0 ? w.p : nullptr) : reinterpret_cast<double *>(b + 3 * vec + t * vecc);
+        w.pr.b[t] = gen ? (t == 0 ? w.p : nullptr) : reinterpret_cast<double *>(pb + t * vecc);
     const size_t small = align_up(sizeof(PcgState), 256) + 2 * align_up(kMaxGrid * 8, 256) +
                          align_up(2 * kMaxGrid * 8, 256) + align_up((size_t)(maxiter + 2) * 8, 256) +
-                         align_up((size_t)(maxiter + 1) * 8, 256) + align_up((size_t)(maxiter + 1) * 8, 256);
-    const size_t gath = P > 1 ? align_up((size_t)P * 8, 256) + align_up((size_t)P * 16, 256) +
-                                    align_up((size_t)P * 2 * kMaxGrid * 8, 256)
-                              : 0;
+                         align_up((size_t)(maxiter + 1) * 8, 256) + align_up((size_t)(maxiter + 1) * 8, 256) + 256;
+    const size_t gath = P > 1 ? align_up((size_t)P * 8, 256) + 2 * align_up((size_t)P * 16, 256) : 0;
     PSK_TRY(A->ws_small.ensure(small + gath));
     char *s = A->ws_small.as<char>();
     w.st = reinterpret_cast<PcgState *>(s);
@@ -404,6 +456,8 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &
     s += align_up((size_t)(maxiter + 1) * 8, 256);
     w.alphas = reinterpret_cast<double *>(s);
     s += align_up((size_t)(maxiter + 1) * 8, 256);
+    w.pinit = reinterpret_cast<double *>(s);
+    s += 256;
     if (P > 1) {
         w.part1g = reinterpret_cast<double *>(s);
         s += align_up((size_t)P * 8, 256);
@@ -413,7 +467,7 @@ static int pcg_workspace(psk_csr *A, int64_t maxiter, bool gen, int P, PcgWork &
     } else {
         w.part1g = w.part1;
         w.part2g = w.part2;
-        w.initg = w.part2;
+        w.initg = w.pinit;
     }
     return PSK_OK;
 }
@@ -426,6 +480,11 @@ static void set_msg(psk_result *res, const char *m) {
 
 using namespace psk;
 
+// Per-call cost (round 4): the host-mapped poll word, the staging buffer and every
+// event come from the device's SolveKit (allocated once); the init's sums and the solver state are
+// finished inside the init launch; a device-resident b is read in place and a device-resident x is
+// written in place (no staging copies); the history is copied back only when the caller asks for it;
+// the state, the gridsum error word and the end event share ONE stream synchronisation.
 extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, double *xout,
                        const psk_ctl *ctl, psk_result *res, double *hist, int32_t loc) {
     if (!Ac || !b || !xout || !ctl || !res) return fail(PSK_ERR_ARG, "psk_pcg: NULL argument");
@@ -435,6 +494,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     psk_csr *A = const_cast<psk_csr *>(Ac);
     Context *c;
     PSK_TRY(ctx(&c));
+    std::lock_guard<std::mutex> solve_lock(c->solve_mu);
     hipStream_t s = c->stream;
     std::memset(res, 0, sizeof(*res));
     const int64_t n = A->n, maxiter = ctl->maxiter;
@@ -444,72 +504,68 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // sharded: P ranks, scalars gathered (not all-reduced) and summed in rank order on every rank
     const bool sharded = A->comm != nullptr;
     const int P = sharded ? A->comm->nranks : 1;
+    const bool dev_io = loc == PSK_DEVICE;
     PcgWork w;
-    PSK_TRY(pcg_workspace(A, maxiter, gen, P, w));
+    PSK_TRY(pcg_workspace(A, maxiter, gen, !dev_io, P, w));
+    if (dev_io) w.x = xout;   // b and x in HBM: read b in place, write x in place
+    SolveKit *kit;
+    PSK_TRY(solve_kit(c, ctl->time_kernels > 0, &kit));
     const double *dinv = (M && M->kind == PSK_PREC_JACOBI) ? M->dinv : nullptr;
     const int jac = !dinv ? 0 : M->dinv_uniform ? 2 : 1;
     const double ds = jac == 2 ? M->dinv_value : 0.0;
-    const int gv = grid_for_rows(c, n, kVecTile);    // persistent grid of the init kernels
-    // one-shot grid of K2/K3 (one 512-element tile per workgroup); K1/K2 finish their dot products
+    // one-shot grid of K0/K2/K3 (one 512-element tile per workgroup); K0/K1/K2 finish their dot products
     // in-launch (gridsum), so the loop's scalars are part1[0] = p.Ap and part2[0..1] = (r.r, u.r)
     const int64_t nv = n > 0 ? (n + kVecTile - 1) / kVecTile : 1;
     if (nv > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: vector too long for a one-shot grid");
-    GridSum gs2, gs3;
+    GridSum gs0, gs2, gs3;
+    PSK_TRY(gridsum_prepare(c, nv, 2, w.pinit, &gs0));
     PSK_TRY(gridsum_prepare(c, nv, 2, w.part2, &gs2));
     PSK_TRY(gridsum_prepare(c, nv, 1, w.part3, &gs3));
-    // Sharded: the init partials are gathered as zero-padded kMaxGrid-long arrays (same RCCL count
-    // on every rank whatever its grid); the loop's grid sums as 1 and 2 values per rank.
-    const int npi = sharded ? kMaxGrid : gv;
-    if (sharded) PSK_HIP(hipMemsetAsync(w.part2, 0, 2 * kMaxGrid * sizeof(double), s));
-
-    hipEvent_t ev0, ev1;
-    PSK_HIP(hipEventCreate(&ev0));
-    PSK_HIP(hipEventCreate(&ev1));
-    // b staged in the Ap buffer (unused until the first SpMV)
-    PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
-    PSK_HIP(hipEventRecord(ev0, s));
+    // the host-mapped done stamp the kernels write (set_done); no kernel of an earlier solve is running
+    volatile int64_t *hdone = kit->hmap;
+    *hdone = 0;
+    const PcgInitFin fin{ctl->tau, w.st, w.udr, const_cast<int64_t *>(hdone), gen ? 1 : 0};
+    const double *bd = b;
+    if (!dev_io) {   // host b staged in the Ap buffer (unused until the first SpMV)
+        PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
+        bd = w.Ap;
+    }
+    PSK_HIP(hipEventRecord(kit->ev0, s));
+    const dim3 gk((unsigned)nv);
     if (gen) {
         const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
-        if (n > 0) hipLaunchKernelGGL(pcg_gen_init_kernel, dim3(nb), dim3(kBlock), 0, s, n, w.Ap, w.x, w.r);
+        if (n > 0) hipLaunchKernelGGL(pcg_gen_init_kernel, dim3(nb), dim3(kBlock), 0, s, n, bd, w.x, w.r);
         PSK_TRY(prec_apply_dev(M, n, w.r, w.u, s));                   // p = precond.applyRight(r)  :98
-        hipLaunchKernelGGL(pcg_gen_init2_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.r, w.u, w.p, w.part2);
+        hipLaunchKernelGGL(pcg_gen_init2_kernel, gk, dim3(kBlock), 0, s, n, w.r, w.u, w.p, gs0, fin);
     } else {
-        hipLaunchKernelGGL(pcg_init_kernel, dim3(gv), dim3(kBlock), 0, s, n, w.Ap, dinv, w.x, w.r, w.p, w.part2);
+#define PSK_PCG_INIT(J, F) \
+        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gk, dim3(kBlock), 0, s, n, bd, dinv, ds, w.r, w.p, gs0, fin)
+        if (jac == 2) { if (sharded) PSK_PCG_INIT(2, false); else PSK_PCG_INIT(2, true); }
+        else if (jac == 1) { if (sharded) PSK_PCG_INIT(1, false); else PSK_PCG_INIT(1, true); }
+        else { if (sharded) PSK_PCG_INIT(0, false); else PSK_PCG_INIT(0, true); }
+#undef PSK_PCG_INIT
     }
     PSK_HIP(hipGetLastError());
-    if (sharded) PSK_TRY(allgather(A, w.part2, w.initg, 2 * npi, s));
-    // polling: every C iterations an event; the host waits on the event L chunks back and then reads the
-    // host-mapped done word the kernels set (set_done). PSK_PCG_FLAG_COPY=1: the round-2/3 scheme, a
-    // 4-byte device-to-host copy of st->done per chunk (a blit kernel on the stream)
-    static const bool flag_copy = [] {
-        const char *e = std::getenv("PSK_PCG_FLAG_COPY");
-        return e && std::atoi(e) == 1;
-    }();
-    const int L = 2, NS = L + 2;
-    int32_t *hflag = nullptr;   // [0, NS): per-chunk copies (flag_copy); then the mapped int64 stamp
-    PSK_HIP(hipHostMalloc(&hflag, (NS + 2) * sizeof(int64_t), hipHostMallocCoherent));
-    volatile int64_t *hdone = reinterpret_cast<int64_t *>(hflag) + NS;
-    *hdone = 0;
-    hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.initg, P * npi, ctl->tau, w.st,
-                       w.udr, flag_copy ? nullptr : const_cast<int64_t *>(hdone));
-    PSK_HIP(hipGetLastError());
+    if (sharded) {
+        PSK_TRY(allgather(A, w.pinit, w.initg, 2, s));
+        hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(64), 0, s, w.initg, P, ctl->tau, w.st, w.udr,
+                           const_cast<int64_t *>(hdone));
+        PSK_HIP(hipGetLastError());
+    }
 
+    // polling: every C iterations an event; the host waits on the event L chunks back and then reads the
+    // host-mapped done word the kernels set (set_done)
+    const int L = 2, NS = kPollSlots;
+    static_assert(kPollSlots >= L + 2, "poll slots");
     int C = ctl->check_every > 0 ? ctl->check_every : (n >= (1 << 20) ? 2 : 16);
-    hipEvent_t fev[NS];
-    for (int i = 0; i < NS; ++i) PSK_HIP(hipEventCreateWithFlags(&fev[i], hipEventDisableTiming));
+    hipEvent_t *fev = kit->fev;
     // optional SpMV timing ring
-    const int TP = 64;
-    hipEvent_t ta[TP], tb[TP];
-    int64_t tk[TP];
+    const int TP = kTimedSlots;
+    hipEvent_t *ta = kit->ta, *tb = kit->tb;
+    int64_t tk[kTimedSlots];
+    for (int i = 0; i < TP; ++i) tk[i] = -1;
     std::vector<float> spmv_ms;
-    if (ctl->time_kernels) {
-        for (int i = 0; i < TP; ++i) {
-            PSK_HIP(hipEventCreate(&ta[i]));
-            PSK_HIP(hipEventCreate(&tb[i]));
-            tk[i] = -1;
-        }
-        spmv_ms.assign((size_t)maxiter, 0.0f);
-    }
+    if (ctl->time_kernels) spmv_ms.assign((size_t)maxiter, 0.0f);
     auto harvest = [&](int slot) -> int {
         if (tk[slot] < 0) return PSK_OK;
         float ms = 0.f;
@@ -524,25 +580,19 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // or the last nv - ov_hi K3 tiles (row-block shards of a banded matrix: one grid line each side),
     // those tiles run first and the exchange of p overlaps the remaining tiles of K3
     int64_t ov_lo = 0, ov_hi = nv;
-    // Default since round 3 (PSK_HALO_OVERLAP=0 turns it off). In round 2 the N = 2 rehearsal of bench.py
-    // with both ranks on one GPU stopped with an expired grid-reduction wait with the overlap on: the
-    // round-2 gridsum waited for lower workgroup ids, i.e. assumed a dispatch order, which a second
-    // process's / stream's kernels occupying an XCD can break. The ticket gridsum (psk_internal.hpp)
-    // waits only for work that has started, and the same rehearsal runs with the overlap
-    // (profiles/r3_multirank_rehearsal.txt).
+    // On by default (PSK_HALO_OVERLAP=0 turns it off); DESIGN.md §6 states the rule: the overlap moves
+    // no arithmetic (sharded histories are bit-identical either way) and takes the halo's latency off
+    // the critical path whenever K3's interior tiles outlast the exchange, which they do at every
+    // size the 8-GPU run uses (>= 1.25M rows per rank); an 8-GPU A/B of the driver's run decides it.
     static const bool overlap_on = [] {
         const char *e = std::getenv("PSK_HALO_OVERLAP");
         return !(e && std::atoi(e) == 0);
     }();
     const bool overlap = overlap_on && sharded && !gen && halo_split(A, kVecTile, nv, ov_lo, ov_hi);
     hipStream_t cs = nullptr;
-    hipEvent_t ev_k3a = nullptr, ev_halo = nullptr;
+    hipEvent_t ev_k3a = kit->ev_a, ev_halo = kit->ev_b;
     bool halo_pending = false;
-    if (overlap) {
-        PSK_TRY(comm_stream(c, &cs));
-        PSK_HIP(hipEventCreateWithFlags(&ev_k3a, hipEventDisableTiming));
-        PSK_HIP(hipEventCreateWithFlags(&ev_halo, hipEventDisableTiming));
-    }
+    if (overlap) PSK_TRY(comm_stream(c, &cs));
 
     int64_t launched = 0;
     int rc = PSK_OK;
@@ -550,18 +600,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if (k > 0 && k % C == 0) {
             const int64_t chunk = k / C;   // chunks fully launched
             const int slot = (int)((chunk - 1) % NS);
-            if (flag_copy)
-                rc = hipMemcpyAsync(&hflag[slot], &w.st->done, 4, hipMemcpyDeviceToHost, s) == hipSuccess
-                         ? PSK_OK : fail(PSK_ERR_HIP, "flag copy");
-            if (rc == PSK_OK && hipEventRecord(fev[slot], s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
+            if (hipEventRecord(fev[slot], s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
             if (rc == PSK_OK && chunk - 1 - L >= 0) {
                 const int os = (int)((chunk - 1 - L) % NS);
                 if (hipEventSynchronize(fev[os]) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
-                else if (flag_copy ? hflag[os] != 0 : (*hdone != 0 && *hdone <= (chunk - L) * (int64_t)C + 1)) break;
+                else if (*hdone != 0 && *hdone <= (chunk - L) * (int64_t)C + 1) break;
             }
             if (rc != PSK_OK) break;
         }
-        // p_k and the buffer K3 writes p_{k+1} into (Jacobi/identity: alternating; general: in place)
+        // p_k and the buffer K3 writes p_{k+1} into (Jacobi/identity: a ring of kPcgDefer; general: in place)
         double *pk = gen ? w.p : w.pr.b[k % kPcgDefer];
         double *pn = gen ? w.p : w.pr.b[(k + 1) % kPcgDefer];
         if (halo_pending) {   // exchanged during the previous K3
@@ -583,7 +630,6 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
                               timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr)) != PSK_OK)
             break;
         if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
-        const dim3 gk((unsigned)nv);
         if (jac == 2)
             hipLaunchKernelGGL(pcg_update_kernel<2>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
                                gs2, w.st, w.udr, k);
@@ -633,18 +679,22 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     }
     // a halo exchange still in flight (the host stopped enqueueing first) completes before the end
     if (halo_pending && hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess && rc == PSK_OK) rc = fail(PSK_ERR_HIP, "halo wait");
-    if (rc == PSK_OK && hipEventRecord(ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
-    PcgState hs{};
-    if (rc == PSK_OK && hipMemcpyAsync(&hs, w.st, sizeof(hs), hipMemcpyDeviceToHost, s) != hipSuccess)
+    if (rc == PSK_OK && hipEventRecord(kit->ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
+    // one synchronisation for the state and the gridsum error word (pinned staging)
+    PcgState *hsp = static_cast<PcgState *>(kit->hstage);
+    int32_t *herr = reinterpret_cast<int32_t *>(static_cast<char *>(kit->hstage) + 512);
+    if (rc == PSK_OK && hipMemcpyAsync(hsp, w.st, sizeof(PcgState), hipMemcpyDeviceToHost, s) != hipSuccess)
         rc = fail(PSK_ERR_HIP, "state copy");
+    if (rc == PSK_OK) rc = gridsum_check_enqueue(c, herr);
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg sync");
+    const PcgState hs = *hsp;
+    if (rc == PSK_OK) rc = gridsum_check_result(c, *herr);
     if (rc == PSK_OK && gen) rc = prec_check_error(M, s);
-    if (rc == PSK_OK) rc = gridsum_check(c);
     if (rc == PSK_OK && ctl->time_kernels)
         for (int i = 0; i < TP && rc == PSK_OK; ++i) rc = harvest(i);
     if (rc == PSK_OK) {
         float ms = 0.f;
-        (void)hipEventElapsedTime(&ms, ev0, ev1);
+        (void)hipEventElapsedTime(&ms, kit->ev0, kit->ev1);
         res->loop_ms = ms;
         res->norm_b = hs.normB;
         // nk: iterations whose SpMV ran (the timing count); nhist: iterations that reported a
@@ -677,23 +727,27 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             set_msg(res, "failure to converge");
             nk = nhist = launched;
         }
-        // residual history, the recursive residual and the solution
+        // residual history (only when asked for), the recursive residual and the solution
         const int64_t nh = nhist < maxiter ? nhist : maxiter;
-        std::vector<double> hh((size_t)nh);
-        if (nh > 0 && hipMemcpy(hh.data(), w.hist, (size_t)nh * 8, hipMemcpyDeviceToHost) != hipSuccess)
+        if (hist && nh > 0 && hipMemcpy(hist, w.hist, (size_t)nh * 8, hipMemcpyDeviceToHost) != hipSuccess)
             rc = fail(PSK_ERR_HIP, "hist copy");
         if (rc == PSK_OK) {
-            if (hist) for (int64_t i = 0; i < nh; ++i) hist[i] = hh[(size_t)i];
             res->hist_len = nh;
-            res->resid_recursive = nh > 0 ? hh[(size_t)nh - 1] : hs.normB;
+            res->resid_recursive = nh > 0 ? hs.last_hist : hs.normB;
             if (res->status == PSK_MAXITER) res->resid = maxiter > 0 ? res->resid_recursive : hs.normB;
+            bool x_written = hs.x_written != 0;
             // a dot(p,Ap) breakdown at k: the iterations since the last flush deferred their x updates
             if (!gen && hs.done == 2 && hs.brk_kind != 1 && pcg_pending(hs.iters) > 0 && n > 0) {
                 hipLaunchKernelGGL(pcg_flush_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,
                                    w.x, w.pr, w.alphas, (int64_t)hs.iters);
                 if (hipGetLastError() != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg flush");
+                x_written = true;
             }
-            if (rc == PSK_OK) rc = from_device_vec(w.x, loc, n, xout, s);
+            // no iteration stored x (b = 0, dot(u,r) = 0 at the start, maxiter = 0, or a dot(p,Ap)
+            // breakdown at k = 0): the solution is x0 = 0
+            if (rc == PSK_OK && !x_written && n > 0 && hipMemsetAsync(w.x, 0, (size_t)n * 8, s) != hipSuccess)
+                rc = fail(PSK_ERR_HIP, "x zero");
+            if (rc == PSK_OK && !dev_io) rc = from_device_vec(w.x, loc, n, xout, s);
             if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x copy");
         }
         if (ctl->time_kernels) {
@@ -705,16 +759,5 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             res->spmv_ms = nt > 0 ? tot / (double)nt : 0.0;
         }
     }
-    if (ctl->time_kernels)
-        for (int i = 0; i < TP; ++i) {
-            (void)hipEventDestroy(ta[i]);
-            (void)hipEventDestroy(tb[i]);
-        }
-    for (int i = 0; i < NS; ++i) (void)hipEventDestroy(fev[i]);
-    (void)hipHostFree(hflag);
-    (void)hipEventDestroy(ev0);
-    (void)hipEventDestroy(ev1);
-    if (ev_k3a) (void)hipEventDestroy(ev_k3a);
-    if (ev_halo) (void)hipEventDestroy(ev_halo);
     return rc;
 }

@@ -18,6 +18,33 @@ int fail(int code, const std::string &msg) {
 
 static std::mutex g_ctx_mu;
 static Context g_ctx[64];
+static bool g_shut = false;
+
+bool lib_shut_down() { return g_shut; }
+
+int solve_kit(Context *c, bool timed, SolveKit **out) {
+    SolveKit &k = c->kit;
+    if (!k.ready) {
+        PSK_HIP(hipHostMalloc(&k.hmap, 64 * sizeof(int64_t), hipHostMallocCoherent));
+        std::memset(k.hmap, 0, 64 * sizeof(int64_t));
+        PSK_HIP(hipHostMalloc(&k.hstage, kStageBytes, hipHostMallocDefault));
+        PSK_HIP(hipEventCreate(&k.ev0));
+        PSK_HIP(hipEventCreate(&k.ev1));
+        for (auto &e : k.fev) PSK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        PSK_HIP(hipEventCreateWithFlags(&k.ev_a, hipEventDisableTiming));
+        PSK_HIP(hipEventCreateWithFlags(&k.ev_b, hipEventDisableTiming));
+        k.ready = true;
+    }
+    if (timed && !k.timed_ready) {
+        for (int i = 0; i < kTimedSlots; ++i) {
+            PSK_HIP(hipEventCreate(&k.ta[i]));
+            PSK_HIP(hipEventCreate(&k.tb[i]));
+        }
+        k.timed_ready = true;
+    }
+    *out = &k;
+    return PSK_OK;
+}
 
 int comm_stream(Context *c, hipStream_t *out) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
@@ -27,6 +54,7 @@ int comm_stream(Context *c, hipStream_t *out) {
 }
 
 int ctx(Context **out) {
+    if (g_shut) return fail(PSK_ERR_ARG, "libpsk was shut down (psk_shutdown)");
     int dev = 0;
     PSK_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(PSK_ERR_ARG, "device index out of range");
@@ -122,14 +150,49 @@ int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs) {
     return PSK_OK;
 }
 
-int gridsum_check(Context *c) {
-    if (!c->gs_err) return PSK_OK;
-    int32_t h = 0;
-    PSK_HIP(hipMemcpyAsync(&h, c->gs_err, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    PSK_HIP(hipStreamSynchronize(c->stream));
+// Every ticket counter must be back at zero between launches: a launch that left one non-zero (a
+// grid that differs from gs.nt, a tile that drew but never published, an aborted launch) would make
+// every later reduction of that group skip its reducer silently. One workgroup scans the
+// kGridSumMaxGroups + 1 counters and flags a non-zero one in gs_err (bit 4); cheap enough to run at
+// the end of every solve.
+__global__ __launch_bounds__(kBlock) void gridsum_counter_check_kernel(const uint32_t *cnt, int32_t *err) {
+    uint32_t any = 0;
+    for (int g = threadIdx.x; g <= kGridSumMaxGroups; g += kBlock) any |= cnt[(int64_t)g * kGridSumCntStride];
+    if (__syncthreads_or(any != 0) && threadIdx.x == 0) atomicOr(err, 4);
+}
+
+int gridsum_check_enqueue(Context *c, int32_t *host_word) {
+    if (!c->gs_err) {
+        *host_word = 0;
+        return PSK_OK;
+    }
+    hipLaunchKernelGGL(gridsum_counter_check_kernel, dim3(1), dim3(kBlock), 0, c->stream, c->gs_cnt, c->gs_err);
+    PSK_HIP(hipGetLastError());
+    PSK_HIP(hipMemcpyAsync(host_word, c->gs_err, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
+    return PSK_OK;
+}
+
+int gridsum_check_result(Context *c, int32_t h) {
     if (h == 0) return PSK_OK;
     PSK_HIP(hipMemsetAsync(c->gs_err, 0, sizeof(int32_t), c->stream));
+    if (h & 4) {   // re-arm the counters so that later solves reduce again
+        const size_t cb = (size_t)(kGridSumMaxGroups + 1) * kGridSumCntStride * sizeof(uint32_t);
+        PSK_HIP(hipMemsetAsync(c->gs_cnt, 0, cb, c->stream));
+    }
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    if (h & 2) return fail(PSK_ERR_HIP, "grid reduction: a launch's grid differs from the tiles it was prepared for");
+    if (h & 4) return fail(PSK_ERR_HIP, "grid reduction: a ticket counter was left non-zero by a launch");
     return fail(PSK_ERR_HIP, "grid reduction: an issued partial-sum store never landed (1.3 s wait expired)");
+}
+
+int gridsum_check(Context *c) {
+    if (!c->gs_err) return PSK_OK;
+    SolveKit *k;
+    PSK_TRY(solve_kit(c, false, &k));
+    int32_t *h = reinterpret_cast<int32_t *>(static_cast<char *>(k->hstage) + kStageBytes - 64);
+    PSK_TRY(gridsum_check_enqueue(c, h));
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    return gridsum_check_result(c, *h);
 }
 
 int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s) {
@@ -187,8 +250,63 @@ int psk_dmalloc(int64_t bytes, void **dptr) {
 }
 
 int psk_dfree(void *dptr) {
+    if (g_shut) return PSK_OK;   // process exit: the runtime reclaims it
     if (dptr) PSK_HIP(hipFree(dptr));
     return PSK_OK;
+}
+
+// Drains every device's stream and releases what the library holds for the process lifetime (the
+// SolveKit's host-mapped words, pinned staging and events, the gridsum arrays, the streams), while the
+// HIP runtime is still fully alive. Python registers it with atexit (pysolvers_amd/_native.py) so that
+// nothing of libpsk is left for the runtime's own static destructors at exit(); afterwards every
+// entry point that needs a device fails with PSK_ERR_ARG and the destroy entry points are no-ops
+// (objects still alive then are reclaimed with the process).
+int psk_shutdown(void) {
+    std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if (g_shut) return PSK_OK;
+    int rc = PSK_OK;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int d = 0; d < 64; ++d) {
+        Context &c = g_ctx[d];
+        if (c.stream == nullptr) continue;
+        if (hipSetDevice(d) != hipSuccess) continue;
+        if (hipStreamSynchronize(c.stream) != hipSuccess && rc == PSK_OK) rc = fail(PSK_ERR_HIP, "psk_shutdown: sync");
+        if (c.comm_stream) (void)hipStreamSynchronize(c.comm_stream);
+        SolveKit &k = c.kit;
+        if (k.ready) {
+            (void)hipEventDestroy(k.ev0);
+            (void)hipEventDestroy(k.ev1);
+            for (auto e : k.fev) (void)hipEventDestroy(e);
+            (void)hipEventDestroy(k.ev_a);
+            (void)hipEventDestroy(k.ev_b);
+            (void)hipHostFree(k.hmap);
+            (void)hipHostFree(k.hstage);
+        }
+        if (k.timed_ready)
+            for (int i = 0; i < kTimedSlots; ++i) {
+                (void)hipEventDestroy(k.ta[i]);
+                (void)hipEventDestroy(k.tb[i]);
+            }
+        k = SolveKit{};
+        for (uint64_t *p : c.gs_retired) (void)hipFree(p);
+        c.gs_retired.clear();
+        void *bufs[] = {c.gs_slots, c.gs_gslots, c.gs_cnt, c.gs_err};
+        for (void *p : bufs)
+            if (p) (void)hipFree(p);
+        c.gs_slots = nullptr;
+        c.gs_gslots = nullptr;
+        c.gs_cnt = nullptr;
+        c.gs_err = nullptr;
+        c.gs_cap = 0;
+        if (c.comm_stream) (void)hipStreamDestroy(c.comm_stream);
+        (void)hipStreamDestroy(c.stream);
+        c.comm_stream = nullptr;
+        c.stream = nullptr;
+    }
+    (void)hipSetDevice(cur);
+    g_shut = true;
+    return rc;
 }
 
 int psk_h2d(void *dst, const void *src, int64_t bytes) {

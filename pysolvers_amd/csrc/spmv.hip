@@ -254,7 +254,11 @@ __device__ __forceinline__ double spmv_finish_row(bool has, int64_t row, double 
         } else if (MODE == kSpmvAdd) {
             y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
         } else {
+#ifdef PSK_LAB_Y_DEFAULT
+            y[row] = sum;   // lab: default policy (Ap read by the next kernel)
+#else
             __builtin_nontemporal_store(sum, y + row);
+#endif
             if (MODE != kSpmvPlain) acc = eq * sum;   // x.(Ax) or q.(Ax)
         }
     }
@@ -363,6 +367,181 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
     if (MODE == kSpmvDot) eq = diag_x<UW>(cc, xv, row32, x, has);
     const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
     if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
+}
+
+// The dot epilogue of a workgroup holding TPW gridsum tiles: first every tile's slot is combined in LDS
+// and stored (no wait of any kind), only then does a wave that published a tile holding its group's
+// last ticket reduce that group. Storing every slot before any reduction keeps the protocol's
+// guarantee: a reducer only waits on tiles that drew their tickets earlier, and those store all their
+// slots without waiting — a wave reducing tile 0's group while tile 1's slot were still unstored could
+// otherwise close a cycle of reducers across workgroups.
+template <int TPW>
+__device__ __forceinline__ void spmv_publish_multi(const GridSum &gs, GridSumTile<1> *L, const double *acc,
+                                                   const uint32_t *ticket, const int64_t *tl, const bool *tv) {
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    bool mine[TPW];
+    uint32_t tk[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        mine[q] = false;
+        tk[q] = 0;
+        if (!tv[q]) continue;   // uniform: the last workgroup's missing slice
+        const double ws = wave_total(acc[q]);
+        uint32_t old = 0;
+        if (lane0) {
+            L[q].part[wave] = ws;
+            if (threadIdx.x == 0) L[q].ticket = ticket[q];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            old = atomicAdd(&L[q].cnt, 1u);
+        }
+        if (__builtin_amdgcn_readfirstlane(old) != kWaves - 1) continue;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        double sum = L[q].part[0];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) sum += L[q].part[w];   // wave order
+        tk[q] = L[q].ticket;
+        if (lane0)
+            gridsum_put(gs.grp_log2 < 0 ? gs.gslots + tl[q] : gs.slots + gridsum_slot(gs, tl[q]), sum);
+        mine[q] = true;
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        if (!mine[q]) continue;
+        if (gs.grp_log2 < 0) {
+            gridsum_final_wave<1>(gs);
+            continue;
+        }
+        const int64_t g = gridsum_group_of(tl[q], gs.grp_log2);
+        int64_t base;
+        const int64_t cnt = gridsum_members(gs, g, base);
+        if (tk[q] != (uint32_t)(cnt - 1)) continue;
+        double r[1];
+        gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
+        if (lane0) {
+            gridsum_reset(gridsum_counter(gs, g));
+            gridsum_put(gs.gslots + g, r[0]);
+        }
+        gridsum_final_wave<1>(gs);
+    }
+}
+
+// The uniform kernel with TPW slices per workgroup, one row of each per lane (rows t*256 + lane of the
+// TPW consecutive slices t of the workgroup): every stream load of all TPW slices is issued first, then
+// every gather, so a wave keeps TPW times the bytes in flight of the one-slice kernel (the in-loop
+// SpMV at N = 10M moves ~24 KiB per CU at once with one slice, below what streaming needs). The grid
+// sums stay per 256-row slice (one gridsum tile each, its own ticket and LDS combine), so p.Ap has the
+// same bits as the one-slice kernel and the CSR layout.
+template <int MODE, int DK, int UW, bool CMP, int TPW>
+__global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
+    int64_t n, const int32_t *__restrict__ spcol, const double *__restrict__ sval, const double *__restrict__ sdict,
+    const double *__restrict__ x, double *__restrict__ y, const double *__restrict__ aux_d,
+    const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done, TileMap tm, int64_t ntiles) {
+    constexpr int NP = (UW + 1) / 2;
+    static_assert(!CMP || (DK == 2 && (UW & 1)), "compact stream: odd width, 2-entry dictionary");
+    constexpr int NI = DK > 0 && !CMP ? (UW + 3) / 4 : 0;
+    const int32_t dn = *(done ? done : &g_spmv_never_done);
+    const int tid = threadIdx.x;
+    const int64_t grp = tile_of_block(tm);
+    int64_t tl[TPW];     // slice of each part (clamped to a valid slice for the loads)
+    bool tv[TPW];        // the part is a real slice
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t t = grp * TPW + q;
+        tv[q] = t < ntiles;
+        tl[q] = tv[q] ? t : ntiles - 1;
+    }
+    uint32_t cw[TPW][NP], iw[TPW][NI > 0 ? NI : 1];
+    double vv[TPW][UW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int32_t *pword = spcol + tl[q] * (int64_t)((NP + NI) * kSlice) + tid;
+#pragma unroll
+        for (int p = 0; p < NP; ++p) cw[q][p] = (uint32_t)ld_stream(pword + p * kSlice);
+        if (DK > 0) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) iw[q][i] = (uint32_t)ld_stream(pword + (NP + i) * kSlice);
+            if (CMP) iw[q][0] = 0;
+        } else {
+            const double *v0 = sval + tl[q] * (int64_t)(UW * kSlice);
+#pragma unroll
+            for (int p = 0; p < UW / 2; ++p) {
+                const dv2 v2 = __builtin_nontemporal_load(reinterpret_cast<const dv2 *>(v0 + 2 * p * kSlice) + tid);
+                vv[q][2 * p] = v2.x;
+                vv[q][2 * p + 1] = v2.y;
+            }
+            if (UW & 1) vv[q][UW - 1] = ld_stream(v0 + (UW - 1) * kSlice + tid);
+        }
+    }
+    double eq[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        eq[q] = 0.0;
+        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+            eq[q] = aux_q[row < n ? row : 0];
+    }
+    const DictRegs dv = load_dict<DK>(sdict);
+    if (dn != 0) {
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+#pragma unroll
+            for (int p = 0; p < NP; ++p) __asm__ volatile("" ::"v"(cw[q][p]));
+            if (DK > 0) {
+#pragma unroll
+                for (int i = 0; i < NI; ++i) __asm__ volatile("" ::"v"(iw[q][i]));
+            } else {
+#pragma unroll
+                for (int j = 0; j < UW; ++j) __asm__ volatile("" ::"v"(vv[q][j]));
+            }
+        }
+        return;
+    }
+    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
+    __shared__ GridSumTile<1> gsl[TPW];
+    uint32_t ticket[TPW];
+    const bool pub = PUB && spmv_publishes<MODE>(gs);
+    if (pub) {
+        if (tid < TPW) gsl[tid].cnt = 0;
+        if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            ticket[q] = 0;
+            if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
+                ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+        }
+    }
+    int32_t cc[TPW][UW];
+    double xv[TPW][UW], acc[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int32_t row32 = (int32_t)(tl[q] * kSlice + tid);
+#pragma unroll
+        for (int j = 0; j < UW; ++j) {
+            cc[q][j] = unpack_delta(row32, (int16_t)((j & 1) ? (cw[q][j >> 1] >> 16) : (cw[q][j >> 1] & 0xffff)));
+            const int32_t cl = cc[q][j] >= 0 ? cc[q][j] : 0;
+            xv[q][j] = x[cl];
+            if (MODE == kSpmvJacobiDot) xv[q][j] = aux_d[cl] * xv[q][j];
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        const bool has = tv[q] && row < n;
+        if (DK > 0) {
+#pragma unroll
+            for (int j = 0; j < UW; ++j)
+                vv[q][j] = dict_pick<DK>(dv, CMP ? (cw[q][NP - 1] >> (16 + j)) & 1u : (iw[q][j >> 2] >> (8 * (j & 3))) & 0xff);
+        }
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < UW; ++j)
+            if (cc[q][j] >= 0) sum = sum + vv[q][j] * xv[q][j];   // stored order, rounded product
+        if (MODE == kSpmvDot) eq[q] = diag_x<UW>(cc[q], xv[q], (int32_t)row, x, has);
+        acc[q] = spmv_finish_row<MODE>(has, row, sum, eq[q], y);
+    }
+    if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
 }
 
 // General sliced layout (per-slice widths, offsets and formats loaded from the slice header).
@@ -786,6 +965,14 @@ static bool spmv_xcd_bands() {
     return on;
 }
 
+static int spmv_tpw() {
+    static const int v = [] {
+        const char *e = std::getenv("PSK_SPMV_TPW");
+        return e && std::atoi(e) == 2 ? 2 : 1;
+    }();
+    return v;
+}
+
 static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) / A->tile_rows; }
 
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
@@ -803,6 +990,11 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     // 0.057 ms); the CSR tile kernel measured 2-3% slower with them (3163^2 and 16384^2), so it keeps
     // block order
     const TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands());
+    // compact uniform layout: slices per workgroup (PSK_SPMV_TPW=2: spmv_uniform_multi_kernel)
+    const int tpw = spmv_tpw();
+    const int64_t nwg2 = (nwg + 1) / 2;
+    const dim3 gd2((unsigned)(nwg2 > 0 ? nwg2 : 1));
+    const TileMap tm2 = tile_map_for(nwg2, sliced && spmv_xcd_bands());
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
@@ -828,8 +1020,14 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         }                                                                                                      \
     } while (0)
 #define PSK_UNI_LAUNCH_C(M, UW)                                                                                \
-    hipExtLaunchKernelGGL((spmv_uniform_kernel<M, 2, UW, true>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol, A->sl_val, \
-                          A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm)
+    do {                                                                                                       \
+        if (tpw == 2)                                                                                          \
+            hipExtLaunchKernelGGL((spmv_uniform_multi_kernel<M, 2, UW, true, 2>), gd2, bd, 0, s, ev0, ev1, 0, A->n,   \
+                                  A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm2, nwg);  \
+        else                                                                                                   \
+            hipExtLaunchKernelGGL((spmv_uniform_kernel<M, 2, UW, true>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol,  \
+                                  A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm);                 \
+    } while (0)
 #define PSK_SLICED_LAUNCH(M)                                                                                   \
     do {                                                                                                       \
         if (A->sl_compact) {   /* uniform, odd width, 2-entry dictionary */                                    \
@@ -1175,7 +1373,7 @@ int psk_csr_download(const psk_csr *A, int32_t *rowptr, int32_t *colidx, double 
 }
 
 int psk_csr_destroy(psk_csr *A) {
-    if (!A) return PSK_OK;
+    if (!A || lib_shut_down()) return PSK_OK;   // after psk_shutdown: reclaimed with the process
     csr_free(A);
     delete A;
     return PSK_OK;
@@ -1389,7 +1587,7 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
 }
 
 int psk_prec_destroy(psk_prec *M) {
-    if (!M) return PSK_OK;
+    if (!M || lib_shut_down()) return PSK_OK;   // after psk_shutdown: reclaimed with the process
     void *ptrs[] = {M->dinv, M->gather_in, M->gather_out, M->work, M->err};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);

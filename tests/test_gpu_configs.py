@@ -3,8 +3,9 @@
 configs[2]: GMRES(30) + RightILUT on FDLaplacian2D. The reference's own ILUT (spilu drop_tol=1e-3,
 fill_factor=15; ILUTPreconditioner.py:51-53) cannot be formed at 4096^2 by scipy's SuperLU
 (SUPERLU_MALLOC fails, in the reference too), so the largest formable side, 2896, is the test size:
-the first 30 Arnoldi steps (one full restart cycle) on the device vs the oracle GMRES(m) driven by
-the SAME SuperLU factors (ILU.solve on the host, ILUTPreconditioner.py:77-78).
+the first 60 Arnoldi steps (two GMRES(30) cycles, so the restart r = b - A x and a second cycle
+from it are crossed at size) on the device vs the oracle GMRES(m) driven by the SAME SuperLU factors
+(ILU.solve on the host, ILUTPreconditioner.py:77-78).
 
 configs[4]: PCG + AMG(numIters=2, 5 levels) on -FDLaplacian2D 8192^2 (FDBratu2D.py:15 sign): the
 hierarchy's level sizes, every device operator against the host scipy operators bit for bit, each
@@ -42,15 +43,16 @@ def _bitwise(A, B):
 
 
 def test_configs2_gmres30_ilut_fd2896(psk):
-    """configs[2] at FD 2896^2 (8.4M rows, L+U ~ 3.7e8 entries): 30 GMRES(30)+ILUT steps, residual
-    history within 1e-10 ||b|| of the oracle's and the iterate within 1e-10 relative."""
+    """configs[2] at FD 2896^2 (8.4M rows, L+U ~ 3.7e8 entries): 60 GMRES(30)+ILUT steps = two restart
+    cycles (GMRESSolver.py:87-160 per cycle), residual history within 1e-10 ||b|| of the oracle's and
+    the iterate within 1e-10 relative."""
     from oracle import fdlap, krylov
     m = 2896
     A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
     b = A @ np.random.default_rng(12345).random(m * m)
     M = psk.RightILUT().form(A)                  # spilu on the host, factors uploaded once
     ilu = M.ILU()
-    steps = 30
+    steps = 60
     ctl = _ctl(maxiter=steps, tau=0.0, failOnMaxiter=False)
     s = psk.GMRES(control=ctl, precond=psk.RightILUT(), restart=30).makeSolver()
     s.precond = M                                # the same factors, as a frozen preconditioner

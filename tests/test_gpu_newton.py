@@ -61,6 +61,14 @@ def test_default_direct_matches_reference():
         assert bool(st.success()) == case["success"] and st.msg() == case["msg"]
         assert bool(np.all(np.isnan(st.soln()))) == case["soln_all_nan"]
         assert sorted({type(i.message).__name__ for i in w}) == case["warnings"] == [MatrixRankWarning.__name__]
+    for case in direct_manifest()["singular_dense"]:   # the reference's npla.solve: LinAlgError -> failure
+        st = psk.DefaultDirect().makeSolver().solve(np.array(case["dense"]), np.array(case["b"]))
+        assert bool(st.success()) == case["success"] is False and st.msg() == case["msg"]
+        assert (st.soln() is None) == case["soln_is_none"]
+    for case in direct_manifest()["dense"]:
+        st = psk.DefaultDirect().makeSolver().solve(np.array(case["dense"]), np.array(case["b"]))
+        assert st.success() == case["success"] and st.msg() == case["msg"]
+        assert np.linalg.norm(st.soln() - np.array(case["soln"])) <= 1e-14 * np.linalg.norm(case["soln"])
 
 
 def test_default_direct_refactors_a_matrix_updated_in_place():
