@@ -1114,10 +1114,16 @@ struct GridRec {
 #ifndef PSK_GRID_MARKSTEIN
 #define PSK_GRID_MARKSTEIN 1
 #endif
+// Exactness needs 1/d, r/d and the remainder normal: the host keeps the dictionary only for
+// diagonals 2^-100 <= |d| <= 2^100, and a right-hand side outside [2^-900, 2^900] (or not finite)
+// takes the IEEE division (a lane-divergent branch that no stencil solve takes;
+// tools/markstein_check.c covers both ends of the range and the zero/subnormal edges).
 __device__ __forceinline__ double div_markstein(double r, double d, double rd) {
     const double q0 = r * rd;
     const double q1 = fma(fma(-q0, d, r), rd, q0);
     const double q2 = fma(fma(-q1, d, r), rd, q1);
+    const double ar = fabs(r);
+    if (!(ar >= 0x1p-900 && ar <= 0x1p+900) && r != 0.0) return r / d;
     return r == 0.0 ? q0 : q2;
 }
 // Buffer (bounds-checked) access for the solver wave's rhs loads and x stores: an out-of-range
@@ -2188,6 +2194,19 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         const char *gde = std::getenv("PSK_TRISOLVE_GRID_DICT");
         if (!(gde && std::atoi(gde) == 0))
             build_grid_dict(gb, nsteps, SB, gp.K, oc, od, gidx, gdict, T.grid_dict_n);
+        // the dictionary kernel divides by Markstein correction from RN(1/d) (div_markstein), which
+        // equals IEEE r / d only while 1/d, the quotient and the remainder stay normal: keep the
+        // dictionary only for diagonals with 2^-100 <= |d| <= 2^100 (the kernel itself falls back to
+        // r / d for right-hand sides outside [2^-900, 2^900]); otherwise the per-step records
+        for (int i = 0; i < T.grid_dict_n; ++i) {
+            const double d = std::fabs(gdict[(size_t)T.grid_dict_n * gp.K + (size_t)i]);
+            if (!(d >= 0x1p-100 && d <= 0x1p+100)) {
+                T.grid_dict_n = 0;
+                std::vector<double>().swap(gdict);
+                std::vector<uint32_t>().swap(gidx);
+                break;
+            }
+        }
         if (T.grid_dict_n > 0) std::vector<double>().swap(gcoef);   // the records are not uploaded
     }
     // partitioned schedule: planned for factors too large for one CU and not solved by the grid

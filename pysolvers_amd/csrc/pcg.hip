@@ -151,7 +151,7 @@ template <int JAC>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv, double ds,
     const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st, const double *__restrict__ udr,
-    int64_t k) {
+    int64_t k, TileMap tm) {
     if (st->done) return;
     __shared__ double sh[kWaves];
     const double pTAp = rank_sum(pap, nparts, 1, 0);         // np.dot(p, Ap)  :113 (K1's grid sum)
@@ -167,7 +167,10 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     // K3 (x update) runs iff this K2 did: it tests `live`, written by the previous kernel, never its
     // own done flag, which its first workgroup may set while later ones are still starting
     if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
-    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    // tile of this workgroup: XCD-banded like the SpMV's (tm), so the Ap rows a tile reads were
+    // written through the same XCD's L2; the grid sums are published by tile (order-independent)
+    const int64_t tile = tile_of_block(tm);
+    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
     // cache policy: Ap is dead after this kernel (non-temporal); r and dinv are re-read by K3
@@ -175,7 +178,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2(dinv + i);
-        ticket = gridsum_ticket(gs);
+        ticket = gridsum_ticket(gs, tile);
         dv2 rn;
         rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
         rn.y = ro.y - alpha * a.y;
@@ -190,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
-        ticket = gridsum_ticket(gs);
+        ticket = gridsum_ticket(gs, tile);
         const double rn = r[i] - alpha * Ap[i];
         const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
@@ -198,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = u0 * rn;
     }
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
-    gridsum_publish<2>(gs, v, sh, ticket);
+    gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
 }
 
 // Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
@@ -271,11 +274,12 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ r, PRing pr, const double *__restrict__ dinv,
     double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts, PcgState *st,
     double *__restrict__ udr, double *__restrict__ hist, double *__restrict__ alphas, int64_t k, int64_t maxiter,
-    int fail_on_maxiter, int64_t tile_base) {
+    int fail_on_maxiter, int64_t tile_base, TileMap tm) {
     if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
-    // halo exchange then overlaps the rest); tile 0 alone writes the solver state
-    const int64_t tile = tile_base + blockIdx.x;
+    // halo exchange then overlaps the rest); tile 0 alone writes the solver state. tm: XCD bands
+    // over the launch's tiles (see K2)
+    const int64_t tile = tile_base + tile_of_block(tm);
     const double *pcur = pr.b[k % kPcgDefer];
     // NOT __restrict__: on a flush iteration pnext is p_{k+1-kPcgDefer}'s buffer, which the x catch-up
     // below reads through pr.b first; the store to pnext must stay after those loads
@@ -589,6 +593,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         return !(e && std::atoi(e) == 0);
     }();
     const bool overlap = overlap_on && sharded && !gen && halo_split(A, kVecTile, nv, ov_lo, ov_hi);
+    // K2/K3 tile order (round 4): PSK_K23_BANDS=0 block order; 1 XCD bands walked forward like the
+    // SpMV's (a tile of K2/K3 = the 512 rows of one two-slice SpMV workgroup, on the same XCD);
+    // 2 the same bands, the walking direction alternating from kernel to kernel (SpMV, K2, K3 of
+    // iteration k: rev = k&1, !(k&1), k&1), so each kernel first reads what its predecessor wrote last
+    static const int k23_bands = [] {
+        const char *e = std::getenv("PSK_K23_BANDS");
+        return e ? std::atoi(e) : 0;
+    }();
     hipStream_t cs = nullptr;
     hipEvent_t ev_k3a = kit->ev_a, ev_halo = kit->ev_b;
     bool halo_pending = false;
@@ -626,19 +638,21 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
         }
         // a timed launch records its events in its own dispatch (kernel start / end)
+        const bool odd = (k & 1) != 0 && k23_bands == 2;
         if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s,
-                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr)) != PSK_OK)
+                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr, odd ? 1 : 0)) != PSK_OK)
             break;
+        const TileMap tm2 = tile_map_for(nv, k23_bands != 0, k23_bands == 2 && !odd);
         if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
         if (jac == 2)
             hipLaunchKernelGGL(pcg_update_kernel<2>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2, w.st, w.udr, k);
+                               gs2, w.st, w.udr, k, tm2);
         else if (jac == 1)
             hipLaunchKernelGGL(pcg_update_kernel<1>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2, w.st, w.udr, k);
+                               gs2, w.st, w.udr, k, tm2);
         else
             hipLaunchKernelGGL(pcg_update_kernel<0>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2, w.st, w.udr, k);
+                               gs2, w.st, w.udr, k, tm2);
         if (sharded && (rc = allgather(A, w.part2, w.part2g, 2, s)) != PSK_OK) break;
         if (gen) {
             if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
@@ -649,18 +663,19 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             auto k3 = [&](int64_t t0, int64_t t1) {   // K3 over tiles [t0, t1)
                 if (t1 <= t0) return;
                 const dim3 g3((unsigned)(t1 - t0));
+                const TileMap tm3 = tile_map_for(t1 - t0, k23_bands != 0, odd);
                 if (jac == 2)
                     hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
-                                       ctl->fail_on_maxiter, t0);
+                                       ctl->fail_on_maxiter, t0, tm3);
                 else if (jac == 1)
                     hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
-                                       ctl->fail_on_maxiter, t0);
+                                       ctl->fail_on_maxiter, t0, tm3);
                 else
                     hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
-                                       ctl->fail_on_maxiter, t0);
+                                       ctl->fail_on_maxiter, t0, tm3);
             };
             if (overlap && k + 1 < maxiter) {
                 // the tiles holding the rows the neighbours need first, then their halo exchange on the

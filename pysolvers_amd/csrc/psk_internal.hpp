@@ -494,12 +494,15 @@ __device__ __forceinline__ int64_t gridsum_slot(const GridSum &gs, int64_t t) {
 // ---- workgroup slots (every thread of every workgroup calls these; barriers inside) ---------
 // The ticket (meaningful in thread 0 only; read at publish time). Call once the workgroup is known
 // to publish (after any launch-uniform early exit), best after its first stream loads are issued.
-__device__ __forceinline__ uint32_t gridsum_ticket(const GridSum &gs) {
+// `tile`: the gridsum tile this workgroup publishes (default: its block index); a launch that maps
+// blocks to tiles by any bijection (XCD bands) publishes by tile, so the sums do not depend on it.
+__device__ __forceinline__ uint32_t gridsum_ticket(const GridSum &gs, int64_t tile) {
     uint32_t t = 0;
     if (threadIdx.x == 0 && gridDim.x != gs.nt) atomicOr(gs.err, 2);   // prepared for another grid
-    if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(blockIdx.x, gs.grp_log2)));
+    if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tile, gs.grp_log2)));
     return t;
 }
+__device__ __forceinline__ uint32_t gridsum_ticket(const GridSum &gs) { return gridsum_ticket(gs, blockIdx.x); }
 
 // no-op finisher (below)
 struct GridSumNoFin {
@@ -531,9 +534,8 @@ __device__ __forceinline__ void gridsum_final(const GridSum &gs, double *sh, con
 // Called with the workgroup's W sums (identical in all threads, e.g. from block_sum) and the raw
 // ticket from gridsum_ticket. Kernel-uniform control flow. fin: see gridsum_final.
 template <int W, class F = GridSumNoFin>
-__device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double *v, double *sh, uint32_t ticket,
-                                                const F &fin = F()) {
-    const int64_t b = blockIdx.x;
+__device__ __forceinline__ void gridsum_publish_tile(const GridSum &gs, const double *v, double *sh, uint32_t ticket,
+                                                     int64_t b, const F &fin = F()) {
     if (gs.grp_log2 < 0) {
         if (threadIdx.x == 0)
 #pragma unroll
@@ -562,6 +564,11 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
         for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
     }
     gridsum_final<W>(gs, sh, fin);
+}
+template <int W, class F = GridSumNoFin>
+__device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double *v, double *sh, uint32_t ticket,
+                                                const F &fin = F()) {
+    gridsum_publish_tile<W>(gs, v, sh, ticket, blockIdx.x, fin);
 }
 
 // ---- per-wave partials combined in LDS (the SpMV's dot epilogue) ------------------------------
@@ -686,17 +693,19 @@ int gridsum_check_result(Context *c, int32_t host_word);
 // round-robin puts them on other XCDs and x is fetched ~3 times) are then read through the same L2.
 // TileMap{0, 0} is the identity. Bijective for any tile count.
 struct TileMap {
-    int64_t a;   // tiles / 8 (0 = identity)
-    int32_t r;   // tiles mod 8: classes k < r hold one more tile
+    int64_t a;     // tiles / 8 (0 = identity)
+    int32_t r;     // tiles mod 8: classes k < r hold one more tile
+    int32_t rev;   // 1: each XCD walks its band from the end (the lines its predecessor wrote last first)
 };
-inline TileMap tile_map_for(int64_t ntiles, bool banded) {
-    return banded && ntiles >= 64 ? TileMap{ntiles >> 3, (int32_t)(ntiles & 7)} : TileMap{0, 0};
+inline TileMap tile_map_for(int64_t ntiles, bool banded, bool rev = false) {
+    return banded && ntiles >= 64 ? TileMap{ntiles >> 3, (int32_t)(ntiles & 7), rev ? 1 : 0} : TileMap{0, 0, 0};
 }
 __device__ __forceinline__ int64_t tile_of_block(TileMap tm) {
     const int64_t b = blockIdx.x;
     if (tm.a == 0) return b;
     const int64_t k = b & 7, j = b >> 3;
-    return k * tm.a + (k < tm.r ? k : tm.r) + j;
+    const int64_t start = k * tm.a + (k < tm.r ? k : tm.r);
+    return tm.rev ? start + (tm.a + (k < tm.r ? 1 : 0)) - 1 - j : start + j;
 }
 
 // 16-byte vector accesses; *_nt = non-temporal (streamed data that is not re-read soon)
@@ -769,6 +778,6 @@ void sliced_free(psk_csr *A);
 // (hipExtLaunchKernel), so their interval is the kernel alone, without the launch gaps around it
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s,
-                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int rev = 0);
 
 }  // namespace psk

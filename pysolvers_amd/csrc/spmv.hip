@@ -968,7 +968,8 @@ static bool spmv_xcd_bands() {
 static int spmv_tpw() {
     static const int v = [] {
         const char *e = std::getenv("PSK_SPMV_TPW");
-        return e && std::atoi(e) == 2 ? 2 : 1;
+        const int t = e ? std::atoi(e) : 2;
+        return t >= 1 && t <= 4 ? t : 2;
     }();
     return v;
 }
@@ -977,7 +978,7 @@ static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) /
 
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s, hipEvent_t ev0,
-                hipEvent_t ev1) {
+                hipEvent_t ev1, int rev) {
     if (A->n == 0) return PSK_OK;
     Context *c;
     PSK_TRY(ctx(&c));
@@ -989,18 +990,28 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     // XCD bands for the sliced layouts (N = 10M in the loop 0.078 -> 0.072 ms, back to back 0.067 ->
     // 0.057 ms); the CSR tile kernel measured 2-3% slower with them (3163^2 and 16384^2), so it keeps
     // block order
-    const TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands());
-    // compact uniform layout: slices per workgroup (PSK_SPMV_TPW=2: spmv_uniform_multi_kernel)
+    // rev: each XCD walks its band backwards (the PCG loop alternates directions, PSK_K23_BANDS=2)
+    const TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands(), rev != 0);
+    // uniform layouts (compact, and double values): slices per workgroup, spmv_uniform_multi_kernel
+    // (round 4: 2 by default, PSK_SPMV_TPW=1 the one-slice kernel; 3 and 4 compact only, lab). Two
+    // slices per workgroup: in-loop SpMV at N = 10M 0.0657 -> 0.0611 ms, 16384^2 1.60 -> 1.49 ms, same
+    // bits (profiles/r4_spmv_tpw_ab.txt)
     const int tpw = spmv_tpw();
-    const int64_t nwg2 = (nwg + 1) / 2;
+    const int64_t nwg2 = (nwg + tpw - 1) / tpw;
     const dim3 gd2((unsigned)(nwg2 > 0 ? nwg2 : 1));
-    const TileMap tm2 = tile_map_for(nwg2, sliced && spmv_xcd_bands());
+    const TileMap tm2 = tile_map_for(nwg2, sliced && spmv_xcd_bands(), rev != 0);
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
 #define PSK_UNI_LAUNCH(M, DK, UW)                                                                              \
-    hipExtLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol, A->sl_val, A->sl_dict, \
-                       x, y, aux_d, aux_q, gs, done_flag, tm)
+    do {                                                                                                       \
+        if (DK == 0 && tpw == 2)                                                                               \
+            hipExtLaunchKernelGGL((spmv_uniform_multi_kernel<M, 0, UW, false, 2>), gd2, bd, 0, s, ev0, ev1, 0, A->n, \
+                                  A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm2, nwg);  \
+        else                                                                                                   \
+            hipExtLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol,     \
+                                  A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm);                 \
+    } while (0)
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
     do {                                                                                                       \
         switch (uw) {                                                                                          \
@@ -1023,6 +1034,12 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     do {                                                                                                       \
         if (tpw == 2)                                                                                          \
             hipExtLaunchKernelGGL((spmv_uniform_multi_kernel<M, 2, UW, true, 2>), gd2, bd, 0, s, ev0, ev1, 0, A->n,   \
+                                  A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm2, nwg);  \
+        else if (tpw == 3)                                                                                     \
+            hipExtLaunchKernelGGL((spmv_uniform_multi_kernel<M, 2, UW, true, 3>), gd2, bd, 0, s, ev0, ev1, 0, A->n,   \
+                                  A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm2, nwg);  \
+        else if (tpw == 4)                                                                                     \
+            hipExtLaunchKernelGGL((spmv_uniform_multi_kernel<M, 2, UW, true, 4>), gd2, bd, 0, s, ev0, ev1, 0, A->n,   \
                                   A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm2, nwg);  \
         else                                                                                                   \
             hipExtLaunchKernelGGL((spmv_uniform_kernel<M, 2, UW, true>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol,  \

@@ -1,36 +1,20 @@
 #!/bin/bash
-# One GPU-box session: smoke -> GPU parity tests -> bench -> rocprofv3 kernel stats.
-# Every GPU step has its own time limit; a crash/timeout stops the script (no retries).
+# Round-4 GPU check: the -m gpu suite, the driver-style bench (--steps 20 --warmup 5) and the
+# rocprofv3 trace of the configs[2]/[4] keys with the process maps dumped at exit (exit-fault hunt).
+# Each GPU step has its own time limit; a step that ends by signal/timeout stops the script.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out
-mkdir -p $OUT
-TAG=${TAG:-r1}
-
-stop_if_crashed() {  # $1 = exit code of the previous GPU step
-    case "$1" in
-        0|1) return 0 ;;             # ok / test failures: the GPU is fine
-        *) echo "GPU step exited $1: stopping"; exit "$1" ;;
-    esac
-}
-
-echo "== smoke"; timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1
-rc=$?; tail -3 $OUT/smoke_$TAG.log; stop_if_crashed $rc
-
-if [ "${SKIP_TESTS:-0}" != "1" ]; then
-  echo "== pytest -m gpu"; timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.log 2>&1
-  rc=$?; tail -15 $OUT/pytest_gpu_$TAG.log; stop_if_crashed $rc
-fi
-
-echo "== bench"; timeout -k 10 900 python bench.py ${BENCH_ARGS:-} > $OUT/bench_$TAG.json 2> $OUT/bench_$TAG.err
-rc=$?; cat $OUT/bench_$TAG.json; tail -5 $OUT/bench_$TAG.err; stop_if_crashed $rc
-
-if [ "${PROFILE:-1}" = "1" ]; then
-  echo "== rocprofv3 kernel trace"
-  export TMPDIR=/tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof_$TAG -o run --output-format csv -- \
-      python bench.py ${PROF_ARGS:---cpu-iters 0 --spmv10m 0 --config1 0} > $OUT/prof_bench_$TAG.json 2> $OUT/prof_$TAG.err
-  rc=$?; tail -3 $OUT/prof_$TAG.err; stop_if_crashed $rc
-  find $OUT/prof_$TAG -name '*kernel_stats.csv' -exec head -20 {} \;
-fi
-echo "== done"
+OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
+TAG=${1:-r4}
+ok() { local c=$1; [ $c -eq 0 ] || [ $c -eq 1 ]; }   # 0 pass, 1 test/bench failure; anything else: stop
+sha256sum pysolvers_amd/_lib/libpsk.so > $OUT/${TAG}_lib.sha256
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $OUT/${TAG}_pytest.log 2>&1
+c=$?; echo "pytest exit $c"; tail -3 $OUT/${TAG}_pytest.log; ok $c || exit $c
+timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err
+c=$?; echo "bench exit $c"; ok $c || exit $c
+PSK_DUMP_MAPS=$OUT/${TAG}_maps.txt timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/${TAG}_prof -o run --output-format csv -- \
+    python -u bench.py --steps 20 --warmup 2 --cpu-iters 0 --general 0 --config1 0 --gmres 0 --scaling-side 0 \
+    > $OUT/${TAG}_prof.json 2> $OUT/${TAG}_prof.err
+echo "profiled exit $?"
+python tools/trace_stats.py $(find $OUT/${TAG}_prof -name "*kernel_trace.csv" | head -1) > $OUT/${TAG}_trace_stats.csv
+rm -rf $OUT/${TAG}_prof
