@@ -22,6 +22,13 @@
 #include <cmath>
 #include <cstdio>
 
+#ifndef PSK_LAB_K2_DPP
+#define PSK_LAB_K2_DPP 0   // lab: K2's tile sums by DPP wave totals + LDS combine (gridsum_tile_*)
+#endif
+#ifndef PSK_LAB_WT
+#define PSK_LAB_WT 0   // lab: write-through stores, bit 0 K3's p, bit 1 K2's r, bit 2 K3's x flush
+#endif
+
 namespace psk {
 
 struct PcgState {
@@ -173,7 +180,47 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
-    // cache policy: Ap is dead after this kernel (non-temporal); r and dinv are re-read by K3
+#if PSK_LAB_K2_DPP
+    // DPP wave totals combined in LDS by the last wave (no workgroup barrier at the end), as the SpMV;
+    // the arming barrier of gridsum_tile_begin sits right after the loads are issued (uniform path)
+    (void)sh;
+    __shared__ GridSumTile<2> gsl;
+    const bool full = i + 1 < n;
+    dv2 ro{0.0, 0.0}, a{0.0, 0.0}, d{ds, ds};
+    if (full) {
+        ro = ld2(r + i);
+        a = ld2nt(Ap + i);
+        if (JAC == 1) d = ld2(dinv + i);
+    }
+    ticket = gridsum_tile_begin<2>(gs, gsl, tile);
+    if (full) {
+        dv2 rn;
+        rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
+        rn.y = ro.y - alpha * a.y;
+        double u0 = rn.x, u1 = rn.y;
+        if (JAC) {
+            u0 = d.x * rn.x;                                 // u = precond.applyRight(r)  :123
+            u1 = d.y * rn.y;
+        }
+#if (PSK_LAB_WT & 2)
+        st2wt(r, n, i, rn);
+#else
+        st2(r + i, rn);
+#endif
+        rr = fma(rn.x, rn.x, rr);
+        rr = fma(rn.y, rn.y, rr);
+        ur = fma(u0, rn.x, ur);
+        ur = fma(u1, rn.y, ur);
+    } else if (i < n) {   // odd tail element
+        const double rn = r[i] - alpha * Ap[i];
+        const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
+        r[i] = rn;
+        rr = rn * rn;
+        ur = u0 * rn;
+    }
+    const double v[2] = {wave_total(rr), wave_total(ur)};
+    gridsum_tile_publish<2>(gs, gsl, v, ticket, tile);
+#else
     if (i + 1 < n) {
         const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
@@ -187,7 +234,11 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
             u0 = d.x * rn.x;                                 // u = precond.applyRight(r)  :123
             u1 = d.y * rn.y;
         }
+#if (PSK_LAB_WT & 2)
+        st2wt(r, n, i, rn);   // lab: write-through
+#else
         st2(r + i, rn);
+#endif
         rr = fma(rn.x, rn.x, rr);
         rr = fma(rn.y, rn.y, rr);
         ur = fma(u0, rn.x, ur);
@@ -202,6 +253,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     }
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
+#endif
 }
 
 // Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
@@ -324,13 +376,19 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
             dv2 xn;
             xn.x = xo.x + alpha * po.x;                      // :121
             xn.y = xo.y + alpha * po.y;
+#if (PSK_LAB_WT & 4)
+            st2wt(x, n, i, xn);
+#else
             st2nt(x + i, xn);
+#endif
         }
         dv2 pn;
         pn.x = u0 + beta * po.x;                             // p = u + beta*p  :138
         pn.y = u1 + beta * po.y;
-#ifdef PSK_LAB_K3_PNT
+#if defined(PSK_LAB_K3_PNT)
         st2nt(pnext + i, pn);   // lab: p stored non-temporally (the K3 -> SpMV boundary's dirty bytes)
+#elif (PSK_LAB_WT & 1)
+        st2wt(pnext, n, i, pn);   // lab: write-through
 #else
         st2(pnext + i, pn);
 #endif

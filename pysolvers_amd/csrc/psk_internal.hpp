@@ -717,6 +717,20 @@ __device__ __forceinline__ dv2 ld2nt(const double *p) {
 __device__ __forceinline__ void st2(double *p, dv2 v) { *reinterpret_cast<dv2 *>(p) = v; }
 __device__ __forceinline__ void st2nt(double *p, dv2 v) { __builtin_nontemporal_store(v, reinterpret_cast<dv2 *>(p)); }
 
+// 16-byte write-through store (sc1: the line goes to memory and is dropped from the XCD's L2, so
+// a streaming kernel leaves no dirty lines for the kernel boundary to write back; MI355X_MICROARCH.md
+// "boundary": + dirty bytes / 6 TB/s). Buffer store at byte offset `off` of the uniform base `p` of n
+// doubles; falls back to a plain store for arrays of 4 GiB or more (32-bit offsets).
+typedef unsigned int psk_u4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st2wt(double *p, int64_t n, int64_t i, dv2 v) {
+    if (n >= ((int64_t)1 << 29)) {
+        st2(p + i, v);
+        return;
+    }
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(uint32_t)(n * 8), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(psk_u4, v), r, (int)(uint32_t)(i * 8), 0, 0x10);
+}
+
 // contiguous share [b0,b1) of `ntiles` tiles for workgroup `b` of `g`
 __device__ __forceinline__ void block_range(int64_t ntiles, int64_t &t0, int64_t &t1) {
     const int64_t g = gridDim.x, b = blockIdx.x;
