@@ -37,6 +37,9 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
     """Solver base (IterativeLinearSolver.py:60-86) + the device driver."""
 
     _entry = None          # "psk_pcg" / "psk_gmres"
+    # PCGSolver.solve prints 'prec frozen = ...' and 'building prec' on every solve with b != 0
+    # (PCGSolver.py:91,93); PCGSolver sets this (class attribute: a driver may switch it off)
+    _echo_setup = False
 
     def __init__(self, control, precond=IdentityPreconditionerType(), name=''):
         LinearSolver.__init__(self, name=name)
@@ -91,7 +94,12 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
                     x0.zero()
                 return self.handleConvergence(0, _like(b, x0), 0, 0)
         dA = self._device_matrix(A)
+        echo = self._echo_setup and (custom or not _is_zero_norm(b, n))
+        if echo:                                            # PCGSolver.py:91 (unconditional in the reference)
+            print('prec frozen = ', self.precFrozen())
         if self.precond is None or not self.precFrozen():   # PCGSolver.py:92-94
+            if echo:
+                print('building prec')                      # :93
             self.precond = self.precondType().form(dA)
         if custom and self._entry == "psk_pcg":
             return self._host_norm_pcg(dA, b, normb_caller)
@@ -229,6 +237,20 @@ def _like(b, x):
         import torch
         return torch.as_tensor(np.ascontiguousarray(x), dtype=torch.float64, device=b.device)
     return x
+
+
+def _is_zero_norm(b, n):
+    """||b|| == 0 (npla.norm(b) = sqrt(b.b), PCGSolver.py:86): the reference returns before its
+    setup prints then. One dot over b (host numpy, or psk_nrm2 for a device vector)."""
+    if isinstance(b, DeviceVector) or is_device_vector(b):
+        out = ctypes.c_double()
+        p = b._p if isinstance(b, DeviceVector) else N.ptr(b)
+        if not isinstance(b, DeviceVector):
+            torch_stream_ready(b)
+        N.check(N.lib.psk_nrm2(n, p, N.PSK_DEVICE, ctypes.byref(out)), "psk_nrm2")
+        return out.value == 0.0
+    v = np.ascontiguousarray(b, dtype=np.float64)
+    return float(np.dot(v, v)) == 0.0
 
 
 def _host_copy(v):

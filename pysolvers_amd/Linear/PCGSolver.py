@@ -20,6 +20,7 @@ class PCG(IterativeLinearSolverType):
 
 class PCGSolver(IterativeLinearSolver):
     _entry = "psk_pcg"
+    _echo_setup = True     # the reference's two setup prints (PCGSolver.py:91,93)
 
     def __init__(self, control=CommonSolverArgs(), precond=IdentityPreconditionerType(), name='PCG'):
         super().__init__(control=control, precond=precond, name=name)

@@ -300,6 +300,24 @@ def test_frozen_matrix_and_prec_reuse(psk):
     assert a.iters() == b.iters() == 103 and np.array_equal(a.soln(), b.soln())
 
 
+def test_pcg_setup_prints_as_reference(psk, capsys):
+    """PCGSolver.solve prints 'prec frozen = ' + precFrozen() on every solve with b != 0 and
+    'building prec' whenever it forms the preconditioner (PCGSolver.py:91,93: unconditional prints,
+    after the b = 0 early return at :86-88); GMRES prints neither (GMRESSolver.py has no such line)."""
+    d = load_golden("pcg_dh8_identity.npz")
+    A = golden_matrix(d)
+    s = psk.PCG(control=_ctl(maxiter=200)).makeSolver()
+    s.solve(A, d["b"])
+    assert capsys.readouterr().out == "prec frozen =  False\nbuilding prec\n"
+    s.freezePrec()
+    s.solve(A, d["b"])
+    assert capsys.readouterr().out == "prec frozen =  True\n"
+    s.solve(A, np.zeros_like(d["b"]))                        # :86-88 returns before the prints
+    assert capsys.readouterr().out == ""
+    psk.GMRES(control=_ctl(maxiter=200)).makeSolver().solve(A, d["b"])
+    assert capsys.readouterr().out == ""
+
+
 @pytest.mark.parametrize("case", restarted_cases(), ids=lambda c: c["file"][:-4])
 def test_gmres_restarted_matches_reference_cycles(psk, case):
     """GMRES(m) on the device vs the fixtures whose every restart cycle make_restarted.py checked bit
