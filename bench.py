@@ -703,7 +703,7 @@ def gmres_arnoldi(N, m=4096, restart=30, cycles=2, repeats=3):
 
 def trisolve_schedules(N, h):
     """Schedule the library chose for each factor of a triangular-solve chain."""
-    names = {0: "syncfree", 1: "band", 2: "lds"}
+    names = {0: "syncfree", 1: "band", 2: "lds", 3: "grid", 4: "part", 5: "strip"}
     out = []
     for which in (0, 1):
         s, blocks = N.I32(), N.I64()

@@ -202,7 +202,11 @@ struct AmgHierarchy;
 //    (sptrsv_part_kernel).
 // `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds / kSchedGrid / kSchedPart), chosen by host
 // cost models.
-enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4 };
+//  * strip (round 4): natural-index strips as `part`, but the strip's rows run in steps of <= 64
+//    independent rows, one row per lane of one solver wave, in-strip dependencies from an LDS ring
+//    (sptrsv_strip_kernel).
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4,
+                         kSchedStrip = 5 };
 constexpr int kGridMaxPE = 8;   // distinct dependency patterns reaching into the band above
 struct GridExt {
     int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
@@ -242,7 +246,14 @@ struct TriFactor {
     int32_t *part_rp = nullptr, *part_code = nullptr, *part_row = nullptr;
     double *part_va = nullptr;
     int part_P = 0;
-    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0;
+    // strip layout: steps of each strip, row slots and [e][lane] records per step (plan_strip)
+    int64_t *strip_seg = nullptr, *strip_rec = nullptr;
+    int32_t *strip_row0 = nullptr, *strip_slot_row = nullptr, *strip_code = nullptr;
+    double *strip_slot_d = nullptr, *strip_val = nullptr;
+    int strip_P = 0;
+    int64_t strip_steps = 0;
+    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0,
+           est_strip_us = -1.0;
     void release();
 };
 }  // namespace psk
