@@ -1062,6 +1062,7 @@ constexpr int kStripBufs = 3;
 constexpr int kStripChunk = 1024;                // record entries per LDS buffer
 constexpr int kStripRing = 8192;                 // results of the strip kept in LDS (64 KiB)
 constexpr int32_t kStripPad = INT32_MIN;
+constexpr int kStripBatch = 16;                  // entries whose LDS reads are issued together
 constexpr size_t kStripLds = (size_t)kStripRing * 8 + (size_t)kStripBufs * kStripChunk * (4 + 8 + 8) + 64;
 
 template <bool UNIT>
@@ -1135,20 +1136,33 @@ __global__ __launch_bounds__(kStripThreads) void sptrsv_strip_kernel(
             if (b > a && (b - 1) / C > q) wait_chunk(q + 1);
             const bool act = lane < nr;
             double acc = 0.0;
-            for (int e = 0; e < E; ++e) {
-                const int64_t r = a + (int64_t)e * nr + (act ? lane : 0);
-                const int bf = (int)((r / C) % NB), sl = (int)(r % C);
-                const int32_t c = bcode[bf * C + sl];
-                const double v = bval[bf * C + sl];
-                double xv;
-                if (c >= 0) {
-                    xv = ring[c];
-                } else {
-                    xv = __longlong_as_double((long long)__hip_atomic_load(
-                        reinterpret_cast<const uint64_t *>(bext + bf * C + sl), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                    if (c != kStripPad && is_sentinel(xv)) xv = wait_pub(x + ~c, err);
+            // entries in batches of kStripBatch: every LDS read of a batch is issued before the first
+            // is used (one LDS round trip for codes and values, one for the x values: the ring slot and
+            // the staged external value are both read, the code selects), then the fma chain
+            for (int eb = 0; eb < E; eb += kStripBatch) {
+                int32_t cc[kStripBatch], off[kStripBatch];
+                double vv[kStripBatch], xr[kStripBatch], xe[kStripBatch];
+#pragma unroll
+                for (int u = 0; u < kStripBatch; ++u) {
+                    const int e = eb + u;
+                    const int64_t r = a + (int64_t)(e < E ? e : E - 1) * nr + (act ? lane : 0);
+                    off[u] = (int)((r / C) % NB) * C + (int)(r % C);
+                    cc[u] = e < E ? bcode[off[u]] : kStripPad;
+                    vv[u] = bval[off[u]];
                 }
-                if (act && c != kStripPad) acc = fma(v, xv, acc);   // stored order
+#pragma unroll
+                for (int u = 0; u < kStripBatch; ++u) {
+                    xr[u] = ring[cc[u] & (kStripRing - 1)];
+                    xe[u] = __longlong_as_double((long long)__hip_atomic_load(
+                        reinterpret_cast<const uint64_t *>(bext + off[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+                }
+#pragma unroll
+                for (int u = 0; u < kStripBatch; ++u) {
+                    const int32_t c = cc[u];
+                    double xv = c >= 0 ? xr[u] : xe[u];
+                    if (c < 0 && c != kStripPad && is_sentinel(xv)) xv = wait_pub(x + ~c, err);
+                    if (act && c != kStripPad) acc = fma(vv[u], xv, acc);   // stored order
+                }
             }
             if (act) {
                 double res = my_b - acc;
