@@ -1051,12 +1051,14 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
 // pre-read x), polling again the ones still unpublished while they wait for a free buffer, so the
 // solver mostly finds them in LDS (band_narrow's hand-shake: ctl[b] = stagers done with buffer b,
 // ctl[NB] = last chunk the solver released, ctl[NB+1] = strip done).
+// Steps of a strip are consecutive runs of its rows in ASAP order; a row joins the open step only if
+// none of its dependencies on other strips has an ASAP time at or above the step's first row's.
 // Records of step s: rows r0 .. r0+nr-1 (step slots: row, diagonal), entries [e][lane] at rec[s] +
 // e*nr + lane for e < E_s (the step's longest row); codes: >= 0 ring slot (lpos & (ring-1)), < 0 ~row
 // (a published value), kStripPad (a shorter row's padding: skipped). E_s * nr <= kStripChunk, so a
-// step spans at most two chunks. Progress: all strips co-resident (cooperative launch); every strip
-// runs its rows in one topological order (ascending host ASAP time), so the blocked step with the
-// smallest ASAP time always has its dependencies done.
+// step spans at most two chunks. Progress: all strips co-resident (cooperative launch); a blocked step
+// waits only on rows of strictly lower ASAP time than its first row, which sit in steps whose first
+// rows are lower still, so the blocked step with the lowest first ASAP time has its dependencies done.
 constexpr int kStripThreads = 256;
 constexpr int kStripBufs = 3;
 constexpr int kStripChunk = 1024;                // record entries per LDS buffer
@@ -2330,6 +2332,7 @@ static void plan_strip(const HostFactor &F, const std::vector<int32_t> &nat, int
         sp.seg[w] = nsteps;
         int64_t first_slot = (int64_t)sp.slot_row.size(), cur_rows = 0;
         int32_t cur_e = 0;
+        double step_lo = 0.0;
         double cost = 0.0;
         for (; k < n && wg[idx[k]] == w; ++k) {
             const int32_t i = idx[k];
@@ -2337,8 +2340,14 @@ static void plan_strip(const HostFactor &F, const std::vector<int32_t> &nat, int
             bool conflict = cur_rows == 0;   // no open step yet
             if (!conflict && (cur_rows == 64 || (int64_t)std::max(cur_e, len) * (cur_rows + 1) > kStripChunk))
                 conflict = true;
-            for (int32_t j = F.rp[i]; j < F.rp[i + 1] && !conflict; ++j)
-                conflict = stepid[F.ci[j]] == nsteps - 1 && wg[F.ci[j]] == w;
+            // a local dependency in the open step, or an external one whose ASAP time is not below the
+            // open step's first (lowest) ASAP time: the latter keeps the steps deadlock-free (a blocked
+            // step waits only on rows of strictly lower ASAP time than its own first row, so the chain
+            // of waits descends and ends at a step that can run)
+            for (int32_t j = F.rp[i]; j < F.rp[i + 1] && !conflict; ++j) {
+                const int32_t d = F.ci[j];
+                conflict = wg[d] == w ? stepid[d] == nsteps - 1 : fin[d] >= step_lo;
+            }
             if (conflict) {   // close the open step (if any), open a new one
                 if (cur_rows > 0) {
                     recs += (int64_t)cur_e * cur_rows;
@@ -2349,6 +2358,7 @@ static void plan_strip(const HostFactor &F, const std::vector<int32_t> &nat, int
                 ++nsteps;
                 cur_rows = 0;
                 cur_e = 0;
+                step_lo = fin[i];
             }
             stepid[i] = nsteps - 1;
             lpos[i] = (int32_t)((int64_t)sp.slot_row.size() - first_slot);
