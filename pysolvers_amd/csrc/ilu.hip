@@ -1037,229 +1037,6 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
     }
 }
 
-// Strip (round 4; kSchedStrip): the rows cut into P strips of their NATURAL index (as the partitioned
-// schedule: for ILU the original equation / unknown of every factor row, a band of the mesh), one
-// workgroup per strip and per CU; inside a strip the rows run in STEPS of at most 64 rows that do not
-// depend on each other, one row per LANE of the solver wave (wave 0), every lane summing its row's
-// entries in stored order into one fma chain, then (b - acc) / d. A dependency on a row of the same
-// strip that ran at most kStripRing rows earlier is read from an LDS ring of the strip's results, so
-// the in-strip hand-off is the wave's own program order (an LDS write, then a read one step later),
-// not a published value seen by a polling load (~1 us, the sync-free schedule's cost per level) or the
-// partitioned kernel's tagged LDS cache (~0.4 us, one wave per row). Every other dependency is a
-// published value of x (pre-filled sentinel, agent-scope stores), read ahead by the STAGER waves 1-3
-// while they copy the strip's record stream into NB LDS buffers (NB x kStripChunk entries: code, value,
-// pre-read x), polling again the ones still unpublished while they wait for a free buffer, so the
-// solver mostly finds them in LDS (band_narrow's hand-shake: ctl[b] = stagers done with buffer b,
-// ctl[NB] = last chunk the solver released, ctl[NB+1] = strip done).
-// Steps of a strip are consecutive runs of its rows in ASAP order; a row joins the open step only if
-// none of its dependencies on other strips has an ASAP time at or above the step's first row's.
-// Records of step s: rows r0 .. r0+nr-1 (step slots: row, diagonal), entries [e][lane] at rec[s] +
-// e*nr + lane for e < E_s (the step's longest row); codes: >= 0 ring slot (lpos & (ring-1)), < 0 ~row
-// (a published value), kStripPad (a shorter row's padding: skipped). E_s * nr <= kStripChunk, so a
-// step spans at most two chunks. Progress: all strips co-resident (cooperative launch); a blocked step
-// waits only on rows of strictly lower ASAP time than its first row, which sit in steps whose first
-// rows are lower still, so the blocked step with the lowest first ASAP time has its dependencies done.
-constexpr int kStripThreads = 256;
-constexpr int kStripBufs = 3;
-constexpr int kStripChunk = 1024;                // record entries per LDS buffer
-constexpr int kStripRing = 8192;                 // results of the strip kept in LDS (64 KiB)
-constexpr int32_t kStripPad = INT32_MIN;
-constexpr int kStripBatch = 16;                  // entries whose LDS reads are issued together
-constexpr size_t kStripLds = (size_t)kStripRing * 8 + (size_t)kStripBufs * kStripChunk * (4 + 8 + 8) + 64;
-
-template <bool UNIT>
-__global__ __launch_bounds__(kStripThreads) void sptrsv_strip_kernel(
-    const int64_t *__restrict__ sseg,   // [P+1] step range of each strip
-    const int32_t *__restrict__ srow0,  // [S+1] first row slot of each step
-    const int64_t *__restrict__ srec,   // [S+1] first record entry of each step
-    const int32_t *__restrict__ slot_row, const double *__restrict__ slot_d,   // per row slot
-    const int32_t *__restrict__ rcode, const double *__restrict__ rval,        // records
-    const double *__restrict__ rhs, double *x, int32_t *err) {
-    constexpr int C = kStripChunk, NB = kStripBufs;
-    extern __shared__ __align__(16) unsigned char smem[];
-    double *ring = reinterpret_cast<double *>(smem);
-    double *bval = ring + kStripRing;            // NB x C values
-    double *bext = bval + NB * C;                // NB x C pre-read x (sentinel: local or not yet published)
-    int32_t *bcode = reinterpret_cast<int32_t *>(bext + NB * C);   // NB x C codes
-    int32_t *ctl = bcode + NB * C;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const double sentinel = __longlong_as_double((long long)kSentinel);
-    const int64_t s0 = sseg[blockIdx.x], s1 = sseg[blockIdx.x + 1];
-    if (s1 <= s0) return;   // uniform: an empty strip
-    const int64_t e0 = srec[s0], nrec = srec[s1] - e0, nchunks = (nrec + C - 1) / C;
-    const int32_t q0 = srow0[s0];
-    if (tid <= NB + 1) ctl[tid] = tid == NB ? -1 : 0;
-    __syncthreads();
-    if (wave == 0) {
-        int64_t seen = -1, cur = 0;
-        auto wait_chunk = [&](int64_t q) {
-            if (q <= seen) return;
-            const int32_t need = 3 * (int32_t)(q / NB + 1);
-            int64_t spins = 0;
-            while (lds_load_acq(&ctl[q % NB]) < need) {
-                if (++spins > kMaxSpins) {
-                    atomicExch(err, 1);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            seen = q;
-        };
-        // step headers and the row slots of the next step are loaded one step ahead
-        int32_t r0 = srow0[s0], r1 = srow0[s0 + 1];
-        int64_t ra = srec[s0], rb = srec[s0 + 1];
-        int32_t row = lane < r1 - r0 ? slot_row[r0 + lane] : 0;
-        double dd = UNIT ? 1.0 : (lane < r1 - r0 ? slot_d[r0 + lane] : 1.0);
-        double bb = rhs[row];
-        for (int64_t s = s0; s < s1; ++s) {
-            const int32_t nr = r1 - r0;
-            const int64_t a = ra - e0, b = rb - e0;
-            const int E = nr > 0 ? (int)((b - a) / nr) : 0;
-            const int32_t my_row = row;
-            const double my_d = dd, my_b = bb;
-            const int32_t my_q = r0 + lane - q0;   // local position of this lane's row
-            // prefetch the next step's header and row slot
-            if (s + 1 < s1) {
-                r0 = r1;
-                r1 = srow0[s + 2];
-                ra = rb;
-                rb = srec[s + 2];
-                const bool act = lane < r1 - r0;
-                row = act ? slot_row[r0 + lane] : 0;
-                if (!UNIT) dd = act ? slot_d[r0 + lane] : 1.0;
-                bb = rhs[row];
-            }
-            const int64_t q = a / C;
-            if (q > cur) {   // every step of chunks < q is done: their buffers may be restaged
-                if (lane == 0) __hip_atomic_store(&ctl[NB], (int32_t)(q - 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                cur = q;
-            }
-            wait_chunk(q);
-            if (b > a && (b - 1) / C > q) wait_chunk(q + 1);
-            const bool act = lane < nr;
-            double acc = 0.0;
-            // entries in batches of kStripBatch: every LDS read of a batch is issued before the first
-            // is used (one LDS round trip for codes and values, one for the x values: the ring slot and
-            // the staged external value are both read, the code selects), then the fma chain
-            for (int eb = 0; eb < E; eb += kStripBatch) {
-                int32_t cc[kStripBatch], off[kStripBatch];
-                double vv[kStripBatch], xr[kStripBatch], xe[kStripBatch];
-#pragma unroll
-                for (int u = 0; u < kStripBatch; ++u) {
-                    const int e = eb + u;
-                    const int64_t r = a + (int64_t)(e < E ? e : E - 1) * nr + (act ? lane : 0);
-                    off[u] = (int)((r / C) % NB) * C + (int)(r % C);
-                    cc[u] = e < E ? bcode[off[u]] : kStripPad;
-                    vv[u] = bval[off[u]];
-                }
-#pragma unroll
-                for (int u = 0; u < kStripBatch; ++u) {
-                    xr[u] = ring[cc[u] & (kStripRing - 1)];
-                    xe[u] = __longlong_as_double((long long)__hip_atomic_load(
-                        reinterpret_cast<const uint64_t *>(bext + off[u]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-                }
-#pragma unroll
-                for (int u = 0; u < kStripBatch; ++u) {
-                    const int32_t c = cc[u];
-                    double xv = c >= 0 ? xr[u] : xe[u];
-                    if (c < 0 && c != kStripPad && is_sentinel(xv)) xv = wait_pub(x + ~c, err);
-                    if (act && c != kStripPad) acc = fma(vv[u], xv, acc);   // stored order
-                }
-            }
-            if (act) {
-                double res = my_b - acc;
-                if (!UNIT) res = res / my_d;
-                ring[my_q & (kStripRing - 1)] = res;
-                store_pub(x + my_row, res);
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);   // this step's ring writes before the next step's reads
-            __builtin_amdgcn_wave_barrier();
-        }
-        if (lane == 0) {
-            __hip_atomic_store(&ctl[NB], (int32_t)(nchunks - 1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&ctl[NB + 1], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-    } else {
-        // stager thread st (0..191) owns entries st, st + 192, ... of every buffer
-        constexpr int ST = kStripThreads - 64, PER = (C + ST - 1) / ST;
-        const int st = tid - 64;
-        int64_t last_q[NB];
-        uint32_t pending[NB];   // bit u: entry st + u*ST of buffer b still holds the sentinel
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            last_q[b] = -1;
-            pending[b] = 0;
-        }
-        auto refresh = [&]() {
-            const int32_t done_q = lds_load_acq(&ctl[NB]);
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                if (pending[b] == 0 || last_q[b] <= done_q) continue;
-#pragma unroll
-                for (int u = 0; u < PER; ++u)
-                    if (pending[b] & (1u << u)) {
-                        const int sl = st + u * ST;
-                        const double v = load_pub(x + ~bcode[b * C + sl]);
-                        if (!is_sentinel(v)) {
-                            __hip_atomic_store(reinterpret_cast<uint64_t *>(bext + b * C + sl),
-                                               (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_WORKGROUP);
-                            pending[b] &= ~(1u << u);
-                        }
-                    }
-            }
-        };
-        for (int64_t q = 0; q < nchunks; ++q) {
-            const int b = (int)(q % NB);
-            int64_t spins = 0;
-            while (lds_load_acq(&ctl[NB]) < q - NB) {   // buffer b still holds chunk q - NB
-                refresh();
-                if (++spins > kMaxSpins) {
-                    atomicExch(err, 1);
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(1);
-            }
-            pending[b] = 0;
-            last_q[b] = q;
-            int32_t cs[PER];
-            double vs[PER], xs[PER];
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {   // every load of the chunk first
-                const int sl = st + u * ST;
-                const int64_t r = q * C + sl;
-                const bool ok = sl < C && r < nrec;
-                cs[u] = ok ? rcode[e0 + r] : kStripPad;
-                vs[u] = ok ? rval[e0 + r] : 0.0;
-            }
-#pragma unroll
-            for (int u = 0; u < PER; ++u)
-                xs[u] = (cs[u] < 0 && cs[u] != kStripPad) ? load_pub(x + ~cs[u]) : sentinel;
-#pragma unroll
-            for (int u = 0; u < PER; ++u) {
-                const int sl = st + u * ST;
-                if (sl >= C) continue;
-                bcode[b * C + sl] = cs[u];
-                bval[b * C + sl] = vs[u];
-                bext[b * C + sl] = xs[u];
-                if (cs[u] < 0 && cs[u] != kStripPad && is_sentinel(xs[u])) pending[b] |= 1u << u;
-            }
-            __builtin_amdgcn_s_waitcnt(0xc07f);   // this wave's LDS writes done
-            __builtin_amdgcn_wave_barrier();
-            if (lane == 0) __hip_atomic_fetch_add(&ctl[b], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        int64_t spins = 0;
-        while (lds_load_acq(&ctl[NB + 1]) == 0) {
-            refresh();
-            if (++spins > kMaxSpins) {
-                atomicExch(err, 1);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-}
-
 // Grid: a factor whose dependencies, in solve order q, form a 2-D stencil: with q = y*w + x (w
 // positions per line), every off-diagonal entry of row q refers to q' = q - (yd*w + xd) with
 // 0 <= yd < 64 lines back and, for the skew sigma chosen by the host, ud = xd + sigma*yd >= 1 steps
@@ -1715,17 +1492,6 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         PSK_HIP(hipLaunchCooperativeKernel(k, dim3(T.part_P), dim3(kPartThreads), args, (unsigned)kPartLds, s));
         return PSK_OK;
     }
-    if (T.schedule == kSchedStrip) {
-        if (rhs_idx) return fail(PSK_ERR_ARG, "strip schedule: gathered right-hand side (internal)");
-        const void *k = dg ? reinterpret_cast<const void *>(&sptrsv_strip_kernel<false>)
-                           : reinterpret_cast<const void *>(&sptrsv_strip_kernel<true>);
-        const int64_t *sg = T.strip_seg, *sr = T.strip_rec;
-        const int32_t *r0 = T.strip_row0, *srow = T.strip_slot_row, *sc = T.strip_code;
-        const double *sd = T.strip_slot_d, *sv = T.strip_val;
-        void *args[] = {&sg, &r0, &sr, &srow, &sd, &sc, &sv, &rhs, &x, &err};
-        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(T.strip_P), dim3(kStripThreads), args, (unsigned)kStripLds, s));
-        return PSK_OK;
-    }
     if (T.schedule == kSchedGrid) {
         if (rhs_idx) return fail(PSK_ERR_ARG, "grid schedule: gathered right-hand side (internal)");
         const void *k = nullptr;
@@ -1826,8 +1592,7 @@ static int ilu_apply_impl(const psk_prec *M, const double *v, double *out, bool 
     const double *cur = v;                // current right-hand side
     const int32_t *cur_idx = M->gather_in;
     const TriFactor &first = M->lo.present ? M->lo : M->up;
-    if (cur_idx && first.present &&
-        (first.schedule == kSchedGrid || first.schedule == kSchedPart || first.schedule == kSchedStrip)) {   // rhs[row]
+    if (cur_idx && first.present && (first.schedule == kSchedGrid || first.schedule == kSchedPart)) {   // rhs[row]
         hipLaunchKernelGGL(gather_perm_kernel, dim3(fb), dim3(kBlock), 0, s, n, cur, cur_idx, M->work + 2 * n);
         PSK_HIP(hipGetLastError());
         cur = M->work + 2 * n;
@@ -1873,10 +1638,8 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
 }
 
 void TriFactor::release() {
-    void *ptrs[] = {rowptr,    colidx,    vals,      diag,       order,          rec_row,      rec_end,
-                    rec_c,     rec_v,     rec_d,     gd_code,    gd_coef,        gd_diag,      gd_idx,
-                    gd_dict,   part_seg,  part_rp,   part_code,  part_row,       part_va,      strip_seg,
-                    strip_rec, strip_row0, strip_slot_row, strip_code, strip_slot_d, strip_val};
+    void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,   rec_d,
+                    gd_code, gd_coef, gd_diag, gd_idx, gd_dict, part_seg, part_rp, part_code, part_row, part_va};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -2269,138 +2032,6 @@ void plan_part(const HostFactor &F, const std::vector<int32_t> &nat, int P, Part
     pp.est = tmax;
 }
 
-// Strip schedule (sptrsv_strip_kernel): natural-index strips as plan_part, rows of a strip in ASAP order
-// (local hand-off = one step, kStripPrioStepUs; another strip's row = a published value,
-// kStripPrioRemoteUs), packed greedily into steps: a row opens a new step when one of its local
-// dependencies is in the current step, the step holds 64 rows, or its records would pass one chunk.
-// Estimate: the larger of the ASAP critical path and the longest strip's sum of step costs.
-constexpr double kStripPrioStepUs = 0.25, kStripPrioRemoteUs = 1.5;
-constexpr double kStripStepUs = 0.12, kStripEntryUs = 0.012;   // provisional: set from the first measurement
-constexpr bool kStripByModel = false;
-
-struct StripPlan {
-    bool ok = false;
-    int P = 0;
-    double est = -1.0;
-    std::vector<int64_t> seg, rec;
-    std::vector<int32_t> row0, slot_row, code;
-    std::vector<double> slot_d, val;
-};
-
-static void plan_strip(const HostFactor &F, const std::vector<int32_t> &nat, int P, const std::vector<double> &ova,
-                       const std::vector<double> &dg, StripPlan &sp) {
-    const int64_t n = F.n;
-    sp = StripPlan();
-    sp.P = P;
-    if (n == 0 || P < 1) return;
-    for (int64_t i = 0; i < n; ++i)
-        if (F.rp[i + 1] - F.rp[i] > kStripChunk) return;   // a step must fit one chunk
-    std::vector<int32_t> wg(n);
-    const int per = std::max(1, P / 8);
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t s = (nat.empty() ? i : nat[i]) * P / n;
-        wg[i] = (P % 8 == 0) ? (int32_t)((s % 8) * per + s / 8) : (int32_t)s;
-    }
-    std::vector<double> fin(n, 0.0);
-    double crit = 0.0;
-    for (int64_t p = 0; p < n; ++p) {
-        const int64_t i = F.row(p);
-        double t = 0.0;
-        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j)
-            t = std::max(t, fin[F.ci[j]] + (wg[F.ci[j]] == wg[i] ? kStripPrioStepUs : kStripPrioRemoteUs));
-        fin[i] = t;
-        crit = std::max(crit, t);
-    }
-    std::vector<int32_t> idx(n);
-    for (int64_t i = 0; i < n; ++i) idx[i] = (int32_t)i;
-    std::sort(idx.begin(), idx.end(), [&](int32_t u, int32_t v) {
-        if (wg[u] != wg[v]) return wg[u] < wg[v];
-        if (fin[u] != fin[v]) return fin[u] < fin[v];
-        return F.pos(u) < F.pos(v);
-    });
-    // steps: rows of one strip in ASAP order, packed greedily
-    std::vector<int64_t> stepid(n, -1);
-    std::vector<int32_t> lpos(n, 0);
-    sp.seg.assign((size_t)P + 1, 0);
-    sp.row0.clear();
-    sp.rec.clear();
-    sp.slot_row.clear();
-    sp.slot_row.reserve(n);
-    int64_t k = 0, nsteps = 0, recs = 0;
-    double worst = 0.0;
-    for (int w = 0; w < P; ++w) {
-        sp.seg[w] = nsteps;
-        int64_t first_slot = (int64_t)sp.slot_row.size(), cur_rows = 0;
-        int32_t cur_e = 0;
-        double step_lo = 0.0;
-        double cost = 0.0;
-        for (; k < n && wg[idx[k]] == w; ++k) {
-            const int32_t i = idx[k];
-            const int32_t len = F.rp[i + 1] - F.rp[i];
-            bool conflict = cur_rows == 0;   // no open step yet
-            if (!conflict && (cur_rows == 64 || (int64_t)std::max(cur_e, len) * (cur_rows + 1) > kStripChunk))
-                conflict = true;
-            // a local dependency in the open step, or an external one whose ASAP time is not below the
-            // open step's first (lowest) ASAP time: the latter keeps the steps deadlock-free (a blocked
-            // step waits only on rows of strictly lower ASAP time than its own first row, so the chain
-            // of waits descends and ends at a step that can run)
-            for (int32_t j = F.rp[i]; j < F.rp[i + 1] && !conflict; ++j) {
-                const int32_t d = F.ci[j];
-                conflict = wg[d] == w ? stepid[d] == nsteps - 1 : fin[d] >= step_lo;
-            }
-            if (conflict) {   // close the open step (if any), open a new one
-                if (cur_rows > 0) {
-                    recs += (int64_t)cur_e * cur_rows;
-                    cost += kStripStepUs + cur_e * kStripEntryUs;
-                }
-                sp.row0.push_back((int32_t)sp.slot_row.size());
-                sp.rec.push_back(recs);
-                ++nsteps;
-                cur_rows = 0;
-                cur_e = 0;
-                step_lo = fin[i];
-            }
-            stepid[i] = nsteps - 1;
-            lpos[i] = (int32_t)((int64_t)sp.slot_row.size() - first_slot);
-            sp.slot_row.push_back(i);
-            ++cur_rows;
-            cur_e = std::max(cur_e, len);
-        }
-        if (cur_rows > 0) {
-            recs += (int64_t)cur_e * cur_rows;
-            cost += kStripStepUs + cur_e * kStripEntryUs;
-            // the open step's record count is taken by the next step's rec entry / the sentinel below
-        }
-        // fix the record offset of the steps opened in this strip: rec[s] was pushed before the step's
-        // records were known, which is what we want (the step's first entry)
-        worst = std::max(worst, cost);
-    }
-    sp.seg[P] = nsteps;
-    sp.row0.push_back((int32_t)sp.slot_row.size());
-    sp.rec.push_back(recs);
-    // records [e][lane] per step
-    sp.code.assign((size_t)recs, kStripPad);
-    sp.val.assign((size_t)recs, 0.0);
-    sp.slot_d.assign(sp.slot_row.size(), 1.0);
-    for (int64_t s = 0; s < nsteps; ++s) {
-        const int32_t r0 = sp.row0[s], nr = sp.row0[s + 1] - r0;
-        const int64_t a = sp.rec[s];
-        for (int32_t l = 0; l < nr; ++l) {
-            const int32_t i = sp.slot_row[r0 + l];
-            if (!dg.empty()) sp.slot_d[r0 + l] = dg[i];
-            int e = 0;
-            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j, ++e) {
-                const int32_t d = F.ci[j];
-                const bool loc = wg[d] == wg[i] && lpos[i] - lpos[d] < kStripRing;
-                sp.code[a + (int64_t)e * nr + l] = loc ? (lpos[d] & (kStripRing - 1)) : ~d;
-                sp.val[a + (int64_t)e * nr + l] = ova[j];
-            }
-        }
-    }
-    sp.est = std::max(crit, worst);
-    sp.ok = true;
-}
-
 template <class T>
 static int upload(T **d, const std::vector<T> &h) {
     if (h.empty()) {
@@ -2623,35 +2254,12 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
             }
         }
     }
-    // strip schedule: planned for factors too large for one CU and not solved by the grid schedule
-    // (PSK_TRISOLVE_STRIP=0 disables it, =1 builds it and selects it whenever eligible)
-    StripPlan sp;
-    {
-        const char *se = std::getenv("PSK_TRISOLVE_STRIP");
-        const bool force = se && std::atoi(se) == 1, off = se && std::atoi(se) == 0;
-        if (!off && n > kLdsMaxRows && n >= (int64_t)c->num_cus * 64 && (force || T.schedule != kSchedGrid)) {
-            plan_strip(F, nat, c->num_cus, ova, dg, sp);
-            if (sp.ok) {
-                T.est_strip_us = sp.est;
-                const double cur = T.schedule == kSchedBand ? T.est_band_us
-                                   : T.schedule == kSchedLds  ? T.est_lds_us
-                                   : T.schedule == kSchedGrid ? T.est_grid_us
-                                   : T.schedule == kSchedPart ? T.est_part_us
-                                                              : T.est_syncfree_us;
-                // not chosen by the model until it is calibrated on the device (round 4 lab): forced only
-                if (force || (kStripByModel && sp.est < cur)) T.schedule = kSchedStrip;
-                T.strip_P = sp.P;
-                T.strip_steps = sp.seg.empty() ? 0 : sp.seg.back();
-            }
-        }
-    }
     if (const char *ve = std::getenv("PSK_TRISOLVE_VERBOSE"))   // development: the cost model's view
         if (std::atoi(ve))
             std::fprintf(stderr, "psk trisolve %s n=%lld levels=%lld est_us syncfree=%.0f band=%.0f lds=%.0f grid=%.0f "
-                                 "part=%.0f strip=%.0f (steps %lld) -> schedule %d\n",
+                                 "part=%.0f -> schedule %d\n",
                          upper ? "U" : "L", (long long)n, (long long)nlev, T.est_syncfree_us, T.est_band_us,
-                         T.est_lds_us, T.est_grid_us, T.est_part_us, T.est_strip_us, (long long)T.strip_steps,
-                         T.schedule);
+                         T.est_lds_us, T.est_grid_us, T.est_part_us, T.schedule);
     T.present = true;
     T.upper = upper;
     T.nnz = (int64_t)F.ci.size();
@@ -2714,15 +2322,6 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.part_code, pcode);
     if (rc == PSK_OK) rc = upload(&T.part_row, prow);
     if (rc == PSK_OK) rc = upload(&T.part_va, pva);
-    if (sp.ok) {   // kept whenever planned: psk_prec_trisolve_schedule may switch to it
-        if (rc == PSK_OK) rc = upload(&T.strip_seg, sp.seg);
-        if (rc == PSK_OK) rc = upload(&T.strip_rec, sp.rec);
-        if (rc == PSK_OK) rc = upload(&T.strip_row0, sp.row0);
-        if (rc == PSK_OK) rc = upload(&T.strip_slot_row, sp.slot_row);
-        if (rc == PSK_OK && !dg.empty()) rc = upload(&T.strip_slot_d, sp.slot_d);
-        if (rc == PSK_OK) rc = upload(&T.strip_code, sp.code);
-        if (rc == PSK_OK) rc = upload(&T.strip_val, sp.val);
-    }
     return rc;
 }
 
@@ -2799,11 +2398,8 @@ extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t se
     if (set == kSchedPart && T.part_P == 0)
         return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: partitioned layout not built for this factor "
                                          "(built when chosen, or with PSK_TRISOLVE_PART=1 at creation)");
-    if (set == kSchedStrip && T.strip_P == 0)
-        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: strip layout not planned for this factor "
-                                         "(factors of more than 18432 rows without a grid schedule, or PSK_TRISOLVE_STRIP=1)");
-    if (set >= kSchedSyncFree && set <= kSchedStrip) T.schedule = set;
-    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1 or 0..5");
+    if (set >= kSchedSyncFree && set <= kSchedPart) T.schedule = set;
+    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1, 2, 3 or 4");
     if (schedule) *schedule = T.schedule;
     if (blocks) *blocks = T.band_nblocks;
     if (ring_words) *ring_words = T.ring_words;

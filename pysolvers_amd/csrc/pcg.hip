@@ -22,12 +22,6 @@
 #include <cmath>
 #include <cstdio>
 
-#ifndef PSK_LAB_K2_DPP
-#define PSK_LAB_K2_DPP 0   // lab: K2's tile sums by DPP wave totals + LDS combine (gridsum_tile_*)
-#endif
-#ifndef PSK_LAB_WT
-#define PSK_LAB_WT 0   // lab: write-through stores, bit 0 K3's p, bit 1 K2's r, bit 2 K3's x flush
-#endif
 
 namespace psk {
 
@@ -180,47 +174,6 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     const int64_t i = tile * kVecTile + 2 * threadIdx.x;
     uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
-#if PSK_LAB_K2_DPP
-    // DPP wave totals combined in LDS by the last wave (no workgroup barrier at the end), as the SpMV;
-    // the arming barrier of gridsum_tile_begin sits right after the loads are issued (uniform path)
-    (void)sh;
-    __shared__ GridSumTile<2> gsl;
-    const bool full = i + 1 < n;
-    dv2 ro{0.0, 0.0}, a{0.0, 0.0}, d{ds, ds};
-    if (full) {
-        ro = ld2(r + i);
-        a = ld2nt(Ap + i);
-        if (JAC == 1) d = ld2(dinv + i);
-    }
-    ticket = gridsum_tile_begin<2>(gs, gsl, tile);
-    if (full) {
-        dv2 rn;
-        rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
-        rn.y = ro.y - alpha * a.y;
-        double u0 = rn.x, u1 = rn.y;
-        if (JAC) {
-            u0 = d.x * rn.x;                                 // u = precond.applyRight(r)  :123
-            u1 = d.y * rn.y;
-        }
-#if (PSK_LAB_WT & 2)
-        st2wt(r, n, i, rn);
-#else
-        st2(r + i, rn);
-#endif
-        rr = fma(rn.x, rn.x, rr);
-        rr = fma(rn.y, rn.y, rr);
-        ur = fma(u0, rn.x, ur);
-        ur = fma(u1, rn.y, ur);
-    } else if (i < n) {   // odd tail element
-        const double rn = r[i] - alpha * Ap[i];
-        const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
-        r[i] = rn;
-        rr = rn * rn;
-        ur = u0 * rn;
-    }
-    const double v[2] = {wave_total(rr), wave_total(ur)};
-    gridsum_tile_publish<2>(gs, gsl, v, ticket, tile);
-#else
     if (i + 1 < n) {
         const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
@@ -234,11 +187,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
             u0 = d.x * rn.x;                                 // u = precond.applyRight(r)  :123
             u1 = d.y * rn.y;
         }
-#if (PSK_LAB_WT & 2)
-        st2wt(r, n, i, rn);   // lab: write-through
-#else
         st2(r + i, rn);
-#endif
         rr = fma(rn.x, rn.x, rr);
         rr = fma(rn.y, rn.y, rr);
         ur = fma(u0, rn.x, ur);
@@ -253,7 +202,6 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     }
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
-#endif
 }
 
 // Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
@@ -376,22 +324,12 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
             dv2 xn;
             xn.x = xo.x + alpha * po.x;                      // :121
             xn.y = xo.y + alpha * po.y;
-#if (PSK_LAB_WT & 4)
-            st2wt(x, n, i, xn);
-#else
             st2nt(x + i, xn);
-#endif
         }
         dv2 pn;
         pn.x = u0 + beta * po.x;                             // p = u + beta*p  :138
         pn.y = u1 + beta * po.y;
-#if defined(PSK_LAB_K3_PNT)
-        st2nt(pnext + i, pn);   // lab: p stored non-temporally (the K3 -> SpMV boundary's dirty bytes)
-#elif (PSK_LAB_WT & 1)
-        st2wt(pnext, n, i, pn);   // lab: write-through
-#else
-        st2(pnext + i, pn);
-#endif
+        st2(pnext + i, pn);   // (non-temporal and write-through p stores measured no faster, round 4)
     } else if (i < n) {
         const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
         const double pi = pcur[i];
@@ -651,14 +589,6 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         return !(e && std::atoi(e) == 0);
     }();
     const bool overlap = overlap_on && sharded && !gen && halo_split(A, kVecTile, nv, ov_lo, ov_hi);
-    // K2/K3 tile order (round 4): PSK_K23_BANDS=0 block order; 1 XCD bands walked forward like the
-    // SpMV's (a tile of K2/K3 = the 512 rows of one two-slice SpMV workgroup, on the same XCD);
-    // 2 the same bands, the walking direction alternating from kernel to kernel (SpMV, K2, K3 of
-    // iteration k: rev = k&1, !(k&1), k&1), so each kernel first reads what its predecessor wrote last
-    static const int k23_bands = [] {
-        const char *e = std::getenv("PSK_K23_BANDS");
-        return e ? std::atoi(e) : 0;
-    }();
     hipStream_t cs = nullptr;
     hipEvent_t ev_k3a = kit->ev_a, ev_halo = kit->ev_b;
     bool halo_pending = false;
@@ -696,11 +626,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
         }
         // a timed launch records its events in its own dispatch (kernel start / end)
-        const bool odd = (k & 1) != 0 && k23_bands == 2;
         if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s,
-                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr, odd ? 1 : 0)) != PSK_OK)
+                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr)) != PSK_OK)
             break;
-        const TileMap tm2 = tile_map_for(nv, k23_bands != 0, k23_bands == 2 && !odd);
+        // K2/K3 tiles in block order: XCD bands matching the SpMV's, and bands walked in alternating
+        // directions, measured no faster (round 4, profiles/r4_spmv_ab.txt)
+        const TileMap tm2 = tile_map_for(nv, false);
         if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
         if (jac == 2)
             hipLaunchKernelGGL(pcg_update_kernel<2>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
@@ -721,7 +652,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             auto k3 = [&](int64_t t0, int64_t t1) {   // K3 over tiles [t0, t1)
                 if (t1 <= t0) return;
                 const dim3 g3((unsigned)(t1 - t0));
-                const TileMap tm3 = tile_map_for(t1 - t0, k23_bands != 0, odd);
+                const TileMap tm3 = tile_map_for(t1 - t0, false);
                 if (jac == 2)
                     hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
                                        w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,

@@ -202,11 +202,7 @@ struct AmgHierarchy;
 //    (sptrsv_part_kernel).
 // `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds / kSchedGrid / kSchedPart), chosen by host
 // cost models.
-//  * strip (round 4): natural-index strips as `part`, but the strip's rows run in steps of <= 64
-//    independent rows, one row per lane of one solver wave, in-strip dependencies from an LDS ring
-//    (sptrsv_strip_kernel).
-enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4,
-                         kSchedStrip = 5 };
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4 };
 constexpr int kGridMaxPE = 8;   // distinct dependency patterns reaching into the band above
 struct GridExt {
     int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
@@ -246,14 +242,7 @@ struct TriFactor {
     int32_t *part_rp = nullptr, *part_code = nullptr, *part_row = nullptr;
     double *part_va = nullptr;
     int part_P = 0;
-    // strip layout: steps of each strip, row slots and [e][lane] records per step (plan_strip)
-    int64_t *strip_seg = nullptr, *strip_rec = nullptr;
-    int32_t *strip_row0 = nullptr, *strip_slot_row = nullptr, *strip_code = nullptr;
-    double *strip_slot_d = nullptr, *strip_val = nullptr;
-    int strip_P = 0;
-    int64_t strip_steps = 0;
-    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0,
-           est_strip_us = -1.0;
+    double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0;
     void release();
 };
 }  // namespace psk
@@ -727,20 +716,6 @@ __device__ __forceinline__ dv2 ld2nt(const double *p) {
 }
 __device__ __forceinline__ void st2(double *p, dv2 v) { *reinterpret_cast<dv2 *>(p) = v; }
 __device__ __forceinline__ void st2nt(double *p, dv2 v) { __builtin_nontemporal_store(v, reinterpret_cast<dv2 *>(p)); }
-
-// 16-byte write-through store (sc1: the line goes to memory and is dropped from the XCD's L2, so
-// a streaming kernel leaves no dirty lines for the kernel boundary to write back; MI355X_MICROARCH.md
-// "boundary": + dirty bytes / 6 TB/s). Buffer store at byte offset `off` of the uniform base `p` of n
-// doubles; falls back to a plain store for arrays of 4 GiB or more (32-bit offsets).
-typedef unsigned int psk_u4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ void st2wt(double *p, int64_t n, int64_t i, dv2 v) {
-    if (n >= ((int64_t)1 << 29)) {
-        st2(p + i, v);
-        return;
-    }
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(uint32_t)(n * 8), 0x00020000);
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(psk_u4, v), r, (int)(uint32_t)(i * 8), 0, 0x10);
-}
 
 // contiguous share [b0,b1) of `ntiles` tiles for workgroup `b` of `g`
 __device__ __forceinline__ void block_range(int64_t ntiles, int64_t &t0, int64_t &t1) {

@@ -254,11 +254,7 @@ __device__ __forceinline__ double spmv_finish_row(bool has, int64_t row, double 
         } else if (MODE == kSpmvAdd) {
             y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
         } else {
-#ifdef PSK_LAB_Y_DEFAULT
-            y[row] = sum;   // lab: default policy (Ap read by the next kernel)
-#else
             __builtin_nontemporal_store(sum, y + row);
-#endif
             if (MODE != kSpmvPlain) acc = eq * sum;   // x.(Ax) or q.(Ax)
         }
     }
@@ -992,10 +988,11 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     // block order
     // rev: each XCD walks its band backwards (the PCG loop alternates directions, PSK_K23_BANDS=2)
     const TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands(), rev != 0);
-    // uniform layouts (compact, and double values): slices per workgroup, spmv_uniform_multi_kernel
-    // (round 4: 2 by default, PSK_SPMV_TPW=1 the one-slice kernel; 3 and 4 compact only, lab). Two
-    // slices per workgroup: in-loop SpMV at N = 10M 0.0657 -> 0.0611 ms, 16384^2 1.60 -> 1.49 ms, same
-    // bits (profiles/r4_spmv_tpw_ab.txt)
+    // compact uniform layout (FD and other 2-value stencils): slices per workgroup,
+    // spmv_uniform_multi_kernel (round 4: 2 by default, PSK_SPMV_TPW=1 the one-slice kernel, 3 and 4
+    // lab). Two slices per workgroup: in-loop SpMV at N = 10M 0.0657 -> 0.0611 ms, 16384^2 1.60 ->
+    // 1.49 ms, same bits; with double values (the general path) it measured 4% slower and is not used
+    // there (profiles/r4_spmv_ab.txt)
     const int tpw = spmv_tpw();
     const int64_t nwg2 = (nwg + tpw - 1) / tpw;
     const dim3 gd2((unsigned)(nwg2 > 0 ? nwg2 : 1));
@@ -1004,14 +1001,8 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
 #define PSK_UNI_LAUNCH(M, DK, UW)                                                                              \
-    do {                                                                                                       \
-        if (DK == 0 && tpw == 2)                                                                               \
-            hipExtLaunchKernelGGL((spmv_uniform_multi_kernel<M, 0, UW, false, 2>), gd2, bd, 0, s, ev0, ev1, 0, A->n, \
-                                  A->sl_pcol, A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm2, nwg);  \
-        else                                                                                                   \
-            hipExtLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol,     \
-                                  A->sl_val, A->sl_dict, x, y, aux_d, aux_q, gs, done_flag, tm);                 \
-    } while (0)
+    hipExtLaunchKernelGGL((spmv_uniform_kernel<M, DK, UW>), gd, bd, 0, s, ev0, ev1, 0, A->n, A->sl_pcol, A->sl_val, A->sl_dict, \
+                       x, y, aux_d, aux_q, gs, done_flag, tm)
 #define PSK_SLICED_LAUNCH_DK(M, DK)                                                                            \
     do {                                                                                                       \
         switch (uw) {                                                                                          \
