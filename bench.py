@@ -123,6 +123,12 @@ def main():
         import atexit
         atexit.register(_dump_maps, maps_out)
 
+    # One rank never imports torch (torch.distributed is the N > 1 control plane only): libpsk then runs on
+    # the system ROCm runtime alone. With torch's bundled HIP runtime in the process, a rocprofv3 run
+    # faulted in exit(): the profiler's HSA (loaded first) served torch's HIP, and torch's HIP teardown
+    # called into it after the profiler had finalised it (profiles/r4_exit_fault.txt).
+    if world == 1:
+        os.environ.setdefault("PSK_NO_TORCH", "1")
     from pysolvers_amd import _native as N
     # one GPU per rank: LOCAL_RANK when every GPU is visible to every rank; a launcher that narrows
     # visibility per rank leaves one device (ordinal 0) per process
@@ -844,17 +850,3 @@ def pcg_amg(N, m=8192, levels=5, cycles=2, iters=6, repeats=3):
 
 if __name__ == "__main__":
     main()
-    # Leave without running the C++ static destructors of the GPU runtimes. Under rocprofv3 this
-    # process holds two HSA runtimes (the profiler's /opt/rocm one and torch's bundled one, whose
-    # libamdhip64 binds to the first): at exit() torch's HIP destructor called into the HSA the
-    # profiler had already finalised and faulted (SIGSEGV after "[rocprofv3] tool finalization";
-    # faulting PC resolved with PSK_DUMP_MAPS to libhsa-runtime64 called from torch's libamdhip64,
-    # profiles/r4_exit_fault.txt). Everything the bench owns is released first (psk_shutdown).
-    sys.stdout.flush()
-    sys.stderr.flush()
-    if "pysolvers_amd._native" in sys.modules:
-        sys.modules["pysolvers_amd._native"]._shutdown()
-    maps_out = os.environ.get("PSK_DUMP_MAPS")
-    if maps_out:
-        _dump_maps(maps_out)
-    os._exit(0)

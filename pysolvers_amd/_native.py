@@ -138,9 +138,12 @@ def _pin_runtime():
     `import torch` would map a second HIP runtime into the process (measured here: duplicate
     libamdhip64/libhsa-runtime64/librccl and a heap corruption at exit). So when torch is
     installed it is imported FIRST and libpsk binds to the runtime torch loaded (same sonames);
-    without torch, the system ROCm runtime is used.
+    without torch, or with PSK_NO_TORCH=1 (a process that will never import torch, e.g. a one-GPU
+    bench.py), the system ROCm runtime is used.
     """
     import importlib.util
+    if os.environ.get("PSK_NO_TORCH") == "1":   # the caller never imports torch: the system ROCm runtime
+        return
     if importlib.util.find_spec("torch") is not None:
         import torch  # noqa: F401
 
