@@ -49,6 +49,24 @@ __device__ __forceinline__ void spmv_publish(const GridSum &gs, GridSumTile<1> &
     gridsum_tile_publish<1>(gs, L, &ws, ticket, t);
 }
 
+// The row's y value and dot partial first, the y store after the
+// dot epilogue (gridsum publish). On gfx950 the registers holding a store's data may not be reused
+// until the store has left (a vmcnt wait that also waits for its HBM write): with the y store ahead
+// of the epilogue, every wave waited for it there (kSpmvDot at N = 10M: ~9.5 us over a plain SpMV).
+template <int MODE>
+__device__ __forceinline__ double spmv_row_value(bool has, double sum, double eq, double &acc) {
+    const double yv = MODE == kSpmvResid ? eq - sum : MODE == kSpmvAdd ? eq + sum : sum;   // :163 / VCycleManager.py:55
+    acc = 0.0;
+    if (has && MODE != kSpmvPlain && MODE != kSpmvAdd) acc = MODE == kSpmvResid ? yv * yv : eq * sum;
+    return yv;
+}
+template <int MODE>
+__device__ __forceinline__ void spmv_store_row(bool has, int64_t row, double yv, double *__restrict__ y) {
+    if (!has) return;
+    if (MODE == kSpmvResid || MODE == kSpmvAdd) y[row] = yv;
+    else __builtin_nontemporal_store(yv, y + row);
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void spmv_kernel(
     int64_t n, int trows, const int32_t *__restrict__ rowptr, const int32_t *__restrict__ colidx,
@@ -136,21 +154,11 @@ __global__ __launch_bounds__(kBlock) void spmv_kernel(
             for (int32_t e = a; e < bnd; ++e) sum = sum + prod[e - c0];
         __syncthreads();
     }
-    double acc = 0.0;
-    if (has) {
-        if (MODE == kSpmvResid) {
-            const double r = eq - sum;   // b - A*x (GMRESSolver.py:163)
-            y[row] = r;
-            acc = r * r;
-        } else if (MODE == kSpmvAdd) {
-            y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
-        } else {
-            __builtin_nontemporal_store(sum, y + row);
-            if (MODE != kSpmvPlain) acc = eq * sum;   // x.(Ax) or q.(Ax)
-        }
-    }
+    double acc;
+    const double yv = spmv_row_value<MODE>(has, sum, eq, acc);
     // only the residual mode may be called without partials (AMG smoothing); kernel-uniform test
     if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
+    spmv_store_row<MODE>(has, row, yv, y);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -240,25 +248,6 @@ __device__ __forceinline__ DictRegs load_dict(const double *__restrict__ sdict) 
         dv.d7 = sdict[7];
     }
     return dv;
-}
-
-// y[row] (and the dot partial of the mode) from the row's sum
-template <int MODE>
-__device__ __forceinline__ double spmv_finish_row(bool has, int64_t row, double sum, double eq, double *__restrict__ y) {
-    double acc = 0.0;
-    if (has) {
-        if (MODE == kSpmvResid) {
-            const double r = eq - sum;   // b - A*x (GMRESSolver.py:163)
-            y[row] = r;
-            acc = r * r;
-        } else if (MODE == kSpmvAdd) {
-            y[row] = eq + sum;           // x + P*x2 (VCycleManager.py:55)
-        } else {
-            __builtin_nontemporal_store(sum, y + row);
-            if (MODE != kSpmvPlain) acc = eq * sum;   // x.(Ax) or q.(Ax)
-        }
-    }
-    return acc;
 }
 
 // x[row] for the PCG dot p.Ap (kSpmvDot): the gathered value of the row's diagonal slot when it
@@ -361,8 +350,10 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_kernel(
     for (int j = 0; j < UW; ++j)
         if (cc[j] >= 0) sum = sum + vv[j] * xv[j];   // stored order, rounded product
     if (MODE == kSpmvDot) eq = diag_x<UW>(cc, xv, row32, x, has);
-    const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
+    double acc;
+    const double yv = spmv_row_value<MODE>(has, sum, eq, acc);
     if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
+    spmv_store_row<MODE>(has, row, yv, y);
 }
 
 // The dot epilogue of a workgroup holding TPW gridsum tiles: first every tile's slot is combined in LDS
@@ -387,8 +378,14 @@ __device__ __forceinline__ void spmv_publish_multi(const GridSum &gs, GridSumTil
         uint32_t old = 0;
         if (lane0) {
             L[q].part[wave] = ws;
+#ifndef PSK_LAB_EARLY_TICKET
             if (threadIdx.x == 0) L[q].ticket = ticket[q];
+#endif
+#ifdef PSK_LAB_NOFENCE
+            __asm__ volatile("" ::: "memory");   // LDS operations of one wave execute in order
+#else
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+#endif
             old = atomicAdd(&L[q].cnt, 1u);
         }
         if (__builtin_amdgcn_readfirstlane(old) != kWaves - 1) continue;
@@ -509,7 +506,7 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
         }
     }
     int32_t cc[TPW][UW];
-    double xv[TPW][UW], acc[TPW];
+    double xv[TPW][UW], acc[TPW], yv[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int32_t row32 = (int32_t)(tl[q] * kSlice + tid);
@@ -521,6 +518,14 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
             if (MODE == kSpmvJacobiDot) xv[q][j] = aux_d[cl] * xv[q][j];
         }
     }
+#ifdef PSK_LAB_EARLY_TICKET
+    // the tickets' returns consumed here, once the gathers are issued (they return before the gathers):
+    // the epilogue after the y stores then needs no wait on VMEM (a wait for a returning atomic issued
+    // before the stores was a vmcnt(0) that also waited for the stores)
+    if (pub && tid == 0)
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) gsl[q].ticket = ticket[q];
+#endif
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t row = tl[q] * kSlice + tid;
@@ -535,9 +540,15 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
         for (int j = 0; j < UW; ++j)
             if (cc[q][j] >= 0) sum = sum + vv[q][j] * xv[q][j];   // stored order, rounded product
         if (MODE == kSpmvDot) eq[q] = diag_x<UW>(cc[q], xv[q], (int32_t)row, x, has);
-        acc[q] = spmv_finish_row<MODE>(has, row, sum, eq[q], y);
+        // y stored after the dot epilogue (spmv_row_value)
+        yv[q] = spmv_row_value<MODE>(has, sum, eq[q], acc[q]);
     }
     if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
+    }
 }
 
 // General sliced layout (per-slice widths, offsets and formats loaded from the slice header).
@@ -646,8 +657,10 @@ __global__ __launch_bounds__(kBlock) void spmv_sliced_kernel(
             sum = sum + v * xx;
         }
     }
-    const double acc = spmv_finish_row<MODE>(has, row, sum, eq, y);
+    double acc;
+    const double yv = spmv_row_value<MODE>(has, sum, eq, acc);
     if (spmv_publishes<MODE>(gs)) spmv_publish(gs, gsl, acc, ticket, t);
+    spmv_store_row<MODE>(has, row, yv, y);
 }
 
 // per slice: widest row, and the largest |column - row| of its entries (saturated to int32)
