@@ -1115,16 +1115,22 @@ struct GridRec {
 #define PSK_GRID_MARKSTEIN 1
 #endif
 // Exactness needs 1/d, r/d and the remainder normal: the host keeps the dictionary only for
-// diagonals 2^-100 <= |d| <= 2^100, and a right-hand side outside [2^-900, 2^900] (or not finite)
-// takes the IEEE division (a lane-divergent branch that no stencil solve takes;
-// tools/markstein_check.c covers both ends of the range and the zero/subnormal edges).
+// diagonals 2^-100 <= |d| <= 2^100, and a non-zero right-hand side outside [2^-900, 2^901) (biased
+// exponent outside [123, 1923]: subnormal, huge, not finite) takes the IEEE division
+// (tools/markstein_check.c covers both ends of the range and the zero/subnormal edges). The range test
+// is integer work on r's exponent beside the correction chain and its branch is wave-uniform (a
+// ballot, never taken by a stencil solve): the chain itself is the 5 fmas and a select. (A per-lane
+// branch on floating-point compares of |r| ahead of the chain cost 4.3 -> 5.0 ms per 8192^2 sweep.)
 __device__ __forceinline__ double div_markstein(double r, double d, double rd) {
     const double q0 = r * rd;
     const double q1 = fma(fma(-q0, d, r), rd, q0);
     const double q2 = fma(fma(-q1, d, r), rd, q1);
-    const double ar = fabs(r);
-    if (!(ar >= 0x1p-900 && ar <= 0x1p+900) && r != 0.0) return r / d;
-    return r == 0.0 ? q0 : q2;
+    const uint32_t hi = (uint32_t)__double2hiint(r), e = (hi >> 20) & 0x7ffu;
+    const bool zero = ((hi << 1) | (uint32_t)__double2loint(r)) == 0u;
+    const bool out = e - 123u > 1800u && !zero;
+    double q = zero ? q0 : q2;
+    if (__builtin_amdgcn_ballot_w64(out) != 0) q = out ? r / d : q;
+    return q;
 }
 // Buffer (bounds-checked) access for the solver wave's rhs loads and x stores: an out-of-range
 // offset loads 0 / drops the store in hardware, so every lane issues every load and store with no
@@ -1149,8 +1155,8 @@ __device__ __forceinline__ void grid_bstore(__amdgpu_buffer_rsrc_t r, uint32_t o
 
 template <int K, int D, bool DICT>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
-    int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t S_full, int upper, int pe, int maxyd, int ring_mask,
-    int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
+    int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t off, int64_t S_full, int upper, int pe, int maxyd,
+    int ring_mask, int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
     GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict) {
     extern __shared__ __align__(16) unsigned char smem[];
     const int RW = maxyd + kGridLanes;
@@ -1208,8 +1214,8 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             }
             uint32_t pending = 0;   // lines of this lane's u still to fetch
             for (int L = 0; L < maxyd; ++L) {
-                const int64_t yl = y0 - maxyd + L, xl = u - sigma * yl, q = yl * w + xl;
-                const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q < n;
+                const int64_t yl = y0 - maxyd + L, xl = u - sigma * yl, q = yl * w + xl - off;
+                const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q >= 0 && q < n;
                 if (valid) pending |= 1u << L;
                 else row_slot[L] = 0.0;
             }
@@ -1217,7 +1223,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             while (true) {
                 for (int L = 0; L < maxyd; ++L)
                     if (pending & (1u << L)) {
-                        const int64_t yl = y0 - maxyd + L, q = yl * w + (u - sigma * yl);
+                        const int64_t yl = y0 - maxyd + L, q = yl * w + (u - sigma * yl) - off;
                         const double v = load_pub(x + (upper ? n - 1 - q : q));
                         if (!is_sentinel(v)) {
                             row_slot[L] = v;
@@ -1239,11 +1245,15 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     }
     // ---------------- solver
     const int64_t y = y0 + j;
-    // lane j's line is active for steps [s_beg, s_end): x = s - sigma*j in [0, w_eff)
-    const int64_t w_eff = y < H ? (n - y * w < w ? n - y * w : w) : 0;
-    const int s_beg = (int)(sigma * j), s_end = (int)(sigma * j + (w_eff > 0 ? w_eff : 0));
-    // row of step s: rbase + rstep * s, q = y*w + s - sigma*j
-    const int64_t qb = y * w - sigma * j;
+    // lane j's line holds grid positions [y*w, y*w + w) of [off, n + off) (the first `off` positions of
+    // the first line are empty: a partial line leading the solve order); it is active for steps
+    // [s_beg, s_end): x = s - sigma*j in [x_lo, x_hi)
+    const int64_t x_lo = y * w < off ? off - y * w : 0;
+    const int64_t x_hi = n + off - y * w < w ? n + off - y * w : w;
+    const bool live = y < H && x_hi > x_lo;
+    const int s_beg = (int)(sigma * j + (live ? x_lo : 0)), s_end = live ? (int)(sigma * j + x_hi) : s_beg;
+    // row of step s: rbase + rstep * s, q = y*w + s - sigma*j - off
+    const int64_t qb = y * w - sigma * j - off;
     const int64_t rbase = upper ? n - 1 - qb : qb;
     const int64_t rstep = upper ? -1 : 1;
     const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
@@ -1256,7 +1266,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         if (DICT) {
             sl.code[0] = pidx[(int64_t)sc * kGridLanes];   // the record index
             const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);
-            sl.b = grid_bload(rrhs, w_eff > 0 ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
+            sl.b = grid_bload(rrhs, live ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
             return;
         }
         const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
@@ -1283,7 +1293,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         }
         sl.d = reinterpret_cast<const double *>(st + GridStep<K>::kDiag)[j];
         const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);   // clamped into the line
-        sl.b = grid_bload(rrhs, w_eff > 0 ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
+        sl.b = grid_bload(rrhs, live ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
     };
     auto lookup = [&](uint32_t idx, GridRec<K> &rc) {   // DICT: the record of a step, from LDS
 #pragma unroll
@@ -1510,7 +1520,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         else if (T.grid_K == 8) PSK_GRID_K(8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D));
 #undef PSK_GRID_K
         if (!k) return fail(PSK_ERR_ARG, "grid schedule: bad record width");
-        int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, sfull = T.grid_S;
+        int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, goff = T.grid_off, sfull = T.grid_S;
         int upper = T.upper ? 1 : 0, pe_ = T.grid_pe, myd = T.grid_maxyd, mask = T.grid_ring - 1;
         int unit = T.diag ? 0 : 1;
         const double *gr = T.gd_coef;
@@ -1518,8 +1528,8 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const uint32_t *gi = T.gd_idx;
         const double *gdd = T.gd_dict;
         int nd = T.grid_dict_n;
-        void *args[] = {&nn, &w, &H, &sg, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr, &ext,
-                        &gi, &gdd, &nd};
+        void *args[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr,
+                        &ext, &gi, &gdd, &nd};
         const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
         PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args,
                                 grid_lds_bytes(T.grid_ring, T.grid_maxyd, T.grid_K, T.grid_dict_n), s));
@@ -1872,7 +1882,7 @@ constexpr int64_t kGridMaxYd = 8;   // lines of the band above held in the polle
 
 struct GridPlan {
     bool ok = false;
-    int64_t w = 0, H = 0, sigma = 0;
+    int64_t w = 0, H = 0, sigma = 0, off = 0;
     int K = 0, pe = 0, maxyd = 0, ring = 0;
     GridExt ext{};
     double est = -1.0;
@@ -1897,48 +1907,64 @@ void plan_grid(const HostFactor &F, GridPlan &g) {
         }
     }
     if (kmax == 0 || kmax > 8) return;
-    int64_t w = 0, best = 0;
-    for (const auto &kv : hist)
-        if (kv.second > best || (kv.second == best && kv.first < w)) {
-            w = kv.first;
-            best = kv.second;
-        }
-    if (w < 2 || best * 7 * 8 < n) return;   // at least ~1/8 of the rows hold a distance-w entry
-    // patterns and skew
-    int64_t sigma = 0;
-    int64_t maxyd = 0;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t p = F.pos(i), y = p / w, x = p % w;
-        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
-            const int64_t pd = F.pos(F.ci[j]), yd = y - pd / w, xd = x - pd % w;
-            if (yd > kGridMaxYd) return;
-            maxyd = std::max(maxyd, yd);
-            if (yd >= 1 && xd < 1) sigma = std::max(sigma, (1 - xd + yd - 1) / yd);
-        }
-    }
-    if (sigma > 8) return;
-    int64_t maxud = 0;
+    // line-length candidates: the most frequent distances (a 9-point stencil ties w - 1, w and w + 1),
+    // each holding at least ~1/8 of the rows; the first one that plans is taken
+    std::vector<std::pair<int64_t, int64_t>> cand(hist.begin(), hist.end());   // (distance, count)
+    std::sort(cand.begin(), cand.end(), [](const std::pair<int64_t, int64_t> &a, const std::pair<int64_t, int64_t> &b) {
+        return a.second != b.second ? a.second > b.second : a.first < b.first;
+    });
+    int64_t w = 0;
+    // patterns and skew, with grid position p + off: off = 0, or the offset that makes the solve order
+    // START with a partial line (w - n mod w empty positions before it: an upper factor of a grid whose
+    // last natural line is short, e.g. SA level 2 of -FD 8192^2, 1365 lines of 911 + one of 228)
+    int64_t sigma = 0, maxyd = 0, maxud = 0, off = 0;
     std::vector<int32_t> ext_codes;
-    for (int64_t i = 0; i < n; ++i) {
-        const int64_t p = F.pos(i), y = p / w, x = p % w;
-        for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
-            const int64_t pd = F.pos(F.ci[j]), yd = y - pd / w, xd = x - pd % w, ud = xd + sigma * yd;
-            if (ud < 1 || ud >= 1023) return;
-            maxud = std::max(maxud, ud);
-            const int32_t code = (int32_t)(ud * 64 + yd);
-            if (yd >= 1 && std::find(ext_codes.begin(), ext_codes.end(), code) == ext_codes.end()) {
-                if ((int)ext_codes.size() == kGridMaxPE) return;
-                ext_codes.push_back(code);
+    auto try_off = [&](int64_t o) -> bool {
+        sigma = 0;
+        maxyd = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t p = F.pos(i) + o, y = p / w, x = p % w;
+            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+                const int64_t pd = F.pos(F.ci[j]) + o, yd = y - pd / w, xd = x - pd % w;
+                if (yd > kGridMaxYd) return false;
+                maxyd = std::max(maxyd, yd);
+                if (yd >= 1 && xd < 1) sigma = std::max(sigma, (1 - xd + yd - 1) / yd);
             }
         }
+        if (sigma > 8) return false;
+        maxud = 0;
+        ext_codes.clear();
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t p = F.pos(i) + o, y = p / w, x = p % w;
+            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+                const int64_t pd = F.pos(F.ci[j]) + o, yd = y - pd / w, xd = x - pd % w, ud = xd + sigma * yd;
+                if (ud < 1 || ud >= 1023) return false;
+                maxud = std::max(maxud, ud);
+                const int32_t code = (int32_t)(ud * 64 + yd);
+                if (yd >= 1 && std::find(ext_codes.begin(), ext_codes.end(), code) == ext_codes.end()) {
+                    if ((int)ext_codes.size() == kGridMaxPE) return false;
+                    ext_codes.push_back(code);
+                }
+            }
+        }
+        off = o;
+        return true;
+    };
+    bool planned = false;
+    for (size_t ci = 0; ci < cand.size() && ci < 4 && !planned; ++ci) {
+        w = cand[ci].first;
+        if (w < 2 || cand[ci].second * 7 * 8 < n) break;
+        planned = try_off(0) || (n % w != 0 && try_off(w - n % w));
     }
+    if (!planned) return;
     // ring rows: the deepest dependency, and room for the poller to stay a 64-position chunk ahead
     int ring = ext_codes.empty() ? 1 : 2 * kGridLanes;
     while (ring < maxud + 1 + (ext_codes.empty() ? 0 : kGridLanes)) ring <<= 1;
     if (ring > kGridMaxRing) return;
     g.ok = true;
     g.w = w;
-    g.H = (n + w - 1) / w;
+    g.off = off;
+    g.H = (n + off + w - 1) / w;
     g.sigma = sigma;
     g.K = kmax <= 2 ? 2 : (kmax <= 4 ? 4 : 8);
     g.pe = (int)ext_codes.size();
@@ -2161,8 +2187,9 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         T.grid_w = gp.w;
         T.grid_H = gp.H;
         T.grid_sigma = gp.sigma;
+        T.grid_off = gp.off;
         T.grid_ext = gp.ext;
-        // position p = (y*w + x): band b = y / 64, lane y % 64, step u - sigma*64b with u = x + sigma*y;
+        // grid position p + off = (y*w + x): band b = y / 64, lane y % 64, step u - sigma*64b with u = x + sigma*y;
         // one GridStep block per (band, step): codes (ud*64 + yd), values in stored order, diagonal.
         // Padding: value 0, code 0 (the lane's own column of the current row); empty lanes: diagonal 1
         // so the wave's unused results stay finite (padding entries read them times 0.0)
@@ -2175,14 +2202,14 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         for (int64_t t = 0; t < nsteps; ++t)
             for (int l = 0; l < kGridLanes; ++l) reinterpret_cast<double *>(gb + t * SB + od)[l] = 1.0;
         for (int64_t i = 0; i < n; ++i) {
-            const int64_t p = F.pos(i), y = p / gp.w, x = p % gp.w, b = y / kGridLanes, l = y % kGridLanes;
+            const int64_t p = F.pos(i) + gp.off, y = p / gp.w, x = p % gp.w, b = y / kGridLanes, l = y % kGridLanes;
             const int64_t st = x + gp.sigma * y - gp.sigma * kGridLanes * b;
             unsigned char *blk = gb + (b * T.grid_S + st) * SB;
             uint16_t *codes = reinterpret_cast<uint16_t *>(blk) + l * gp.K;
             double *vals = reinterpret_cast<double *>(blk + oc) + l * gp.K;
             int k = 0;
             for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j, ++k) {
-                const int64_t pd = F.pos(F.ci[j]), yd = y - pd / gp.w, xd = x - pd % gp.w;
+                const int64_t pd = F.pos(F.ci[j]) + gp.off, yd = y - pd / gp.w, xd = x - pd % gp.w;
                 codes[k] = (uint16_t)((xd + gp.sigma * yd) * 64 + yd);
                 vals[k] = ova[j];
             }

@@ -236,6 +236,7 @@ struct TriFactor {
     int grid_dict_n = 0;
     int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
     int64_t grid_w = 0, grid_H = 0, grid_sigma = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
+    int64_t grid_off = 0;   // empty grid positions before the first row (a partial first line)
     GridExt grid_ext{};
     // part layout: position k = part_seg[w] + q (workgroup w's q-th row); rows, entries (codes) in it
     int64_t *part_seg = nullptr;

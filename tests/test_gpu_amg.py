@@ -309,3 +309,38 @@ def test_grid_record_dictionary_bitwise(psk, monkeypatch, m, lower):
     assert np.array_equal(outs[0], outs[1])
     ref = spla.spsolve_triangular(T, v, lower=lower)
     assert _rel(outs[0], ref) <= 1e-12
+
+
+@pytest.mark.parametrize("lower", [False, True])
+def test_grid_schedule_partial_line(psk, lower):
+    """A 9-point stencil on lines of w = 300 whose LAST natural line is partial (n = 300*180 + 77): the
+    upper factor's solve order then STARTS with the partial line (the shape of SA level 2 of -FD
+    8192^2: 1365 lines of 911 after one of 228), which the grid schedule takes with a leading offset
+    of w - n mod w empty positions; the lower factor ends with it. Within 1e-12 of
+    spsolve_triangular and bit-identical to the band schedule."""
+    from pysolvers_amd.Linear import TriangularSolveChain
+    w, n = 300, 300 * 180 + 77
+    q = np.arange(n)
+    y, x = q // w, q % w
+    rows, cols = [], []
+    for dy in (-1, 0, 1):
+        for dx in (-1, 0, 1):
+            if dy == 0 and dx == 0:
+                continue
+            yy, xx = y + dy, x + dx
+            ok = (xx >= 0) & (xx < w) & (yy >= 0) & (yy * w + xx < n)
+            rows.append(q[ok])
+            cols.append((yy * w + xx)[ok])
+    rows, cols = np.concatenate(rows), np.concatenate(cols)
+    A = sp.csr_matrix((np.full(len(rows), -1.0), (rows, cols)), shape=(n, n)) + sp.diags(np.full(n, 8.5))
+    T = (sp.tril(A) if lower else sp.triu(A)).tocsr()
+    v = np.random.default_rng(5).standard_normal(n)
+    ref = spla.spsolve_triangular(T, v, lower=lower)
+    f = "L" if lower else "U"
+    M = TriangularSolveChain(n, **({"L": T} if lower else {"U": T}))
+    assert _grid_available(M, f)
+    g = M.apply(v)
+    assert _rel(g, ref) <= 1e-12
+    assert np.array_equal(M.apply(v), g)
+    M.schedule(f, set="band")
+    assert np.array_equal(M.apply(v), g)
