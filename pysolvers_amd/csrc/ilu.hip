@@ -407,11 +407,15 @@ extern "C" int psk_part_prof_read(unsigned long long *out) {
     unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     return hipMemcpyToSymbol(HIP_SYMBOL(g_part_prof), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
-// per-position stamps (s_memtime) of the first 2^17 positions: [2k] dependencies resolved, [2k+1] result stored
-__device__ unsigned long long g_part_trace[2 << 17];
+// per-position phase stamps (clock64) of the first 2^17 positions, 8 words each: [0] the row's turn
+// (its wave's pipeline loads for later rows issued), [1] local (LDS) dependencies read, [2] every
+// entry's x value in and the lane partial summed (remote polls included), [3] row total (DPP),
+// [4] quotient, [5] x and the LDS cache written (issued); [6] 1 if the spin waited, [7] spins
+constexpr int kPartTraceWords = 8;
+__device__ unsigned long long g_part_trace[kPartTraceWords << 17];
 extern "C" int psk_part_trace_read(unsigned long long *out, int64_t n) {
     if (n > (1 << 17)) n = 1 << 17;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_part_trace), (size_t)n * 16) == hipSuccess ? 0 : -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_part_trace), (size_t)n * 8 * kPartTraceWords) == hipSuccess ? 0 : -1;
 }
 #define PART_PROF(...) __VA_ARGS__
 #else
@@ -527,6 +531,7 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
             head(q + 5 * W, H[(t + 1) & 3]);         // row u+5
             const PtBody &cur = B[t];
             const uint64_t *pc = P[t & 1];
+            PART_PROF(const unsigned long long ph0 = clock64(); unsigned long long nspin = 0;)
             // x values of the row's register chunks: remote ones from the early polls, local ones from
             // the LDS cache, polled by the whole wave until every local entry is present (the spin's
             // control flow is uniform); reused slots and unpublished remote values then wait on x
@@ -563,13 +568,15 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
                     if (lane == 0) atomicExch(err, 2);
                     break;
                 }
-                PART_PROF(waited = true;)
+                PART_PROF(waited = true; ++nspin;)
 #ifndef PSK_PART_SLEEP
 #define PSK_PART_SLEEP 1
 #endif
                 __builtin_amdgcn_s_sleep(PSK_PART_SLEEP);
             }
-            PART_PROF(if (waited) { plw += clock64() - w0; pnl++; })
+            PART_PROF(if (waited) { plw += clock64() - w0; pnl++; }
+                      for (int j = 0; j < kPtChunks; ++j) __asm__ volatile("" ::"v"(xv[j]));
+                      const unsigned long long ph1 = clock64();)
             double acc = 0.0;
 #pragma unroll
             for (int j = 0; j < kPtChunks; ++j) {
@@ -607,11 +614,13 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
                         acc = fma(tv[u], resolve(c, bt, a1, vv, a2), acc);
                     }
             }
-            PART_PROF(const unsigned long long tr0 = clock64();)
+            PART_PROF(__asm__ volatile("" ::"v"(acc)); const unsigned long long ph2 = clock64();)
             const double sum = row_total(acc);
+            PART_PROF(__asm__ volatile("" ::"v"(sum)); const unsigned long long ph3 = clock64();)
             if (lane == 0) {
                 double r = cur.b - sum;
                 if (!UNIT) r = r / cur.d;
+                PART_PROF(__asm__ volatile("" ::"v"(r)); const unsigned long long ph4 = clock64();)
                 store_pub(x + cur.row, r);
                 const int32_t slot = (int32_t)(q & (kPartSlots - 1));
                 __hip_atomic_store(st + slot, kPartWriting, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -619,8 +628,16 @@ __global__ __launch_bounds__(kPartThreads) void sptrsv_part_kernel(
                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_store(st + slot, (int32_t)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 PART_PROF(if (base + q < (1 << 17)) {
-                    g_part_trace[2 * (base + q)] = tr0;
-                    g_part_trace[2 * (base + q) + 1] = clock64();
+                    const unsigned long long ph5 = clock64();
+                    unsigned long long *tr = g_part_trace + kPartTraceWords * (base + q);
+                    tr[0] = ph0;
+                    tr[1] = ph1;
+                    tr[2] = ph2;
+                    tr[3] = ph3;
+                    tr[4] = ph4;
+                    tr[5] = ph5;
+                    tr[6] = waited ? 1 : 0;
+                    tr[7] = nspin;
                 })
             }
         }
@@ -1111,26 +1128,25 @@ struct GridRec {
 // correctly rounded, a correction from any q within one ulp of r/d returns RN(r/d), and q0 is within
 // 1.5 ulp, so the second correction returns the IEEE quotient; r = +-0 keeps q0 (the signed zero).
 // tools/markstein_check.c: 0 mismatches against r / d in 2e8 random pairs after ONE correction.
-#ifndef PSK_GRID_MARKSTEIN
-#define PSK_GRID_MARKSTEIN 1
-#endif
 // Exactness needs 1/d, r/d and the remainder normal: the host keeps the dictionary only for
-// diagonals 2^-100 <= |d| <= 2^100, and a non-zero right-hand side outside [2^-900, 2^901) (biased
-// exponent outside [123, 1923]: subnormal, huge, not finite) takes the IEEE division
-// (tools/markstein_check.c covers both ends of the range and the zero/subnormal edges). The range test
-// is integer work on r's exponent beside the correction chain and its branch is wave-uniform (a
-// ballot, never taken by a stencil solve): the chain itself is the 5 fmas and a select. (A per-lane
-// branch on floating-point compares of |r| ahead of the chain cost 4.3 -> 5.0 ms per 8192^2 sweep.)
-__device__ __forceinline__ double div_markstein(double r, double d, double rd) {
+// diagonals 2^-100 <= |d| <= 2^100, and a right-hand side r must be zero or inside [2^-900, 2^901)
+// (biased exponent in [123, 1923]; tools/markstein_check.c covers both ends of the range and the
+// zero/subnormal/infinite edges). The range test is NOT on the dependency chain: each lane ORs it into
+// a flag (integer work on r's exponent beside the correction chain), the launch reports it at its end,
+// and a conditional pass re-solves the factor with the IEEE division when any step was out of range
+// (never, for a stencil solve) — the result is then that pass's, bit for bit the IEEE one. (A
+// per-step branch around the IEEE division, round 4's first guard, put 22 instructions and two
+// branches on every step: +13% per sweep.)
+// The test: frexp's exponent (r = f 2^ex, 0.5 <= |f| < 1; 0 for zero, inf and NaN) in [-899, 901],
+// and r not inf / NaN (a class test) — two VALU compares beside the chain, OR-ed into a scalar mask.
+__device__ __forceinline__ double div_markstein(double r, double d, double rd, uint64_t &out_of_range) {
     const double q0 = r * rd;
     const double q1 = fma(fma(-q0, d, r), rd, q0);
     const double q2 = fma(fma(-q1, d, r), rd, q1);
-    const uint32_t hi = (uint32_t)__double2hiint(r), e = (hi >> 20) & 0x7ffu;
-    const bool zero = ((hi << 1) | (uint32_t)__double2loint(r)) == 0u;
-    const bool out = e - 123u > 1800u && !zero;
-    double q = zero ? q0 : q2;
-    if (__builtin_amdgcn_ballot_w64(out) != 0) q = out ? r / d : q;
-    return q;
+    const int ex = __builtin_amdgcn_frexp_exp(r);
+    out_of_range |= __builtin_amdgcn_ballot_w64((uint32_t)(ex + 899) > 1800u);
+    out_of_range |= __builtin_amdgcn_ballot_w64(__builtin_amdgcn_class(r, 0x207));   // s/qNaN, -inf, +inf
+    return r == 0.0 ? q0 : q2;
 }
 // Buffer (bounds-checked) access for the solver wave's rhs loads and x stores: an out-of-range
 // offset loads 0 / drops the store in hardware, so every lane issues every load and store with no
@@ -1153,11 +1169,15 @@ __device__ __forceinline__ void grid_bstore(__amdgpu_buffer_rsrc_t r, uint32_t o
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(grid_u2, v), r, off, 0, CPOL);
 }
 
-template <int K, int D, bool DICT>
+// MK (DICT only): Markstein quotient, range flag OR-ed into *rflag at the end (see div_markstein); !MK:
+// IEEE division. gate != nullptr: the conditional re-solve, a no-op unless *gate is set.
+template <int K, int D, bool DICT, bool MK>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t off, int64_t S_full, int upper, int pe, int maxyd,
     int ring_mask, int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
-    GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict) {
+    GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict, int32_t *rflag,
+    const int32_t *gate) {
+    if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;   // uniform
     extern __shared__ __align__(16) unsigned char smem[];
     const int RW = maxyd + kGridLanes;
     double *ring = reinterpret_cast<double *>(smem);                  // [ring][RW]
@@ -1261,6 +1281,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int64_t ext_known = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;   // uniform
     const uint32_t *pidx = gidx + (int64_t)blockIdx.x * S_full * kGridLanes + j;
     const __amdgpu_buffer_rsrc_t rrhs = grid_rsrc(rhs, n), rx = grid_rsrc(x, n);
+    uint64_t rbad = 0;   // MK: lanes with a step's right-hand side outside the Markstein range (div_markstein)
     auto fetch = [&](int s, GridSlot<K> &sl) {
         const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
         if (DICT) {
@@ -1359,7 +1380,12 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
 #pragma unroll
         for (int k = 0; k < K; ++k) acc = fma(sl.cf[k], v[k], acc);   // stored order; padding adds +-0
         double r = sl.b - acc;
-        if (!unit) r = (DICT && PSK_GRID_MARKSTEIN) ? div_markstein(r, sl.d, rd) : r / sl.d;
+        if (DICT && MK) {   // a select, not a branch, on `unit` (the chain stays branch-free)
+            const double q = div_markstein(r, sl.d, rd, rbad);
+            r = unit ? r : q;
+        } else if (!unit) {
+            r = r / sl.d;
+        }
 #ifdef PSK_GRID_PROF
         __asm__ volatile("" ::"v"(r));
         const unsigned long long p3 = __builtin_amdgcn_s_memtime();
@@ -1402,6 +1428,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             __hip_atomic_store(&ctl[1], u_lo + s0 + D - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     if (j == 0) __hip_atomic_store(&ctl[1], INT64_MAX / 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (MK && !unit && rbad != 0 && j == 0) atomicOr(rflag, 1);
 #ifdef PSK_GRID_PROF
     if (j == 0 && blockIdx.x < 8192) {
         g_grid_prof[blockIdx.x * 8 + 0] = t_start;
@@ -1415,6 +1442,21 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     }
 #endif
 }
+
+// x = sentinel on the rows the grid schedule publishes — lines y with y mod 64 >= 64 - maxyd, the ones
+// the band below polls (every other row is read only after the launch): maxyd/64 of the vector instead
+// of all of it. gate != nullptr: only when *gate is set (before the conditional re-solve).
+__global__ void grid_fill_published_kernel(int64_t n, int64_t w, int64_t H, int64_t off, int maxyd, int upper,
+                                           double *x, const int32_t *gate) {
+    if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
+    const int64_t total = ((H + kGridLanes - 1) / kGridLanes) * maxyd * w;
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t li = t / w, xx = t - li * w;
+        const int64_t y = (li / maxyd) * kGridLanes + (kGridLanes - maxyd) + li % maxyd, q = y * w + xx - off;
+        if (y < H && q >= 0 && q < n) reinterpret_cast<uint64_t *>(x)[upper ? n - 1 - q : q] = kSentinel;
+    }
+}
+__global__ void grid_flag_reset_kernel(int32_t *flag) { *flag = 0; }
 
 static size_t grid_lds_bytes(int ring, int maxyd, int K = 0, int ndict = 0) {
     return (size_t)ring * (kGridLanes + maxyd) * sizeof(double) + 2 * sizeof(int64_t) +
@@ -1471,6 +1513,25 @@ static int syncfree_grid(const Context *c) {
     return c->num_cus * per_cu;
 }
 
+static unsigned grid_fill_blocks(const TriFactor &T) {
+    const int64_t total = ((T.grid_H + kGridLanes - 1) / kGridLanes) * T.grid_maxyd * T.grid_w;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((total + kBlock - 1) / kBlock, 4096));
+}
+
+// the output of one factor before its solve: the sentinel where the schedule's waits read it (the grid
+// schedule: only its published lines; every other schedule: every row)
+static int fill_factor_output(const TriFactor &T, int64_t n, double *x, hipStream_t s) {
+    if (T.schedule == kSchedGrid) {
+        if (T.grid_pe == 0 || T.grid_maxyd == 0) return PSK_OK;   // no band waits on another
+        hipLaunchKernelGGL(grid_fill_published_kernel, dim3(grid_fill_blocks(T)), dim3(kBlock), 0, s, n, T.grid_w,
+                           T.grid_H, T.grid_off, T.grid_maxyd, T.upper ? 1 : 0, x, nullptr);
+    } else {
+        hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, x);
+    }
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
 // x = T^-1 rhs[rhs_idx] for one factor, with the factor's schedule
 static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const double *rhs, const int32_t *rhs_idx,
                          double *x, int32_t *err, hipStream_t s) {
@@ -1504,7 +1565,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
     }
     if (T.schedule == kSchedGrid) {
         if (rhs_idx) return fail(PSK_ERR_ARG, "grid schedule: gathered right-hand side (internal)");
-        const void *k = nullptr;
+        const void *k = nullptr, *kf = nullptr;
 #ifndef PSK_GRID_D
 #define PSK_GRID_D 12
 #endif
@@ -1513,8 +1574,11 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
 #endif
         const bool dict = T.grid_dict_n > 0;
 #define PSK_GRID_K(KK, DN)                                                                                    \
-    k = dict ? reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, PSK_GRID_DD, true>)                      \
-             : reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DN, false>)
+    do {                                                                                                      \
+        k = dict ? reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, PSK_GRID_DD, true, true>)            \
+                 : reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, DN, false, false>);                  \
+        kf = reinterpret_cast<const void *>(&sptrsv_grid_kernel<KK, PSK_GRID_DD, true, false>);                \
+    } while (0)
         if (T.grid_K == 2) PSK_GRID_K(2, PSK_GRID_D);
         else if (T.grid_K == 4) PSK_GRID_K(4, (PSK_GRID_D > 8 ? 8 : PSK_GRID_D));
         else if (T.grid_K == 8) PSK_GRID_K(8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D));
@@ -1528,11 +1592,27 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const uint32_t *gi = T.gd_idx;
         const double *gdd = T.gd_dict;
         int nd = T.grid_dict_n;
+        int32_t *flag = dict ? T.grid_flag : nullptr;
+        const int32_t *nogate = nullptr;
         void *args[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr,
-                        &ext, &gi, &gdd, &nd};
+                        &ext, &gi, &gdd, &nd, &flag, &nogate};
         const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
-        PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args,
-                                grid_lds_bytes(T.grid_ring, T.grid_maxyd, T.grid_K, T.grid_dict_n), s));
+        const size_t lds = grid_lds_bytes(T.grid_ring, T.grid_maxyd, T.grid_K, T.grid_dict_n);
+        PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args, lds, s));
+        if (dict) {   // conditional IEEE re-solve (div_markstein): no-ops unless a step was out of range
+            const int32_t *gate = T.grid_flag;
+            int32_t *noflag = nullptr;
+            if (pe_ > 0 && myd > 0) {
+                hipLaunchKernelGGL(grid_fill_published_kernel, dim3(grid_fill_blocks(T)), dim3(kBlock), 0, s, nn, w,
+                                   H, goff, myd, upper, x, gate);
+                PSK_HIP(hipGetLastError());
+            }
+            void *fargs[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr,
+                             &ext, &gi, &gdd, &nd, &noflag, &gate};
+            PSK_HIP(hipLaunchKernel(kf, dim3(nb), dim3(2 * kGridLanes), fargs, lds, s));
+            hipLaunchKernelGGL(grid_flag_reset_kernel, dim3(1), dim3(1), 0, s, T.grid_flag);
+            PSK_HIP(hipGetLastError());
+        }
         return PSK_OK;
     }
     if (T.schedule == kSchedBand && T.band_narrow) {
@@ -1594,10 +1674,14 @@ static int ilu_apply_impl(const psk_prec *M, const double *v, double *out, bool 
     const unsigned fb = (unsigned)((n + kBlock - 1) / kBlock);
     double *y = M->work, *z = M->work + n;
     const int nbuf = (M->lo.present ? 1 : 0) + (M->up.present ? 1 : 0);
-    if (nbuf > 0) {
+    const bool grid_any = (M->lo.present && M->lo.schedule == kSchedGrid) || (M->up.present && M->up.schedule == kSchedGrid);
+    if (nbuf > 0 && !grid_any) {
         hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((nbuf * n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            s, nbuf * n, y);   // y and z are contiguous
         PSK_HIP(hipGetLastError());
+    } else if (nbuf > 0) {
+        if (M->lo.present) PSK_TRY(fill_factor_output(M->lo, n, y, s));
+        if (M->up.present) PSK_TRY(fill_factor_output(M->up, n, M->lo.present ? z : y, s));
     }
     const double *cur = v;                // current right-hand side
     const int32_t *cur_idx = M->gather_in;
@@ -1649,7 +1733,8 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
 
 void TriFactor::release() {
     void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,   rec_d,
-                    gd_code, gd_coef, gd_diag, gd_idx, gd_dict, part_seg, part_rp, part_code, part_row, part_va};
+                    gd_code, gd_coef, gd_diag, gd_idx, gd_dict, part_seg, part_rp, part_code, part_row, part_va,
+                    grid_flag};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -2344,6 +2429,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.gd_diag, gdiag);
     if (rc == PSK_OK) rc = upload(&T.gd_idx, gidx);
     if (rc == PSK_OK) rc = upload(&T.gd_dict, gdict);
+    if (rc == PSK_OK) rc = upload(&T.grid_flag, std::vector<int32_t>(T.grid_dict_n > 0 ? 1 : 0, 0));
     if (rc == PSK_OK) rc = upload(&T.part_seg, pseg);
     if (rc == PSK_OK) rc = upload(&T.part_rp, prp);
     if (rc == PSK_OK) rc = upload(&T.part_code, pcode);

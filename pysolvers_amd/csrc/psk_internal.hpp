@@ -234,6 +234,7 @@ struct TriFactor {
     uint32_t *gd_idx = nullptr;
     double *gd_dict = nullptr;
     int grid_dict_n = 0;
+    int32_t *grid_flag = nullptr;   // dictionary kernel: a step's quotient needed the IEEE re-solve (zeroed after it)
     int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
     int64_t grid_w = 0, grid_H = 0, grid_sigma = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
     int64_t grid_off = 0;   // empty grid positions before the first row (a partial first line)

@@ -35,3 +35,6 @@ for pc in default 2 4; do
   timeout -k 10 300 python -u tools/sf_probe.py 2896 >> $OUT/${TAG}_sf.jsonl 2>> $OUT/${TAG}_sf.err
   c=$?; echo "sf per_cu=$pc exit $c"; tail -1 $OUT/${TAG}_sf.jsonl; [ $c -eq 0 ] || exit $c
 done
+# partitioned kernel: per-phase stamps of an LDS hand-off chain (a -DPSK_PART_PROF build)
+PSK_LIBRARY=$PWD/tools/bin/ab_partprof/libpsk.so PART_MICRO_CASES=chain1 timeout -k 10 300 python -u tools/part_micro.py > $OUT/${TAG}_partmicro.json 2> $OUT/${TAG}_partmicro.err
+c=$?; echo "part_micro exit $c"; cat $OUT/${TAG}_partmicro.json; exit $c

@@ -344,3 +344,26 @@ def test_grid_schedule_partial_line(psk, lower):
     assert np.array_equal(M.apply(v), g)
     M.schedule(f, set="band")
     assert np.array_equal(M.apply(v), g)
+
+
+@pytest.mark.parametrize("scale", [1e-280, 1e280])
+def test_grid_markstein_range_fallback(psk, scale):
+    """The grid dictionary kernel divides by a Markstein correction from RN(1/d), exact while the
+    right-hand side stays in [2^-900, 2^901); a step outside it flags the launch and a conditional
+    pass re-solves with the IEEE division. A right-hand side scaled far outside the range must still
+    give the band schedule's (IEEE) bits, and the flag must be cleared for the next, in-range apply."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 300)
+    T = sp.triu(A).tocsr()
+    n = A.shape[0]
+    M = TriangularSolveChain(n, U=T)
+    assert _grid_available(M, "U")
+    v = np.random.default_rng(9).standard_normal(n)
+    vs = v * scale
+    g_small, g = M.apply(vs), M.apply(v)
+    M.schedule("U", set="band")
+    assert np.array_equal(M.apply(vs), g_small)
+    assert np.array_equal(M.apply(v), g)
+    ref = spla.spsolve_triangular(T, vs, lower=False)
+    assert np.all(np.isfinite(g_small)) and _rel(g_small / scale, ref / scale) <= 1e-12   # norms would under/overflow

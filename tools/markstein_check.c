@@ -25,10 +25,9 @@ static inline double mk2(double a, double b, double y) {   // div_markstein as t
     double q0 = a * y;
     double q1 = fma(fma(-q0, b, a), y, q0);
     double q2 = fma(fma(-q1, b, a), y, q1);
-    uint64_t bits;
-    memcpy(&bits, &a, 8);
-    const uint32_t e = (uint32_t)(bits >> 52) & 0x7ffu;
-    if (e - 123u > 1800u && (bits << 1) != 0) return a / b;   // |a| outside [2^-900, 2^901), not zero
+    int ex = 0;
+    if (isfinite(a)) frexp(a, &ex);                          // the kernel's frexp exponent: 0 for 0 / inf / NaN
+    if ((unsigned)(ex + 899) > 1800u || !isfinite(a)) return a / b;   // the conditional IEEE re-solve
     return a == 0.0 ? q0 : q2;
 }
 static inline int same(double u, double v) { return memcmp(&u, &v, 8) == 0 || (isnan(u) && isnan(v)); }

@@ -60,17 +60,25 @@ def main():
             M.schedule("L", set="part")
             M.apply(v)
             N.check(N.lib.psk_synchronize(), "sync")
-            tr = np.zeros(2 * n, np.uint64)
+            tr = np.zeros(8 * n, np.uint64)
             N.lib.psk_part_trace_read(tr.ctypes.data_as(ctypes.c_void_p), ctypes.c_int64(n))
-            t0, t1 = tr[0::2].astype(np.int64), tr[1::2].astype(np.int64)
-            # natural order == position order for these factors when strips are not permuted; use rows
-            # inside one strip (positions base..base+R) where consecutive rows are consecutive hops
+            ph = tr.reshape(n, 8).astype(np.int64)
+            # strip 0's positions (workgroup 0): in these factors position order is natural order, so
+            # consecutive positions of a chain1 strip are consecutive hops (row k needs row k-1)
             R = n // 256
             k = np.arange(1, R)
-            wg0 = np.arange(R)   # workgroup 0's positions (strip 0)
-            out["trace_compute_cycles_median"] = float(np.median(t1[wg0] - t0[wg0]))
-            out["trace_handoff_cycles_median"] = float(np.median(t0[k] - t1[k - 1]))
-            out["trace_row_period_cycles_median"] = float(np.median(t1[k] - t1[k - 1]))
+            prod_done, start = ph[k - 1, 5], ph[k, 0]
+            ready = np.maximum(start, prod_done)   # the consumer's turn AND the producer's value written
+            med = lambda a: float(np.median(a))
+            out["phases_cycles_median"] = {
+                "turn_after_producer": med(start - prod_done),       # < 0: the consumer waited for the value
+                "detect_lds": med(ph[k, 1] - ready),                  # value written -> seen by the spin
+                "values_and_fma": med(ph[k, 2] - ph[k, 1]),           # remote polls + fma chain
+                "row_total_dpp": med(ph[k, 3] - ph[k, 2]),
+                "quotient": med(ph[k, 4] - ph[k, 3]),
+                "publish_issue": med(ph[k, 5] - ph[k, 4]),
+                "hop_period": med(ph[k, 5] - ph[k - 1, 5]),
+                "spin_waited_frac": float(np.mean(ph[k, 6])), "spins_median": med(ph[k, 7])}
         print(json.dumps(out), flush=True)
 
 
