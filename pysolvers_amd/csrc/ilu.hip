@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
 // per dependency level. Per-row arithmetic is the band kernels': fma over the entries in stored
 // order from 0.0, then (b - acc) / diag, so results are bit-identical to the band schedule.
 constexpr int kGridLanes = 64;
-constexpr int kGridMaxRing = 256;   // rows of the LDS ring (<= 256 x 72 doubles)
+constexpr int kGridMaxRing = 128;   // ring rows the plan may ask for (the kernel's mirrored kGridRing)
 #ifdef PSK_GRID_PROF
 // development probe (tools/grid_probe.py): per band start / end s_memtime, waits and cycles waited
 // 8 words per band: start, end, waits on the band above, cycles waited, then the solver's cycles per
@@ -1093,34 +1093,46 @@ struct GridStep {
     static constexpr int64_t kBytes = kDiag + kGridLanes * 8;
 };
 
-template <int K>
-struct GridSlot {
-    uint32_t code[K / 2];   // two 16-bit pattern codes per word
-    double cf[K], d, b;
-};
-
 // Two waves per band. The SOLVER wave (lanes = the band's 64 lines) advances along u. Its records
 // are stored in its access order — slot = (band * S_full + step) * 64 + lane — one 16-B-multiple
 // record per slot, so a step's records are one contiguous 64-lane stream, prefetched D steps ahead;
-// rhs and x stay in natural order (each lane walks its own line). The wave is bound by
-// how many memory operations it can keep in flight (vmcnt saturates at 63), so each step costs
-// about two of them. Dependencies come from ONE LDS ring of `ring` steps x RW = maxyd + 64 columns:
-// columns [0, maxyd) hold the band above's last maxyd lines, written by the POLLER wave as their
-// values get published (64 u-positions polled at a time, the ready prefix announced through an LDS
-// counter after every round trip), columns maxyd + j the solver's own lanes; a dependency (yd lines,
-// ud steps back) of lane j is column j - yd + maxyd of row (s - ud) mod ring whoever produced it. The
-// solver's waits are scalar LDS spins. Padding entries (value 0, code 0 = the lane's own column of
-// the current row: finite) add exactly +-0 to the fma chain. Per-row arithmetic is the band kernels':
-// fma over the entries in stored order from 0.0, then (b - acc) / diag — bit-identical results.
+// rhs and x stay in natural order (each lane walks its own line). Dependencies come from ONE LDS ring
+// of kGridRing steps x kGridRW columns: columns [8 - maxyd, 8) hold the band above's last maxyd lines,
+// written by the POLLER wave as their values get published (64 u-positions polled at a time, the ready
+// prefix announced through an LDS counter after every round trip), column 8 + j the solver's lane j; a
+// dependency (yd lines, ud steps back) of lane j is column 8 + j - yd of ring row (s - ud) whoever
+// produced it. The ring is MIRRORED (every row written at r and r + kGridRing, one ds_write2st64), so a
+// dependency's byte address is the step's row base plus a per-entry constant (kept per dictionary
+// record): one VALU add per entry instead of the modular row arithmetic and an integer multiply.
+// The step is bound by its instruction count (one wave, in order: ~160 instructions per step ran the
+// 5-point sweep at ~630 cycles per step), so everything the step does not need per lane is scalar: the
+// ring row, the wait test on the band above (a step limit), the index prefetch (a buffer load with a
+// scalar offset). The solver's waits are scalar LDS spins. Padding entries (value 0, code 0 = the lane's
+// own column of the current row: finite) add exactly +-0 to the fma chain. Per-row arithmetic is the
+// band kernels': fma over the entries in stored order from 0.0, then (b - acc) / diag — bit-identical.
 // DICT: the records come from a dictionary (TriFactor::grid_dict_n): per lane-step ONE 32-bit index
-// load instead of the three record loads (codes, values, diagonal), the dictionary in LDS, the next
-// step's record looked up while the current step's ring reads are in flight. The grid phase probe
-// (profiles/r3_grid_phase_probe.txt) put the step's cost in its memory instructions.
+// load instead of the three record loads (codes, values, diagonal), the dictionary in LDS as one
+// 64/128-B record per entry (values, diagonal, RN(1/diagonal), ring offsets), the next step's record
+// looked up while the current step's ring reads are in flight.
+constexpr int kGridRW = 72;                          // ring columns: 8 for the band above + 64 lanes
+constexpr int kGridRing = 128;                       // ring rows (steps); the LDS holds 2 x 128 (mirror)
+constexpr uint32_t kGridMirror = kGridRing * kGridRW * 8;   // bytes between a row and its mirror
+template <int K>
+struct GridDict {   // LDS record of a dictionary entry
+    static constexpr int kBytes = K == 8 ? 128 : 64;
+    // [0, 8K) values, [8K, 8K + 16) diagonal and RN(1/diagonal), then K uint32 ring offsets
+    static constexpr int kDg = 8 * K, kOff = 8 * K + 16;
+};
 template <int K>
 struct GridRec {
-    uint32_t code[K / 2];
-    double cf[K], d, rd;   // rd = RN(1 / d), DICT only
+    uint32_t off[K];      // byte offset of each entry's ring word from the step's lane base
+    double cf[K], d, rd;  // rd = RN(1 / d), DICT only
 };
+// ring byte offset of a dependency coded ud*64 + yd, from the lane base (lower copy of the current row,
+// column 8 + j): the upper copy of row s - ud, column 8 + j - yd
+__device__ __forceinline__ uint32_t grid_ring_off(uint32_t c) {
+    return (uint32_t)(kGridRing - (int)(c >> 6)) * (kGridRW * 8) - (c & 63) * 8;
+}
 // (b - acc) / d on the solver's dependency chain without the IEEE division sequence (two
 // dependent scale steps, the reciprocal, five fmas and the fix-up): q0 = RN(r * rd) from the
 // correctly rounded reciprocal rd = RN(1/d) (computed once per dictionary entry, off the chain), then
@@ -1174,24 +1186,27 @@ __device__ __forceinline__ void grid_bstore(__amdgpu_buffer_rsrc_t r, uint32_t o
 template <int K, int D, bool DICT, bool MK>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t off, int64_t S_full, int upper, int pe, int maxyd,
-    int ring_mask, int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
+    int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
     GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict, int32_t *rflag,
     const int32_t *gate) {
     if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;   // uniform
     extern __shared__ __align__(16) unsigned char smem[];
-    const int RW = maxyd + kGridLanes;
-    double *ring = reinterpret_cast<double *>(smem);                  // [ring][RW]
-    int64_t *ctl = reinterpret_cast<int64_t *>(ring + (size_t)(ring_mask + 1) * RW);
-    // dictionary (DICT): [ndict][K] values, [ndict] diagonals, [ndict][K/2] code words (gdict's
-    // layout), then [ndict] reciprocals of the diagonals (computed here)
-    double *dcf = reinterpret_cast<double *>(ctl + 2);
-    double *ddg = dcf + (DICT ? ndict * K : 0);
-    uint32_t *dcode = reinterpret_cast<uint32_t *>(ddg + (DICT ? ndict : 0));
-    const int dwords = DICT ? ndict * (K + 1) + (ndict * K / 2 + 1) / 2 : 0;   // doubles of gdict
-    double *drd = dcf + dwords;
+    double *ring = reinterpret_cast<double *>(smem);                  // [2 * kGridRing][kGridRW]
+    int64_t *ctl = reinterpret_cast<int64_t *>(smem + 2 * kGridMirror);
+    unsigned char *dict = smem + 2 * kGridMirror + 16;                // DICT: ndict GridDict<K> records
+    // gdict (host layout): [ndict][K] values, [ndict] diagonals, [ndict][K/2] code words
     if (DICT) {
-        for (int i = threadIdx.x; i < dwords; i += 2 * kGridLanes) dcf[i] = gdict[i];
-        for (int i = threadIdx.x; i < ndict; i += 2 * kGridLanes) drd[i] = 1.0 / gdict[ndict * K + i];
+        const uint32_t *gcode = reinterpret_cast<const uint32_t *>(gdict + (size_t)ndict * (K + 1));
+        for (int i = threadIdx.x; i < ndict; i += 2 * kGridLanes) {
+            unsigned char *rec = dict + (size_t)i * GridDict<K>::kBytes;
+            double *cf = reinterpret_cast<double *>(rec);
+            for (int k = 0; k < K; ++k) cf[k] = gdict[(size_t)i * K + k];
+            const double dg = gdict[(size_t)ndict * K + i];
+            reinterpret_cast<double *>(rec + GridDict<K>::kDg)[0] = dg;
+            reinterpret_cast<double *>(rec + GridDict<K>::kDg)[1] = 1.0 / dg;
+            uint32_t *ro = reinterpret_cast<uint32_t *>(rec + GridDict<K>::kOff);
+            for (int k = 0; k < K; ++k) ro[k] = grid_ring_off((gcode[(size_t)i * (K / 2) + k / 2] >> (16 * (k & 1))) & 0xffff);
+        }
     }
     // ctl[0]: last u of the band above present in the ring (poller -> solver)
     // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
@@ -1207,7 +1222,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         max_ud = ud > max_ud ? ud : max_ud;
     }
     const bool has_ext = blockIdx.x > 0 && pe > 0;
-    for (int i = tid; i < (ring_mask + 1) * RW; i += 2 * kGridLanes) ring[i] = 0.0;
+    for (int i = tid; i < 2 * kGridRing * kGridRW; i += 2 * kGridLanes) ring[i] = 0.0;
     if (tid == 0) {
         ctl[0] = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;
         ctl[1] = u_lo - 1;
@@ -1215,7 +1230,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     __syncthreads();
 #ifdef PSK_GRID_PROF
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long n_wait = 0, c_wait = 0, c_fetch = 0, c_lds = 0, c_arith = 0, c_store = 0;
+    unsigned long long n_wait = 0, c_wait = 0;
 #endif
     if (tid >= kGridLanes) {
         // ---------------- poller: u positions [u_lo - max_ud, u_hi - min_ud] of lines y0-maxyd .. y0-1
@@ -1223,12 +1238,13 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         const int64_t ua = u_lo - max_ud, ub = u_hi - min_ud;
         for (int64_t base = ua; base <= ub; base += kGridLanes) {
             const int64_t u = base + j;
-            double *row_slot = ring + (size_t)((u - u_lo) & ring_mask) * RW;
-            // ring capacity: row (u - u_lo) last held u - ring, which the solver reads until it passes
+            double *row_lo = ring + (size_t)((u - u_lo) & (kGridRing - 1)) * kGridRW + (8 - maxyd);
+            double *row_hi = row_lo + kGridRing * kGridRW;
+            // ring capacity: row (u - u_lo) last held u - kGridRing, which the solver reads until it passes
             // that position + max_ud
             int64_t spins = 0;
             while (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                   base + kGridLanes - 1 - (ring_mask + 1) + max_ud) {
+                   base + kGridLanes - 1 - kGridRing + max_ud) {
                 if (++spins > kMaxSpins) { atomicExch(err, (2 << 24) | (int)blockIdx.x); return; }
                 __builtin_amdgcn_s_sleep(2);
             }
@@ -1236,8 +1252,12 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             for (int L = 0; L < maxyd; ++L) {
                 const int64_t yl = y0 - maxyd + L, xl = u - sigma * yl, q = yl * w + xl - off;
                 const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q >= 0 && q < n;
-                if (valid) pending |= 1u << L;
-                else row_slot[L] = 0.0;
+                if (valid) {
+                    pending |= 1u << L;
+                } else {
+                    row_lo[L] = 0.0;
+                    row_hi[L] = 0.0;
+                }
             }
             spins = 0;
             while (true) {
@@ -1246,7 +1266,8 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
                         const int64_t yl = y0 - maxyd + L, q = yl * w + (u - sigma * yl) - off;
                         const double v = load_pub(x + (upper ? n - 1 - q : q));
                         if (!is_sentinel(v)) {
-                            row_slot[L] = v;
+                            row_lo[L] = v;
+                            row_hi[L] = v;
                             pending &= ~(1u << L);
                         }
                     }
@@ -1272,39 +1293,41 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const int64_t x_hi = n + off - y * w < w ? n + off - y * w : w;
     const bool live = y < H && x_hi > x_lo;
     const int s_beg = (int)(sigma * j + (live ? x_lo : 0)), s_end = live ? (int)(sigma * j + x_hi) : s_beg;
-    // row of step s: rbase + rstep * s, q = y*w + s - sigma*j - off
+    const uint32_t s_len = (uint32_t)(s_end - s_beg);
+    // byte offset of step s's row: rb8 + rs8 * s (32-bit: n <= kGridMaxRows; step indices < 2^23, so a
+    // 24-bit multiply), q = y*w + s - sigma*j - off; a line-less lane reads out of range (loads 0)
     const int64_t qb = y * w - sigma * j - off;
-    const int64_t rbase = upper ? n - 1 - qb : qb;
-    const int64_t rstep = upper ? -1 : 1;
+    const uint32_t rb8 = live ? (uint32_t)((upper ? n - 1 - qb : qb) * 8) : kBufOOB - 8;
+    const int32_t rs8 = live ? (upper ? -8 : 8) : 0;
+    const bool pub = j >= kGridLanes - maxyd;   // the lines the band below reads: agent-scope stores
+    const uint32_t lane8 = (uint32_t)(8 + j) * 8;
     const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
                                  (int64_t)blockIdx.x * S_full * GridStep<K>::kBytes;
-    int64_t ext_known = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;   // uniform
-    const uint32_t *pidx = gidx + (int64_t)blockIdx.x * S_full * kGridLanes + j;
+    // the index stream of this band: a buffer with the step in the scalar offset
+    const __amdgpu_buffer_rsrc_t ridx = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<uint32_t *>(DICT ? gidx + (int64_t)blockIdx.x * S_full * kGridLanes : gidx), (short)0,
+        DICT ? (int)(uint32_t)(S_full * kGridLanes * 4) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rrhs = grid_rsrc(rhs, n), rx = grid_rsrc(x, n);
+    // steps up to s_ok need nothing more from the band above (uniform)
+    int s_ok = has_ext ? -max_ud - 1 + min_ud : INT32_MAX / 2;
     uint64_t rbad = 0;   // MK: lanes with a step's right-hand side outside the Markstein range (div_markstein)
-    auto fetch = [&](int s, GridSlot<K> &sl) {
+    struct Slot {
+        uint32_t idx;   // DICT: the record index
+        uint32_t code[K / 2];
+        double cf[K], d, b;
+    };
+    auto fetch = [&](int s, Slot &sl) {
         const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
+        const int sa = __builtin_elementwise_max(__builtin_elementwise_min(s, s_end - 1), s_beg);
+        sl.b = grid_bload(rrhs, rb8 + (uint32_t)__mul24(rs8, sa));
         if (DICT) {
-            sl.code[0] = pidx[(int64_t)sc * kGridLanes];   // the record index
-            const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);
-            sl.b = grid_bload(rrhs, live ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
+            sl.idx = __builtin_amdgcn_raw_buffer_load_b32(ridx, (uint32_t)j * 4, (uint32_t)sc * (kGridLanes * 4), 0);
             return;
         }
         const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
         const uint32_t *pc = reinterpret_cast<const uint32_t *>(st + GridStep<K>::kCode) + j * (K / 2);
-        if (K == 2) {
-            sl.code[0] = pc[0];
-        } else if (K == 4) {
-            const uint2 c = *reinterpret_cast<const uint2 *>(pc);
-            sl.code[0] = c.x;
-            sl.code[1] = c.y;
-        } else {
-            const uint4 c = *reinterpret_cast<const uint4 *>(pc);
-            sl.code[0] = c.x;
-            sl.code[1] = c.y;
-            sl.code[2] = c.z;
-            sl.code[3] = c.w;
-        }
+#pragma unroll
+        for (int k = 0; k < K / 2; ++k) sl.code[k] = pc[k];
         const dv2 *pf = reinterpret_cast<const dv2 *>(st + GridStep<K>::kCoef) + j * (K / 2);
 #pragma unroll
         for (int k = 0; k < K; k += 2) {
@@ -1313,38 +1336,36 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             sl.cf[k + 1] = c.y;
         }
         sl.d = reinterpret_cast<const double *>(st + GridStep<K>::kDiag)[j];
-        const int sa = s < s_beg ? s_beg : (s >= s_end ? s_end - 1 : s);   // clamped into the line
-        sl.b = grid_bload(rrhs, live ? (uint32_t)((rbase + rstep * sa) * 8) : kBufOOB);
     };
     auto lookup = [&](uint32_t idx, GridRec<K> &rc) {   // DICT: the record of a step, from LDS
+        const unsigned char *rec = dict + idx * GridDict<K>::kBytes;
 #pragma unroll
-        for (int k = 0; k < K / 2; ++k) rc.code[k] = dcode[idx * (K / 2) + k];
-#pragma unroll
-        for (int k = 0; k < K; ++k) rc.cf[k] = dcf[idx * K + k];
-        rc.d = ddg[idx];
-        rc.rd = drd[idx];
-    };
-    auto solve = [&](int s, const GridSlot<K> &slr, const GridRec<K> &rec) {
-        // the step's record: from the slot (records streamed) or the dictionary lookup (DICT)
-        GridSlot<K> sl = slr;
-        double rd = 0.0;
-        if (DICT) {
-            rd = rec.rd;
-#pragma unroll
-            for (int k = 0; k < K / 2; ++k) sl.code[k] = rec.code[k];
-#pragma unroll
-            for (int k = 0; k < K; ++k) sl.cf[k] = rec.cf[k];
-            sl.d = rec.d;
+        for (int k = 0; k < K; k += 2) {
+            const dv2 c = *reinterpret_cast<const dv2 *>(rec + 8 * k);
+            rc.cf[k] = c.x;
+            rc.cf[k + 1] = c.y;
         }
-        const int64_t u = u_lo + s;
-        if (has_ext && s < S && ext_known < u - min_ud) {   // uniform: the band above not yet in the ring
+        const dv2 dd = *reinterpret_cast<const dv2 *>(rec + GridDict<K>::kDg);
+        rc.d = dd.x;
+        rc.rd = dd.y;
+#pragma unroll
+        for (int k = 0; k < K; ++k) rc.off[k] = reinterpret_cast<const uint32_t *>(rec + GridDict<K>::kOff)[k];
+    };
+    // the ring values of step t are requested right after step t-1's ring write (one wave: the LDS
+    // queue is in order, so they see it), and the step's other work — the x stores, the prefetch D
+    // steps ahead, the dictionary lookup two steps ahead — runs while they are in flight: the chain
+    // per step is the LDS round trip and the arithmetic, not the step's whole instruction stream
+    auto wait_ext = [&](int t) {
+        if (t > s_ok && t < S) {   // uniform: the band above not yet in the ring
 #ifdef PSK_GRID_PROF
             const unsigned long long tw = __builtin_amdgcn_s_memtime();
 #endif
             int64_t spins = 0;
             do {
-                ext_known = __hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (ext_known >= u - min_ud) break;
+                const int known = __builtin_amdgcn_readfirstlane(
+                    (int)(__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - u_lo));
+                s_ok = known + min_ud;   // ext_known >= u - min_ud  <=>  t <= known + min_ud
+                if (t <= s_ok) break;
                 if (++spins > kMaxSpins) { atomicExch(err, (1 << 24) | (int)blockIdx.x); break; }
                 __builtin_amdgcn_s_sleep(1);
             } while (true);
@@ -1353,76 +1374,66 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             c_wait += __builtin_amdgcn_s_memtime() - tw;
 #endif
         }
-#ifdef PSK_GRID_PROF
-        // phase stamps: each asm consumes the values of the phase before, so the compiler's wait for
-        // them lands in front of the stamp
-        const unsigned long long p0 = __builtin_amdgcn_s_memtime();
+    };
+    auto request = [&](int t, const Slot &sl, const GridRec<K> &rec, double *v) {
+        const uint32_t base = lane8 + (uint32_t)(t & (kGridRing - 1)) * (kGridRW * 8);   // lower copy, row t
 #pragma unroll
-        for (int k = 0; k < K / 2; ++k) __asm__ volatile("" ::"v"(sl.code[k]));
-#pragma unroll
-        for (int k = 0; k < K; ++k) __asm__ volatile("" ::"v"(sl.cf[k]));
-        __asm__ volatile("" ::"v"(sl.d), "v"(sl.b));
-        const unsigned long long p1 = __builtin_amdgcn_s_memtime();
-#endif
-        double v[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) {   // every LDS read first (one round trip)
-            const uint32_t c = (sl.code[k >> 1] >> (16 * (k & 1))) & 0xffff;
-            const int yd = c & 63, ud = c >> 6;
-            v[k] = ring[((s - ud) & ring_mask) * RW + (j + maxyd - yd)];
+        for (int k = 0; k < K; ++k) {
+            const uint32_t ro = DICT ? rec.off[k] : grid_ring_off((sl.code[k >> 1] >> (16 * (k & 1))) & 0xffff);
+            v[k] = *reinterpret_cast<const double *>(smem + base + ro);
         }
-#ifdef PSK_GRID_PROF
-#pragma unroll
-        for (int k = 0; k < K; ++k) __asm__ volatile("" ::"v"(v[k]));
-        const unsigned long long p2 = __builtin_amdgcn_s_memtime();
-#endif
+    };
+    auto solve = [&](int s, const Slot &sl, const GridRec<K> &rec, const double *v) -> double {
         double acc = 0.0;
 #pragma unroll
-        for (int k = 0; k < K; ++k) acc = fma(sl.cf[k], v[k], acc);   // stored order; padding adds +-0
+        for (int k = 0; k < K; ++k) acc = fma(DICT ? rec.cf[k] : sl.cf[k], v[k], acc);   // stored order; padding adds +-0
         double r = sl.b - acc;
+        const double d = DICT ? rec.d : sl.d;
         if (DICT && MK) {   // a select, not a branch, on `unit` (the chain stays branch-free)
-            const double q = div_markstein(r, sl.d, rd, rbad);
+            const double q = div_markstein(r, d, rec.rd, rbad);
             r = unit ? r : q;
         } else if (!unit) {
-            r = r / sl.d;
+            r = r / d;
         }
-#ifdef PSK_GRID_PROF
-        __asm__ volatile("" ::"v"(r));
-        const unsigned long long p3 = __builtin_amdgcn_s_memtime();
-#endif
-        ring[(s & ring_mask) * RW + maxyd + j] = r;
-        // the lines the band below reads are published; the others are read after the kernel
-        // (agent-scope stores on every lane: 732 -> 561 cycles per step plain, 5-point sweep)
-        {
-            const bool act = s >= s_beg && s < s_end, pub = j >= kGridLanes - maxyd;
-            const uint32_t o = act ? (uint32_t)((rbase + rstep * s) * 8) : kBufOOB;
-            grid_bstore<0x10>(rx, pub ? o : kBufOOB, r);
-            grid_bstore<0>(rx, pub ? kBufOOB : o, r);
-        }
-#ifdef PSK_GRID_PROF
-        const unsigned long long p4 = __builtin_amdgcn_s_memtime();
-        c_fetch += p1 - p0;
-        c_lds += p2 - p1;
-        c_arith += p3 - p2;
-        c_store += p4 - p3;
-#endif
+        // both copies of the row (the mirror is kGridMirror bytes above)
+        const uint32_t base = lane8 + (uint32_t)(s & (kGridRing - 1)) * (kGridRW * 8);
+        *reinterpret_cast<double *>(smem + base) = r;
+        *reinterpret_cast<double *>(smem + base + kGridMirror) = r;
+        return r;
     };
-    GridSlot<K> buf[D];
+    auto store_x = [&](int s, double r) {   // the lines the band below reads are published
+        const bool act = (uint32_t)(s - s_beg) < s_len;
+        const uint32_t o = rb8 + (uint32_t)__mul24(rs8, s);
+        grid_bstore<0x10>(rx, act && pub ? o : kBufOOB, r);
+        grid_bstore<0>(rx, act && !pub ? o : kBufOOB, r);
+    };
+    static_assert(D >= 3 && D % 2 == 0, "the lookup runs two steps ahead; step parity = slot parity");
+    Slot buf[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) fetch(i, buf[i]);
-    GridRec<K> rcur{}, rnext{};
-    if (DICT) lookup(buf[0].code[0], rcur);
-    for (int s0 = 0; s0 < S; s0 += D) {
+    GridRec<K> rq[2] = {};   // DICT: rq[t & 1] = the record of step t
+    if (DICT) {
+        lookup(buf[0].idx, rq[0]);
+        lookup(buf[1].idx, rq[1]);
+    }
+    double vn[K];
+    wait_ext(0);
+    request(0, buf[0], rq[0], vn);
+    for (int s0 = 0; s0 < S; s0 += D) {   // D even: step s0 + i has the parity of i
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            // DICT: the next step's record is looked up now (its index arrived steps ago), so its LDS
-            // round trip overlaps this step's ring reads
-            if (DICT) lookup(buf[i + 1 < D ? i + 1 : 0].code[0], rnext);
-            solve(s0 + i, buf[i], rcur);
-            if (DICT) rcur = rnext;
-            // the ring write of step s0+i precedes the next step's reads (one wave: LDS in order)
+            const int s = s0 + i;
+            const double r = solve(s, buf[i], rq[i & 1], vn);
+            __asm__ volatile("" ::: "memory");   // the ring write before the next step's reads
+            wait_ext(s + 1);
+            request(s + 1, buf[(i + 1) % D], rq[(i + 1) & 1], vn);
+            store_x(s, r);
             __asm__ volatile("" ::: "memory");
-            fetch(s0 + i + D, buf[i]);
+            fetch(s + D, buf[i]);
+            if (DICT) lookup(buf[(i + 2) % D].idx, rq[i & 1]);   // step s + 2's record
+            // issued HERE: left to itself the machine scheduler sank the lookup into the next step,
+            // next to the ring reads that need it (two LDS round trips on the chain)
+            __builtin_amdgcn_sched_barrier(0);
         }
         if (j == 0)   // progress for the poller's ring capacity
             __hip_atomic_store(&ctl[1], u_lo + s0 + D - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1435,10 +1446,6 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         g_grid_prof[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
         g_grid_prof[blockIdx.x * 8 + 2] = n_wait;
         g_grid_prof[blockIdx.x * 8 + 3] = c_wait;
-        g_grid_prof[blockIdx.x * 8 + 4] = c_fetch;
-        g_grid_prof[blockIdx.x * 8 + 5] = c_lds;
-        g_grid_prof[blockIdx.x * 8 + 6] = c_arith;
-        g_grid_prof[blockIdx.x * 8 + 7] = c_store;
     }
 #endif
 }
@@ -1458,9 +1465,9 @@ __global__ void grid_fill_published_kernel(int64_t n, int64_t w, int64_t H, int6
 }
 __global__ void grid_flag_reset_kernel(int32_t *flag) { *flag = 0; }
 
-static size_t grid_lds_bytes(int ring, int maxyd, int K = 0, int ndict = 0) {
-    return (size_t)ring * (kGridLanes + maxyd) * sizeof(double) + 2 * sizeof(int64_t) +
-           (ndict > 0 ? (size_t)ndict * (K + 2) * sizeof(double) + ((size_t)ndict * K / 2 + 1) / 2 * sizeof(double) : 0);
+static size_t grid_lds_bytes(int K, int ndict) {   // mirrored ring, ctl, dictionary records
+    const size_t rec = K == 8 ? GridDict<8>::kBytes : K == 4 ? GridDict<4>::kBytes : GridDict<2>::kBytes;
+    return 2 * (size_t)kGridMirror + 2 * sizeof(int64_t) + (ndict > 0 ? (size_t)ndict * rec : 0);
 }
 
 static size_t narrow_lds_bytes(int ring_words, int K) {
@@ -1585,7 +1592,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
 #undef PSK_GRID_K
         if (!k) return fail(PSK_ERR_ARG, "grid schedule: bad record width");
         int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, goff = T.grid_off, sfull = T.grid_S;
-        int upper = T.upper ? 1 : 0, pe_ = T.grid_pe, myd = T.grid_maxyd, mask = T.grid_ring - 1;
+        int upper = T.upper ? 1 : 0, pe_ = T.grid_pe, myd = T.grid_maxyd;
         int unit = T.diag ? 0 : 1;
         const double *gr = T.gd_coef;
         GridExt ext = T.grid_ext;
@@ -1594,10 +1601,10 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         int nd = T.grid_dict_n;
         int32_t *flag = dict ? T.grid_flag : nullptr;
         const int32_t *nogate = nullptr;
-        void *args[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr,
-                        &ext, &gi, &gdd, &nd, &flag, &nogate};
+        void *args[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext, &gi,
+                        &gdd, &nd, &flag, &nogate};
         const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
-        const size_t lds = grid_lds_bytes(T.grid_ring, T.grid_maxyd, T.grid_K, T.grid_dict_n);
+        const size_t lds = grid_lds_bytes(T.grid_K, T.grid_dict_n);
         PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args, lds, s));
         if (dict) {   // conditional IEEE re-solve (div_markstein): no-ops unless a step was out of range
             const int32_t *gate = T.grid_flag;
@@ -1607,8 +1614,8 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
                                    H, goff, myd, upper, x, gate);
                 PSK_HIP(hipGetLastError());
             }
-            void *fargs[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &mask, &unit, &rhs, &x, &err, &gr,
-                             &ext, &gi, &gdd, &nd, &noflag, &gate};
+            void *fargs[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext,
+                             &gi, &gdd, &nd, &noflag, &gate};
             PSK_HIP(hipLaunchKernel(kf, dim3(nb), dim3(2 * kGridLanes), fargs, lds, s));
             hipLaunchKernelGGL(grid_flag_reset_kernel, dim3(1), dim3(1), 0, s, T.grid_flag);
             PSK_HIP(hipGetLastError());

@@ -58,6 +58,8 @@ def main():
                          "dur": int(a[b, 1] - a[b, 0]), "waits": int(a[b, 2]), "wait_ticks": int(a[b, 3])}
                         for b in sorted(set([0, 1, 2, len(a) // 2, len(a) - 2, len(a) - 1]))]
         out["total_ticks"] = int(a[:, 1].max() - t0)
+        out["bands_start_dur_waits_waitticks"] = [[int(a[b, 0] - t0), int(a[b, 1] - a[b, 0]), int(a[b, 2]), int(a[b, 3])]
+                                                  for b in range(len(a))]
         out["waits_total"] = int(a[:, 2].sum())
         # per-step phases (s_memtime ticks summed over every step of every band; the last apply's)
         steps = 0.0 if args.level3 else float(m + 63) * len(a)   # FD: w = m, sigma = 1: S = w + 63 per band
