@@ -126,6 +126,13 @@ int         psk_synchronize(void);
  * PSK_ERR_ARG and psk_csr_destroy / psk_prec_destroy / psk_dfree are no-ops. No reference
  * counterpart (process teardown). */
 int         psk_shutdown(void);
+/* psk_shutdown with options. PSK_SHUTDOWN_RESET_DEVICE: afterwards hipDeviceReset() every device the
+ * library used, releasing the HIP runtime's own per-device state (e.g. its cooperative-launch queue) while
+ * HSA is alive; only for a process in which libpsk is the only HIP user (the Python binding passes it
+ * when torch was never imported) and skipped while an RCCL communicator is alive. No reference
+ * counterpart (process teardown). */
+#define PSK_SHUTDOWN_RESET_DEVICE 1
+int         psk_shutdown_ex(int32_t flags);
 /* device memory helpers (so a host binding can keep vectors resident in HBM) */
 int psk_dmalloc(int64_t bytes, void **dptr);
 int psk_dfree(void *dptr);

@@ -6,6 +6,7 @@ module raises ImportError, and every solve goes through the HIP kernels.
 import atexit
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -50,6 +51,7 @@ SIGNATURES = {
     "psk_set_device": (ctypes.c_int, [I32]),
     "psk_synchronize": (ctypes.c_int, []),
     "psk_shutdown": (ctypes.c_int, []),
+    "psk_shutdown_ex": (ctypes.c_int, [ctypes.c_int32]),
     "psk_dmalloc": (ctypes.c_int, [I64, PP]),
     "psk_dfree": (ctypes.c_int, [P]),
     "psk_h2d": (ctypes.c_int, [P, P, I64]),
@@ -163,6 +165,7 @@ def _load():
     return lib
 
 
+PSK_SHUTDOWN_RESET_DEVICE = 1
 lib = _load()
 shut_down = False
 
@@ -175,7 +178,9 @@ def _shutdown():
     global shut_down
     if not shut_down:
         shut_down = True
-        lib.psk_shutdown()
+        # with torch never imported libpsk is the process's only HIP user: release the runtime's own device
+        # state too (a cooperative launch otherwise left exit() faulting under rocprofv3)
+        lib.psk_shutdown_ex(PSK_SHUTDOWN_RESET_DEVICE if "torch" not in sys.modules else 0)
 
 
 atexit.register(_shutdown)

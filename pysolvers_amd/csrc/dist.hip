@@ -329,6 +329,7 @@ int psk_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, psk_comm **ou
         delete c;
         return fail(PSK_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
     }
+    rccl_comm_count(1);
     *out = c;
     return PSK_OK;
 }
@@ -346,7 +347,10 @@ int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out) {
 
 int psk_comm_destroy(psk_comm *c) {
     if (!c) return PSK_OK;
-    if (c->nccl) (void)ncclCommDestroy(c->nccl);
+    if (c->nccl) {
+        (void)ncclCommDestroy(c->nccl);
+        rccl_comm_count(-1);
+    }
     shm_close(c);
     delete c;
     return PSK_OK;

@@ -385,7 +385,7 @@ __global__ __launch_bounds__(kLdsThreads) void sptrsv_lds_kernel(int64_t n, cons
 // that sees the same tag before and after reading the value has that row's value, a newer tag means
 // the slot was reused (the value is then read from x), an older one that the row is not done. Same
 // per-row arithmetic as sync-free (same entry order, lane partials, row_total), so bit-identical to it.
-// Progress: all P workgroups are co-resident (cooperative launch); the globally ASAP-first unsolved
+// Progress: all P workgroups are co-resident (one per CU, P <= CUs); the globally ASAP-first unsolved
 // row has all its dependencies solved and every earlier row of its wave is ASAP-earlier.
 constexpr int kPartThreads = 1024;
 constexpr int kPartWaves = kPartThreads / 64;
@@ -1506,7 +1506,11 @@ static int coop_grid(const Context *c, const void *kern, size_t lds) {
 
 // Sync-free grid: every resident slot the occupancy API reports minus one workgroup per CU (the
 // hardware admits one fewer than the API at some SGPR counts, MI355X_MICROARCH.md "Residency"); all
-// waves must be co-resident, since a row's wave may wait on any earlier position.
+// waves must be co-resident, since a row's wave may wait on any earlier position. The spin-waiting
+// schedules (sync-free, band, partitioned) size their grids to fit and launch them plainly: a
+// cooperative launch adds nothing they use (no grid barrier), and it left HIP holding per-process
+// state whose teardown in exit() faulted under rocprofv3 (profiles/r4_exit_fault.txt). Every wait is
+// bounded, so a workgroup that never became resident would surface as a reported error, not a hang.
 static int syncfree_grid(const Context *c) {
     static int per_cu = -1;
     if (per_cu < 0) {
@@ -1567,7 +1571,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const int32_t *prp = T.part_rp, *pc = T.part_code, *prow = T.part_row;
         const double *pv = T.part_va;
         void *args[] = {&sg, &prp, &pc, &pv, &dg, &rhs, &x, &err, &prow};
-        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(T.part_P), dim3(kPartThreads), args, (unsigned)kPartLds, s));
+        PSK_HIP(hipLaunchKernel(k, dim3(T.part_P), dim3(kPartThreads), args, (unsigned)kPartLds, s));
         return PSK_OK;
     }
     if (T.schedule == kSchedGrid) {
@@ -1639,7 +1643,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         int64_t nb = T.band_nblocks, B = T.band_B;
         int mask = T.ring_words - 1;
         void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask};
-        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
+        PSK_HIP(hipLaunchKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
         return PSK_OK;
     }
     if (T.schedule == kSchedBand) {
@@ -1659,14 +1663,14 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         int64_t nb = T.band_nblocks, B = T.band_B;
         int mask = T.ring_words > 0 ? T.ring_words - 1 : -1;
         void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask};
-        PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
+        PSK_HIP(hipLaunchKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
         return PSK_OK;
     }
     const void *k = reinterpret_cast<const void *>(&sptrsv_kernel);
     const int g = syncfree_grid(c);
     const int32_t *ord = T.order;
     void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
-    PSK_HIP(hipLaunchCooperativeKernel(k, dim3(g), dim3(kBlock), args, 0, s));
+    PSK_HIP(hipLaunchKernel(k, dim3(g), dim3(kBlock), args, 0, s));
     return PSK_OK;
 }
 

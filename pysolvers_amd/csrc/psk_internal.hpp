@@ -93,6 +93,7 @@ int comm_stream(Context *c, hipStream_t *out);
 int solve_kit(Context *c, bool timed, SolveKit **out);
 // true once psk_shutdown ran: destroy entry points become no-ops (the process is exiting)
 bool lib_shut_down();
+void rccl_comm_count(int delta);   // live RCCL communicators (psk_shutdown_ex resets the device only at 0)
 
 // ---------------------------------------------------------------------------------------------
 // grow-only device buffer

@@ -2,6 +2,7 @@
 #include "psk_internal.hpp"
 
 #include <mutex>
+#include <atomic>
 
 namespace psk {
 
@@ -21,6 +22,8 @@ static Context g_ctx[64];
 static bool g_shut = false;
 
 bool lib_shut_down() { return g_shut; }
+static std::atomic<int> g_live_rccl{0};   // RCCL communicators alive (psk_comm_init .. psk_comm_destroy)
+void rccl_comm_count(int delta) { g_live_rccl += delta; }
 
 int solve_kit(Context *c, bool timed, SolveKit **out) {
     SolveKit &k = c->kit;
@@ -261,7 +264,9 @@ int psk_dfree(void *dptr) {
 // nothing of libpsk is left for the runtime's own static destructors at exit(); afterwards every
 // entry point that needs a device fails with PSK_ERR_ARG and the destroy entry points are no-ops
 // (objects still alive then are reclaimed with the process).
-int psk_shutdown(void) {
+int psk_shutdown(void) { return psk_shutdown_ex(0); }
+
+int psk_shutdown_ex(int32_t flags) {
     std::lock_guard<std::mutex> lk(g_ctx_mu);
     if (g_shut) return PSK_OK;
     int rc = PSK_OK;
@@ -303,6 +308,10 @@ int psk_shutdown(void) {
         (void)hipStreamDestroy(c.stream);
         c.comm_stream = nullptr;
         c.stream = nullptr;
+        // the HIP runtime's own per-device state too (its cooperative-launch queue among it), while HSA is
+        // still alive: under rocprofv3 the profiler finalises HSA in its exit hook, and a HIP teardown
+        // after that — in exit(), once any cooperative launch ran — faulted (profiles/r4_exit_fault.txt)
+        if ((flags & PSK_SHUTDOWN_RESET_DEVICE) && g_live_rccl.load() == 0) (void)hipDeviceReset();
     }
     (void)hipSetDevice(cur);
     g_shut = true;

@@ -6,9 +6,6 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out; mkdir -p $OUT; export TMPDIR=/tmp
 TAG=${1:-r4f}
 sha256sum pysolvers_amd/_lib/libpsk.so > $OUT/${TAG}_lib.sha256
-# A/B first: the y store after the dot epilogue (in-tree) vs before it (tools/bin/ab_yfirst, the previous spmv.hip)
-timeout -k 10 600 python -u tools/ab_pcg.py --sides 3163,16384 --rounds 2 ylast= yfirst=@tools/bin/ab_yfirst/libpsk.so ylastdot=PSK_SPMV_TIMED_MODE=1 > $OUT/${TAG}_ab.jsonl 2> $OUT/${TAG}_ab.err
-c=$?; echo "ab exit $c"; [ $c -le 1 ] || exit $c
 timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread > $OUT/${TAG}_pytest.log 2>&1
 c=$?; echo "pytest exit $c"; tail -3 $OUT/${TAG}_pytest.log; [ $c -le 1 ] || exit $c
 timeout -k 10 400 python -u bench.py --steps 20 --warmup 5 > $OUT/${TAG}_bench.json 2> $OUT/${TAG}_bench.err

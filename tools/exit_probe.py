@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Exit-fault probe (lab): one small solve of the chosen kind, then a normal interpreter exit. Run
 under rocprofv3 to see which libpsk path leaves the process in a state whose exit() faults there.
-    python tools/exit_probe.py pcg|ilu|amg|none
+    python tools/exit_probe.py pcg|ilu|amg|coop|lds|none
+
+coop / lds: one 30000-row triangular solve on the sync-free schedule (a cooperative launch) / the LDS
+schedule (a plain launch).
 """
 import os
 import sys
@@ -22,6 +25,15 @@ elif kind == "ilu":
     st = psk.GMRES(control=ctl, precond=psk.RightILUT(), restart=10).makeSolver().solve(A, b)
 elif kind == "amg":
     st = psk.PCG(control=ctl, precond=psk.AMG(numIters=1, numLevels=2)).makeSolver().solve(-A, -b)
+elif kind in ("coop", "lds"):
+    import scipy.sparse as sp
+    from pysolvers_amd.Linear import TriangularSolveChain
+    n = 16000 if kind == "lds" else 30000
+    L = (sp.diags(np.full(n, 2.0)) + sp.diags(np.full(n - 1, -0.5), -1)).tocsr()
+    M = TriangularSolveChain(n, L=L)
+    M.schedule("L", set="syncfree" if kind == "coop" else "lds")
+    M.apply(np.ones(n))
+    st = None
 else:
     st = None
 print(kind, None if st is None else (st.success(), st.iters()), flush=True)
