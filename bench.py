@@ -474,7 +474,7 @@ def median(v):
 def spmv_kernel_label(layout, mode):
     """Descriptive name of the SpMV kernel a layout runs when no PMC profile of the build names it."""
     return ("spmv_kernel<%d> (CSR layout)" % mode) if layout == 0 else \
-        ("spmv_uniform_kernel / spmv_sliced_kernel <MODE=%d> (%s layout)" % (mode, LAYOUT_NAMES[layout]))
+        ("spmv_uniform(_multi)_kernel / spmv_sliced_kernel <MODE=%d> (%s layout)" % (mode, LAYOUT_NAMES[layout]))
 
 
 def lib_sha256():
@@ -606,7 +606,7 @@ def pmc_traffic(path, m, world, mode, sliced):
         return {"traffic": None, "traffic_note": "%s is for another side / rank count" % src}
     if d.get("libpsk_sha256") != lib_sha256():
         return {"traffic": None, "traffic_note": "%s was captured with another libpsk.so build" % src}
-    pat = re.compile((r"psk::spmv_(uniform|sliced)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
+    pat = re.compile((r"psk::spmv_(uniform_multi|uniform|sliced)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
     hits = [k for k in d["kernels"] if pat.search(k)]
     if len(hits) != 1:
         return {"traffic": None, "traffic_note": "%s holds %d SpMV kernels of mode %d" % (src, len(hits), mode)}
