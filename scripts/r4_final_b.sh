@@ -11,6 +11,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/${TAG}_prof -o run --
     python -u bench.py --steps 20 --warmup 5 --cpu-iters 0 > $OUT/${TAG}_prof.json 2> $OUT/${TAG}_prof.err
 c=$?; echo "profiled bench exit $c"
 python tools/trace_stats.py $(find $OUT/${TAG}_prof -name "*kernel_trace.csv" | head -1) > $OUT/${TAG}_trace_stats.csv
+# the headline regions' own SpMV launches (the bench line's roofline.avg_launch_ms samples every 8th of them)
+python tools/region_trace.py $(find $OUT/${TAG}_prof -name "*kernel_trace.csv" | head -1) > $OUT/${TAG}_headline_regions.json
 cp $(find $OUT/${TAG}_prof -name "*kernel_stats.csv" | head -1) $OUT/${TAG}_kernel_stats.csv
 rm -rf $OUT/${TAG}_prof
 [ $c -eq 0 ] || exit $c

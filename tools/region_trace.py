@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""The headline regions' SpMV launches in a rocprofv3 --kernel-trace CSV of `bench.py` (evidence tool).
+
+    python tools/region_trace.py run_kernel_trace.csv [--kernel spmv_uniform_multi_kernel<1] \
+        [--workgroups 19541] [--warmup 5] [--steps 20] [--regions 5]
+
+bench.py's first launches of the in-loop SpMV at the headline size are the warmup solve's (`--warmup`
+iterations), then the timed regions (`--regions` x `--steps`). Prints the mean duration over exactly those
+timed launches, per region, and over every launch of the kernel at that grid in the whole run (what a
+`--stats` summary averages), so the bench line's `roofline.avg_launch_ms` (HIP events on every 8th launch of
+the median region) can be compared with the profiler on the same launches.
+"""
+import argparse
+import csv
+import json
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    ap.add_argument("--kernel", default="spmv_uniform_multi_kernel<1,")
+    ap.add_argument("--workgroups", type=int, default=19541)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--regions", type=int, default=5)
+    a = ap.parse_args()
+    launches = []
+    for r in csv.DictReader(open(a.trace)):
+        name = r["Kernel_Name"].replace(" ", "")
+        if a.kernel.replace(" ", "") not in name:
+            continue
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        wg = int(r["Workgroup_Size_X"]) * int(r["Workgroup_Size_Y"]) * int(r["Workgroup_Size_Z"])
+        if grid // max(wg, 1) != a.workgroups:
+            continue
+        launches.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
+    launches.sort()
+    durs = [d for _, d in launches]
+    timed = durs[a.warmup:a.warmup + a.steps * a.regions]
+    per_region = [statistics.mean(timed[i * a.steps:(i + 1) * a.steps]) / 1e3 for i in range(a.regions)
+                  if timed[i * a.steps:(i + 1) * a.steps]]
+    print(json.dumps({"kernel": a.kernel, "workgroups": a.workgroups, "launches_in_trace": len(durs),
+                      "timed_launches": len(timed),
+                      "timed_mean_us": statistics.mean(timed) / 1e3 if timed else None,
+                      "timed_per_region_mean_us": per_region,
+                      "median_region_mean_us": statistics.median(per_region) if per_region else None,
+                      "all_launches_mean_us": statistics.mean(durs) / 1e3 if durs else None}))
+
+
+if __name__ == "__main__":
+    main()
