@@ -16,6 +16,7 @@ python tools/region_trace.py $(find $OUT/${TAG}_prof -name "*kernel_trace.csv" |
 cp $(find $OUT/${TAG}_prof -name "*kernel_stats.csv" | head -1) $OUT/${TAG}_kernel_stats.csv
 rm -rf $OUT/${TAG}_prof
 [ $c -eq 0 ] || exit $c
+[ "${SKIP_PMC:-0}" = 1 ] && exit 0
 TAG=$TAG PMC_ARGS="--steps 20 --warmup 2 --repeats 1 --cpu-iters 0 --config1 0 --config2 0 --config4 0 --general 0 --gmres 0 --scaling-side 0" \
     bash scripts/gpu_pmc.sh
 c=$?; echo "pmc exit $c"; [ $c -eq 0 ] || exit $c
