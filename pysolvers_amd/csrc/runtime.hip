@@ -40,8 +40,11 @@ int solve_kit(Context *c, bool timed, SolveKit **out) {
     }
     if (timed && !k.timed_ready) {
         for (int i = 0; i < kTimedSlots; ++i) {
-            PSK_HIP(hipEventCreate(&k.ta[i]));
-            PSK_HIP(hipEventCreate(&k.tb[i]));
+            // timing only: no system-scope fence at record (its L2 writeback of the SpMV's freshly
+            // written y landed inside the bracket: +4-6 us per sampled launch at N = 10M against the
+            // profiler's kernel time, profiles/r4_headline_regions_rocprof.json)
+            PSK_HIP(hipEventCreateWithFlags(&k.ta[i], hipEventDisableSystemFence));
+            PSK_HIP(hipEventCreateWithFlags(&k.tb[i], hipEventDisableSystemFence));
         }
         k.timed_ready = true;
     }

@@ -1432,8 +1432,8 @@ int psk_spmv_timed(const psk_csr *A, const double *x, double *y, int32_t reps, d
     Context *c;
     PSK_TRY(ctx(&c));
     hipEvent_t e0, e1;
-    PSK_HIP(hipEventCreate(&e0));
-    PSK_HIP(hipEventCreate(&e1));
+    PSK_HIP(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));   // timing only (runtime.hip)
+    PSK_HIP(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
     // PSK_SPMV_TIMED_MODE=1: the PCG loop's kSpmvDot launch (dot epilogue + gridsum) instead of a
     // plain y = A x (lab switch: separates the epilogue from the loop context)
     static const int mode = [] {
