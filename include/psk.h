@@ -237,6 +237,11 @@ int psk_prec_create_amg(int32_t num_levels, psk_csr *const *A, psk_csr *const *P
  * queries. Any out pointer may be NULL. */
 int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t *schedule, int64_t *blocks,
                                int32_t *ring_words, double *est_syncfree_us, double *est_band_us);
+/* Grid-schedule shape of factor `which` (0 = L, 1 = U): out[0..6] = line width w, lines H, twice the
+ * skew sigma2 and its phase (a solve-order position y*w + x - off runs at step x + ((sigma2*y + phase)
+ * >> 1)), leading empty positions off, steps per 64-line band, dictionary records (0 = per-step
+ * records). PSK_ERR_UNSUPPORTED when the factor is not a 2-D stencil. No compute (diagnostics, tests). */
+int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out);
 /* kind, size and triangular-solve shape of a preconditioner (any out pointer may be NULL). */
 int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, int64_t *nnz_u,
                   int64_t *levels_l, int64_t *levels_u);

@@ -79,6 +79,13 @@ class TriangularSolveChain(DeviceOperator, GenericPreconditioner):
         return dict(schedule=("syncfree", "band", "lds", "grid", "part")[sc.value], blocks=bl.value, ring_words=rw.value,
                     est_syncfree_us=e0.value, est_band_us=e1.value)
 
+    def grid_info(self, which):
+        """Grid-schedule shape of factor `which` (psk_prec_trisolve_grid_info): dict(w, H, sigma2, phase, off,
+        steps, dict_records) — position y*w + x - off runs at step x + ((sigma2*y + phase) >> 1)."""
+        out = (N.I64 * 7)()
+        N.check(N.lib.psk_prec_trisolve_grid_info(self._h, {"L": 0, "U": 1}[which], out), "psk_prec_trisolve_grid_info")
+        return dict(zip(("w", "H", "sigma2", "phase", "off", "steps", "dict_records"), list(out)))
+
 
 def superlu_transposed_solver(lu):
     """x = lu.solve(b, trans='T') as a chain: with Pr B Pc = L U, B^T x = b gives

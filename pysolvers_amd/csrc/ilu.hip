@@ -1056,15 +1056,18 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
 
 // Grid: a factor whose dependencies, in solve order q, form a 2-D stencil: with q = y*w + x (w
 // positions per line), every off-diagonal entry of row q refers to q' = q - (yd*w + xd) with
-// 0 <= yd < 64 lines back and, for the skew sigma chosen by the host, ud = xd + sigma*yd >= 1 steps
-// back along u = x + sigma*y (the 5-point Gauss-Seidel factor triu(A): (0,1), (1,0), sigma = 1; an
-// SA coarse operator of a 2-D grid: up to 2 lines back with diagonal neighbours). One wave per band
+// 0 <= yd < 64 lines back and, for the skew chosen by the host, ud = xd + g(y) - g(y - yd) >= 1 steps
+// back along u = x + g(y) (the 5-point Gauss-Seidel factor triu(A): (0,1), (1,0), g(y) = y; an
+// SA coarse operator of a 2-D grid: up to 2 lines back with diagonal neighbours). The skew may be a
+// half integer, g(y) = (sigma2 * y + phase) >> 1 with sigma2 odd: SA level 3 of -FD 4096^2 (2048 lines
+// of 1366) has a dependency (1 line, 2 positions ahead) on every other line only, which an integer
+// skew can only meet with g(y) = 3y; g(y) = (5y + 1) >> 1 meets it with 13.6% fewer steps. One wave per band
 // of 64 lines; lane j owns line y0+j and all lanes advance together along u, so step s solves 64
 // rows that do not depend on each other; a dependency on the same band is a read of the LDS ring
 // holding the band's last `ring` steps (ring[(s mod ring)*64 + lane]); only lanes j < yd reach into
 // the band above, through the published values (pre-filled sentinel, agent-scope store / poll as
 // the other schedules), prefetched D steps ahead with everything else a step needs. The critical
-// path is the u range (w + sigma*H steps) plus one hand-off lag per band, instead of one hand-off
+// path is the u range (w + g(H) steps) plus one hand-off lag per band, instead of one hand-off
 // per dependency level. Per-row arithmetic is the band kernels': fma over the entries in stored
 // order from 0.0, then (b - acc) / diag, so results are bit-identical to the band schedule.
 constexpr int kGridLanes = 64;
@@ -1133,6 +1136,10 @@ struct GridRec {
 __device__ __forceinline__ uint32_t grid_ring_off(uint32_t c) {
     return (uint32_t)(kGridRing - (int)(c >> 6)) * (kGridRW * 8) - (c & 63) * 8;
 }
+// the skewed step of line y's first position: g(y) = (sigma2 * y + phase) >> 1 (sigma2 = twice the skew)
+__host__ __device__ __forceinline__ int64_t grid_g(int64_t sigma2, int64_t phase, int64_t y) {
+    return (sigma2 * y + phase) >> 1;
+}
 // (b - acc) / d on the solver's dependency chain without the IEEE division sequence (two
 // dependent scale steps, the reciprocal, five fmas and the fix-up): q0 = RN(r * rd) from the
 // correctly rounded reciprocal rd = RN(1/d) (computed once per dictionary entry, off the chain), then
@@ -1185,7 +1192,8 @@ __device__ __forceinline__ void grid_bstore(__amdgpu_buffer_rsrc_t r, uint32_t o
 // IEEE division. gate != nullptr: the conditional re-solve, a no-op unless *gate is set.
 template <int K, int D, bool DICT, bool MK>
 __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
-    int64_t n, int64_t w, int64_t H, int64_t sigma, int64_t off, int64_t S_full, int upper, int pe, int maxyd,
+    int64_t n, int64_t w, int64_t H, int64_t sigma2, int64_t phase, int64_t off, int64_t S_full, int upper, int pe,
+    int maxyd,
     int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
     GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict, int32_t *rflag,
     const int32_t *gate) {
@@ -1213,7 +1221,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const int tid = threadIdx.x, j = tid & 63;
     const int64_t y0 = (int64_t)blockIdx.x * kGridLanes;
     const int64_t ylast = (y0 + kGridLanes - 1 < H - 1) ? y0 + kGridLanes - 1 : H - 1;
-    const int64_t u_lo = sigma * y0, u_hi = (w - 1) + sigma * ylast;
+    const int64_t u_lo = grid_g(sigma2, phase, y0), u_hi = (w - 1) + grid_g(sigma2, phase, ylast);
     const int S = (int)(u_hi - u_lo + 1);
     int min_ud = 1 << 30, max_ud = 0;
     for (int e = 0; e < pe; ++e) {
@@ -1250,7 +1258,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             }
             uint32_t pending = 0;   // lines of this lane's u still to fetch
             for (int L = 0; L < maxyd; ++L) {
-                const int64_t yl = y0 - maxyd + L, xl = u - sigma * yl, q = yl * w + xl - off;
+                const int64_t yl = y0 - maxyd + L, xl = u - grid_g(sigma2, phase, yl), q = yl * w + xl - off;
                 const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q >= 0 && q < n;
                 if (valid) {
                     pending |= 1u << L;
@@ -1263,7 +1271,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             while (true) {
                 for (int L = 0; L < maxyd; ++L)
                     if (pending & (1u << L)) {
-                        const int64_t yl = y0 - maxyd + L, q = yl * w + (u - sigma * yl) - off;
+                        const int64_t yl = y0 - maxyd + L, q = yl * w + (u - grid_g(sigma2, phase, yl)) - off;
                         const double v = load_pub(x + (upper ? n - 1 - q : q));
                         if (!is_sentinel(v)) {
                             row_lo[L] = v;
@@ -1288,15 +1296,16 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const int64_t y = y0 + j;
     // lane j's line holds grid positions [y*w, y*w + w) of [off, n + off) (the first `off` positions of
     // the first line are empty: a partial line leading the solve order); it is active for steps
-    // [s_beg, s_end): x = s - sigma*j in [x_lo, x_hi)
+    // [s_beg, s_end): x = s - gy in [x_lo, x_hi), gy = g(y) - g(y0) (the line's first step in the band)
     const int64_t x_lo = y * w < off ? off - y * w : 0;
     const int64_t x_hi = n + off - y * w < w ? n + off - y * w : w;
     const bool live = y < H && x_hi > x_lo;
-    const int s_beg = (int)(sigma * j + (live ? x_lo : 0)), s_end = live ? (int)(sigma * j + x_hi) : s_beg;
+    const int64_t gy = grid_g(sigma2, phase, y) - u_lo;
+    const int s_beg = (int)(gy + (live ? x_lo : 0)), s_end = live ? (int)(gy + x_hi) : s_beg;
     const uint32_t s_len = (uint32_t)(s_end - s_beg);
     // byte offset of step s's row: rb8 + rs8 * s (32-bit: n <= kGridMaxRows; step indices < 2^23, so a
-    // 24-bit multiply), q = y*w + s - sigma*j - off; a line-less lane reads out of range (loads 0)
-    const int64_t qb = y * w - sigma * j - off;
+    // 24-bit multiply), q = y*w + s - gy - off; a line-less lane reads out of range (loads 0)
+    const int64_t qb = y * w - gy - off;
     const uint32_t rb8 = live ? (uint32_t)((upper ? n - 1 - qb : qb) * 8) : kBufOOB - 8;
     const int32_t rs8 = live ? (upper ? -8 : 8) : 0;
     const bool pub = j >= kGridLanes - maxyd;   // the lines the band below reads: agent-scope stores
@@ -1595,7 +1604,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         else if (T.grid_K == 8) PSK_GRID_K(8, (PSK_GRID_D > 6 ? 6 : PSK_GRID_D));
 #undef PSK_GRID_K
         if (!k) return fail(PSK_ERR_ARG, "grid schedule: bad record width");
-        int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, goff = T.grid_off, sfull = T.grid_S;
+        int64_t w = T.grid_w, H = T.grid_H, sg = T.grid_sigma, gph = T.grid_phase, goff = T.grid_off, sfull = T.grid_S;
         int upper = T.upper ? 1 : 0, pe_ = T.grid_pe, myd = T.grid_maxyd;
         int unit = T.diag ? 0 : 1;
         const double *gr = T.gd_coef;
@@ -1605,7 +1614,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         int nd = T.grid_dict_n;
         int32_t *flag = dict ? T.grid_flag : nullptr;
         const int32_t *nogate = nullptr;
-        void *args[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext, &gi,
+        void *args[] = {&nn, &w, &H, &sg, &gph, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext, &gi,
                         &gdd, &nd, &flag, &nogate};
         const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
         const size_t lds = grid_lds_bytes(T.grid_K, T.grid_dict_n);
@@ -1618,7 +1627,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
                                    H, goff, myd, upper, x, gate);
                 PSK_HIP(hipGetLastError());
             }
-            void *fargs[] = {&nn, &w, &H, &sg, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext,
+            void *fargs[] = {&nn, &w, &H, &sg, &gph, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext,
                              &gi, &gdd, &nd, &noflag, &gate};
             PSK_HIP(hipLaunchKernel(kf, dim3(nb), dim3(2 * kGridLanes), fargs, lds, s));
             hipLaunchKernelGGL(grid_flag_reset_kernel, dim3(1), dim3(1), 0, s, T.grid_flag);
@@ -1968,7 +1977,9 @@ void build_band(const HostFactor &F, int64_t B, int num_cus, int per_cu_max, int
 
 // Grid schedule plan (sptrsv_grid_kernel): width w = the most frequent solve-order distance >= 2
 // (the line length of a 2-D stencil), every dependency as (yd lines, xd positions) back, the
-// smallest skew sigma making ud = xd + sigma*yd >= 1 for all of them, and the ring depth. Rejected
+// smallest skew making ud = xd + g(y) - g(y - yd) >= 1 for all of them — the integer skew sigma
+// (g(y) = sigma*y), then sigma - 1/2 (g(y) = ((2 sigma - 1) y + phase) >> 1, either phase) when that
+// also holds — and the ring depth. Rejected
 // (ok = false) when the factor is not such a stencil: wide rows (> 8 entries), a dependency 64 or
 // more lines back, a skew above 8, more than kGridMaxPE patterns reaching into the band above, a
 // ring deeper than kGridMaxRing, or too few dependencies at distance w to call it a grid.
@@ -1978,7 +1989,7 @@ constexpr int64_t kGridMaxYd = 8;   // lines of the band above held in the polle
 
 struct GridPlan {
     bool ok = false;
-    int64_t w = 0, H = 0, sigma = 0, off = 0;
+    int64_t w = 0, H = 0, sigma2 = 0, phase = 0, off = 0;   // g(y) = (sigma2 * y + phase) >> 1
     int K = 0, pe = 0, maxyd = 0, ring = 0;
     GridExt ext{};
     double est = -1.0;
@@ -2013,10 +2024,33 @@ void plan_grid(const HostFactor &F, GridPlan &g) {
     // patterns and skew, with grid position p + off: off = 0, or the offset that makes the solve order
     // START with a partial line (w - n mod w empty positions before it: an upper factor of a grid whose
     // last natural line is short, e.g. SA level 2 of -FD 8192^2, 1365 lines of 911 + one of 228)
-    int64_t sigma = 0, maxyd = 0, maxud = 0, off = 0;
+    int64_t sigma2 = 0, phase = 0, maxyd = 0, maxud = 0, off = 0;
     std::vector<int32_t> ext_codes;
+    // the dependency codes under g(y) = (s2 * y + ph) >> 1; false when a dependency is not >= 1 step back
+    auto try_skew = [&](int64_t o, int64_t s2, int64_t ph) -> bool {
+        maxud = 0;
+        ext_codes.clear();
+        for (int64_t i = 0; i < n; ++i) {
+            const int64_t p = F.pos(i) + o, y = p / w, x = p % w;
+            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
+                const int64_t pd = F.pos(F.ci[j]) + o, yd = y - pd / w, xd = x - pd % w;
+                const int64_t ud = xd + grid_g(s2, ph, y) - grid_g(s2, ph, y - yd);
+                if (ud < 1 || ud >= 1023) return false;
+                maxud = std::max(maxud, ud);
+                const int32_t code = (int32_t)(ud * 64 + yd);
+                if (yd >= 1 && std::find(ext_codes.begin(), ext_codes.end(), code) == ext_codes.end()) {
+                    if ((int)ext_codes.size() == kGridMaxPE) return false;
+                    ext_codes.push_back(code);
+                }
+            }
+        }
+        off = o;
+        sigma2 = s2;
+        phase = ph;
+        return true;
+    };
     auto try_off = [&](int64_t o) -> bool {
-        sigma = 0;
+        int64_t sigma = 0;
         maxyd = 0;
         for (int64_t i = 0; i < n; ++i) {
             const int64_t p = F.pos(i) + o, y = p / w, x = p % w;
@@ -2028,23 +2062,14 @@ void plan_grid(const HostFactor &F, GridPlan &g) {
             }
         }
         if (sigma > 8) return false;
-        maxud = 0;
-        ext_codes.clear();
-        for (int64_t i = 0; i < n; ++i) {
-            const int64_t p = F.pos(i) + o, y = p / w, x = p % w;
-            for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j) {
-                const int64_t pd = F.pos(F.ci[j]) + o, yd = y - pd / w, xd = x - pd % w, ud = xd + sigma * yd;
-                if (ud < 1 || ud >= 1023) return false;
-                maxud = std::max(maxud, ud);
-                const int32_t code = (int32_t)(ud * 64 + yd);
-                if (yd >= 1 && std::find(ext_codes.begin(), ext_codes.end(), code) == ext_codes.end()) {
-                    if ((int)ext_codes.size() == kGridMaxPE) return false;
-                    ext_codes.push_back(code);
-                }
-            }
-        }
-        off = o;
-        return true;
+        // half a step less skew when the dependencies that need sigma occur on every other line only
+        // (PSK_GRID_HALF_SKEW=0: integer skews only)
+        static const bool half = [] {
+            const char *e = std::getenv("PSK_GRID_HALF_SKEW");
+            return !(e && std::atoi(e) == 0);
+        }();
+        if (half && sigma >= 2 && (try_skew(o, 2 * sigma - 1, 0) || try_skew(o, 2 * sigma - 1, 1))) return true;
+        return try_skew(o, 2 * sigma, 0);
     };
     bool planned = false;
     for (size_t ci = 0; ci < cand.size() && ci < 4 && !planned; ++ci) {
@@ -2061,19 +2086,19 @@ void plan_grid(const HostFactor &F, GridPlan &g) {
     g.w = w;
     g.off = off;
     g.H = (n + off + w - 1) / w;
-    g.sigma = sigma;
+    g.sigma2 = sigma2;
+    g.phase = phase;
     g.K = kmax <= 2 ? 2 : (kmax <= 4 ? 4 : 8);
     g.pe = (int)ext_codes.size();
     g.maxyd = (int)maxyd;
     g.ring = ring;
     for (int e = 0; e < g.pe; ++e) {
-        const int32_t yd = ext_codes[e] & 63, ud = ext_codes[e] >> 6;
+        const int32_t yd = ext_codes[e] & 63;
         g.ext.delta[e] = ext_codes[e];
         g.ext.yd[e] = yd;
-        g.ext.dq[e] = (int64_t)yd * w + (ud - sigma * yd);
     }
     const int64_t nbands = (g.H + kGridLanes - 1) / kGridLanes;
-    g.est = (double)((w - 1) + sigma * (g.H - 1) + 1) * kGridStepUs + (double)nbands * kGridLagUs;
+    g.est = (double)((w - 1) + grid_g(sigma2, phase, g.H - 1) + 1) * kGridStepUs + (double)nbands * kGridLagUs;
     (void)ndeps;
 }
 
@@ -2282,14 +2307,16 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         T.grid_ring = gp.ring;
         T.grid_w = gp.w;
         T.grid_H = gp.H;
-        T.grid_sigma = gp.sigma;
+        T.grid_sigma = gp.sigma2;
+        T.grid_phase = gp.phase;
         T.grid_off = gp.off;
         T.grid_ext = gp.ext;
-        // grid position p + off = (y*w + x): band b = y / 64, lane y % 64, step u - sigma*64b with u = x + sigma*y;
+        // grid position p + off = (y*w + x): band b = y / 64, lane y % 64, step u - g(64b) with u = x + g(y);
         // one GridStep block per (band, step): codes (ud*64 + yd), values in stored order, diagonal.
         // Padding: value 0, code 0 (the lane's own column of the current row); empty lanes: diagonal 1
         // so the wave's unused results stay finite (padding entries read them times 0.0)
-        T.grid_S = (gp.w - 1) + gp.sigma * (kGridLanes - 1) + 1;
+        // steps per band: g(y0 + 63) - g(y0) is the same for every band (sigma2 * y0 is even)
+        T.grid_S = (gp.w - 1) + grid_g(gp.sigma2, gp.phase, kGridLanes - 1) - grid_g(gp.sigma2, gp.phase, 0) + 1;
         const int64_t SB = gp.K == 2 ? GridStep<2>::kBytes : gp.K == 4 ? GridStep<4>::kBytes : GridStep<8>::kBytes;
         const int64_t nb = (gp.H + kGridLanes - 1) / kGridLanes, nsteps = nb * T.grid_S;
         const int64_t oc = kGridLanes * 2 * gp.K, od = oc + kGridLanes * 8 * gp.K;
@@ -2299,14 +2326,14 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
             for (int l = 0; l < kGridLanes; ++l) reinterpret_cast<double *>(gb + t * SB + od)[l] = 1.0;
         for (int64_t i = 0; i < n; ++i) {
             const int64_t p = F.pos(i) + gp.off, y = p / gp.w, x = p % gp.w, b = y / kGridLanes, l = y % kGridLanes;
-            const int64_t st = x + gp.sigma * y - gp.sigma * kGridLanes * b;
+            const int64_t st = x + grid_g(gp.sigma2, gp.phase, y) - grid_g(gp.sigma2, gp.phase, kGridLanes * b);
             unsigned char *blk = gb + (b * T.grid_S + st) * SB;
             uint16_t *codes = reinterpret_cast<uint16_t *>(blk) + l * gp.K;
             double *vals = reinterpret_cast<double *>(blk + oc) + l * gp.K;
             int k = 0;
             for (int32_t j = F.rp[i]; j < F.rp[i + 1]; ++j, ++k) {
                 const int64_t pd = F.pos(F.ci[j]) + gp.off, yd = y - pd / gp.w, xd = x - pd % gp.w;
-                codes[k] = (uint16_t)((xd + gp.sigma * yd) * 64 + yd);
+                codes[k] = (uint16_t)((xd + grid_g(gp.sigma2, gp.phase, y) - grid_g(gp.sigma2, gp.phase, y - yd)) * 64 + yd);
                 vals[k] = ova[j];
             }
             reinterpret_cast<double *>(blk + od)[l] = dg.empty() ? 1.0 : dg[i];
@@ -2503,6 +2530,17 @@ extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int
     for (int64_t i = 0; i < n; ++i) pinv[perm_r[i]] = (int32_t)i;
     return psk_prec_create_trisolve(n, l_rowptr, l_colidx, l_vals, 1, u_rowptr, u_colidx, u_vals, 0, pinv.data(),
                                     perm_c, out);
+}
+
+extern "C" int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out) {
+    if (!M || M->kind != PSK_PREC_ILU || (which != 0 && which != 1) || !out)
+        return fail(PSK_ERR_ARG, "psk_prec_trisolve_grid_info: not a triangular-solve chain / bad factor");
+    const TriFactor &T = which == 0 ? M->lo : M->up;
+    if (!T.present || T.grid_K == 0)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_grid_info: factor is not a 2-D stencil (grid schedule)");
+    const int64_t v[7] = {T.grid_w, T.grid_H, T.grid_sigma, T.grid_phase, T.grid_off, T.grid_S, T.grid_dict_n};
+    for (int i = 0; i < 7; ++i) out[i] = v[i];
+    return PSK_OK;
 }
 
 extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t *schedule,

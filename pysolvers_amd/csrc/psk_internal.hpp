@@ -194,9 +194,11 @@ struct AmgHierarchy;
 //    an LDS ring of `ring_words` doubles (0 = none) serves the in-block dependencies.
 //  * LDS: small factors (x fits LDS) solved by one workgroup, sync-free inside it with x in LDS.
 //  * grid: factors whose dependencies form a 2-D stencil in solve order (grid_w positions per line,
-//    every dependency (lines back, positions back) within 63 lines and skewable by grid_sigma):
+//    every dependency (lines back, positions back) within 63 lines and skewable):
 //    one wave per band of 64 lines, all 64 lines advancing together along the skewed coordinate
-//    u = x + sigma y, in-band dependencies through an LDS ring of the last grid_ring steps, only
+//    u = x + g(y), g(y) = (grid_sigma * y + grid_phase) >> 1 (grid_sigma is TWICE the skew, so a
+//    half-integer skew is an odd grid_sigma), in-band dependencies through an LDS ring of the last
+//    grid_ring steps, only
 //    the band above through published values (sptrsv_grid_kernel).
 //  * part: rows cut into strips of their natural index, one workgroup per strip (per CU), the
 //    strip's own dependencies through an LDS cache, the others through published values
@@ -208,7 +210,6 @@ constexpr int kGridMaxPE = 8;   // distinct dependency patterns reaching into th
 struct GridExt {
     int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
     int32_t yd[kGridMaxPE];     // lines back
-    int64_t dq[kGridMaxPE];     // solve-order distance yd * w + xd
 };
 struct TriFactor {
     bool present = false, upper = false;
@@ -237,7 +238,8 @@ struct TriFactor {
     int grid_dict_n = 0;
     int32_t *grid_flag = nullptr;   // dictionary kernel: a step's quotient needed the IEEE re-solve (zeroed after it)
     int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
-    int64_t grid_w = 0, grid_H = 0, grid_sigma = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
+    int64_t grid_w = 0, grid_H = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
+    int64_t grid_sigma = 0, grid_phase = 0;      // g(y) = (grid_sigma * y + grid_phase) >> 1 (twice the skew)
     int64_t grid_off = 0;   // empty grid positions before the first row (a partial first line)
     GridExt grid_ext{};
     // part layout: position k = part_seg[w] + q (workgroup w's q-th row); rows, entries (codes) in it

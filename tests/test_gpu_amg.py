@@ -9,6 +9,8 @@ Bars (written here, not inferred):
 Solver-level parity of PCG/GMRES + AMG / RightIC runs in test_gpu_parity.test_solver_matches_reference
 (the golden manifest carries those cases).
 """
+import functools
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -267,7 +269,9 @@ def test_grid_schedule_sa_coarse_operator(psk):
     """An SA coarse operator of a 2-D grid (level 3 of the -FD 1024^2 hierarchy: 342 x 512 aggregate
     lines, dependencies up to 2 lines back with diagonal neighbours): the grid schedule takes it, and
     matches the band schedule bit for bit and spsolve_triangular to 1e-12; with a permuted input and
-    output (the pre-gather path) it matches the same solve done by numpy indexing."""
+    output (the pre-gather path) it matches the same solve done by numpy indexing. Its dependency
+    (1 line back, 2 positions ahead) sits on every other line only, so the plan takes the half-integer
+    skew 5/2 (g(y) = (5y + 1) >> 1: 1620 steps per sweep where the integer skew 3 needs 1874)."""
     from oracle import fdlap
     from pysolvers_amd.Linear import SmoothedAggregationMLHierarchy, TriangularSolveChain
     A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 1024)
@@ -279,6 +283,9 @@ def test_grid_schedule_sa_coarse_operator(psk):
     ref = spla.spsolve_triangular(U, v, lower=False)
     M = TriangularSolveChain(n, U=U)
     assert _grid_available(M, "U")
+    gi = M.grid_info("U")
+    assert (gi["w"], gi["sigma2"], gi["phase"]) == (342, 5, 1), gi
+    assert gi["dict_records"] > 0
     g = M.apply(v)
     assert _rel(g, ref) <= 1e-12
     M.schedule("U", set="band")
@@ -288,6 +295,43 @@ def test_grid_schedule_sa_coarse_operator(psk):
     P = TriangularSolveChain(n, U=U, gather_in=pin, gather_out=pout)
     assert _grid_available(P, "U")
     assert np.array_equal(P.apply(v), M.apply(v[pin])[pout])
+
+
+@functools.lru_cache(maxsize=1)
+def _fd2048_sa_levels():
+    from oracle import fdlap
+    from pysolvers_amd.Linear import SmoothedAggregationMLHierarchy
+    h = SmoothedAggregationMLHierarchy(-fdlap.fd_laplacian_2d(-1.0, 1.0, 2048), numLevels=5)
+    return {lev: h.matrix(lev).tocsr() for lev in (2, 3)}
+
+
+@pytest.mark.parametrize("level,lower", [(3, False), (3, True), (2, False), (2, True)])
+def test_grid_half_skew_sa_levels(psk, monkeypatch, level, lower):
+    """SA levels 3 and 2 of the -FD 2048^2 hierarchy (1024 x 683 and 342 x 228 aggregate lines) take
+    the half-integer skew 3/2 (their dependencies 1 line back and 1 ahead sit on every other line),
+    upper and lower factors: within 1e-12 of spsolve_triangular, and bit-identical to the band
+    schedule and to the grid schedule's per-step records (no dictionary)."""
+    from pysolvers_amd.Linear import TriangularSolveChain
+    Al = _fd2048_sa_levels()[level]
+    T = (sp.tril(Al) if lower else sp.triu(Al)).tocsr()
+    n = Al.shape[0]
+    f = "L" if lower else "U"
+    v = np.random.default_rng(level).standard_normal(n)
+    ref = spla.spsolve_triangular(T, v, lower=lower)
+    outs = []
+    for dict_on in ("1", "0"):
+        monkeypatch.setenv("PSK_TRISOLVE_GRID_DICT", dict_on)
+        M = TriangularSolveChain(n, **({"L": T} if lower else {"U": T}))
+        assert _grid_available(M, f)
+        gi = M.grid_info(f)
+        assert gi["sigma2"] % 2 == 1, gi
+        assert (gi["dict_records"] > 0) == (dict_on == "1"), gi
+        outs.append(M.apply(v))
+        assert np.array_equal(M.apply(v), outs[-1])      # re-apply (sentinel refill), deterministic
+    assert np.array_equal(outs[0], outs[1])
+    assert _rel(outs[0], ref) <= 1e-12
+    M.schedule(f, set="band")
+    assert np.array_equal(M.apply(v), outs[0])
 
 
 @pytest.mark.parametrize("m,lower", [(300, False), (300, True), (1024, False)])
