@@ -242,6 +242,11 @@ int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t 
  * >> 1)), leading empty positions off, steps per 64-line band, dictionary records (0 = per-step
  * records). PSK_ERR_UNSUPPORTED when the factor is not a 2-D stencil. No compute (diagnostics, tests). */
 int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out);
+/* Host-only: the grid plan psk_prec_create_trisolve would make for one triangular factor (CSR with its
+ * diagonal; upper = 1: solved from the last row up), without any device work — out[0..6] = w, H,
+ * sigma2, phase, off, steps per band, record width K. PSK_ERR_UNSUPPORTED when it is not a 2-D stencil. */
+int psk_trisolve_grid_plan(int64_t n, const int32_t *rowptr, const int32_t *colidx, const double *vals,
+                           int32_t upper, int64_t *out);
 /* kind, size and triangular-solve shape of a preconditioner (any out pointer may be NULL). */
 int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, int64_t *nnz_u,
                   int64_t *levels_l, int64_t *levels_u);

@@ -87,6 +87,22 @@ class TriangularSolveChain(DeviceOperator, GenericPreconditioner):
         return dict(zip(("w", "H", "sigma2", "phase", "off", "steps", "dict_records"), list(out)))
 
 
+def grid_plan(T, upper):
+    """The grid plan (psk_trisolve_grid_plan, host only) of triangular factor T (CSR with its diagonal;
+    upper: solved from the last row up): dict(w, H, sigma2, phase, off, steps, K), or None when T is not
+    a 2-D stencil. Position y*w + x - off runs at step x + ((sigma2*y + phase) >> 1)."""
+    T = sp.csr_matrix(T)
+    rp = np.ascontiguousarray(T.indptr, dtype=np.int32)
+    ci = np.ascontiguousarray(T.indices, dtype=np.int32)
+    va = np.ascontiguousarray(T.data, dtype=np.float64)
+    out = (N.I64 * 7)()
+    rc = N.lib.psk_trisolve_grid_plan(T.shape[0], N.ptr(rp), N.ptr(ci), N.ptr(va), 1 if upper else 0, out)
+    if rc == -5:   # PSK_ERR_UNSUPPORTED
+        return None
+    N.check(rc, "psk_trisolve_grid_plan")
+    return dict(zip(("w", "H", "sigma2", "phase", "off", "steps", "K"), list(out)))
+
+
 def superlu_transposed_solver(lu):
     """x = lu.solve(b, trans='T') as a chain: with Pr B Pc = L U, B^T x = b gives
     x = Pr^T L^-T U^-T Pc^T b, i.e. gather_in = perm_c^-1, lower = U^T (non-unit),

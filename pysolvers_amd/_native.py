@@ -79,6 +79,7 @@ SIGNATURES = {
     "psk_prec_trisolve_schedule": (ctypes.c_int, [P, I32, I32, ctypes.POINTER(I32), ctypes.POINTER(I64),
                                                    ctypes.POINTER(I32), ctypes.POINTER(F64), ctypes.POINTER(F64)]),
     "psk_prec_trisolve_grid_info": (ctypes.c_int, [P, I32, ctypes.POINTER(I64)]),
+    "psk_trisolve_grid_plan": (ctypes.c_int, [I64, P, P, P, I32, ctypes.POINTER(I64)]),
     "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),
     "psk_mm_info": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.POINTER(I64)] * 3),
     "psk_mm_read": (ctypes.c_int, [ctypes.c_char_p, P, P, P, ctypes.POINTER(I64)]),

@@ -2532,6 +2532,25 @@ extern "C" int psk_prec_create_ilu(int64_t n, const int32_t *l_rowptr, const int
                                     perm_c, out);
 }
 
+extern "C" int psk_trisolve_grid_plan(int64_t n, const int32_t *rowptr, const int32_t *colidx, const double *vals,
+                                      int32_t upper, int64_t *out) {
+    if (n <= 0 || !rowptr || !colidx || !vals || !out) return fail(PSK_ERR_ARG, "psk_trisolve_grid_plan: bad arguments");
+    HostFactor F;
+    F.n = n;
+    F.upper = upper != 0;
+    std::vector<double> ova, dg;
+    PSK_TRY(split_factor(n, rowptr, colidx, vals, upper == 0, false, F.rp, F.ci, ova, dg));
+    GridPlan gp;
+    plan_grid(F, gp);
+    if (!gp.ok || n > kGridMaxRows)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_trisolve_grid_plan: factor is not a 2-D stencil (grid schedule)");
+    const int64_t v[7] = {gp.w, gp.H, gp.sigma2, gp.phase, gp.off,
+                          (gp.w - 1) + grid_g(gp.sigma2, gp.phase, kGridLanes - 1) - grid_g(gp.sigma2, gp.phase, 0) + 1,
+                          (int64_t)gp.K};
+    for (int i = 0; i < 7; ++i) out[i] = v[i];
+    return PSK_OK;
+}
+
 extern "C" int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out) {
     if (!M || M->kind != PSK_PREC_ILU || (which != 0 && which != 1) || !out)
         return fail(PSK_ERR_ARG, "psk_prec_trisolve_grid_info: not a triangular-solve chain / bad factor");
