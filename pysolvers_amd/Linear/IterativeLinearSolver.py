@@ -88,13 +88,16 @@ class IterativeLinearSolver(LinearSolver, IterativeSolver):
         normb_caller = 0.0
         if custom:
             normb_caller = float(self.norm(_host_copy(b)))     # self.norm(b)  PCGSolver.py:86, GMRESSolver.py:66
-            if normb_caller == 0.0:                            # :87-88 / :67-68
-                x0 = DeviceVector(n) if isinstance(b, DeviceVector) else np.zeros(n)
-                if isinstance(x0, DeviceVector):
-                    x0.zero()
-                return self.handleConvergence(0, _like(b, x0), 0, 0)
+            zero_b = normb_caller == 0.0
+        else:
+            zero_b = _is_zero_norm(b, n)                       # the default norm: ||b|| == 0 iff b.b == 0
+        if zero_b:                                             # :87-88 / :67-68: x = 0, before the
+            x0 = DeviceVector(n) if isinstance(b, DeviceVector) else np.zeros(n)   # preconditioner is formed
+            if isinstance(x0, DeviceVector):
+                x0.zero()
+            return self.handleConvergence(0, _like(b, x0), 0, 0)
         dA = self._device_matrix(A)
-        echo = self._echo_setup and (custom or not _is_zero_norm(b, n))
+        echo = self._echo_setup
         if echo:                                            # PCGSolver.py:91 (unconditional in the reference)
             print('prec frozen = ', self.precFrozen())
         if self.precond is None or not self.precFrozen():   # PCGSolver.py:92-94

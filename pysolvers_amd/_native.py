@@ -180,9 +180,12 @@ def _shutdown():
     global shut_down
     if not shut_down:
         shut_down = True
-        # with torch never imported libpsk is the process's only HIP user: release the runtime's own device
-        # state too (a cooperative launch otherwise left exit() faulting under rocprofv3)
-        lib.psk_shutdown_ex(PSK_SHUTDOWN_RESET_DEVICE if "torch" not in sys.modules else 0)
+        # The exit fault under rocprofv3 (profiles/r4_exit_fault.txt) was fixed by launching the triangular
+        # solves without hipLaunchCooperativeKernel and by keeping torch's bundled HIP runtime out of a one-rank
+        # bench; a device reset did not change it. It would also destroy every other HIP user's allocations
+        # in the process, so it is opt-in (PSK_SHUTDOWN_RESET=1).
+        reset = os.environ.get("PSK_SHUTDOWN_RESET") == "1"
+        lib.psk_shutdown_ex(PSK_SHUTDOWN_RESET_DEVICE if reset else 0)
 
 
 atexit.register(_shutdown)

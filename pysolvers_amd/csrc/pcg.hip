@@ -34,6 +34,7 @@ struct PcgState {
     double tauNormB;
     int64_t live;      // k of the last K2 that ran to completion (no breakdown); -1 before the loop
     int64_t *hdone;    // host-mapped stamp of the iteration that set `done` (nullptr: none), see set_done
+    int64_t hgen;      // this solve's generation in the stamp's high bits (kStampGenShift)
     double last_hist;  // the latest reported ||r_k|| (resid_recursive without copying the history back)
     int32_t x_written; // 1 once x has been stored (Jacobi/identity: x0 = 0 is implicit until the first flush)
     int32_t pad;
@@ -45,17 +46,22 @@ struct PcgState {
 // device-to-host copy (a blit kernel) on the solver's stream. The stamp lets the host act on the state
 // as of the chunk it waited for, not a later one its GPU has already run: every rank of a sharded
 // solve then stops after the same chunk and enqueues the same collectives.
+// The word is shared by every solve on the device; each solve tags its stamps with its own generation
+// (high bits), so a kernel still queued from an earlier solve that failed on the host side cannot leave a
+// stamp the next solve's poll would act on.
+constexpr int kStampGenShift = 40;
+constexpr int64_t kStampMask = ((int64_t)1 << kStampGenShift) - 1;
 __device__ __forceinline__ void set_done(PcgState *st, int32_t v, int64_t stamp) {
     st->done = v;
     if (st->hdone) {
-        __hip_atomic_store(st->hdone, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(st->hdone, st->hgen | stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __threadfence_system();
     }
 }
 
 // the solver state after the init sums bb = b.b and ur = u.r (PCGSolver.py:86-105)
 __device__ __forceinline__ void pcg_init_state(double bb, double ur, double tau, PcgState *st, double *udr,
-                                               int64_t *hdone, int32_t x_written) {
+                                               int64_t *hdone, int64_t hgen, int32_t x_written) {
     const double normB = sqrt(bb);                 // self.norm(b)   :86
     st->normB = normB;
     st->tauNormB = tau * normB;
@@ -64,6 +70,7 @@ __device__ __forceinline__ void pcg_init_state(double bb, double ur, double tau,
     st->brk_kind = 0;
     st->live = -1;
     st->hdone = hdone;
+    st->hgen = hgen;
     st->last_hist = normB;
     st->x_written = x_written;
     udr[0] = ur;
@@ -85,8 +92,9 @@ struct PcgInitFin {
     PcgState *st;
     double *udr;
     int64_t *hdone;
+    int64_t hgen;
     int32_t x_written;
-    __device__ void operator()(const double *r) const { pcg_init_state(r[0], r[1], tau, st, udr, hdone, x_written); }
+    __device__ void operator()(const double *r) const { pcg_init_state(r[0], r[1], tau, st, udr, hdone, hgen, x_written); }
 };
 
 // ---- K0 (Jacobi/identity): r = b; p_0 = M r; [b.b, u.r] -----------------------------------
@@ -140,8 +148,8 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const doubl
 
 // sharded init: the per-rank sums all-gathered, added in rank order (bit-identical on every rank)
 __global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgState *st, double *udr,
-                                       int64_t *hdone) {
-    if (threadIdx.x == 0) pcg_init_state(rank_sum(g, P, 2, 0), rank_sum(g, P, 2, 1), tau, st, udr, hdone, 0);
+                                       int64_t *hdone, int64_t hgen) {
+    if (threadIdx.x == 0) pcg_init_state(rank_sum(g, P, 2, 0), rank_sum(g, P, 2, 1), tau, st, udr, hdone, hgen, 0);
 }
 
 // ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
@@ -523,8 +531,9 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     PSK_TRY(gridsum_prepare(c, nv, 1, w.part3, &gs3));
     // the host-mapped done stamp the kernels write (set_done); no kernel of an earlier solve is running
     volatile int64_t *hdone = kit->hmap;
+    const int64_t hgen = (int64_t)(++kit->solve_gen & 0x7FFFFF) << kStampGenShift;
     *hdone = 0;
-    const PcgInitFin fin{ctl->tau, w.st, w.udr, const_cast<int64_t *>(hdone), gen ? 1 : 0};
+    const PcgInitFin fin{ctl->tau, w.st, w.udr, const_cast<int64_t *>(hdone), hgen, gen ? 1 : 0};
     const double *bd = b;
     if (!dev_io) {   // host b staged in the Ap buffer (unused until the first SpMV)
         PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
@@ -549,7 +558,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     if (sharded) {
         PSK_TRY(allgather(A, w.pinit, w.initg, 2, s));
         hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(64), 0, s, w.initg, P, ctl->tau, w.st, w.udr,
-                           const_cast<int64_t *>(hdone));
+                           const_cast<int64_t *>(hdone), hgen);
         PSK_HIP(hipGetLastError());
     }
 
@@ -604,7 +613,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             if (rc == PSK_OK && chunk - 1 - L >= 0) {
                 const int os = (int)((chunk - 1 - L) % NS);
                 if (hipEventSynchronize(fev[os]) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
-                else if (*hdone != 0 && *hdone <= (chunk - L) * (int64_t)C + 1) break;
+                else {
+                    const int64_t hv = *hdone;   // a stamp of this solve only (its generation)
+                    if ((hv & ~kStampMask) == hgen && (hv & kStampMask) != 0 &&
+                        (hv & kStampMask) <= (chunk - L) * (int64_t)C + 1)
+                        break;
+                }
             }
             if (rc != PSK_OK) break;
         }
@@ -763,5 +777,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             res->spmv_ms = nt > 0 ? tot / (double)nt : 0.0;
         }
     }
+    // a solve that failed on the host side leaves no kernel of its own running behind the next solve
+    if (rc != PSK_OK) (void)hipStreamSynchronize(s);
     return rc;
 }

@@ -61,6 +61,7 @@ constexpr int kTimedSlots = 64;   // sampled SpMV timing event pairs of one solv
 // (VERDICT r3 weak #3). One solve at a time per device: `solve_mu` is held by psk_pcg/psk_gmres.
 struct SolveKit {
     bool ready = false;
+    uint64_t solve_gen = 0;       // PCG solves started (tags the done stamps, pcg.hip set_done)
     int64_t *hmap = nullptr;      // host-mapped coherent words the kernels write (PCG done stamp at [0])
     void *hstage = nullptr;       // pinned staging for the end-of-solve state / error-word copies (4 KiB)
     hipEvent_t ev0 = nullptr, ev1 = nullptr;   // loop_ms (timing)

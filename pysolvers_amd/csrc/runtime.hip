@@ -19,9 +19,10 @@ int fail(int code, const std::string &msg) {
 
 static std::mutex g_ctx_mu;
 static Context g_ctx[64];
-static bool g_shut = false;
+// set FIRST by psk_shutdown_ex (before anything is torn down), read without a lock by every entry point
+static std::atomic<bool> g_shut{false};
 
-bool lib_shut_down() { return g_shut; }
+bool lib_shut_down() { return g_shut.load(std::memory_order_acquire); }
 static std::atomic<int> g_live_rccl{0};   // RCCL communicators alive (psk_comm_init .. psk_comm_destroy)
 void rccl_comm_count(int delta) { g_live_rccl += delta; }
 
@@ -65,6 +66,7 @@ int ctx(Context **out) {
     PSK_HIP(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(PSK_ERR_ARG, "device index out of range");
     std::lock_guard<std::mutex> lk(g_ctx_mu);
+    if (g_shut) return fail(PSK_ERR_ARG, "libpsk was shut down (psk_shutdown)");
     Context &c = g_ctx[dev];
     if (c.stream == nullptr) {
         PSK_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
@@ -270,8 +272,13 @@ int psk_dfree(void *dptr) {
 int psk_shutdown(void) { return psk_shutdown_ex(0); }
 
 int psk_shutdown_ex(int32_t flags) {
-    std::lock_guard<std::mutex> lk(g_ctx_mu);
-    if (g_shut) return PSK_OK;
+    {
+        // refuse new work first: ctx() (which tests the flag under the same lock) fails from here on, so no
+        // context is created and no solve starts on one being torn down. The lock is not held below: a
+        // running solve holds its context's solve_mu and may take g_ctx_mu (comm_stream).
+        std::lock_guard<std::mutex> lk(g_ctx_mu);
+        if (g_shut.exchange(true, std::memory_order_acq_rel)) return PSK_OK;
+    }
     int rc = PSK_OK;
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -279,6 +286,9 @@ int psk_shutdown_ex(int32_t flags) {
         Context &c = g_ctx[d];
         if (c.stream == nullptr) continue;
         if (hipSetDevice(d) != hipSuccess) continue;
+        // a solve already running on this device (another thread) finishes before its streams, events and
+        // staging go away
+        std::lock_guard<std::mutex> solve_lk(c.solve_mu);
         if (hipStreamSynchronize(c.stream) != hipSuccess && rc == PSK_OK) rc = fail(PSK_ERR_HIP, "psk_shutdown: sync");
         if (c.comm_stream) (void)hipStreamSynchronize(c.comm_stream);
         SolveKit &k = c.kit;
@@ -311,13 +321,13 @@ int psk_shutdown_ex(int32_t flags) {
         (void)hipStreamDestroy(c.stream);
         c.comm_stream = nullptr;
         c.stream = nullptr;
-        // the HIP runtime's own per-device state too (its cooperative-launch queue among it), while HSA is
-        // still alive: under rocprofv3 the profiler finalises HSA in its exit hook, and a HIP teardown
-        // after that — in exit(), once any cooperative launch ran — faulted (profiles/r4_exit_fault.txt)
+        // hipDeviceReset only when the caller asks for it (PSK_SHUTDOWN_RESET_DEVICE; the Python binding
+        // passes it only with PSK_SHUTDOWN_RESET=1): it destroys every allocation of the device, other HIP
+        // users' in the process included. It is not what fixed the exit fault under rocprofv3 — dropping the
+        // cooperative launches was (profiles/r4_exit_fault.txt:35: the reset changed nothing).
         if ((flags & PSK_SHUTDOWN_RESET_DEVICE) && g_live_rccl.load() == 0) (void)hipDeviceReset();
     }
     (void)hipSetDevice(cur);
-    g_shut = true;
     return rc;
 }
 

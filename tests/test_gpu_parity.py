@@ -174,6 +174,10 @@ def test_zero_rhs(psk, kind):
     f = psk.PCG if kind == "pcg" else psk.GMRES
     st = f(control=_ctl(maxiter=50)).makeSolver().solve(A, np.zeros(A.shape[0]))
     assert st.success() and st.iters() == 1 and not np.any(st.soln())
+    # PCGSolver.py:86-88 / GMRESSolver.py:66-68 return before the preconditioner is formed
+    s = f(control=_ctl(maxiter=50), precond=psk.Jacobi()).makeSolver()
+    st = s.solve(A, psk.DeviceVector.from_numpy(np.zeros(A.shape[0])))
+    assert st.success() and st.iters() == 1 and not np.any(st.soln().numpy()) and s.precond is None
 
 
 def test_pcg_breakdown_zero_matrix(psk):
