@@ -56,7 +56,7 @@ def spmv_bytes(n, nnz):
 
 
 PCG_VEC_BYTES_PER_ROW = 74   # K2 (r, Ap, dinv in; r out) + K3 (r, p, dinv in; p out; x and p_{k-3..k-1} every 4th iteration), Jacobi
-LAYOUT_NAMES = {0: "csr", 1: "sliced", 2: "sliced_wide", 3: "sliced_dict"}   # PSK_LAYOUT_*
+LAYOUT_NAMES = {0: "csr", 1: "sliced", 2: "sliced_wide", 3: "sliced_dict", 4: "diag"}   # PSK_LAYOUT_*
 
 
 def pcg_iter_bytes(n, nnz, jacobi=True):
@@ -606,7 +606,7 @@ def pmc_traffic(path, m, world, mode, sliced):
         return {"traffic": None, "traffic_note": "%s is for another side / rank count" % src}
     if d.get("libpsk_sha256") != lib_sha256():
         return {"traffic": None, "traffic_note": "%s was captured with another libpsk.so build" % src}
-    pat = re.compile((r"psk::spmv_(uniform_multi|uniform|sliced)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
+    pat = re.compile((r"psk::spmv_(uniform_multi|uniform|sliced|diag)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
     hits = [k for k in d["kernels"] if pat.search(k)]
     if len(hits) != 1:
         return {"traffic": None, "traffic_note": "%s holds %d SpMV kernels of mode %d" % (src, len(hits), mode)}

@@ -163,20 +163,28 @@ int psk_csr_info(const psk_csr *A, int64_t *n, int64_t *nnz);
  *   PSK_LAYOUT_SLICED_WIDE  the same with 32-bit columns in every slice;
  *   PSK_LAYOUT_SLICED_DICT  SLICED with the values replaced by one-byte indices into a dictionary of
  *                           the matrix's distinct values (at most 8 bit patterns: stencils, graph
- *                           Laplacians), 3 B per slot with 16-bit columns.
- * Every creation path picks SLICED_DICT (values permitting) or SLICED when its stream is no larger
- * than the CSR stream (12 B/entry + 4 B/row); env PSK_SPMV_LAYOUT=csr|sliced|sliced_wide|sliced_dict
- * overrides (sliced: no dictionary). Forcing SLICED_DICT on a matrix with more than 8 distinct
- * values fails with PSK_ERR_UNSUPPORTED. set = -1 queries, a PSK_LAYOUT_*
+ *                           Laplacians), 3 B per slot with 16-bit columns;
+ *   PSK_LAYOUT_DIAG         (round 5) diagonal storage: every row's entries lie, in stored order, on
+ *                           a subsequence of K <= 8 diagonals c = row + d_j (a row-block shard's
+ *                           outside columns mapped to its halo) and all entries of a diagonal hold
+ *                           one value (constant-coefficient stencils such as FDLaplacian2D); the
+ *                           offsets and values are kernel arguments, one presence byte per row.
+ * Every creation path picks DIAG when the matrix has one, else SLICED_DICT (values permitting) or
+ * SLICED when its stream is no larger than the CSR stream (12 B/entry + 4 B/row); env
+ * PSK_SPMV_LAYOUT=csr|sliced|sliced_wide|sliced_dict|diag overrides (sliced: no dictionary),
+ * PSK_SPMV_DIAG=0 leaves DIAG out of the automatic choice. Forcing SLICED_DICT on a matrix with more
+ * than 8 distinct values, or DIAG on one without the diagonal structure, fails with
+ * PSK_ERR_UNSUPPORTED. set = -1 queries, a PSK_LAYOUT_*
  * value switches (building or freeing the copy). Out: *slots = padded slots of the sliced copy (0
- * without one), *packed_slots = those in 16-bit slices, *stream_bytes = matrix bytes one SpMV
- * streams in the current layout (CSR: 12 nnz + 4 (n+1)). Out pointers may be NULL. Replaces
+ * without one; DIAG: n K), *packed_slots = those in 16-bit slices, *stream_bytes = matrix bytes one
+ * SpMV streams in the current layout (CSR: 12 nnz + 4 (n+1); DIAG: n). Out pointers may be NULL. Replaces
  * nothing in the reference (scipy keeps CSR): a device storage choice under mvmult
  * (IterativeLinearSolver.py:94-106). */
 #define PSK_LAYOUT_CSR         0
 #define PSK_LAYOUT_SLICED      1
 #define PSK_LAYOUT_SLICED_WIDE 2
 #define PSK_LAYOUT_SLICED_DICT 3
+#define PSK_LAYOUT_DIAG        4
 int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int64_t *packed_slots,
                    int64_t *stream_bytes);
 /* Copy the arrays back to host buffers (any pointer may be NULL). */
@@ -242,6 +250,16 @@ int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t 
  * >> 1)), leading empty positions off, steps per 64-line band, dictionary records (0 = per-step
  * records). PSK_ERR_UNSUPPORTED when the factor is not a 2-D stencil. No compute (diagnostics, tests). */
 int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out);
+/* Lab / tests of the triangular solves' forward progress (round 5; replaces nothing in the reference).
+ * psk_lab_occupy_begin starts `wgs` workgroups of 1024 threads holding `lds_bytes` of LDS each on a
+ * stream of their own, spinning until psk_lab_occupy_end releases them behind everything enqueued on the
+ * solver's stream so far (or `seconds` pass: *timed_out = 1); a solve enqueued in between can use only
+ * what they leave free. psk_lab_trisolve_workers: the workgroups the last sync-free launch of factor
+ * `which` enrolled and the grid it was launched with (the sync-free schedule deals its rows over the
+ * workgroups that started, not over the grid). */
+int psk_lab_occupy_begin(int32_t wgs, int32_t lds_bytes, double seconds);
+int psk_lab_occupy_end(int32_t *timed_out);
+int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid);
 /* Host-only: the grid plan psk_prec_create_trisolve would make for one triangular factor (CSR with its
  * diagonal; upper = 1: solved from the last row up), without any device work — out[0..6] = w, H,
  * sigma2, phase, off, steps per band, record width K. PSK_ERR_UNSUPPORTED when it is not a 2-D stencil. */

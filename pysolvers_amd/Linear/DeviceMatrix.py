@@ -140,7 +140,7 @@ class DeviceCSR:
     def handle(self):
         return self._h
 
-    _LAYOUTS = {"csr": 0, "sliced": 1, "sliced_wide": 2, "sliced_dict": 3}
+    _LAYOUTS = {"csr": 0, "sliced": 1, "sliced_wide": 2, "sliced_dict": 3, "diag": 4}
 
     @property
     def layout(self):

@@ -19,7 +19,7 @@ PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_EXIT_NONE, PSK_EXIT_TOLERANCE, PSK_EXIT_ARNOLDI_BREAKDOWN, PSK_EXIT_MAXITER, PSK_EXIT_DOT_BREAKDOWN = 0, 1, 2, 3, 4
 PSK_HOST, PSK_DEVICE = 0, 1
 PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
-PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE, PSK_LAYOUT_SLICED_DICT = 0, 1, 2, 3
+PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE, PSK_LAYOUT_SLICED_DICT, PSK_LAYOUT_DIAG = 0, 1, 2, 3, 4
 PSK_UNIQUE_ID_BYTES = 128
 
 STATUS_NAMES = {PSK_CONVERGED: "converged", PSK_MAXITER: "maxiter", PSK_BREAKDOWN: "breakdown",
@@ -79,6 +79,9 @@ SIGNATURES = {
     "psk_prec_trisolve_schedule": (ctypes.c_int, [P, I32, I32, ctypes.POINTER(I32), ctypes.POINTER(I64),
                                                    ctypes.POINTER(I32), ctypes.POINTER(F64), ctypes.POINTER(F64)]),
     "psk_prec_trisolve_grid_info": (ctypes.c_int, [P, I32, ctypes.POINTER(I64)]),
+    "psk_lab_occupy_begin": (ctypes.c_int, [I32, I32, F64]),
+    "psk_lab_occupy_end": (ctypes.c_int, [ctypes.POINTER(I32)]),
+    "psk_lab_trisolve_workers": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "psk_trisolve_grid_plan": (ctypes.c_int, [I64, P, P, P, I32, ctypes.POINTER(I64)]),
     "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),
     "psk_mm_info": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.POINTER(I64)] * 3),

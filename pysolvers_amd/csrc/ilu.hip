@@ -36,6 +36,7 @@
 #include "psk_internal.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <unordered_map>
 #include <cstdio>
 #include <cstring>
@@ -73,6 +74,104 @@ __device__ __forceinline__ double wait_pub(const double *p, int32_t *err) {
         xv = load_pub(p);
     }
     return xv;
+}
+
+// ---- forward progress without co-residency (round 5) ---------------------
+// The spin-waiting schedules no longer assume that every workgroup of their grid is resident at once (a
+// plain launch promises nothing: a caller's kernels on other streams, a second process on the device or
+// the halo exchange's kernels may hold CUs). Each takes its work from counters in TriFactor::sched (words
+// on separate 256-B lines, zero between launches):
+//  * band / narrow band / grid: a workgroup draws its next block (band) from a ticket counter instead of
+//    deriving it from blockIdx.x. A block waits only on earlier blocks, and every earlier block was drawn
+//    by a workgroup that has started and runs to completion, so the lowest unfinished block can always
+//    proceed. The drawer of the launch's last ticket re-arms the counter.
+//  * sync-free: a row may wait on ANY earlier position, so rows are dealt round-robin over the waves that
+//    ENROLLED: the first workgroup to start waits until all gridDim.x have enrolled or kEnrollWaitTicks
+//    have passed, closes the enrolment and publishes the count R; positions are dealt over those 4R waves,
+//    and workgroups that arrive later leave at once. Every row is then held by a running wave. The last
+//    workgroup to leave re-arms the words.
+// The grid is unchanged when the device is free (all workgroups enrol within a few us); under contention
+// the solve runs on fewer waves instead of waiting on workgroups that cannot start.
+constexpr int kSchedTicket = 0, kSchedPub = 64, kSchedExit = 128, kSchedLast = 192, kSchedWords = 256;
+constexpr uint32_t kEnrollClosed = 0x80000000u;
+constexpr uint64_t kEnrollWaitTicks = 2000;   // s_memrealtime (100 MHz): 20 us
+
+__device__ __forceinline__ uint32_t sched_add(uint32_t *w, uint32_t v) {
+    return __hip_atomic_fetch_add(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t sched_load(const uint32_t *w) {
+    return __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void sched_store(uint32_t *w, uint32_t v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// thread 0: the next block of a ticket-dealt launch (every workgroup draws until it gets one >= nblocks,
+// so the launch draws exactly nblocks + gridDim.x tickets; the last drawer re-arms the counter)
+__device__ __forceinline__ int64_t sched_next_block(uint32_t *sched, int64_t nblocks) {
+    const uint32_t t = sched_add(sched + kSchedTicket, 1u);
+    if ((int64_t)t == nblocks + (int64_t)gridDim.x - 1) sched_store(sched + kSchedTicket, 0u);
+    return t;
+}
+
+// thread 0: the block of a launch in which every workgroup draws exactly one (the grid schedule's bands);
+// the drawer of ticket gridDim.x - 1 re-arms the counter
+__device__ __forceinline__ int64_t sched_one_block(uint32_t *sched) {
+    const uint32_t t = sched_add(sched + kSchedTicket, 1u);
+    if (t == gridDim.x - 1) sched_store(sched + kSchedTicket, 0u);
+    return t;
+}
+
+// every thread: enrol this workgroup (see above); returns its worker rank (-1: arrived after the close) and
+// the worker count R in *R. Bounded: the decider waits at most kEnrollWaitTicks.
+__device__ __forceinline__ int sched_enroll(uint32_t *sched, uint32_t *R, int32_t *err) {
+    __shared__ int s_rank;
+    __shared__ uint32_t s_R;
+    if (threadIdx.x == 0) {
+        const uint32_t G = gridDim.x;
+        const uint32_t old = sched_add(sched + kSchedTicket, 1u);
+        if (old & kEnrollClosed) {
+            s_rank = -1;
+            s_R = 0;
+        } else if (old == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while ((sched_load(sched + kSchedTicket) & ~kEnrollClosed) < G &&
+                   __builtin_amdgcn_s_memrealtime() - t0 < kEnrollWaitTicks)
+                __builtin_amdgcn_s_sleep(2);
+            const uint32_t r = __hip_atomic_fetch_or(sched + kSchedTicket, kEnrollClosed, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) & ~kEnrollClosed;
+            sched_store(sched + kSchedPub, r);
+            sched_store(sched + kSchedLast, r);   // kept after the launch (psk_lab_trisolve_workers)
+            s_rank = 0;
+            s_R = r;
+        } else {
+            uint32_t r;
+            int64_t spins = 0;
+            while ((r = sched_load(sched + kSchedPub)) == 0) {
+                if (++spins > kMaxSpins) {
+                    atomicExch(err, 4 << 24);
+                    r = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            s_rank = (int)old;
+            s_R = r;
+        }
+    }
+    __syncthreads();
+    *R = s_R;
+    return s_rank;
+}
+
+// every thread, at the very end of an enrolled launch (after the workgroup's last use of the words)
+__device__ __forceinline__ void sched_leave(uint32_t *sched) {
+    __syncthreads();
+    if (threadIdx.x == 0 && sched_add(sched + kSchedExit, 1u) == gridDim.x - 1) {
+        sched_store(sched + kSchedTicket, 0u);
+        sched_store(sched + kSchedPub, 0u);
+        sched_store(sched + kSchedExit, 0u);
+    }
 }
 
 __global__ void fill_sentinel_kernel(int64_t n, double *x) {
@@ -163,14 +262,11 @@ struct SfRow {
     double v[kSfChunks], b, d;
 };
 
-__global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
-                                                        const int32_t *__restrict__ kci, const double *__restrict__ kva,
-                                                        const double *__restrict__ diag, const double *__restrict__ rhs,
-                                                        const int32_t *__restrict__ rhs_idx, double *x,
-                                                        int32_t *err, const int32_t *__restrict__ krow) {
+__device__ __forceinline__ void sptrsv_rows(int64_t n, const int32_t *__restrict__ krp, const int32_t *__restrict__ kci,
+                                            const double *__restrict__ kva, const double *__restrict__ diag,
+                                            const double *__restrict__ rhs, const int32_t *__restrict__ rhs_idx, double *x,
+                                            int32_t *err, const int32_t *__restrict__ krow, int64_t wave, int64_t W) {
     const int lane = threadIdx.x & 63;
-    const int64_t wave = ((int64_t)blockIdx.x * kBlock + threadIdx.x) >> 6;
-    const int64_t W = (int64_t)gridDim.x * kWaves;
     if (wave >= n) return;
     auto head = [&](int64_t k, SfHead &h) {
         if (k < n) {
@@ -252,6 +348,20 @@ __global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t
         }
         cur = nxt;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void sptrsv_kernel(int64_t n, const int32_t *__restrict__ krp,
+                                                        const int32_t *__restrict__ kci, const double *__restrict__ kva,
+                                                        const double *__restrict__ diag, const double *__restrict__ rhs,
+                                                        const int32_t *__restrict__ rhs_idx, double *x,
+                                                        int32_t *err, const int32_t *__restrict__ krow,
+                                                        uint32_t *sched) {
+    // positions dealt over the waves of the workgroups that enrolled (sched_enroll), not over the grid
+    uint32_t R = 0;
+    const int rank = sched_enroll(sched, &R, err);
+    if (rank >= 0) sptrsv_rows(n, krp, kci, kva, diag, rhs, rhs_idx, x, err, krow, (int64_t)rank * kWaves + (threadIdx.x >> 6),
+                               (int64_t)R * kWaves);
+    sched_leave(sched);
 }
 
 // LDS-resident: a factor small enough for x to live in LDS (the AMG coarse LU: 16.6k rows, 3008
@@ -688,8 +798,9 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
     int64_t n, int upper, const double *__restrict__ rhs, const int32_t *__restrict__ rhs_idx, double *x,
     int32_t *err, const int32_t *__restrict__ rec_row, const int32_t *__restrict__ rec_end,
     const int32_t *__restrict__ rec_c, const double *__restrict__ rec_v, const double *__restrict__ rec_d,
-    int64_t nblocks, int64_t B, int ring_mask) {
+    int64_t nblocks, int64_t B, int ring_mask, uint32_t *sched) {
     extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int64_t s_blk;
     const int ring_words = ring_mask + 1;
     double *ring = reinterpret_cast<double *>(smem);
     // two chunk buffers, SoA: v[K][C], d[C], b[C], e[K][C] (doubles) then row[C], end[C], c[K][C] (ints)
@@ -730,7 +841,11 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_kernel(
         ib[tid] = r.row;
         ib[kBandChunk + tid] = r.end;
     };
-    for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    for (;;) {   // blocks drawn from the ticket counter (sched_next_block): forward progress at any residency
+        if (tid == 0) s_blk = sched_next_block(sched, nblocks);
+        __syncthreads();
+        const int64_t blk = s_blk;
+        if (blk >= nblocks) break;
         const int64_t p_lo = blk * B, p_hi = (p_lo + B < n) ? p_lo + B : n, nrec = p_hi - p_lo;
         const int64_t nchunks = (nrec + kBandChunk - 1) / kBandChunk;
         BandChunkRegs<K> next;
@@ -851,9 +966,10 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
     int64_t n, int upper, const double *__restrict__ rhs, const int32_t *__restrict__ rhs_idx, double *x,
     int32_t *err, const int32_t *__restrict__ rec_row, const int32_t *__restrict__ rec_end,
     const int32_t *__restrict__ rec_c, const double *__restrict__ rec_v, const double *__restrict__ rec_d,
-    int64_t nblocks, int64_t B, int ring_mask) {
+    int64_t nblocks, int64_t B, int ring_mask, uint32_t *sched) {
     constexpr int C = kNarrowChunk, NB = kNarrowBufs, kD = 2 * K + 2;
     extern __shared__ __align__(16) unsigned char smem[];
+    __shared__ int64_t s_blk;
     const int ring_words = ring_mask + 1;
     double *ring = reinterpret_cast<double *>(smem);
     double *dbuf = ring + ring_words;                                        // NB x [v[K], d, b, e[K]] x C
@@ -861,7 +977,11 @@ __global__ __launch_bounds__(kBlock) void sptrsv_band_narrow_kernel(
     int32_t *ctl = ibuf + NB * (K + 2) * C;
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const double sentinel = __longlong_as_double((long long)kSentinel);
-    for (int64_t blk = blockIdx.x; blk < nblocks; blk += gridDim.x) {
+    for (;;) {   // blocks drawn from the ticket counter (sched_next_block)
+        if (tid == 0) s_blk = sched_next_block(sched, nblocks);
+        __syncthreads();
+        const int64_t blk = s_blk;
+        if (blk >= nblocks) break;
         const int64_t p_lo = blk * B, p_hi = (p_lo + B < n) ? p_lo + B : n, nrec = p_hi - p_lo;
         const int64_t nchunks = (nrec + C - 1) / C;
         if (tid <= NB + 1) ctl[tid] = tid == NB ? -1 : 0;
@@ -1196,9 +1316,15 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     int maxyd,
     int unit, const double *__restrict__ rhs, double *x, int32_t *err, const double *__restrict__ grec,
     GridExt ext, const uint32_t *__restrict__ gidx, const double *__restrict__ gdict, int ndict, int32_t *rflag,
-    const int32_t *gate) {
+    const int32_t *gate, uint32_t *sched) {
     if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;   // uniform
     extern __shared__ __align__(16) unsigned char smem[];
+    // the band this workgroup solves: drawn from the ticket counter (band b waits only on band b - 1, drawn
+    // earlier by a running workgroup; sched_next_block)
+    __shared__ int64_t s_band;
+    if (threadIdx.x == 0) s_band = sched_one_block(sched);
+    __syncthreads();
+    const int64_t band = s_band;
     double *ring = reinterpret_cast<double *>(smem);                  // [2 * kGridRing][kGridRW]
     int64_t *ctl = reinterpret_cast<int64_t *>(smem + 2 * kGridMirror);
     unsigned char *dict = smem + 2 * kGridMirror + 16;                // DICT: ndict GridDict<K> records
@@ -1219,7 +1345,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     // ctl[0]: last u of the band above present in the ring (poller -> solver)
     // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
     const int tid = threadIdx.x, j = tid & 63;
-    const int64_t y0 = (int64_t)blockIdx.x * kGridLanes;
+    const int64_t y0 = band * kGridLanes;
     const int64_t ylast = (y0 + kGridLanes - 1 < H - 1) ? y0 + kGridLanes - 1 : H - 1;
     const int64_t u_lo = grid_g(sigma2, phase, y0), u_hi = (w - 1) + grid_g(sigma2, phase, ylast);
     const int S = (int)(u_hi - u_lo + 1);
@@ -1229,7 +1355,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         min_ud = ud < min_ud ? ud : min_ud;
         max_ud = ud > max_ud ? ud : max_ud;
     }
-    const bool has_ext = blockIdx.x > 0 && pe > 0;
+    const bool has_ext = band > 0 && pe > 0;
     for (int i = tid; i < 2 * kGridRing * kGridRW; i += 2 * kGridLanes) ring[i] = 0.0;
     if (tid == 0) {
         ctl[0] = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;
@@ -1253,7 +1379,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             int64_t spins = 0;
             while (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
                    base + kGridLanes - 1 - kGridRing + max_ud) {
-                if (++spins > kMaxSpins) { atomicExch(err, (2 << 24) | (int)blockIdx.x); return; }
+                if (++spins > kMaxSpins) { atomicExch(err, (2 << 24) | (int)band); return; }
                 __builtin_amdgcn_s_sleep(2);
             }
             uint32_t pending = 0;   // lines of this lane's u still to fetch
@@ -1286,7 +1412,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
                 if (j == 0 && r > 0)
                     __hip_atomic_store(&ctl[0], base + r - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (!notready) break;
-                if (++spins > kMaxSpins) { atomicExch(err, (3 << 24) | (int)blockIdx.x); return; }
+                if (++spins > kMaxSpins) { atomicExch(err, (3 << 24) | (int)band); return; }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -1311,10 +1437,10 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const bool pub = j >= kGridLanes - maxyd;   // the lines the band below reads: agent-scope stores
     const uint32_t lane8 = (uint32_t)(8 + j) * 8;
     const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
-                                 (int64_t)blockIdx.x * S_full * GridStep<K>::kBytes;
+                                 band * S_full * GridStep<K>::kBytes;
     // the index stream of this band: a buffer with the step in the scalar offset
     const __amdgpu_buffer_rsrc_t ridx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t *>(DICT ? gidx + (int64_t)blockIdx.x * S_full * kGridLanes : gidx), (short)0,
+        const_cast<uint32_t *>(DICT ? gidx + band * S_full * kGridLanes : gidx), (short)0,
         DICT ? (int)(uint32_t)(S_full * kGridLanes * 4) : 0, 0x00020000);
     const __amdgpu_buffer_rsrc_t rrhs = grid_rsrc(rhs, n), rx = grid_rsrc(x, n);
     // steps up to s_ok need nothing more from the band above (uniform)
@@ -1375,7 +1501,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
                     (int)(__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - u_lo));
                 s_ok = known + min_ud;   // ext_known >= u - min_ud  <=>  t <= known + min_ud
                 if (t <= s_ok) break;
-                if (++spins > kMaxSpins) { atomicExch(err, (1 << 24) | (int)blockIdx.x); break; }
+                if (++spins > kMaxSpins) { atomicExch(err, (1 << 24) | (int)band); break; }
                 __builtin_amdgcn_s_sleep(1);
             } while (true);
 #ifdef PSK_GRID_PROF
@@ -1450,11 +1576,11 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     if (j == 0) __hip_atomic_store(&ctl[1], INT64_MAX / 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     if (MK && !unit && rbad != 0 && j == 0) atomicOr(rflag, 1);
 #ifdef PSK_GRID_PROF
-    if (j == 0 && blockIdx.x < 8192) {
-        g_grid_prof[blockIdx.x * 8 + 0] = t_start;
-        g_grid_prof[blockIdx.x * 8 + 1] = __builtin_amdgcn_s_memtime();
-        g_grid_prof[blockIdx.x * 8 + 2] = n_wait;
-        g_grid_prof[blockIdx.x * 8 + 3] = c_wait;
+    if (j == 0 && band < 8192) {
+        g_grid_prof[band * 8 + 0] = t_start;
+        g_grid_prof[band * 8 + 1] = __builtin_amdgcn_s_memtime();
+        g_grid_prof[band * 8 + 2] = n_wait;
+        g_grid_prof[band * 8 + 3] = c_wait;
     }
 #endif
 }
@@ -1614,8 +1740,9 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         int nd = T.grid_dict_n;
         int32_t *flag = dict ? T.grid_flag : nullptr;
         const int32_t *nogate = nullptr;
+        uint32_t *sch = T.sched;
         void *args[] = {&nn, &w, &H, &sg, &gph, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext, &gi,
-                        &gdd, &nd, &flag, &nogate};
+                        &gdd, &nd, &flag, &nogate, &sch};
         const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
         const size_t lds = grid_lds_bytes(T.grid_K, T.grid_dict_n);
         PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args, lds, s));
@@ -1628,7 +1755,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
                 PSK_HIP(hipGetLastError());
             }
             void *fargs[] = {&nn, &w, &H, &sg, &gph, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext,
-                             &gi, &gdd, &nd, &noflag, &gate};
+                             &gi, &gdd, &nd, &noflag, &gate, &sch};
             PSK_HIP(hipLaunchKernel(kf, dim3(nb), dim3(2 * kGridLanes), fargs, lds, s));
             hipLaunchKernelGGL(grid_flag_reset_kernel, dim3(1), dim3(1), 0, s, T.grid_flag);
             PSK_HIP(hipGetLastError());
@@ -1651,7 +1778,8 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const double *rv = T.rec_v, *rd = T.diag ? T.rec_d : nullptr;
         int64_t nb = T.band_nblocks, B = T.band_B;
         int mask = T.ring_words - 1;
-        void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask};
+        uint32_t *sch = T.sched;
+        void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask, &sch};
         PSK_HIP(hipLaunchKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
         return PSK_OK;
     }
@@ -1671,14 +1799,16 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const double *rv = T.rec_v, *rd = T.diag ? T.rec_d : nullptr;
         int64_t nb = T.band_nblocks, B = T.band_B;
         int mask = T.ring_words > 0 ? T.ring_words - 1 : -1;
-        void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask};
+        uint32_t *sch = T.sched;
+        void *args[] = {&nn, &upper, &rhs, &rhs_idx, &x, &err, &rr, &re, &rc, &rv, &rd, &nb, &B, &mask, &sch};
         PSK_HIP(hipLaunchKernel(k, dim3(g), dim3(kBlock), args, (unsigned)lds, s));
         return PSK_OK;
     }
     const void *k = reinterpret_cast<const void *>(&sptrsv_kernel);
     const int g = syncfree_grid(c);
     const int32_t *ord = T.order;
-    void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
+    uint32_t *sch = T.sched;
+    void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord, &sch};
     PSK_HIP(hipLaunchKernel(k, dim3(g), dim3(kBlock), args, 0, s));
     return PSK_OK;
 }
@@ -1746,15 +1876,123 @@ int ilu_check_error(const psk_prec *M, hipStream_t s) {
     int32_t h = 0;
     PSK_HIP(hipMemcpyAsync(&h, M->err, 4, hipMemcpyDeviceToHost, s));
     PSK_HIP(hipStreamSynchronize(s));
-    if (h) return fail(PSK_ERR_HIP, "triangular solve: dependency wait exceeded its bound (not co-resident?) code " +
-                                        std::to_string(h));
+    if (h) {
+        // a launch that stopped waiting may have left its scheduling words armed: re-zero them (and the
+        // error word) so that the next apply starts clean
+        for (const TriFactor *T : {&M->lo, &M->up})
+            if (T->present && T->sched) (void)hipMemsetAsync(T->sched, 0, kSchedWords * sizeof(uint32_t), s);
+        (void)hipMemsetAsync(M->err, 0, sizeof(int32_t), s);
+        (void)hipStreamSynchronize(s);
+        return fail(PSK_ERR_HIP, "triangular solve: dependency wait exceeded its bound, code " + std::to_string(h));
+    }
     return PSK_OK;
 }
+
+// ---- lab: a co-running kernel that holds CUs while a solve runs (tests of the forward-progress rule) ----
+// occupy_kernel: `wgs` workgroups of 1024 threads (16 waves each) with `lds` bytes of LDS each, on a
+// stream of their own, every wave spinning until the flag is set on the solver's stream (occupy_end) or
+// the time limit passes. A solve enqueued between begin and end can only use what the occupiers leave.
+__global__ __launch_bounds__(1024) void occupy_kernel(uint32_t *flag, int64_t *started, uint64_t ticks,
+                                                      int32_t *timed_out) {
+    extern __shared__ unsigned char occ_lds[];
+    if (threadIdx.x == 0) {
+        occ_lds[0] = 1;
+        __hip_atomic_fetch_add(started, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+            if (threadIdx.x == 0) atomicOr(timed_out, 1);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+__global__ void occupy_release_kernel(uint32_t *flag) {
+    __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+namespace {
+struct Occupier {
+    hipStream_t s = nullptr;
+    uint32_t *dw = nullptr;       // [0] release flag, [64] timed-out word
+    int64_t *started = nullptr;   // host-mapped count of started occupier workgroups
+    bool active = false;
+};
+Occupier g_occ;
+}  // namespace
+
+}  // namespace psk
+
+extern "C" int psk_lab_occupy_begin(int32_t wgs, int32_t lds_bytes, double seconds) {
+    using namespace psk;
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (g_occ.active) return fail(PSK_ERR_ARG, "psk_lab_occupy_begin: already active");
+    if (wgs < 1 || lds_bytes < 16 || lds_bytes > 160 * 1024 || seconds <= 0)
+        return fail(PSK_ERR_ARG, "psk_lab_occupy_begin: bad arguments");
+    if (!g_occ.s) {
+        PSK_HIP(hipStreamCreateWithFlags(&g_occ.s, hipStreamNonBlocking));
+        PSK_HIP(hipMalloc(&g_occ.dw, 128 * sizeof(uint32_t)));
+        PSK_HIP(hipHostMalloc(&g_occ.started, 64, hipHostMallocCoherent));
+    }
+    PSK_HIP(hipMemsetAsync(g_occ.dw, 0, 128 * sizeof(uint32_t), g_occ.s));
+    PSK_HIP(hipStreamSynchronize(g_occ.s));
+    *reinterpret_cast<volatile int64_t *>(g_occ.started) = 0;
+    const uint64_t ticks = (uint64_t)(seconds * 1e8);
+    hipLaunchKernelGGL(occupy_kernel, dim3((unsigned)wgs), dim3(1024), (size_t)lds_bytes, g_occ.s, g_occ.dw,
+                       g_occ.started, ticks, reinterpret_cast<int32_t *>(g_occ.dw + 64));
+    PSK_HIP(hipGetLastError());
+    g_occ.active = true;
+    // every occupier resident before the caller enqueues its solve (bounded: 5 s)
+    const auto t0 = std::chrono::steady_clock::now();
+    while (*reinterpret_cast<volatile int64_t *>(g_occ.started) < wgs &&
+           std::chrono::steady_clock::now() - t0 < std::chrono::seconds(5)) {
+    }
+    const int64_t got = *reinterpret_cast<volatile int64_t *>(g_occ.started);
+    return got >= wgs ? PSK_OK : fail(PSK_ERR_HIP, "psk_lab_occupy_begin: only " + std::to_string(got) + " of " +
+                                                       std::to_string(wgs) + " occupiers started");
+}
+
+// releases the occupiers behind everything enqueued on the solver's stream so far, waits for them;
+// *timed_out = 1 when they hit their time limit first (the solve could not finish while they held CUs)
+extern "C" int psk_lab_occupy_end(int32_t *timed_out) {
+    using namespace psk;
+    Context *c;
+    PSK_TRY(ctx(&c));
+    if (!g_occ.active) return fail(PSK_ERR_ARG, "psk_lab_occupy_end: not active");
+    hipLaunchKernelGGL(occupy_release_kernel, dim3(1), dim3(1), 0, c->stream, g_occ.dw);
+    PSK_HIP(hipGetLastError());
+    PSK_HIP(hipStreamSynchronize(g_occ.s));
+    int32_t h = 0;
+    PSK_HIP(hipMemcpy(&h, g_occ.dw + 64, sizeof(int32_t), hipMemcpyDeviceToHost));
+    g_occ.active = false;
+    if (timed_out) *timed_out = h;
+    return PSK_OK;
+}
+
+// workers (waves / 4) the last sync-free launch of a factor enrolled, and the grid it was launched with
+extern "C" int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid) {
+    using namespace psk;
+    if (!M || M->kind != PSK_PREC_ILU) return fail(PSK_ERR_ARG, "psk_lab_trisolve_workers: not a triangular-solve chain");
+    const TriFactor &T = which == 0 ? M->lo : M->up;
+    if (!T.present || !T.sched) return fail(PSK_ERR_ARG, "psk_lab_trisolve_workers: factor absent");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    uint32_t v = 0;
+    PSK_HIP(hipStreamSynchronize(c->stream));
+    PSK_HIP(hipMemcpy(&v, T.sched + kSchedLast, sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (enrolled) *enrolled = (int32_t)v;
+    if (grid) *grid = syncfree_grid(c);
+    return PSK_OK;
+}
+
+namespace psk {
 
 void TriFactor::release() {
     void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,   rec_d,
                     gd_code, gd_coef, gd_diag, gd_idx, gd_dict, part_seg, part_rp, part_code, part_row, part_va,
-                    grid_flag};
+                    grid_flag, sched};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -2261,7 +2499,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         build_band(F, B, c->num_cus, 2, K, bd);
         int64_t wmax = 0;
         for (size_t L = 0; L + 1 < bd.lvl_ptr.size(); ++L) wmax = std::max(wmax, bd.lvl_ptr[L + 1] - bd.lvl_ptr[L]);
-        const bool ok = wmax <= kBandChunk && band_lds_bytes(bd.ring_words, K) <= 160 * 1024;
+        const bool ok = wmax <= kBandChunk && band_lds_bytes(bd.ring_words, K) <= 160 * 1024 - 64;   // + the static block ticket
         if (ok && (!band_ok || bd.est < best.est)) {
             best = std::move(bd);
             band_ok = true;
@@ -2270,7 +2508,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     }
     // narrow band (one solving wave, staging waves): every local level at most one wave wide, ring present
     bool narrow = false;
-    if (band_ok && best.ring_words > 0 && narrow_lds_bytes(best.ring_words, K) <= 160 * 1024) {
+    if (band_ok && best.ring_words > 0 && narrow_lds_bytes(best.ring_words, K) <= 160 * 1024 - 64) {
         int64_t wmax = 0;
         for (size_t L = 0; L + 1 < best.lvl_ptr.size(); ++L) wmax = std::max(wmax, best.lvl_ptr[L + 1] - best.lvl_ptr[L]);
         const char *ne = std::getenv("PSK_BAND_NARROW");
@@ -2468,6 +2706,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.gd_idx, gidx);
     if (rc == PSK_OK) rc = upload(&T.gd_dict, gdict);
     if (rc == PSK_OK) rc = upload(&T.grid_flag, std::vector<int32_t>(T.grid_dict_n > 0 ? 1 : 0, 0));
+    if (rc == PSK_OK) rc = upload(&T.sched, std::vector<uint32_t>(kSchedWords, 0u));   // block tickets / enrolment
     if (rc == PSK_OK) rc = upload(&T.part_seg, pseg);
     if (rc == PSK_OK) rc = upload(&T.part_rp, prp);
     if (rc == PSK_OK) rc = upload(&T.part_code, pcode);

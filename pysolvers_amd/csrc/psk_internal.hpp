@@ -169,6 +169,15 @@ struct psk_csr {
     int32_t sl_compact = 0;      // uniform, odd width, <= 2 dictionary values: the value-index bits sit in
                                  // the last delta word's free half (no index words; spmv_uniform_kernel CMP)
     int64_t sl_slots = 0, sl_packed_slots = 0, sl_stream_bytes = 0;
+    // diagonal layout (spmv.hip, "diagonal layout"; round 5): every row's entries lie, in stored order, on
+    // a subsequence of dg_K <= 8 diagonals c = row + dg_d[j] (columns outside [0, n) of a row-block shard
+    // mapped to its halo by dg_lo / dg_hi) with ONE value dg_v[j] per diagonal; per row a presence mask
+    // byte (dg_mask, padded to whole 256-row slices). Present instead of the sliced copy when it applies.
+    uint8_t *dg_mask = nullptr;
+    int32_t dg_K = 0, dg_jd = -1;     // jd: the diagonal d = 0 (-1: none)
+    int32_t dg_d[8] = {};
+    double dg_v[8] = {};
+    int64_t dg_lo = 0, dg_hi = 0;
     // distributed
     psk_comm *comm = nullptr;
     int64_t n_global = 0, row_begin = 0, row_end = 0;
@@ -238,6 +247,7 @@ struct TriFactor {
     double *gd_dict = nullptr;
     int grid_dict_n = 0;
     int32_t *grid_flag = nullptr;   // dictionary kernel: a step's quotient needed the IEEE re-solve (zeroed after it)
+    uint32_t *sched = nullptr;      // block tickets / worker enrolment of the spin-waiting schedules (ilu.hip)
     int grid_K = 0, grid_pe = 0, grid_maxyd = 0, grid_ring = 0;
     int64_t grid_w = 0, grid_H = 0, grid_S = 0;   // grid_S: steps per band (slot stride)
     int64_t grid_sigma = 0, grid_phase = 0;      // g(y) = (grid_sigma * y + grid_phase) >> 1 (twice the skew)

@@ -551,6 +551,154 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Diagonal layout (round 5; DIA format, Saad's "diagonal storage", with one value per diagonal): when every
+// row's entries lie, IN STORED ORDER, on a subsequence of K <= 8 diagonals c = row + d_j, and every entry
+// of diagonal j holds the same double v_j (constant-coefficient stencils: FDLaplacian2D's rows are
+// [diag, -m, +m, -1, +1] minus the absent neighbours, two distinct values), the whole matrix is the K
+// offsets, the K values and ONE presence byte per row (bit j: the row stores an entry on diagonal j).
+// Detected at creation (diag_build) by checking every stored entry against the rule, so a row's present
+// diagonals, visited in j order, ARE its stored entries in stored order: each lane sums its row from 0.0
+// with rounded products exactly as csr_matvec does, and y is bit-identical to the CSR and sliced layouts.
+// A row-block shard of such a matrix maps columns outside [0, n) to its halo (c + lo below, c + hi
+// above: the FD shard's [owned | halo_lo | halo_hi] columns), checked the same way.
+// Stream: 1 B per row instead of the compact sliced layout's 12 (FD at N = 10M: 10 MB instead of 120 MB
+// per SpMV); x is gathered and y written as before (16 B per row). Same 256-row slices, one row per lane,
+// TPW slices per workgroup and gridsum tiles as spmv_uniform_multi_kernel: p.Ap has the same bits.
+constexpr int kDiagMax = 8;
+struct DiagDesc {
+    int32_t d[kDiagMax];   // diagonal offsets, in every row's stored order
+    double v[kDiagMax];    // the value (bit pattern) of every entry on diagonal j
+    int64_t lo, hi;        // local column of c = row + d: c + lo when c < 0, c + hi when c >= n (shards)
+    int64_t ncols;
+    int32_t K, jd;         // diagonals; jd = the one with d = 0 (-1: none)
+};
+
+__device__ __forceinline__ int64_t diag_col(const DiagDesc &dd, int64_t n, int64_t row, int j) {
+    int64_t c = row + dd.d[j];
+    c += c < 0 ? dd.lo : (c >= n ? dd.hi : 0);
+    return c < 0 ? 0 : (c >= dd.ncols ? dd.ncols - 1 : c);   // absent diagonals gather a valid x (unused)
+}
+
+template <int MODE, int KM, int TPW>
+__global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
+    int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd, const double *__restrict__ x, double *__restrict__ y,
+    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
+    TileMap tm, int64_t ntiles) {
+    const int32_t dn = *(done ? done : &g_spmv_never_done);
+    const int tid = threadIdx.x;
+    const int64_t grp = tile_of_block(tm);
+    int64_t tl[TPW];
+    bool tv[TPW];
+    uint32_t mk[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t t = grp * TPW + q;
+        tv[q] = t < ntiles;
+        tl[q] = tv[q] ? t : ntiles - 1;
+        mk[q] = __builtin_nontemporal_load(mask + tl[q] * kSlice + tid);   // padded to whole slices
+    }
+    double eq[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        eq[q] = 0.0;
+        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+            eq[q] = aux_q[row < n ? row : 0];
+    }
+    if (dn != 0) {
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) __asm__ volatile("" ::"v"(mk[q]));
+        return;
+    }
+    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
+    __shared__ GridSumTile<1> gsl[TPW];
+    uint32_t ticket[TPW];
+    const bool pub = PUB && spmv_publishes<MODE>(gs);
+    if (pub) {
+        if (tid < TPW) gsl[tid].cnt = 0;
+        if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            ticket[q] = 0;
+            if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
+                ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+        }
+    }
+    // every diagonal's x gathered unconditionally (absent ones at a clamped address), then the sums
+    double xv[TPW][KM], acc[TPW], yv[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            const int64_t c = diag_col(dd, n, row, j);
+            xv[q][j] = x[c];
+            if (MODE == kSpmvJacobiDot) xv[q][j] = aux_d[c] * xv[q][j];   // (DInv*q)[c], rounded
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        const bool has = tv[q] && row < n;
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+            if ((mk[q] >> j) & 1u) sum = sum + dd.v[j] * xv[q][j];   // stored order, rounded product
+        if (MODE == kSpmvDot) {   // x[row]: the gathered diagonal when the row stores it
+            double d = 0.0;
+            bool found = false;
+#pragma unroll
+            for (int j = 0; j < KM; ++j)
+                if (j == dd.jd && ((mk[q] >> j) & 1u)) {
+                    d = xv[q][j];
+                    found = true;
+                }
+            if (!found && has) d = x[row];
+            eq[q] = d;
+        }
+        yv[q] = spmv_row_value<MODE>(has, sum, eq[q], acc[q]);
+    }
+    if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
+    }
+}
+
+// Diagonal-layout detection: row `row`'s stored entries must be, in order, entries of strictly increasing
+// diagonals j with column diag_col's mapping and value v_j; the presence byte is written (0 past n) and
+// any violation sets *bad.
+__global__ __launch_bounds__(kBlock) void diag_detect_kernel(int64_t n, const int32_t *__restrict__ rowptr,
+                                                             const int32_t *__restrict__ colidx,
+                                                             const double *__restrict__ vals, DiagDesc dd,
+                                                             uint8_t *__restrict__ mask, int64_t npad,
+                                                             int32_t *__restrict__ bad) {
+    const int64_t row = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (row >= npad) return;
+    uint32_t mk = 0;
+    if (row < n) {
+        int j = 0;
+        bool ok = true;
+        for (int32_t e = rowptr[row]; e < rowptr[row + 1] && ok; ++e) {
+            const int64_t c = colidx[e];
+            const double v = vals[e];
+            while (j < dd.K) {
+                int64_t cj = row + dd.d[j];
+                cj += cj < 0 ? dd.lo : (cj >= n ? dd.hi : 0);
+                if (cj == c && same_bits(v, dd.v[j])) break;
+                ++j;
+            }
+            if (j == dd.K) ok = false;
+            else mk |= 1u << j++;
+        }
+        if (!ok) atomicOr(bad, 1);
+    }
+    mask[row] = (uint8_t)mk;
+}
+
 // General sliced layout (per-slice widths, offsets and formats loaded from the slice header).
 // DK: dictionary size class (0 = double values, 2 / 4 / 8 entries).
 template <int MODE, int DK>
@@ -799,6 +947,123 @@ void sliced_free(psk_csr *A) {
     A->sl_stream_bytes = 0;
 }
 
+void diag_free(psk_csr *A) {
+    if (A->dg_mask) (void)hipFree(A->dg_mask);
+    A->dg_mask = nullptr;
+    A->dg_K = 0;
+    A->dg_jd = -1;
+}
+
+static DiagDesc diag_desc(const psk_csr *A) {
+    DiagDesc dd{};
+    for (int j = 0; j < kDiagMax; ++j) {
+        dd.d[j] = A->dg_d[j];
+        dd.v[j] = A->dg_v[j];
+    }
+    dd.lo = A->dg_lo;
+    dd.hi = A->dg_hi;
+    dd.ncols = A->ncols;
+    dd.K = A->dg_K;
+    dd.jd = A->dg_jd;
+    return dd;
+}
+
+// The diagonal layout of A when it has one (see spmv_diag_kernel): the diagonals and their values are
+// read off one full-width row of owned columns, the halo mapping of a shard from its column count, and then
+// EVERY row is checked against them on the device. Quietly leaves A alone when the rule does not hold
+// (force: fails with PSK_ERR_UNSUPPORTED).
+static int diag_build(psk_csr *A, hipStream_t s, bool force) {
+    auto no = [&](const char *why) { return force ? fail(PSK_ERR_UNSUPPORTED, std::string("diagonal layout: ") + why) : PSK_OK; };
+    const int64_t n = A->n, nt = (n + kSlice - 1) / kSlice;
+    if (n == 0 || A->nnz == 0) return no("empty matrix");
+    if (nt > INT32_MAX) return no("too many slices");
+    DevBuf tmp;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } rel{tmp};
+    PSK_TRY(tmp.ensure((size_t)nt * 2 * sizeof(int32_t) + 64));
+    int32_t *dw = tmp.as<int32_t>(), *dspan = dw + nt;
+    int32_t *dbad = dw + 2 * nt;
+    hipLaunchKernelGGL(sliced_shape_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, n, A->rowptr, A->colidx, dw, dspan);
+    PSK_HIP(hipGetLastError());
+    std::vector<int32_t> wd((size_t)nt);
+    PSK_HIP(hipMemcpyAsync(wd.data(), dw, (size_t)nt * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    const int32_t K = *std::max_element(wd.begin(), wd.end());
+    if (K < 1 || K > kDiagMax) return no("rows wider than 8 entries");
+    // the template row: a row of K entries, all in owned columns, from slices taken from the middle out
+    // (a shard's first and last lines reach into its halo)
+    std::vector<int32_t> rp(kSlice + 1), cols(K);
+    std::vector<double> vals(K);
+    int64_t trow = -1;
+    for (int64_t tries = 0, i = 0; i < nt && tries < 64 && trow < 0; ++i) {
+        const int64_t t = (nt / 2 + i) % nt;
+        if (wd[(size_t)t] != K) continue;
+        ++tries;
+        const int64_t r0 = t * kSlice, nr = std::min<int64_t>(kSlice, n - r0);
+        PSK_HIP(hipMemcpy(rp.data(), A->rowptr + r0, (size_t)(nr + 1) * sizeof(int32_t), hipMemcpyDeviceToHost));
+        for (int64_t r = 0; r < nr && trow < 0; ++r) {
+            if (rp[(size_t)r + 1] - rp[(size_t)r] != K) continue;
+            PSK_HIP(hipMemcpy(cols.data(), A->colidx + rp[(size_t)r], (size_t)K * 4, hipMemcpyDeviceToHost));
+            bool owned = true;
+            for (int j = 0; j < K; ++j) owned = owned && cols[(size_t)j] >= 0 && cols[(size_t)j] < n;
+            if (!owned) continue;
+            PSK_HIP(hipMemcpy(vals.data(), A->vals + rp[(size_t)r], (size_t)K * 8, hipMemcpyDeviceToHost));
+            trow = r0 + r;
+        }
+    }
+    if (trow < 0) return no("no full-width row of owned columns");
+    DiagDesc dd{};
+    dd.K = K;
+    dd.jd = -1;
+    int64_t dmin = 0;
+    for (int j = 0; j < K; ++j) {
+        const int64_t d = (int64_t)cols[(size_t)j] - trow;
+        for (int i = 0; i < j; ++i)
+            if (dd.d[i] == d) return no("repeated column in a row");
+        dd.d[j] = (int32_t)d;
+        dd.v[j] = vals[(size_t)j];
+        if (d == 0) dd.jd = j;
+        dmin = std::min(dmin, d);
+    }
+    // halo mapping of a row-block shard with columns [owned | below | above] (psk_csr_create_fd2d_dist):
+    // the lines below hold -dmin columns; a shard with one halo has it right after the owned block
+    const int64_t halo = A->ncols - n;
+    dd.lo = halo > 0 ? n - dmin : 0;
+    dd.hi = halo > 0 && halo == -2 * dmin ? -dmin : 0;
+    dd.ncols = A->ncols;
+    uint8_t *mask = nullptr;
+    if (hipMalloc(&mask, (size_t)nt * kSlice) != hipSuccess) {
+        (void)hipGetLastError();
+        return force ? fail(PSK_ERR_ALLOC, "diagonal layout: hipMalloc") : PSK_OK;
+    }
+    PSK_HIP(hipMemsetAsync(dbad, 0, sizeof(int32_t), s));
+    hipLaunchKernelGGL(diag_detect_kernel, dim3((unsigned)nt), dim3(kBlock), 0, s, n, A->rowptr, A->colidx, A->vals, dd,
+                       mask, nt * kSlice, dbad);
+    int32_t bad = 0;
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, dbad, sizeof(int32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess || bad) {
+        (void)hipFree(mask);
+        if (e != hipSuccess) return fail(PSK_ERR_HIP, std::string("diagonal layout: ") + hipGetErrorString(e));
+        return no("an entry off the diagonals or with another value");
+    }
+    sliced_free(A);
+    diag_free(A);
+    A->dg_mask = mask;
+    A->dg_K = K;
+    A->dg_jd = dd.jd;
+    for (int j = 0; j < kDiagMax; ++j) {
+        A->dg_d[j] = j < K ? dd.d[j] : 0;
+        A->dg_v[j] = j < K ? dd.v[j] : 0.0;
+    }
+    A->dg_lo = dd.lo;
+    A->dg_hi = dd.hi;
+    return PSK_OK;
+}
+
 // The distinct values of A (bit patterns) when there are at most kDictMax of them, else empty:
 // detection passes over A->vals, each adding every new value it was offered (<= kDictMax + 1 passes,
 // one for a matrix of arbitrary values).
@@ -847,6 +1112,7 @@ static int find_value_dict(const psk_csr *A, hipStream_t s, std::vector<double> 
 // row), i.e. padding costs nothing, and quietly keeps CSR if HBM cannot hold the copy.
 static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool use_dict, bool force_dict) {
     sliced_free(A);
+    diag_free(A);
     std::vector<double> dict;
     if (use_dict) PSK_TRY(find_value_dict(A, s, dict));
     if (force_dict && dict.empty())
@@ -948,6 +1214,15 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
 int csr_choose_layout(psk_csr *A, hipStream_t s) {
     const char *e = std::getenv("PSK_SPMV_LAYOUT");
     if (e && std::strcmp(e, "csr") == 0) return PSK_OK;
+    // the diagonal layout first, when the matrix has one (it streams 1 B per row): automatically and with
+    // PSK_SPMV_LAYOUT=diag (which otherwise falls back to the automatic choice); PSK_SPMV_DIAG=0 leaves it out
+    const char *de = std::getenv("PSK_SPMV_DIAG");
+    const bool diag_env = e && std::strcmp(e, "diag") == 0;
+    if ((!e || diag_env) && !(de && std::atoi(de) == 0)) {
+        PSK_TRY(diag_build(A, s, false));
+        if (A->dg_mask) return PSK_OK;
+    }
+    if (diag_env) e = nullptr;
     const bool wide = e && std::strcmp(e, "sliced_wide") == 0;
     const bool plain = e && std::strcmp(e, "sliced") == 0;
     const bool force = e && (plain || wide || std::strcmp(e, "sliced_dict") == 0);
@@ -991,7 +1266,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     if (A->n == 0) return PSK_OK;
     Context *c;
     PSK_TRY(ctx(&c));
-    const bool sliced = A->sl_off != nullptr;
+    const bool sliced = A->sl_off != nullptr || A->dg_mask != nullptr;   // 256-row slices
     const int64_t nwg = sliced ? (A->n + kSlice - 1) / kSlice : spmv_tiles(A);
     GridSum gs{nullptr, nullptr, nullptr, nullptr, 0, 0, -1, nullptr};
     if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
@@ -1010,6 +1285,34 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     const int64_t nwg2 = (nwg + tpw - 1) / tpw;
     const dim3 gd2((unsigned)(nwg2 > 0 ? nwg2 : 1));
     const TileMap tm2 = tile_map_for(nwg2, sliced && spmv_xcd_bands(), rev != 0);
+    if (A->dg_mask) {   // diagonal layout: TPW slices per workgroup as the compact kernel
+        const DiagDesc dd = diag_desc(A);
+        const int km = A->dg_K <= 3 ? 3 : A->dg_K <= 5 ? 5 : 8;
+#define PSK_DIAG_LAUNCH(M, KM)                                                                                     \
+    hipExtLaunchKernelGGL((spmv_diag_kernel<M, KM, 2>), gd2, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, x, y, aux_d, \
+                          aux_q, gs, done_flag, tm2, nwg)
+#define PSK_DIAG_MODE(M)                                                                                           \
+    do {                                                                                                           \
+        if (km == 3) PSK_DIAG_LAUNCH(M, 3);                                                                        \
+        else if (km == 5) PSK_DIAG_LAUNCH(M, 5);                                                                   \
+        else PSK_DIAG_LAUNCH(M, 8);                                                                                \
+    } while (0)
+        if (tpw != 2) return fail(PSK_ERR_UNSUPPORTED, "diagonal layout: PSK_SPMV_TPW must be 2");
+        switch (mode) {
+        case kSpmvPlain: PSK_DIAG_MODE(kSpmvPlain); break;
+        case kSpmvDot: PSK_DIAG_MODE(kSpmvDot); break;
+        case kSpmvJacobiDot: PSK_DIAG_MODE(kSpmvJacobiDot); break;
+        case kSpmvPlainDot: PSK_DIAG_MODE(kSpmvPlainDot); break;
+        case kSpmvResid: PSK_DIAG_MODE(kSpmvResid); break;
+        case kSpmvAdd: PSK_DIAG_MODE(kSpmvAdd); break;
+        default:
+            return fail(PSK_ERR_ARG, "unknown spmv mode");
+        }
+#undef PSK_DIAG_MODE
+#undef PSK_DIAG_LAUNCH
+        PSK_HIP(hipGetLastError());
+        return PSK_OK;
+    }
     if (sliced) {
         const int dk = !A->sl_dict ? 0 : A->sl_dict_n <= 2 ? 2 : A->sl_dict_n <= 4 ? 4 : 8;
         const int uw = A->sl_uniform_w;   // 0, or the uniform width (<= kSliceRegs)
@@ -1245,6 +1548,7 @@ static void csr_free(psk_csr *A) {
     A->colidx = nullptr;
     A->vals = nullptr;
     sliced_free(A);
+    diag_free(A);
     A->ws.release();
     A->ws_small.release();
     A->sendbuf.release();
@@ -1357,25 +1661,33 @@ int psk_csr_layout(psk_csr *A, int32_t set, int32_t *layout, int64_t *slots, int
                    int64_t *stream_bytes) {
     if (!A) return fail(PSK_ERR_ARG, "psk_csr_layout: NULL matrix");
     if (set != -1 && set != PSK_LAYOUT_CSR && set != PSK_LAYOUT_SLICED && set != PSK_LAYOUT_SLICED_WIDE &&
-        set != PSK_LAYOUT_SLICED_DICT)
+        set != PSK_LAYOUT_SLICED_DICT && set != PSK_LAYOUT_DIAG)
         return fail(PSK_ERR_ARG, "psk_csr_layout: set must be -1 or a PSK_LAYOUT_* value");
     if (set != -1) {
         Context *c;
         PSK_TRY(ctx(&c));
         PSK_HIP(hipStreamSynchronize(c->stream));   // queued launches may still read the old layout
-        if (set == PSK_LAYOUT_CSR) sliced_free(A);
-        else
+        if (set == PSK_LAYOUT_CSR) {
+            sliced_free(A);
+            diag_free(A);
+        } else if (set == PSK_LAYOUT_DIAG) {
+            PSK_TRY(diag_build(A, c->stream, true));
+        } else {
             PSK_TRY(sliced_build(A, c->stream, true, set != PSK_LAYOUT_SLICED_WIDE, set == PSK_LAYOUT_SLICED_DICT,
                                  set == PSK_LAYOUT_SLICED_DICT));
+        }
     }
     if (layout)
-        *layout = !A->sl_off                  ? PSK_LAYOUT_CSR
+        *layout = A->dg_mask                  ? PSK_LAYOUT_DIAG
+                  : !A->sl_off                ? PSK_LAYOUT_CSR
                   : A->sl_dict                ? PSK_LAYOUT_SLICED_DICT
                   : A->sl_packed_slots == 0   ? PSK_LAYOUT_SLICED_WIDE
                                               : PSK_LAYOUT_SLICED;
-    if (slots) *slots = A->sl_slots;
-    if (packed_slots) *packed_slots = A->sl_packed_slots;
-    if (stream_bytes) *stream_bytes = A->sl_off ? A->sl_stream_bytes : 12 * A->nnz + 4 * (A->n + 1);
+    if (slots) *slots = A->dg_mask ? A->n * A->dg_K : A->sl_slots;
+    if (packed_slots) *packed_slots = A->dg_mask ? 0 : A->sl_packed_slots;
+    // the diagonal layout streams one presence byte per row (its K offsets and values are kernel arguments)
+    if (stream_bytes)
+        *stream_bytes = A->dg_mask ? A->n : A->sl_off ? A->sl_stream_bytes : 12 * A->nnz + 4 * (A->n + 1);
     return PSK_OK;
 }
 

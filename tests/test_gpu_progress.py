@@ -1,0 +1,101 @@
+"""Forward progress of the spin-waiting triangular-solve schedules when their grid cannot be co-resident
+(ADVICE r4): a co-running kernel (psk_lab_occupy_begin, on a stream of its own) holds part
+of the CUs while the solve runs, and is released only BEHIND the solve on the solver's stream — so the
+solve has to complete on whatever the occupiers leave. It must, bit-identical to the unloaded solve, with
+no expired wait and without the occupiers reaching their time limit.
+
+Before round 5 the sync-free schedule dealt row k to wave k mod W of a grid sized to the device and the
+band schedule block b to workgroup b mod g: with part of that grid unable to start, the resident waves
+spun on rows nobody would ever solve (ilu.hip "forward progress without co-residency").
+Bar: bit-exact against the same factor's solve on an idle device (same schedule, same per-row arithmetic).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def psk():
+    import pysolvers_amd
+    from pysolvers_amd import _native as N
+    assert N.device_count() >= 1, "no GPU visible to libpsk"
+    return pysolvers_amd
+
+
+def _under_occupiers(wgs, lds, fn):
+    from pysolvers_amd import _native as N
+    N.check(N.lib.psk_lab_occupy_begin(wgs, lds, 30.0), "psk_lab_occupy_begin")
+    timed_out = N.I32()
+    try:
+        out = fn()
+    finally:
+        N.check(N.lib.psk_lab_occupy_end(ctypes.byref(timed_out)), "psk_lab_occupy_end")
+    assert timed_out.value == 0, "the occupiers hit their time limit: the solve waited for them"
+    return out
+
+
+def _workers(handle, which):
+    from pysolvers_amd import _native as N
+    e, g = N.I32(), N.I32()
+    N.check(N.lib.psk_lab_trisolve_workers(handle, which, ctypes.byref(e), ctypes.byref(g)), "workers")
+    return e.value, g.value
+
+
+def test_syncfree_ilu_apply_beside_occupiers(psk):
+    """RightILUT (the reference's spilu arguments) on FD 384^2, both factors on the sync-free schedule.
+    128 occupiers of 16 waves and 100 KiB of LDS each sit on 128 CUs, leaving room for 4 of the 7
+    sync-free workgroups per CU there: the grid cannot all start, the enrolled workers deal the rows."""
+    from oracle import fdlap
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, 384)
+    M = psk.RightILUT().form(psk.DeviceCSR.from_scipy(A))
+    from pysolvers_amd import _native as N
+    for f in (0, 1):   # 0 = sync-free (psk_prec_trisolve_schedule)
+        N.check(N.lib.psk_prec_trisolve_schedule(M.device_handle, f, 0, None, None, None, None, None), "schedule")
+    v = psk.DeviceVector.from_numpy(np.random.default_rng(5).standard_normal(A.shape[0]))
+    ref = M.applyRight(v).numpy()
+    idle = [_workers(M.device_handle, f) for f in (0, 1)]
+    out = _under_occupiers(128, 100 * 1024, lambda: M.applyRight(v).numpy())
+    busy = [_workers(M.device_handle, f) for f in (0, 1)]
+    assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+    for (ei, g), (eb, g2) in zip(idle, busy):
+        assert g == g2 and ei >= g // 2, (ei, g)     # an idle device: (nearly) every workgroup enrolled
+        assert 0 < eb < g, (eb, g)                   # beside the occupiers: fewer workers, still solved
+
+
+@pytest.mark.parametrize("sched", ["band", "grid"])
+def test_block_schedules_beside_occupiers(psk, sched):
+    """triu(-FD 1024^2) — the Gauss-Seidel smoother's factor (ClassicSmoothers.py:33) — on the band
+    schedule (blocks of the solve order) and the grid schedule (64-line bands): workgroups draw their
+    blocks from a ticket counter, so a block only ever waits on blocks held by running workgroups. The
+    band grid is 2 workgroups per CU; occupiers leave 1 on half the CUs. For the grid schedule the
+    occupiers hold every CU but one, so the 16 bands run one after another."""
+    import scipy.sparse.linalg as spla
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 1024)
+    U = sp.triu(A).tocsr()
+    v = np.random.default_rng(9).standard_normal(A.shape[0])
+    M = TriangularSolveChain(A.shape[0], U=U)
+    M.schedule("U", set=sched)
+    ref = M.apply(v)
+    assert np.max(np.abs(ref - spla.spsolve_triangular(U, v, lower=False))) <= 1e-12 * np.max(np.abs(ref))
+    wgs = 128 if sched == "band" else 255
+    out = _under_occupiers(wgs, 100 * 1024, lambda: M.apply(v))
+    assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
+    assert np.array_equal(M.apply(v).view(np.uint64), ref.view(np.uint64))   # counters re-armed
+
+
+def test_amg_apply_beside_occupiers(psk):
+    """A whole AMG V-cycle (every level's smoother factor on its own schedule, the coarse LU, the
+    transfer SpMVs) beside occupiers on half the CUs: same bits as on an idle device."""
+    from oracle import fdlap
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 512)
+    M = psk.AMG(numIters=2, numLevels=4, smoother=psk.GaussSeidelSmoother).form(psk.DeviceCSR.from_scipy(A))
+    v = psk.DeviceVector.from_numpy(np.random.default_rng(2).standard_normal(A.shape[0]))
+    ref = M.applyRight(v).numpy()
+    out = _under_occupiers(128, 100 * 1024, lambda: M.applyRight(v).numpy())
+    assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
