@@ -173,6 +173,13 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
         N.check(N.lib.psk_comm_init(world, rank, uid, ctypes.byref(comm)), "psk_comm_init")
+    # the ranks' dot products: device-side stores into a host-shared mailbox (default; one node) or RCCL
+    # all-gathers (PSK_DOT_TRANSPORT=rccl); the halo of p always goes over the transport above
+    dots = os.environ.get("PSK_DOT_TRANSPORT", "mailbox")
+    if world > 1 and dots == "mailbox":
+        obj = [("/psk_mb_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        N.check(N.lib.psk_comm_mailbox(comm, obj[0]), "psk_comm_mailbox")
 
     # ---- the headline: the metric's N = 10M system on `world` GPUs ----------------------------------
     m = args.side
@@ -211,7 +218,11 @@ def main():
             "config": {"workload": "PCG+Jacobi, FDLaplacian2D %dx%d (n=%d, nnz=%d; the metric's N=10M), tau=0 "
                                    "fixed-iteration" % (m, m, n, nnz),
                        "m": m, "precond": "jacobi", "parallelism": "row-block x%d (%s)" % (world, "RCCL" if transport == "rccl" else "host-shm rehearsal")
-                       if world > 1 else "single GPU"},
+                       if world > 1 else "single GPU",
+                       "transport": {"halo": "rccl send/recv" if transport == "rccl" else "host-shm rehearsal",
+                                     "dots": "mailbox (kernel stores to host-shared memory)" if dots == "mailbox"
+                                     else ("rccl allgather" if transport == "rccl" else "host-shm allgather")}
+                       if world > 1 else None},
             "repeats": {"regions": len(regions), "value_is": "median region",
                         "it_s": [args.steps / r[0] for r in regions],
                         "spmv_avg_launch_ms": [r[1] for r in regions]},

@@ -320,6 +320,13 @@ int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out);
  * solvers run with nranks > 1 on a single GPU, where RCCL refuses duplicate devices. Slow; never
  * used for timing. */
 int psk_comm_init_host(int32_t nranks, int32_t rank, const char *name, psk_comm **out);
+/* Device-side exchange of the sharded solvers' scalars (round 5): attach the host-shared mailbox `name`
+ * ('/...', a POSIX shared-memory name, the same on every rank; collective over the ranks of c, which
+ * must share one node). psk_pcg then exchanges its per-rank dot products by direct system-scope stores
+ * of the kernels that finish them into every rank's mailbox slot and a one-wave gather kernel per rank,
+ * instead of ncclAllGather (the halo of p stays on RCCL / the host transport). Same bits as the
+ * all-gather: every rank still sums the P values in rank order. Replaces nothing in the reference. */
+int psk_comm_mailbox(psk_comm *c, const char *name);
 int psk_comm_destroy(psk_comm *c);
 /* Rank `rank`'s row block of FDLaplacian2D(a,b,m): rows [row_begin,row_end) split on
  * whole grid lines; local columns are [owned | halo_lo | halo_hi]. */

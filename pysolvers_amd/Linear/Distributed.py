@@ -44,6 +44,7 @@ class Communicator:
             uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES).from_buffer_copy(bytes(unique_id))
             N.check(N.lib.psk_comm_init(self.nranks, self.rank, uid, ctypes.byref(h)), "psk_comm_init")
         self._h = h
+        self.mailbox = None
 
     @staticmethod
     def unique_id():
@@ -52,17 +53,30 @@ class Communicator:
         return bytes(uid)
 
     @classmethod
-    def from_torch_distributed(cls, group=None, transport="rccl"):
+    def from_torch_distributed(cls, group=None, transport="rccl", mailbox=False):
         """Collective over the torch.distributed group (any backend; gloo is enough, it only
-        carries the RCCL unique id / the shared segment name)."""
+        carries the RCCL unique id / the shared segment names). mailbox=True also attaches the
+        host-shared mailbox of the device-side scalar exchange (attach_mailbox; ranks on one node)."""
         import os
         import torch.distributed as dist
         rank, world = dist.get_rank(group), dist.get_world_size(group)
+        uid = mbn = None
         if rank == 0:
             uid = cls.unique_id() if transport == "rccl" else ("/psk_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode()
-        obj = [uid if rank == 0 else None]
+            mbn = ("/psk_mb_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode()
+        obj = [uid, mbn]
         dist.broadcast_object_list(obj, src=0, group=group)
-        return cls(world, rank, obj[0], transport=transport)
+        comm = cls(world, rank, obj[0], transport=transport)
+        if mailbox:
+            comm.attach_mailbox(obj[1])
+        return comm
+
+    def attach_mailbox(self, name):
+        """psk_comm_mailbox (collective, one node): the sharded PCG then exchanges its per-rank dot
+        products through kernel stores into a host-shared mailbox instead of all-gathers; same bits."""
+        name = name if isinstance(name, bytes) else str(name).encode()
+        N.check(N.lib.psk_comm_mailbox(self._h, name), "psk_comm_mailbox")
+        self.mailbox = name
 
     @property
     def handle(self):

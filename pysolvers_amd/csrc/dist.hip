@@ -10,8 +10,15 @@
 #include "psk_internal.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <climits>
 #include <cmath>
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <thread>
+#include <unistd.h>
 
 namespace psk {
 
@@ -94,6 +101,85 @@ int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipSt
     if (A->comm->shm) return shm_allgather(A->comm, send, recv, count, s);
     PSK_RCCL(ncclAllGather(send, recv, (size_t)count, ncclDouble, A->comm->nccl, s));
     return PSK_OK;
+}
+
+// ---- device-side scalar exchange through a host-shared mailbox (round 5; psk_internal.hpp Mailbox) ----
+// An RCCL all-gather of a few bytes costs a collective kernel launch and its protocol on the solver's
+// stream (tens of us at P = 8 by DESIGN.md's budget), twice per PCG iteration, on the critical path. Here
+// the kernel that finishes a rank's grid sums (gridsum_mail) stores them directly into every rank's slot,
+// and each rank's one-wave gather kernel polls its own slot: one posted system-scope store per value and
+// one host-memory round trip per poll. Value-is-flag: a slot holds a signalling-NaN sentinel until its
+// value lands; the reader re-arms it after copying. Ring of kMbRing exchanges: exchange e + kMbRing is
+// written by a rank only after it consumed exchange e + kMbRing - 1 from every rank, and every rank
+// consumed e before producing e + 1 (each exchange's values come from a kernel that follows the gather
+// of the previous one), so a slot is never overwritten before its reader re-armed it.
+constexpr size_t kMbHeader = 4096;
+constexpr uint64_t kMbSentinel = 0x7FF0DEAD5EED0001ull;   // sNaN payload: never an arithmetic result
+constexpr uint64_t kMbWaitTicks = (uint64_t)2 << 27;       // s_memrealtime (100 MHz): ~2.7 s
+
+static inline size_t mb_index(const Mailbox &m, int q, int64_t slot, int r, int c) {
+    return (((size_t)q * kMbRing + (size_t)slot) * (size_t)m.P + (size_t)r) * kMbW + (size_t)c;
+}
+
+uint64_t mbox_next(psk_comm *c, GridSum *gs) {
+    Mailbox &m = *c->mb;
+    const uint64_t e = m.seq++;
+    gs->mb = m.dev + mb_index(m, 0, (int64_t)(e % kMbRing), m.rank, 0);
+    gs->mb_q = (int64_t)kMbRing * m.P * kMbW;
+    gs->mb_P = m.P;
+    return e;
+}
+
+// lane q < P: writer q's W values of this rank's slot -> recv[q*W + c], then re-armed
+__global__ void mbox_gather_kernel(uint64_t *mine, int P, int W, double *__restrict__ recv, const int32_t *done,
+                                   int32_t *err) {
+    if (done && __hip_atomic_load(done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;   // uniform
+    const int q = threadIdx.x;
+    if (q >= P) return;
+    for (int c = 0; c < W; ++c) {
+        uint64_t *p = mine + (size_t)q * kMbW + c;
+        uint64_t v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v == kMbSentinel) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while ((v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) == kMbSentinel) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > kMbWaitTicks) {
+                    atomicOr(err, 8);
+                    v = 0x7FF8000000000000ull;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        recv[q * W + c] = __longlong_as_double((long long)v);
+        __hip_atomic_store(p, kMbSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s) {
+    Context *cx;
+    PSK_TRY(ctx(&cx));
+    if (!cx->gs_err) {   // the error word gridsum_check reports (allocated with the first grid sum)
+        GridSum tmp;
+        PSK_TRY(gridsum_prepare(cx, 1, 1, recv, &tmp));
+    }
+    Mailbox &m = *c->mb;
+    if (W < 1 || W > kMbW) return fail(PSK_ERR_ARG, "mbox_gather: bad width");
+    hipLaunchKernelGGL(mbox_gather_kernel, dim3(1), dim3(64), 0, s, m.dev + mb_index(m, m.rank, (int64_t)(seq % kMbRing), 0, 0),
+                       m.P, W, recv, done, cx->gs_err);
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
+static void mbox_close(psk_comm *c) {
+    Mailbox *m = c->mb;
+    if (!m) return;
+    if (m->host) {
+        (void)hipHostUnregister(m->host);
+        munmap(m->host, m->bytes);
+    }
+    if (m->rank == 0) shm_unlink(m->name.c_str());
+    delete m;
+    c->mb = nullptr;
 }
 
 // Row-block plan of the m x m 5-point matrix over P ranks: whole grid lines per rank; local column
@@ -345,8 +431,70 @@ int psk_comm_init_dry(int32_t nranks, int32_t rank, psk_comm **out) {
     return PSK_OK;
 }
 
+// Attach the host-shared mailbox `name` to the communicator (collective: every rank of c, one node).
+// Each rank maps the segment, arms its own reader slots, then waits until all P have attached.
+int psk_comm_mailbox(psk_comm *c, const char *name) {
+    if (!c || !name || name[0] != '/' || std::strlen(name) > 200)
+        return fail(PSK_ERR_ARG, "psk_comm_mailbox: bad arguments (name must start with '/')");
+    if (c->dry) return fail(PSK_ERR_UNSUPPORTED, "psk_comm_mailbox: dry communicator");
+    if (c->mb) return fail(PSK_ERR_ARG, "psk_comm_mailbox: already attached");
+    Mailbox *m = new Mailbox();
+    m->name = name;
+    m->P = c->nranks;
+    m->rank = c->rank;
+    m->bytes = kMbHeader + (size_t)m->P * kMbRing * m->P * kMbW * sizeof(uint64_t);
+    auto bail = [&](int code, const std::string &msg) {
+        c->mb = m;
+        mbox_close(c);
+        return fail(code, "psk_comm_mailbox: " + msg);
+    };
+    const int fd = shm_open(name, O_CREAT | O_RDWR, 0600);
+    if (fd < 0) {
+        delete m;
+        return fail(PSK_ERR_ARG, std::string("psk_comm_mailbox: shm_open ") + name);
+    }
+    struct stat st;
+    if (fstat(fd, &st) == 0 && (size_t)st.st_size < m->bytes && ftruncate(fd, (off_t)m->bytes) != 0) {
+        close(fd);
+        delete m;
+        return fail(PSK_ERR_ALLOC, "psk_comm_mailbox: ftruncate");
+    }
+    void *p = mmap(nullptr, m->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (p == MAP_FAILED) {
+        delete m;
+        return fail(PSK_ERR_ALLOC, "psk_comm_mailbox: mmap");
+    }
+    m->host = static_cast<char *>(p);
+    // mapped for the kernels (fine-grained: system-scope stores and loads are coherent across devices)
+    if (hipHostRegister(m->host, m->bytes, hipHostRegisterMapped | hipHostRegisterPortable) != hipSuccess) {
+        (void)hipGetLastError();
+        munmap(m->host, m->bytes);
+        m->host = nullptr;
+        return bail(PSK_ERR_HIP, "hipHostRegister of the shared segment");
+    }
+    void *dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, m->host, 0) != hipSuccess) return bail(PSK_ERR_HIP, "hipHostGetDevicePointer");
+    m->dev = reinterpret_cast<uint64_t *>(static_cast<char *>(dp) + kMbHeader);
+    uint64_t *slots = reinterpret_cast<uint64_t *>(m->host + kMbHeader);
+    for (int64_t e = 0; e < kMbRing; ++e)   // this rank's reader slots: only it reads and re-arms them
+        for (int r = 0; r < m->P; ++r)
+            for (int k = 0; k < kMbW; ++k) slots[mb_index(*m, m->rank, e, r, k)] = kMbSentinel;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    auto *attached = reinterpret_cast<std::atomic<int32_t> *>(m->host);
+    attached->fetch_add(1);
+    const auto t0 = std::chrono::steady_clock::now();
+    while (attached->load() < m->P) {
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return bail(PSK_ERR_RCCL, "peers did not attach");
+        std::this_thread::yield();
+    }
+    c->mb = m;
+    return PSK_OK;
+}
+
 int psk_comm_destroy(psk_comm *c) {
     if (!c) return PSK_OK;
+    mbox_close(c);
     if (c->nccl) {
         (void)ncclCommDestroy(c->nccl);
         rccl_comm_count(-1);

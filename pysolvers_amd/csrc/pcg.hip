@@ -539,6 +539,11 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
         bd = w.Ap;
     }
+    // sharded with a mailbox (psk_comm_mailbox): the ranks' scalars go kernel -> mailbox -> gather kernel
+    // instead of ncclAllGather; same gathered arrays, same rank-order sums
+    psk_comm *mbc = sharded && A->comm->mb ? A->comm : nullptr;
+    uint64_t seq0 = 0;
+    if (mbc) seq0 = mbox_next(mbc, &gs0);
     PSK_HIP(hipEventRecord(kit->ev0, s));
     const dim3 gk((unsigned)nv);
     if (gen) {
@@ -556,7 +561,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     }
     PSK_HIP(hipGetLastError());
     if (sharded) {
-        PSK_TRY(allgather(A, w.pinit, w.initg, 2, s));
+        if (mbc) PSK_TRY(mbox_gather(mbc, seq0, 2, w.initg, nullptr, s));
+        else PSK_TRY(allgather(A, w.pinit, w.initg, 2, s));
         hipLaunchKernelGGL(pcg_init_finish_kernel, dim3(1), dim3(64), 0, s, w.initg, P, ctl->tau, w.st, w.udr,
                            const_cast<int64_t *>(hdone), hgen);
         PSK_HIP(hipGetLastError());
@@ -640,23 +646,31 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
         }
         // a timed launch records its events in its own dispatch (kernel start / end)
+        uint64_t seq1 = 0;
         if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s,
-                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr)) != PSK_OK)
+                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr, 0, mbc ? &seq1 : nullptr)) != PSK_OK)
             break;
         // K2/K3 tiles in block order: XCD bands matching the SpMV's, and bands walked in alternating
-        // directions, measured no faster (round 4, profiles/r4_spmv_ab.txt)
+        // directions (a serpentine over SpMV, K2, K3 meant to re-read Ap, r and p from the Infinity Cache),
+        // measured no faster (round 4, profiles/r4_spmv_ab.txt: band1 / band2)
         const TileMap tm2 = tile_map_for(nv, false);
-        if (sharded && (rc = allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK) break;
+        if (sharded && (rc = mbc ? mbox_gather(mbc, seq1, 1, w.part1g, &w.st->done, s)
+                                 : allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK)
+            break;
+        GridSum gs2k = gs2;   // this iteration's mailbox slot (sharded with a mailbox)
+        const uint64_t seq2 = mbc ? mbox_next(mbc, &gs2k) : 0;
         if (jac == 2)
             hipLaunchKernelGGL(pcg_update_kernel<2>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2, w.st, w.udr, k, tm2);
+                               gs2k, w.st, w.udr, k, tm2);
         else if (jac == 1)
             hipLaunchKernelGGL(pcg_update_kernel<1>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2, w.st, w.udr, k, tm2);
+                               gs2k, w.st, w.udr, k, tm2);
         else
             hipLaunchKernelGGL(pcg_update_kernel<0>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2, w.st, w.udr, k, tm2);
-        if (sharded && (rc = allgather(A, w.part2, w.part2g, 2, s)) != PSK_OK) break;
+                               gs2k, w.st, w.udr, k, tm2);
+        if (sharded && (rc = mbc ? mbox_gather(mbc, seq2, 2, w.part2g, &w.st->done, s)
+                                 : allgather(A, w.part2, w.part2g, 2, s)) != PSK_OK)
+            break;
         if (gen) {
             if ((rc = prec_apply_dev(M, n, w.r, w.u, s)) != PSK_OK) break;          // u = M^-1 r  :123
             hipLaunchKernelGGL(pcg_dot_kernel, gk, dim3(kBlock), 0, s, n, w.u, w.r, gs3, w.st);

@@ -119,6 +119,23 @@ struct HaloPeer {
 };
 
 struct ShmComm;
+
+// Device-side exchange of the solvers' per-rank scalars through a host-shared mailbox (dist.hip,
+// psk_comm_mailbox; round 5): the kernel that finishes a rank's grid sums stores them straight into
+// every rank's slot of the exchange (system-scope stores to pinned host memory mapped by all ranks of
+// the node), and a one-wave kernel on each rank waits for the P values of its own slot, copies them to
+// the gathered array the solver sums in rank order and re-arms the slot. Slot index (reader q, ring
+// position e mod kMbRing of exchange e, writer r, component c): ((q*kMbRing + e%kMbRing)*P + r)*kMbW + c.
+constexpr int kMbRing = 4;
+constexpr int kMbW = 2;
+struct Mailbox {
+    std::string name;
+    char *host = nullptr;     // the mapped segment (4 KiB header, then the slots)
+    size_t bytes = 0;
+    uint64_t *dev = nullptr;  // device address of the slots
+    int P = 1, rank = 0;
+    uint64_t seq = 0;         // exchanges issued on this communicator (identical on every rank)
+};
 }  // namespace psk
 
 struct psk_comm {
@@ -128,6 +145,7 @@ struct psk_comm {
     ncclComm_t nccl = nullptr;
     bool dry = false;     // psk_comm_init_dry: builds shards, no collectives (single-GPU validation)
     psk::ShmComm *shm = nullptr;   // psk_comm_init_host: shared-memory transport (shmcomm.hip)
+    psk::Mailbox *mb = nullptr;    // psk_comm_mailbox: device-side scalar exchange (dist.hip)
 };
 
 namespace psk {
@@ -396,7 +414,21 @@ struct GridSum {
     int64_t ngroups;    // groups of tiles (one-level: nt)
     int32_t grp_log2;   // tiles of a full group = 2^grp_log2; -1 = one level (nt <= kBlock)
     int32_t *err;       // set when a wait expires (reported by gridsum_check)
+    uint64_t *mb;       // sharded solves: the W grid sums also go to mb[q * mb_q + c] for every rank q < mb_P
+    int64_t mb_q;       // (this rank's writer slot of one exchange in each reader's mailbox; nullptr: none)
+    int32_t mb_P;
 };
+
+// the finished W sums into every rank's mailbox slot (system scope: pinned host memory other ranks poll)
+template <int W>
+__device__ __forceinline__ void gridsum_mail(const GridSum &gs, const double *r) {
+    if (!gs.mb) return;
+    for (int q = 0; q < gs.mb_P; ++q)
+#pragma unroll
+        for (int c = 0; c < W; ++c)
+            __hip_atomic_store(gs.mb + q * gs.mb_q + c, (uint64_t)__double_as_longlong(r[c]), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // tiles of a full group ~ sqrt(nt) (both reductions stay short), and ngroups <= kGridSumMaxGroups
 inline int32_t gridsum_grp_log2(int64_t nt) {
@@ -543,6 +575,7 @@ __device__ __forceinline__ void gridsum_final(const GridSum &gs, double *sh, con
         gridsum_reset(gridsum_counter(gs, kGridSumMaxGroups));
 #pragma unroll
         for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+        gridsum_mail<W>(gs, r);
         fin(r);
     }
 }
@@ -631,6 +664,7 @@ __device__ __forceinline__ void gridsum_final_wave(const GridSum &gs) {
         gridsum_reset(gridsum_counter(gs, kGridSumMaxGroups));
 #pragma unroll
         for (int c = 0; c < W; ++c) gs.out[c] = r[c];
+        gridsum_mail<W>(gs, r);
     }
 }
 
@@ -758,6 +792,11 @@ bool halo_split(const psk_csr *A, int64_t tile, int64_t nv, int64_t &lo, int64_t
 // recv[q*count + i] = rank q's send[i]: no arithmetic, so every rank holds the same bits and
 // reduces them in rank order itself (RCCL's reduction order is algorithm- and rank-dependent)
 int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipStream_t s);
+// mailbox exchanges (psk_comm::mb): the next exchange's writer slots into gs (producer launch), and the
+// gather of that exchange into recv[q*W + c] on s (skipped on the device when *done is set: the producer
+// did not run either); returns the exchange number
+uint64_t mbox_next(psk_comm *c, GridSum *gs);
+int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s);
 
 // SpMV launch (defined in spmv.hip); modes below
 enum SpmvMode : int {
@@ -792,8 +831,9 @@ void sliced_free(psk_csr *A);
 // one-shot SpMV (grid = tiles of A->tile_rows rows); dot modes write their grid sum to partial[0].
 // ev0/ev1 (optional): HIP events the dispatch itself records at the kernel's start and end
 // (hipExtLaunchKernel), so their interval is the kernel alone, without the launch gaps around it
+// mail: the dot sum also goes to the communicator's next mailbox exchange (*mail_seq = its number)
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s,
-                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int rev = 0);
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr, int rev = 0, uint64_t *mail_seq = nullptr);
 
 }  // namespace psk

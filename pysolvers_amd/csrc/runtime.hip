@@ -140,6 +140,9 @@ int gridsum_prepare(Context *c, int64_t nt, int W, double *out, GridSum *gs) {
     gs->ngroups = gridsum_ngroups(nt, gs->grp_log2);
     if (gs->ngroups > kGridSumMaxGroups) return fail(PSK_ERR_ARG, "gridsum_prepare: too many groups");
     gs->err = c->gs_err;
+    gs->mb = nullptr;
+    gs->mb_q = 0;
+    gs->mb_P = 0;
     gs->gslots = c->gs_gslots;
     gs->cnt = c->gs_cnt;
     gs->slots = nullptr;
@@ -188,6 +191,7 @@ int gridsum_check_result(Context *c, int32_t h) {
         PSK_HIP(hipMemsetAsync(c->gs_cnt, 0, cb, c->stream));
     }
     PSK_HIP(hipStreamSynchronize(c->stream));
+    if (h & 8) return fail(PSK_ERR_RCCL, "mailbox exchange: a rank's value did not arrive (2 s wait expired)");
     if (h & 2) return fail(PSK_ERR_HIP, "grid reduction: a launch's grid differs from the tiles it was prepared for");
     if (h & 4) return fail(PSK_ERR_HIP, "grid reduction: a ticket counter was left non-zero by a launch");
     return fail(PSK_ERR_HIP, "grid reduction: an issued partial-sum store never landed (1.3 s wait expired)");

@@ -1240,6 +1240,14 @@ int tile_rows_for(int64_t n, int64_t nnz) {
     return r;
 }
 
+// the dot of an SpMV over no rows: 0, into partial[0] and the mailbox like a finished grid sum
+__global__ void spmv_empty_dot_kernel(GridSum gs, const int32_t *done) {
+    if (threadIdx.x != 0 || (done && *done)) return;
+    const double z[1] = {0.0};
+    gs.out[0] = 0.0;
+    gridsum_mail<1>(gs, z);
+}
+
 // PSK_SPMV_XCD_BANDS=0: tiles in block order (A/B runs); default: XCD-banded (psk_internal.hpp)
 static bool spmv_xcd_bands() {
     static const bool on = [] {
@@ -1262,14 +1270,25 @@ static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) /
 
 int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const double *aux_d,
                 const double *aux_q, double *partial, const int32_t *done_flag, hipStream_t s, hipEvent_t ev0,
-                hipEvent_t ev1, int rev) {
-    if (A->n == 0) return PSK_OK;
+                hipEvent_t ev1, int rev, uint64_t *mail_seq) {
     Context *c;
     PSK_TRY(ctx(&c));
     const bool sliced = A->sl_off != nullptr || A->dg_mask != nullptr;   // 256-row slices
     const int64_t nwg = sliced ? (A->n + kSlice - 1) / kSlice : spmv_tiles(A);
-    GridSum gs{nullptr, nullptr, nullptr, nullptr, 0, 0, -1, nullptr};
-    if (partial) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
+    GridSum gs{nullptr, nullptr, nullptr, nullptr, 0, 0, -1, nullptr, nullptr, 0, 0};
+    if (partial && nwg > 0) PSK_TRY(gridsum_prepare(c, nwg, 1, partial, &gs));
+    if (partial && nwg == 0) gs.out = partial;
+    if (mail_seq) {
+        if (!partial || !A->comm || !A->comm->mb) return fail(PSK_ERR_ARG, "launch_spmv: mailbox without a dot");
+        *mail_seq = mbox_next(A->comm, &gs);
+    }
+    if (A->n == 0) {   // no rows (an empty shard): the dot is 0, still published
+        if (partial) {
+            hipLaunchKernelGGL(spmv_empty_dot_kernel, dim3(1), dim3(64), 0, s, gs, done_flag);
+            PSK_HIP(hipGetLastError());
+        }
+        return PSK_OK;
+    }
     dim3 gd((unsigned)nwg), bd(kBlock);
     // XCD bands for the sliced layouts (N = 10M in the loop 0.078 -> 0.072 ms, back to back 0.067 ->
     // 0.057 ms); the CSR tile kernel measured 2-3% slower with them (3163^2 and 16384^2), so it keeps

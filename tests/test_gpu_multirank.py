@@ -33,7 +33,7 @@ def _matrix(name):
     return golden_matrix(load_golden("pcg_%s_identity.npz" % name))
 
 
-def _worker(rank, world, port, name, kind, out_dir):
+def _worker(rank, world, port, name, kind, out_dir, mailbox=False):
     import sys
     sys.path.insert(0, REPO)
     import torch.distributed as dist
@@ -43,7 +43,7 @@ def _worker(rank, world, port, name, kind, out_dir):
     from oracle import fdlap
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     N.check(N.lib.psk_set_device(0), "psk_set_device")
-    comm = Communicator.from_torch_distributed(transport="host")
+    comm = Communicator.from_torch_distributed(transport="host", mailbox=mailbox)
     A = _matrix(name)
     b, _ = fdlap.manufactured_rhs(A, 12345)
     if kind == "fd":
@@ -63,16 +63,19 @@ def _worker(rank, world, port, name, kind, out_dir):
 # fd512 x 2: shards of 128 slices whose first/last slices (halo lines) keep 32-bit columns while the
 # rest are packed — the sliced SpMV layout across the halo
 # overlap: PSK_HALO_OVERLAP=1, the halo exchange on a second stream overlapping K3 (opt-in)
-@pytest.mark.parametrize("name,kind,world,overlap", [("fd64", "fd", 2, 0), ("fd96", "fd", 3, 0),
-                                                     ("dh12", "general", 3, 0), ("fd50", "general", 4, 0),
-                                                     ("fd512", "fd", 2, 0), ("fd512", "fd", 2, 1),
-                                                     ("fd96", "fd", 3, 1)])
-def test_multirank_pcg_on_one_gpu(tmp_path, monkeypatch, name, kind, world, overlap):
+# mailbox: the ranks' dot products through the host-shared mailbox (psk_comm_mailbox: kernel stores +
+# one-wave gather kernels) instead of the transport's all-gathers; must give the same bits
+@pytest.mark.parametrize("name,kind,world,overlap,mailbox", [
+    ("fd64", "fd", 2, 0, 0), ("fd96", "fd", 3, 0, 0), ("dh12", "general", 3, 0, 0), ("fd50", "general", 4, 0, 0),
+    ("fd512", "fd", 2, 0, 0), ("fd512", "fd", 2, 1, 0), ("fd96", "fd", 3, 1, 0),
+    ("fd64", "fd", 2, 0, 1), ("fd96", "fd", 3, 1, 1), ("dh12", "general", 3, 0, 1), ("fd50", "general", 4, 0, 1),
+    ("fd512", "fd", 4, 1, 1)])
+def test_multirank_pcg_on_one_gpu(tmp_path, monkeypatch, name, kind, world, overlap, mailbox):
     import torch.multiprocessing as mp
     from oracle import fdlap, krylov
     monkeypatch.setenv("PSK_HALO_OVERLAP", str(overlap))   # inherited by the spawned ranks
-    mp.start_processes(_worker, args=(world, _free_port(), name, kind, str(tmp_path)), nprocs=world, join=True,
-                       start_method="spawn")
+    mp.start_processes(_worker, args=(world, _free_port(), name, kind, str(tmp_path), bool(mailbox)), nprocs=world,
+                       join=True, start_method="spawn")
     parts = [dict(np.load(tmp_path / ("r%d.npz" % r))) for r in range(world)]
     A = _matrix(name)
     b, _ = fdlap.manufactured_rhs(A, 12345)
