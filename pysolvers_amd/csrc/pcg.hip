@@ -97,17 +97,17 @@ struct PcgInitFin {
     __device__ void operator()(const double *r) const { pcg_init_state(r[0], r[1], tau, st, udr, hdone, hgen, x_written); }
 };
 
-// ---- K0 (Jacobi/identity): r = b; p_0 = M r; [b.b, u.r] -----------------------------------
+// ---- K0 (Jacobi/identity): p_0 = M b; [b.b, u.r] --------------------------------------------
 // One-shot like K2 (one 512-element tile per workgroup), the two sums finished in the same launch by
 // gridsum and, unsharded, the solver state set by the workgroup that completes them (PcgInitFin; a
-// sharded solve all-gathers the per-rank sums and runs pcg_init_finish_kernel). x0 = 0 is not stored:
+// sharded solve gathers the per-rank sums and runs pcg_init_finish_kernel). x0 = 0 is not stored:
 // K3's first flush of the deferred x updates starts from the literal 0.0 (x = np.zeros_like(b) :100,
-// then x + alpha*p :121: the same roundings), so the init streams 24 B/row instead of 32.
+// then x + alpha*p :121: the same roundings). r = np.copy(b) (:97) is not stored either (round 5): K2
+// of iteration 0 reads b where it would read r, and writes r. The init streams 16 B/row (was 32).
 template <int JAC, bool FUSED>
 __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const double *__restrict__ b,
                                                           const double *__restrict__ dinv, double ds,
-                                                          double *__restrict__ r, double *__restrict__ p, GridSum gs,
-                                                          PcgInitFin fin) {
+                                                          double *__restrict__ p, GridSum gs, PcgInitFin fin) {
     __shared__ double sh[kWaves];
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
     uint32_t ticket = 0;
@@ -122,8 +122,7 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const doubl
             u.x = d.x * bi.x;                          // p = precond.applyRight(r)  :98
             u.y = d.y * bi.y;
         }
-        st2(r + i, bi);                                // r = np.copy(b)             :97
-        st2(p + i, u);
+        st2(p + i, u);                                 // (r = np.copy(b) :97 is read from b by K2)
         bb = fma(bi.x, bi.x, bb);
         bb = fma(bi.y, bi.y, bb);
         ur = fma(u.x, bi.x, ur);                       // uDotR = np.dot(u, r)       :102
@@ -133,7 +132,6 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const doubl
         if (i < n) {   // odd tail element
             const double bi = b[i];
             const double u0 = JAC == 2 ? ds * bi : JAC ? dinv[i] * bi : bi;
-            r[i] = bi;
             p[i] = u0;
             bb = bi * bi;
             ur = u0 * bi;
@@ -156,11 +154,12 @@ __global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgSt
 // One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses). JAC: Jacobi
 // preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
 // diagonal matrices such as stencils: the same products, 8 B/row less per kernel).
-template <int JAC>
+// FIRST (iteration 0): r_0 = b is read from b (the init does not copy it, K0 above).
+template <int JAC, bool FIRST>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
-    int64_t n, double *__restrict__ r, const double *__restrict__ Ap, const double *__restrict__ dinv, double ds,
-    const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st, const double *__restrict__ udr,
-    int64_t k, TileMap tm) {
+    int64_t n, double *__restrict__ r, const double *__restrict__ b, const double *__restrict__ Ap,
+    const double *__restrict__ dinv, double ds, const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st,
+    const double *__restrict__ udr, int64_t k, TileMap tm) {
     if (st->done) return;
     __shared__ double sh[kWaves];
     const double pTAp = rank_sum(pap, nparts, 1, 0);         // np.dot(p, Ap)  :113 (K1's grid sum)
@@ -183,7 +182,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
     if (i + 1 < n) {
-        const dv2 ro = ld2(r + i), a = ld2nt(Ap + i);
+        const dv2 ro = FIRST ? ld2nt(b + i) : ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2(dinv + i);
         ticket = gridsum_ticket(gs, tile);
@@ -202,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
         ticket = gridsum_ticket(gs, tile);
-        const double rn = r[i] - alpha * Ap[i];
+        const double rn = (FIRST ? b[i] : r[i]) - alpha * Ap[i];
         const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
         rr = rn * rn;
@@ -351,6 +350,24 @@ __global__ void pcg_flush_kernel(int64_t n, double *__restrict__ x, PRing pr, co
                                  int64_t k) {
     const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i < n) x[i] = pcg_catch_up(k < kPcgDefer ? 0.0 : x[i], &pr, pcg_pending(k), k, alphas, i);
+}
+
+// ---- end of a solve: the state, the scan of the gridsum ticket counters (gridsum_counter_check_kernel's)
+// and the gridsum error word into the host-mapped words at kit->hmap + kPcgFinishWord (system scope)
+constexpr int kPcgStateWords = (int)(sizeof(PcgState) / 8);
+constexpr int kPcgFinishWord = 8;
+static_assert(sizeof(PcgState) % 8 == 0 && kPcgFinishWord + kPcgStateWords + 1 <= 64, "SolveKit::hmap words");
+__global__ __launch_bounds__(kBlock) void pcg_finish_kernel(const PcgState *st, const uint32_t *cnt, const int32_t *err,
+                                                            int64_t *hw) {
+    uint32_t any = 0;
+    for (int g = threadIdx.x; g <= kGridSumMaxGroups; g += kBlock) any |= cnt[(int64_t)g * kGridSumCntStride];
+    const bool bad = __syncthreads_or(any != 0);
+    if (threadIdx.x < kPcgStateWords)
+        __hip_atomic_store(hw + threadIdx.x, reinterpret_cast<const int64_t *>(st)[threadIdx.x], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0)
+        __hip_atomic_store(hw + kPcgStateWords, (int64_t)(*err | (bad ? 4 : 0)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---- general preconditioner (ILU, ...): u = M^-1 r is materialised by the preconditioner's own
@@ -535,9 +552,10 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     *hdone = 0;
     const PcgInitFin fin{ctl->tau, w.st, w.udr, const_cast<int64_t *>(hdone), hgen, gen ? 1 : 0};
     const double *bd = b;
-    if (!dev_io) {   // host b staged in the Ap buffer (unused until the first SpMV)
-        PSK_TRY(to_device_vec(b, loc, n, w.Ap, s));
-        bd = w.Ap;
+    if (!dev_io) {   // host b staged in r (r_0 = b already: K2 of iteration 0 then reads r as usual), or, on
+                     // the general path, in Ap (unused until the first SpMV; its init copies r = b)
+        PSK_TRY(to_device_vec(b, loc, n, gen ? w.Ap : w.r, s));
+        bd = gen ? w.Ap : w.r;
     }
     // sharded with a mailbox (psk_comm_mailbox): the ranks' scalars go kernel -> mailbox -> gather kernel
     // instead of ncclAllGather; same gathered arrays, same rank-order sums
@@ -553,7 +571,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         hipLaunchKernelGGL(pcg_gen_init2_kernel, gk, dim3(kBlock), 0, s, n, w.r, w.u, w.p, gs0, fin);
     } else {
 #define PSK_PCG_INIT(J, F) \
-        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gk, dim3(kBlock), 0, s, n, bd, dinv, ds, w.r, w.p, gs0, fin)
+        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gk, dim3(kBlock), 0, s, n, bd, dinv, ds, w.p, gs0, fin)
         if (jac == 2) { if (sharded) PSK_PCG_INIT(2, false); else PSK_PCG_INIT(2, true); }
         else if (jac == 1) { if (sharded) PSK_PCG_INIT(1, false); else PSK_PCG_INIT(1, true); }
         else { if (sharded) PSK_PCG_INIT(0, false); else PSK_PCG_INIT(0, true); }
@@ -659,15 +677,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             break;
         GridSum gs2k = gs2;   // this iteration's mailbox slot (sharded with a mailbox)
         const uint64_t seq2 = mbc ? mbox_next(mbc, &gs2k) : 0;
-        if (jac == 2)
-            hipLaunchKernelGGL(pcg_update_kernel<2>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2k, w.st, w.udr, k, tm2);
-        else if (jac == 1)
-            hipLaunchKernelGGL(pcg_update_kernel<1>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2k, w.st, w.udr, k, tm2);
-        else
-            hipLaunchKernelGGL(pcg_update_kernel<0>, gk, dim3(kBlock), 0, s, n, w.r, w.Ap, dinv, ds, w.part1g, P,
-                               gs2k, w.st, w.udr, k, tm2);
+        // the general path copied r = b in its init (pcg_gen_init_kernel): it never takes the FIRST form
+        const bool first = k == 0 && !gen && dev_io;
+#define PSK_PCG_K2(J, F)                                                                                       \
+        hipLaunchKernelGGL((pcg_update_kernel<J, F>), gk, dim3(kBlock), 0, s, n, w.r, bd, w.Ap, dinv, ds, w.part1g, \
+                           P, gs2k, w.st, w.udr, k, tm2)
+        if (jac == 2) { if (first) PSK_PCG_K2(2, true); else PSK_PCG_K2(2, false); }
+        else if (jac == 1) { if (first) PSK_PCG_K2(1, true); else PSK_PCG_K2(1, false); }
+        else { if (first) PSK_PCG_K2(0, true); else PSK_PCG_K2(0, false); }
+#undef PSK_PCG_K2
         if (sharded && (rc = mbc ? mbox_gather(mbc, seq2, 2, w.part2g, &w.st->done, s)
                                  : allgather(A, w.part2, w.part2g, 2, s)) != PSK_OK)
             break;
@@ -712,15 +730,17 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // a halo exchange still in flight (the host stopped enqueueing first) completes before the end
     if (halo_pending && hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess && rc == PSK_OK) rc = fail(PSK_ERR_HIP, "halo wait");
     if (rc == PSK_OK && hipEventRecord(kit->ev1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
-    // one synchronisation for the state and the gridsum error word (pinned staging)
-    PcgState *hsp = static_cast<PcgState *>(kit->hstage);
-    int32_t *herr = reinterpret_cast<int32_t *>(static_cast<char *>(kit->hstage) + 512);
-    if (rc == PSK_OK && hipMemcpyAsync(hsp, w.st, sizeof(PcgState), hipMemcpyDeviceToHost, s) != hipSuccess)
-        rc = fail(PSK_ERR_HIP, "state copy");
-    if (rc == PSK_OK) rc = gridsum_check_enqueue(c, herr);
+    // one launch and one synchronisation for the state, the ticket-counter scan and the gridsum error word,
+    // all written by pcg_finish_kernel into the host-mapped words (round 5: was two copies and a kernel)
+    int64_t *hw = kit->hmap + kPcgFinishWord;
+    if (rc == PSK_OK) {
+        hipLaunchKernelGGL(pcg_finish_kernel, dim3(1), dim3(kBlock), 0, s, w.st, c->gs_cnt, c->gs_err, hw);
+        if (hipGetLastError() != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg finish");
+    }
     if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg sync");
-    const PcgState hs = *hsp;
-    if (rc == PSK_OK) rc = gridsum_check_result(c, *herr);
+    PcgState hs;
+    std::memcpy(&hs, hw, sizeof(PcgState));
+    if (rc == PSK_OK) rc = gridsum_check_result(c, (int32_t)hw[kPcgStateWords]);
     if (rc == PSK_OK && gen) rc = prec_check_error(M, s);
     if (rc == PSK_OK && ctl->time_kernels)
         for (int i = 0; i < TP && rc == PSK_OK; ++i) rc = harvest(i);
@@ -777,10 +797,13 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             }
             // no iteration stored x (b = 0, dot(u,r) = 0 at the start, maxiter = 0, or a dot(p,Ap)
             // breakdown at k = 0): the solution is x0 = 0
-            if (rc == PSK_OK && !x_written && n > 0 && hipMemsetAsync(w.x, 0, (size_t)n * 8, s) != hipSuccess)
-                rc = fail(PSK_ERR_HIP, "x zero");
+            bool more = x_written != (hs.x_written != 0) || !dev_io;   // work enqueued after the sync
+            if (rc == PSK_OK && !x_written && n > 0) {
+                if (hipMemsetAsync(w.x, 0, (size_t)n * 8, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x zero");
+                more = true;
+            }
             if (rc == PSK_OK && !dev_io) rc = from_device_vec(w.x, loc, n, xout, s);
-            if (rc == PSK_OK && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x copy");
+            if (rc == PSK_OK && more && hipStreamSynchronize(s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x copy");
         }
         if (ctl->time_kernels) {
             double tot = 0.0;

@@ -229,6 +229,21 @@ __device__ __forceinline__ double dict_pick(const DictRegs dv, uint32_t idx) {
 // branch on the pointer, so its load goes out with the slice header)
 __device__ int32_t g_spmv_never_done = 0;
 
+#ifdef PSK_SPMV_PROF
+// development probe (tools/spmv_probe.py, a -DPSK_SPMV_PROF build): s_memrealtime (100 MHz, one clock for
+// every XCD) per workgroup of the last launch: [0] entry, [1] sums done (before the dot epilogue), [2] end;
+// per group reduction [start, end] at kSpmvProfGrp + 2g, the final reduction at kSpmvProfFin
+constexpr int kSpmvProfWg = 32768, kSpmvProfGrp = 3 * kSpmvProfWg, kSpmvProfFin = kSpmvProfGrp + 2 * 4096;
+__device__ unsigned long long g_spmv_prof[kSpmvProfFin + 2];
+extern "C" int psk_spmv_prof_read(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_spmv_prof), sizeof(g_spmv_prof)) == hipSuccess ? 0 : -1;
+}
+#define PSK_SPMV_PROF_AT(slot) \
+    do { if (threadIdx.x == 0 && blockIdx.x < kSpmvProfWg) g_spmv_prof[blockIdx.x * 3 + (slot)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PSK_SPMV_PROF_AT(slot) do { } while (0)
+#endif
+
 // The dictionary entries DK needs, as scalar loads (the buffer is padded to kDictMax entries).
 template <int DK>
 __device__ __forceinline__ DictRegs load_dict(const double *__restrict__ sdict) {
@@ -409,13 +424,29 @@ __device__ __forceinline__ void spmv_publish_multi(const GridSum &gs, GridSumTil
         int64_t base;
         const int64_t cnt = gridsum_members(gs, g, base);
         if (tk[q] != (uint32_t)(cnt - 1)) continue;
+#ifdef PSK_SPMV_PROF
+        if (lane0 && g < 4096) g_spmv_prof[kSpmvProfGrp + 2 * g] = __builtin_amdgcn_s_memrealtime();
+#endif
         double r[1];
         gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
         if (lane0) {
             gridsum_reset(gridsum_counter(gs, g));
             gridsum_put(gs.gslots + g, r[0]);
         }
+#ifdef PSK_SPMV_PROF
+        if (lane0 && g < 4096) g_spmv_prof[kSpmvProfGrp + 2 * g + 1] = __builtin_amdgcn_s_memrealtime();
+        const uint64_t tf = __builtin_amdgcn_s_memrealtime();
+#endif
         gridsum_final_wave<1>(gs);
+#ifdef PSK_SPMV_PROF
+        if (lane0) {
+            const uint64_t te = __builtin_amdgcn_s_memrealtime();
+            if (te - tf > 20) {   // > 200 ns: this wave ran the final reduction (a non-final return is immediate)
+                g_spmv_prof[kSpmvProfFin] = tf;
+                g_spmv_prof[kSpmvProfFin + 1] = te;
+            }
+        }
+#endif
     }
 }
 
@@ -566,6 +597,10 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
 // per SpMV); x is gathered and y written as before (16 B per row). Same 256-row slices, one row per lane,
 // TPW slices per workgroup and gridsum tiles as spmv_uniform_multi_kernel: p.Ap has the same bits.
 constexpr int kDiagMax = 8;
+#ifndef PSK_DIAG_TPW
+#define PSK_DIAG_TPW 2
+#endif
+constexpr int kDiagTpw = PSK_DIAG_TPW;   // slices per workgroup
 struct DiagDesc {
     int32_t d[kDiagMax];   // diagonal offsets, in every row's stored order
     double v[kDiagMax];    // the value (bit pattern) of every entry on diagonal j
@@ -586,6 +621,7 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
     TileMap tm, int64_t ntiles) {
     const int32_t dn = *(done ? done : &g_spmv_never_done);
+    PSK_SPMV_PROF_AT(0);
     const int tid = threadIdx.x;
     const int64_t grp = tile_of_block(tm);
     int64_t tl[TPW];
@@ -660,12 +696,17 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
         }
         yv[q] = spmv_row_value<MODE>(has, sum, eq[q], acc[q]);
     }
+#ifdef PSK_SPMV_PROF
+    if (threadIdx.x == 0) __asm__ volatile("" ::"v"(acc[0]));
+#endif
+    PSK_SPMV_PROF_AT(1);
     if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t row = tl[q] * kSlice + tid;
         spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
     }
+    PSK_SPMV_PROF_AT(2);
 }
 
 // Diagonal-layout detection: row `row`'s stored entries must be, in order, entries of strictly increasing
@@ -1304,19 +1345,21 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     const int64_t nwg2 = (nwg + tpw - 1) / tpw;
     const dim3 gd2((unsigned)(nwg2 > 0 ? nwg2 : 1));
     const TileMap tm2 = tile_map_for(nwg2, sliced && spmv_xcd_bands(), rev != 0);
-    if (A->dg_mask) {   // diagonal layout: TPW slices per workgroup as the compact kernel
+    if (A->dg_mask) {   // diagonal layout: kDiagTpw slices per workgroup
         const DiagDesc dd = diag_desc(A);
         const int km = A->dg_K <= 3 ? 3 : A->dg_K <= 5 ? 5 : 8;
+        const int64_t nwgd = (nwg + kDiagTpw - 1) / kDiagTpw;
+        const dim3 gdd((unsigned)(nwgd > 0 ? nwgd : 1));
+        const TileMap tmd = tile_map_for(nwgd, spmv_xcd_bands(), rev != 0);
 #define PSK_DIAG_LAUNCH(M, KM)                                                                                     \
-    hipExtLaunchKernelGGL((spmv_diag_kernel<M, KM, 2>), gd2, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, x, y, aux_d, \
-                          aux_q, gs, done_flag, tm2, nwg)
+    hipExtLaunchKernelGGL((spmv_diag_kernel<M, KM, kDiagTpw>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, x, y, \
+                          aux_d, aux_q, gs, done_flag, tmd, nwg)
 #define PSK_DIAG_MODE(M)                                                                                           \
     do {                                                                                                           \
         if (km == 3) PSK_DIAG_LAUNCH(M, 3);                                                                        \
         else if (km == 5) PSK_DIAG_LAUNCH(M, 5);                                                                   \
         else PSK_DIAG_LAUNCH(M, 8);                                                                                \
     } while (0)
-        if (tpw != 2) return fail(PSK_ERR_UNSUPPORTED, "diagonal layout: PSK_SPMV_TPW must be 2");
         switch (mode) {
         case kSpmvPlain: PSK_DIAG_MODE(kSpmvPlain); break;
         case kSpmvDot: PSK_DIAG_MODE(kSpmvDot); break;
@@ -1922,6 +1965,10 @@ int psk_prec_apply(const psk_prec *M, int64_t n, const double *v, double *outv, 
         return PSK_OK;
     }
     DevBuf tmp;
+    struct Release {   // (DevBuf has no destructor: the staging buffer was leaked before round 5)
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } rel{tmp};
     const double *dv = v;
     double *dout = outv;
     if (loc == PSK_HOST || v == outv) {

@@ -305,18 +305,19 @@ def test_diag_layout_bitwise(psk, which):
     if rect:
         return
     b = A @ rng.random(A.shape[0])
-    sols = []
+    sols = {}
     for lay in ("diag", "sliced_dict", "csr"):
         dA.set_layout(lay)
+        sols[lay] = []
         for f, pre in ((psk.PCG, psk.Jacobi()), (psk.GMRES, psk.Jacobi()), (psk.GMRES, None)):
             kw = {"precond": pre} if pre is not None else {}
-            sols.append(f(control=_ctl(maxiter=60, tau=1e-9), **kw).makeSolver().solve(dA, b))
-    k = len(sols) // 3
-    for i in range(k):
-        for j in (k, 2 * k):
-            assert sols[i].iters() == sols[i + j].iters()
-            assert np.array_equal(sols[i].soln(), sols[i + j].soln())
-            assert np.array_equal(sols[i].info["hist"], sols[i + j].info["hist"])
+            sols[lay].append(f(control=_ctl(maxiter=60, tau=1e-9), **kw).makeSolver().solve(dA, b))
+    for d, s, c in zip(sols["diag"], sols["sliced_dict"], sols["csr"]):
+        # the sliced layout sums the fused dot products over the same 256-row slices: identical bits; the
+        # CSR kernel's tiles are 128 rows when rows are long (lap3d), so its dots round differently
+        assert d.iters() == s.iters() == c.iters()
+        assert np.array_equal(d.soln(), s.soln()) and np.array_equal(d.info["hist"], s.info["hist"])
+        assert np.max(np.abs(d.soln() - c.soln())) <= 1e-10 * np.max(np.abs(c.soln()))
 
 
 def test_diag_layout_refused(psk):

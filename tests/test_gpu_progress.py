@@ -26,16 +26,25 @@ def psk():
     return pysolvers_amd
 
 
-def _under_occupiers(wgs, lds, fn):
+def _apply_under_occupiers(handle, v, wgs, lds=100 * 1024):
+    """psk_prec_apply of device vector v into a device buffer allocated beforehand, beside the occupiers;
+    the result read back after they are released. Nothing is freed inside the window: hipFree waits for
+    the whole device, the occupiers' stream included, which would make the test wait for them."""
     from pysolvers_amd import _native as N
+    out = psk_mod().DeviceVector(v.n)
     N.check(N.lib.psk_lab_occupy_begin(wgs, lds, 30.0), "psk_lab_occupy_begin")
     timed_out = N.I32()
     try:
-        out = fn()
+        N.check(N.lib.psk_prec_apply(handle, v.n, v._p, out._p, N.PSK_DEVICE), "psk_prec_apply")
     finally:
         N.check(N.lib.psk_lab_occupy_end(ctypes.byref(timed_out)), "psk_lab_occupy_end")
     assert timed_out.value == 0, "the occupiers hit their time limit: the solve waited for them"
-    return out
+    return out.numpy()
+
+
+def psk_mod():
+    import pysolvers_amd
+    return pysolvers_amd
 
 
 def _workers(handle, which):
@@ -58,7 +67,7 @@ def test_syncfree_ilu_apply_beside_occupiers(psk):
     v = psk.DeviceVector.from_numpy(np.random.default_rng(5).standard_normal(A.shape[0]))
     ref = M.applyRight(v).numpy()
     idle = [_workers(M.device_handle, f) for f in (0, 1)]
-    out = _under_occupiers(128, 100 * 1024, lambda: M.applyRight(v).numpy())
+    out = _apply_under_occupiers(M.device_handle, v, 128)
     busy = [_workers(M.device_handle, f) for f in (0, 1)]
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
     for (ei, g), (eb, g2) in zip(idle, busy):
@@ -72,7 +81,8 @@ def test_block_schedules_beside_occupiers(psk, sched):
     schedule (blocks of the solve order) and the grid schedule (64-line bands): workgroups draw their
     blocks from a ticket counter, so a block only ever waits on blocks held by running workgroups. The
     band grid is 2 workgroups per CU; occupiers leave 1 on half the CUs. For the grid schedule the
-    occupiers hold every CU but one, so the 16 bands run one after another."""
+    occupiers hold 31 of the 32 CUs of every XCD (workgroups are dealt to the XCDs round-robin and only
+    start on their own XCD's CUs), so at most one band per XCD runs at a time."""
     import scipy.sparse.linalg as spla
     from oracle import fdlap
     from pysolvers_amd.Linear import TriangularSolveChain
@@ -83,8 +93,8 @@ def test_block_schedules_beside_occupiers(psk, sched):
     M.schedule("U", set=sched)
     ref = M.apply(v)
     assert np.max(np.abs(ref - spla.spsolve_triangular(U, v, lower=False))) <= 1e-12 * np.max(np.abs(ref))
-    wgs = 128 if sched == "band" else 255
-    out = _under_occupiers(wgs, 100 * 1024, lambda: M.apply(v))
+    wgs = 128 if sched == "band" else 248
+    out = _apply_under_occupiers(M.device_handle, psk.DeviceVector.from_numpy(v), wgs)
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
     assert np.array_equal(M.apply(v).view(np.uint64), ref.view(np.uint64))   # counters re-armed
 
@@ -97,5 +107,5 @@ def test_amg_apply_beside_occupiers(psk):
     M = psk.AMG(numIters=2, numLevels=4, smoother=psk.GaussSeidelSmoother).form(psk.DeviceCSR.from_scipy(A))
     v = psk.DeviceVector.from_numpy(np.random.default_rng(2).standard_normal(A.shape[0]))
     ref = M.applyRight(v).numpy()
-    out = _under_occupiers(128, 100 * 1024, lambda: M.applyRight(v).numpy())
+    out = _apply_under_occupiers(M.device_handle, v, 128)
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))

@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Lab probe of the triangular solves beside occupiers (tests/test_gpu_progress.py's setting, verbose).
+
+    python tools/progress_probe.py [--m 384] [--wgs 128] [--lds 102400] [--seconds 8] [--sched syncfree]
+
+Prints, for an idle device and then beside `wgs` occupier workgroups: the apply's wall time, the
+enrolled workers / grid of each sync-free factor, whether the occupiers timed out, the error word, and
+whether the result kept its bits.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=384)
+    ap.add_argument("--wgs", type=int, default=128)
+    ap.add_argument("--lds", type=int, default=100 * 1024)
+    ap.add_argument("--seconds", type=float, default=8.0)
+    ap.add_argument("--sched", default="syncfree")
+    a = ap.parse_args()
+    os.environ.setdefault("PSK_NO_TORCH", "1")
+    import pysolvers_amd as psk
+    from pysolvers_amd import _native as N
+    from oracle import fdlap
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, a.m)
+    M = psk.RightILUT().form(psk.DeviceCSR.from_scipy(A))
+    code = {"syncfree": 0, "band": 1, "part": 4}[a.sched]
+    for f in (0, 1):
+        N.check(N.lib.psk_prec_trisolve_schedule(M.device_handle, f, code, None, None, None, None, None), "schedule")
+    v = psk.DeviceVector.from_numpy(np.random.default_rng(5).standard_normal(A.shape[0]))
+
+    def workers():
+        out = []
+        for f in (0, 1):
+            e, g = N.I32(), N.I32()
+            N.check(N.lib.psk_lab_trisolve_workers(M.device_handle, f, ctypes.byref(e), ctypes.byref(g)), "workers")
+            out.append((e.value, g.value))
+        return out
+
+    out = psk.DeviceVector(A.shape[0])
+
+    def timed():   # nothing allocated or freed inside (hipFree waits for the whole device)
+        t0 = time.perf_counter()
+        try:
+            N.check(N.lib.psk_prec_apply(M.device_handle, A.shape[0], v._p, out._p, N.PSK_DEVICE), "apply")
+            err = None
+        except N.PskError as e:
+            err = str(e)
+        return (time.perf_counter() - t0) * 1e3, err
+
+    ms, err = timed()
+    print(json.dumps({"phase": "idle", "ms": ms, "err": err, "workers": workers()}), flush=True)
+    ms, err = timed()
+    ref = out.numpy()
+    print(json.dumps({"phase": "idle2", "ms": ms, "err": err, "workers": workers()}), flush=True)
+    N.check(N.lib.psk_lab_occupy_begin(a.wgs, a.lds, a.seconds), "occupy_begin")
+    ms, err = timed()
+    to = N.I32()
+    N.check(N.lib.psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
+    y = out.numpy()
+    print(json.dumps({"phase": "occupied", "ms": ms, "err": err, "timed_out": to.value, "workers": workers(),
+                      "same_bits": None if y is None else bool(np.array_equal(y.view(np.uint64), ref.view(np.uint64)))}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()
