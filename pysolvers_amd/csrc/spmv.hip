@@ -615,18 +615,30 @@ __device__ __forceinline__ int64_t diag_col(const DiagDesc &dd, int64_t n, int64
     return c < 0 ? 0 : (c >= dd.ncols ? dd.ncols - 1 : c);   // absent diagonals gather a valid x (unused)
 }
 
+// a zero the compiler cannot see through: turns a uniform load into a per-lane (vector) load
+__device__ __forceinline__ int32_t spmv_vzero() {
+    int32_t z;
+    __asm__ volatile("v_mov_b32 %0, 0" : "=v"(z));
+    return z;
+}
+
 template <int MODE, int KM, int TPW>
 __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
     int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd, const double *__restrict__ x, double *__restrict__ y,
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
     TileMap tm, int64_t ntiles) {
-    const int32_t dn = *(done ? done : &g_spmv_never_done);
     PSK_SPMV_PROF_AT(0);
+    // ONE memory round trip per workgroup: the done flag (a vector load, so that waiting for it leaves the
+    // loads issued after it in flight), the presence bytes and every diagonal's x (clamped addresses that do
+    // not depend on the bytes) all go out before anything waits. Tested first, the flag's scalar load and
+    // the presence bytes each cost a round trip of their own in front of the gathers (round 5 probe).
+    const int32_t dnv = (done ? done : &g_spmv_never_done)[spmv_vzero()];
     const int tid = threadIdx.x;
     const int64_t grp = tile_of_block(tm);
     int64_t tl[TPW];
     bool tv[TPW];
     uint32_t mk[TPW];
+    double xv[TPW][KM], eq[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t t = grp * TPW + q;
@@ -634,36 +646,6 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
         tl[q] = tv[q] ? t : ntiles - 1;
         mk[q] = __builtin_nontemporal_load(mask + tl[q] * kSlice + tid);   // padded to whole slices
     }
-    double eq[TPW];
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-        const int64_t row = tl[q] * kSlice + tid;
-        eq[q] = 0.0;
-        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
-            eq[q] = aux_q[row < n ? row : 0];
-    }
-    if (dn != 0) {
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) __asm__ volatile("" ::"v"(mk[q]));
-        return;
-    }
-    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
-    __shared__ GridSumTile<1> gsl[TPW];
-    uint32_t ticket[TPW];
-    const bool pub = PUB && spmv_publishes<MODE>(gs);
-    if (pub) {
-        if (tid < TPW) gsl[tid].cnt = 0;
-        if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            ticket[q] = 0;
-            if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
-                ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
-        }
-    }
-    // every diagonal's x gathered unconditionally (absent ones at a clamped address), then the sums
-    double xv[TPW][KM], acc[TPW], yv[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t row = tl[q] * kSlice + tid;
@@ -673,25 +655,61 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
             xv[q][j] = x[c];
             if (MODE == kSpmvJacobiDot) xv[q][j] = aux_d[c] * xv[q][j];   // (DInv*q)[c], rounded
         }
+        eq[q] = 0.0;
+        if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+            eq[q] = aux_q[row < n ? row : 0];
     }
+    // the tiles' gridsum tickets drawn now, while the loads are in flight (their values are read at publish)
+    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
+    const bool pub = PUB && spmv_publishes<MODE>(gs);
+    uint32_t ticket[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        ticket[q] = 0;
+        if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
+            ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+    }
+    if (__builtin_amdgcn_readfirstlane(dnv) != 0) {   // uniform: the solve has stopped
+        // consumed on this path too, so the loads are issued before the test on both; the tickets are
+        // handed back (every workgroup of this launch leaves here: nobody reduces)
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            __asm__ volatile("" ::"v"(mk[q]));
+#pragma unroll
+            for (int j = 0; j < KM; ++j) __asm__ volatile("" ::"v"(xv[q][j]));
+            if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
+                __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    __shared__ GridSumTile<1> gsl[TPW];
+    if (pub) {
+        if (tid < TPW) gsl[tid].cnt = 0;
+        if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
+        __syncthreads();
+    }
+    double acc[TPW], yv[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t row = tl[q] * kSlice + tid;
         const bool has = tv[q] && row < n;
         double sum = 0.0;
 #pragma unroll
-        for (int j = 0; j < KM; ++j)
-            if ((mk[q] >> j) & 1u) sum = sum + dd.v[j] * xv[q][j];   // stored order, rounded product
+        for (int j = 0; j < KM; ++j) {   // stored order, rounded product; absent diagonals by a select
+            const double t = sum + dd.v[j] * xv[q][j];
+            sum = ((mk[q] >> j) & 1u) ? t : sum;
+        }
         if (MODE == kSpmvDot) {   // x[row]: the gathered diagonal when the row stores it
             double d = 0.0;
             bool found = false;
 #pragma unroll
-            for (int j = 0; j < KM; ++j)
-                if (j == dd.jd && ((mk[q] >> j) & 1u)) {
-                    d = xv[q][j];
-                    found = true;
-                }
-            if (!found && has) d = x[row];
+            for (int j = 0; j < KM; ++j) {
+                const bool here = j == dd.jd && ((mk[q] >> j) & 1u);
+                d = here ? xv[q][j] : d;
+                found = found || here;
+            }
+            if (!found && has) d = x[row];   // rare: a row without its diagonal
             eq[q] = d;
         }
         yv[q] = spmv_row_value<MODE>(has, sum, eq[q], acc[q]);
@@ -707,6 +725,105 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
         spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
     }
     PSK_SPMV_PROF_AT(2);
+}
+
+// Persistent form of spmv_diag_kernel (round 5 lab, PSK_SPMV_PERSIST=1): one resident grid, each workgroup
+// walking units of TPW slices of its XCD's band, the next unit's presence bytes and x gathers issued before
+// the current unit's dot epilogue and y stores, so a workgroup keeps its memory pipeline full instead of
+// ending after one unit and waiting for the dispatcher to start the next (the one-shot kernel at N = 10M:
+// ~4 us per workgroup, starts spread over 55 us, tools/spmv_probe.py). Same tiles, same per-tile gridsum
+// slots and tickets: the same bits. Tickets of a unit are drawn after the previous unit's reductions, so a
+// workgroup never holds an unpublished ticket while it waits.
+template <int MODE, int KM, int TPW>
+__global__ __launch_bounds__(kBlock) void spmv_diag_persist_kernel(
+    int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd, const double *__restrict__ x, double *__restrict__ y,
+    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
+    int64_t nunits, int64_t ntiles) {
+    if (*(done ? done : &g_spmv_never_done) != 0) return;   // uniform
+    const int tid = threadIdx.x;
+    // XCD band: workgroups are dealt round-robin over the 8 XCDs; XCD k walks units [s, e) with its Gk workgroups
+    const int64_t b = blockIdx.x, G = gridDim.x;
+    const int k = (int)(b & 7);
+    const int64_t j = b >> 3, Gk = (G - k + 7) >> 3;
+    const int64_t a = nunits >> 3, rr = nunits & 7;
+    const int64_t s0 = k * a + (k < rr ? k : rr), e0 = s0 + a + (k < rr ? 1 : 0);
+    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
+    const bool pub = PUB && spmv_publishes<MODE>(gs);
+    __shared__ GridSumTile<1> gsl[TPW];
+    uint32_t mk[TPW];
+    double xv[TPW][KM], eq[TPW];
+    auto load = [&](int64_t u) {
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const int64_t t0 = u * TPW + q, t = t0 < ntiles ? t0 : ntiles - 1;
+            const int64_t row = t * kSlice + tid;
+            mk[q] = __builtin_nontemporal_load(mask + row);   // padded to whole slices
+            eq[q] = 0.0;
+            if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
+                eq[q] = aux_q[row < n ? row : 0];
+#pragma unroll
+            for (int jj = 0; jj < KM; ++jj) {
+                const int64_t c = diag_col(dd, n, row, jj);
+                xv[q][jj] = x[c];
+                if (MODE == kSpmvJacobiDot) xv[q][jj] = aux_d[c] * xv[q][jj];
+            }
+        }
+    };
+    int64_t u = s0 + j;
+    if (u < e0) load(u);
+    for (; u < e0; u += Gk) {
+        int64_t tl[TPW];
+        bool tv[TPW];
+        uint32_t ticket[TPW];
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const int64_t t = u * TPW + q;
+            tv[q] = t < ntiles;
+            tl[q] = tv[q] ? t : ntiles - 1;
+        }
+        if (pub) {
+            __syncthreads();   // every wave is past the previous unit's LDS combine
+            if (tid < TPW) gsl[tid].cnt = 0;
+            __syncthreads();
+#pragma unroll
+            for (int q = 0; q < TPW; ++q) {
+                ticket[q] = 0;
+                if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
+                    ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+            }
+        }
+        double acc[TPW], yv[TPW];
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const int64_t row = tl[q] * kSlice + tid;
+            const bool has = tv[q] && row < n;
+            double sum = 0.0;
+#pragma unroll
+            for (int jj = 0; jj < KM; ++jj)
+                if ((mk[q] >> jj) & 1u) sum = sum + dd.v[jj] * xv[q][jj];   // stored order, rounded product
+            double e = eq[q];
+            if (MODE == kSpmvDot) {
+                double d = 0.0;
+                bool found = false;
+#pragma unroll
+                for (int jj = 0; jj < KM; ++jj)
+                    if (jj == dd.jd && ((mk[q] >> jj) & 1u)) {
+                        d = xv[q][jj];
+                        found = true;
+                    }
+                if (!found && has) d = x[row];
+                e = d;
+            }
+            yv[q] = spmv_row_value<MODE>(has, sum, e, acc[q]);
+        }
+        if (u + Gk < e0) load(u + Gk);   // the next unit's loads fly during this unit's epilogue
+        if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const int64_t row = tl[q] * kSlice + tid;
+            spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
+        }
+    }
 }
 
 // Diagonal-layout detection: row `row`'s stored entries must be, in order, entries of strictly increasing
@@ -1298,6 +1415,23 @@ static bool spmv_xcd_bands() {
     return on;
 }
 
+// lab: the persistent diagonal-layout kernel (PSK_SPMV_PERSIST=1) and its workgroups per CU
+static bool spmv_persist() {
+    static const bool on = [] {
+        const char *e = std::getenv("PSK_SPMV_PERSIST");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+static int spmv_persist_per_cu() {
+    static const int v = [] {
+        const char *e = std::getenv("PSK_SPMV_PERSIST_PER_CU");
+        const int t = e ? std::atoi(e) : 8;
+        return t >= 1 && t <= 16 ? t : 8;
+    }();
+    return v;
+}
+
 static int spmv_tpw() {
     static const int v = [] {
         const char *e = std::getenv("PSK_SPMV_TPW");
@@ -1351,9 +1485,18 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const int64_t nwgd = (nwg + kDiagTpw - 1) / kDiagTpw;
         const dim3 gdd((unsigned)(nwgd > 0 ? nwgd : 1));
         const TileMap tmd = tile_map_for(nwgd, spmv_xcd_bands(), rev != 0);
+        const bool persist = spmv_persist();
+        int64_t gp = std::min<int64_t>(nwgd, (int64_t)c->num_cus * spmv_persist_per_cu());
+        gp = std::max<int64_t>(8, gp - gp % 8);
 #define PSK_DIAG_LAUNCH(M, KM)                                                                                     \
-    hipExtLaunchKernelGGL((spmv_diag_kernel<M, KM, kDiagTpw>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, x, y, \
-                          aux_d, aux_q, gs, done_flag, tmd, nwg)
+    do {                                                                                                           \
+        if (persist)                                                                                               \
+            hipExtLaunchKernelGGL((spmv_diag_persist_kernel<M, KM, kDiagTpw>), dim3((unsigned)gp), bd, 0, s, ev0, ev1, \
+                                  0, A->n, A->dg_mask, dd, x, y, aux_d, aux_q, gs, done_flag, nwgd, nwg);            \
+        else                                                                                                       \
+            hipExtLaunchKernelGGL((spmv_diag_kernel<M, KM, kDiagTpw>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, \
+                                  x, y, aux_d, aux_q, gs, done_flag, tmd, nwg);                                     \
+    } while (0)
 #define PSK_DIAG_MODE(M)                                                                                           \
     do {                                                                                                           \
         if (km == 3) PSK_DIAG_LAUNCH(M, 3);                                                                        \
