@@ -155,14 +155,34 @@ __global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgSt
 // preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
 // diagonal matrices such as stencils: the same products, 8 B/row less per kernel).
 // FIRST (iteration 0): r_0 = b is read from b (the init does not copy it, K0 above).
+// Load order (round 5): the tile's stream loads go out first and the solver scalars (done flag, p.Ap, uDotR)
+// after them as independent loads, so a workgroup waits for memory once. Before, the scalars came first as a
+// chain of dependent scalar loads, each behind its own wait, and every workgroup spent that chain before it
+// issued a vector load (the kernels are workgroup-latency bound: ~2000 resident workgroups, one tile each).
 template <int JAC, bool FIRST>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ r, const double *__restrict__ b, const double *__restrict__ Ap,
     const double *__restrict__ dinv, double ds, const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st,
     const double *__restrict__ udr, int64_t k, TileMap tm) {
-    if (st->done) return;
     __shared__ double sh[kWaves];
+    // tile of this workgroup: XCD-banded like the SpMV's (tm), so the Ap rows a tile reads were
+    // written through the same XCD's L2; the grid sums are published by tile (order-independent)
+    const int64_t tile = tile_of_block(tm);
+    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+    const bool full = i + 1 < n;
+    dv2 ro{0.0, 0.0}, a{0.0, 0.0}, d{ds, ds};
+    if (full) {
+        ro = FIRST ? ld2nt(b + i) : ld2(r + i);
+        a = ld2nt(Ap + i);
+        if (JAC == 1) d = ld2(dinv + i);
+    }
+    const int32_t done = st->done;
     const double pTAp = rank_sum(pap, nparts, 1, 0);         // np.dot(p, Ap)  :113 (K1's grid sum)
+    const double urk = udr[k];
+    if (done) {   // uniform: stopped earlier (the loads above are consumed so they stay ahead of the test)
+        __asm__ volatile("" ::"v"(ro), "v"(a), "v"(d));
+        return;
+    }
     if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
@@ -171,21 +191,13 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         }
         return;
     }
-    const double alpha = udr[k] / pTAp;                      // :118
+    const double alpha = urk / pTAp;                         // :118
     // K3 (x update) runs iff this K2 did: it tests `live`, written by the previous kernel, never its
     // own done flag, which its first workgroup may set while later ones are still starting
     if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
-    // tile of this workgroup: XCD-banded like the SpMV's (tm), so the Ap rows a tile reads were
-    // written through the same XCD's L2; the grid sums are published by tile (order-independent)
-    const int64_t tile = tile_of_block(tm);
-    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
-    uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
+    const uint32_t ticket = i < n ? gridsum_ticket(gs, tile) : 0u;   // thread 0's value is the one read
     double rr = 0.0, ur = 0.0;
-    if (i + 1 < n) {
-        const dv2 ro = FIRST ? ld2nt(b + i) : ld2(r + i), a = ld2nt(Ap + i);
-        dv2 d{ds, ds};
-        if (JAC == 1) d = ld2(dinv + i);
-        ticket = gridsum_ticket(gs, tile);
+    if (full) {
         dv2 rn;
         rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
         rn.y = ro.y - alpha * a.y;
@@ -200,7 +212,6 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
-        ticket = gridsum_ticket(gs, tile);
         const double rn = (FIRST ? b[i] : r[i]) - alpha * Ap[i];
         const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
@@ -240,19 +251,20 @@ __device__ __forceinline__ double pcg_catch_up(double xj, const PRing *pr, int q
 // (K2's expression on the same partials), the convergence test, beta. Returns false when the
 // solve stopped at this iteration; x (which K3 owns) is then still advanced over the tile.
 // pr != nullptr: the q = pcg_pending(k) deferred x updates are applied first.
+// udrk = udr[k] and tau = st->tauNormB, loaded by the caller with its other scalars (one round trip)
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
-                                             double pTAp, double rr, double ur, PcgState *st,
+                                             double pTAp, double rr, double ur, double udrk, double tau, PcgState *st,
                                              double *__restrict__ udr, double *__restrict__ hist, int64_t k,
                                              int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
                                              int64_t tile, const PRing *pr = nullptr,
                                              const double *__restrict__ alphas = nullptr) {
-    alpha = udr[k] / pTAp;                                   // :118
+    alpha = udrk / pTAp;                                     // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (tile == 0 && threadIdx.x == 0) {
         hist[k] = normR;                                     // reportIter  :126
         st->last_hist = normR;
     }
-    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+    if (normR <= tau || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
         const int64_t i = tile * kVecTile + 2 * threadIdx.x;
         // deferred updates (pr): before the first flush (k < kPcgDefer) x is still the implicit x0 = 0
         const bool x0 = pr && k < kPcgDefer;
@@ -269,7 +281,7 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
         }
         return false;
     }
-    beta = ur / udr[k];                                      // :134-135
+    beta = ur / udrk;                                        // :134-135
     if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
     return true;
 }
@@ -282,7 +294,6 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts, PcgState *st,
     double *__restrict__ udr, double *__restrict__ hist, double *__restrict__ alphas, int64_t k, int64_t maxiter,
     int fail_on_maxiter, int64_t tile_base, TileMap tm) {
-    if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
     // halo exchange then overlaps the rest); tile 0 alone writes the solver state. tm: XCD bands
     // over the launch's tiles (see K2)
@@ -292,35 +303,49 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     // below reads through pr.b first; the store to pnext must stay after those loads
     double *pnext = pr.b[(k + 1) % kPcgDefer];
     const int q = pcg_pending(k);
-    double alpha, beta;
-    if (!pcg_direction_scalars(n, x, pcur, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
-                               rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta, tile, &pr, alphas))
-        return;
     const bool flush = q == kPcgDefer - 1 || k == maxiter - 1;
     const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0 (never loaded)
+    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+    const bool full = i + 1 < n;
+    // the stream loads first, the scalars after them (see K2): r, dinv and x are not needed again this
+    // iteration (non-temporal); p is gathered by the next SpMV
+    dv2 ro{0.0, 0.0}, po{0.0, 0.0}, d{ds, ds}, xo{0.0, 0.0};
+    dv2 pp[kPcgDefer > 1 ? kPcgDefer - 1 : 1];
+#pragma unroll
+    for (int t = 0; t < (kPcgDefer > 1 ? kPcgDefer - 1 : 1); ++t) pp[t] = dv2{0.0, 0.0};
+    if (full) {
+        ro = ld2nt(r + i);
+        po = ld2(pcur + i);
+        if (JAC == 1) d = ld2nt(dinv + i);
+        if (flush) {
+            if (!x0) xo = ld2nt(x + i);
+#pragma unroll
+            for (int t = 1; t < kPcgDefer; ++t)
+                if (t <= q) pp[t - 1] = ld2nt(pr.b[(k - t) % kPcgDefer] + i);
+        }
+    }
+    const int64_t live = st->live;
+    const double pTAp = rank_sum(pap, nparts, 1, 0), rr = rank_sum(rrur, nparts, 2, 0), urn = rank_sum(rrur, nparts, 2, 1);
+    const double udrk = udr[k], tau = st->tauNormB;
+    if (live != k) {   // K2 returned (stopped earlier, or breakdown at :114); uniform
+        __asm__ volatile("" ::"v"(ro), "v"(po), "v"(d), "v"(xo));
+        return;
+    }
+    double alpha, beta;
+    if (!pcg_direction_scalars(n, x, pcur, pTAp, rr, urn, udrk, tau, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+                               beta, tile, &pr, alphas))
+        return;
     if (tile == 0 && threadIdx.x == 0) {
         alphas[k] = alpha;
         if (flush) st->x_written = 1;
     }
-    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
-    // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
-    if (i + 1 < n) {
-        const dv2 ro = ld2nt(r + i), po = ld2(pcur + i);
-        dv2 d{ds, ds};
-        if (JAC == 1) d = ld2nt(dinv + i);
+    if (full) {
         double u0 = ro.x, u1 = ro.y;
         if (JAC) {
             u0 = d.x * ro.x;
             u1 = d.y * ro.y;
         }
         if (flush) {
-            dv2 xo{0.0, 0.0};
-            if (!x0) xo = ld2nt(x + i);
-            dv2 pp[kPcgDefer > 1 ? kPcgDefer - 1 : 1];
-#pragma unroll
-            for (int t = 1; t < kPcgDefer; ++t)
-                if (t <= q) pp[t - 1] = ld2nt(pr.b[(k - t) % kPcgDefer] + i);
 #pragma unroll
             for (int t = kPcgDefer - 1; t >= 1; --t)
                 if (t <= q) {
@@ -419,7 +444,8 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
     double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
     if (st->live != k) return;
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, udr[k], st->tauNormB, st, udr, hist, k, maxiter,
+                               fail_on_maxiter, alpha,
                                beta, blockIdx.x))
         return;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;

@@ -10,7 +10,7 @@ ok() { local c=$1; [ $c -eq 0 ] || [ $c -eq 1 ]; }
 timeout -k 10 600 python -u -m pytest tests/test_gpu_layout.py tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread > $OUT/${TAG}_tests.log 2>&1
 c=$?; echo "tests exit $c"; tail -3 $OUT/${TAG}_tests.log; ok $c || exit $c
 [ $c -eq 0 ] || exit 1
-timeout -k 10 900 python -u tools/ab_pcg.py --sides 3163,16384 --rounds 2 prev=@tools/bin/ab_prev/libpsk.so base= persist=PSK_SPMV_PERSIST=1 persist4=PSK_SPMV_PERSIST=1,PSK_SPMV_PERSIST_PER_CU=4 > $OUT/${TAG}_ab.jsonl 2> $OUT/${TAG}_ab.err
+timeout -k 10 900 python -u tools/ab_pcg.py --sides 3163,16384 --rounds 2 prev=@tools/bin/ab_prev/libpsk.so spmv=@tools/bin/ab_spmv/libpsk.so base= persist=PSK_SPMV_PERSIST=1 persist4=PSK_SPMV_PERSIST=1,PSK_SPMV_PERSIST_PER_CU=4 > $OUT/${TAG}_ab.jsonl 2> $OUT/${TAG}_ab.err
 c=$?; echo "ab exit $c"; python - $OUT/${TAG}_ab.jsonl <<'PY'
 import json, sys
 for l in open(sys.argv[1]):
