@@ -97,19 +97,8 @@ struct PcgInitFin {
     __device__ void operator()(const double *r) const { pcg_init_state(r[0], r[1], tau, st, udr, hdone, hgen, x_written); }
 };
 
-// Tiles of the Jacobi/identity kernels K0, K2, K3 (round 5): kPcgPL element pairs per lane (16-B accesses),
-// kPcgTile elements per workgroup. These one-shot kernels are bound by the bytes each workgroup keeps in
-// flight over its ~3 us lifetime (32 waves per CU at most): two pairs per lane put twice as many bytes in
-// flight per wave as one.
-#ifndef PSK_PCG_PL
-#define PSK_PCG_PL 2
-#endif
-constexpr int kPcgPL = PSK_PCG_PL;
-constexpr int64_t kPcgTile = (int64_t)kPcgPL * kVecTile;
-static_assert(kPcgPL >= 1 && kPcgPL <= 4, "kPcgPL");
-
 // ---- K0 (Jacobi/identity): p_0 = M b; [b.b, u.r] --------------------------------------------
-// One-shot like K2 (one kPcgTile-element tile per workgroup), the two sums finished in the same launch by
+// One-shot like K2 (one 512-element tile per workgroup), the two sums finished in the same launch by
 // gridsum and, unsharded, the solver state set by the workgroup that completes them (PcgInitFin; a
 // sharded solve gathers the per-rank sums and runs pcg_init_finish_kernel). x0 = 0 is not stored:
 // K3's first flush of the deferred x updates starts from the literal 0.0 (x = np.zeros_like(b) :100,
@@ -120,40 +109,32 @@ __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const doubl
                                                           const double *__restrict__ dinv, double ds,
                                                           double *__restrict__ p, GridSum gs, PcgInitFin fin) {
     __shared__ double sh[kWaves];
-    const int64_t i0 = (int64_t)blockIdx.x * kPcgTile + 2 * threadIdx.x;
-    dv2 bi[kPcgPL], d[kPcgPL];
-#pragma unroll
-    for (int pl = 0; pl < kPcgPL; ++pl) {
-        const int64_t i = i0 + pl * kVecTile;
-        bi[pl] = dv2{0.0, 0.0};
-        d[pl] = dv2{ds, ds};
-        if (i + 1 < n) {
-            bi[pl] = ld2nt(b + i);
-            if (JAC == 1) d[pl] = ld2nt(dinv + i);
-        }
-    }
-    const uint32_t ticket = gridsum_ticket(gs);
+    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
+    uint32_t ticket = 0;
     double bb = 0.0, ur = 0.0;
-#pragma unroll
-    for (int pl = 0; pl < kPcgPL; ++pl) {
-        const int64_t i = i0 + pl * kVecTile;
-        if (i + 1 < n) {
-            dv2 u = bi[pl];
-            if (JAC) {
-                u.x = d[pl].x * bi[pl].x;                  // p = precond.applyRight(r)  :98
-                u.y = d[pl].y * bi[pl].y;
-            }
-            st2(p + i, u);                                 // (r = np.copy(b) :97 is read from b by K2)
-            bb = fma(bi[pl].x, bi[pl].x, bb);
-            bb = fma(bi[pl].y, bi[pl].y, bb);
-            ur = fma(u.x, bi[pl].x, ur);                   // uDotR = np.dot(u, r)       :102
-            ur = fma(u.y, bi[pl].y, ur);
-        } else if (i < n) {   // odd tail element
-            const double bt = b[i];
-            const double u0 = JAC == 2 ? ds * bt : JAC ? dinv[i] * bt : bt;
+    if (i + 1 < n) {
+        const dv2 bi = ld2nt(b + i);
+        dv2 d{ds, ds};
+        if (JAC == 1) d = ld2nt(dinv + i);
+        ticket = gridsum_ticket(gs);
+        dv2 u = bi;
+        if (JAC) {
+            u.x = d.x * bi.x;                          // p = precond.applyRight(r)  :98
+            u.y = d.y * bi.y;
+        }
+        st2(p + i, u);                                 // (r = np.copy(b) :97 is read from b by K2)
+        bb = fma(bi.x, bi.x, bb);
+        bb = fma(bi.y, bi.y, bb);
+        ur = fma(u.x, bi.x, ur);                       // uDotR = np.dot(u, r)       :102
+        ur = fma(u.y, bi.y, ur);
+    } else {
+        ticket = gridsum_ticket(gs);
+        if (i < n) {   // odd tail element
+            const double bi = b[i];
+            const double u0 = JAC == 2 ? ds * bi : JAC ? dinv[i] * bi : bi;
             p[i] = u0;
-            bb = fma(bt, bt, bb);
-            ur = fma(u0, bt, ur);
+            bb = bi * bi;
+            ur = u0 * bi;
         }
     }
     const double v[2] = {block_sum(bb, sh), block_sum(ur, sh)};
@@ -170,45 +151,18 @@ __global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgSt
 }
 
 // ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
-// One-shot: workgroup b owns elements [kPcgTile b, kPcgTile (b+1)), kPcgPL pairs per lane (16-B accesses).
-// JAC: Jacobi preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
+// One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses). JAC: Jacobi
+// preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
 // diagonal matrices such as stencils: the same products, 8 B/row less per kernel).
 // FIRST (iteration 0): r_0 = b is read from b (the init does not copy it, K0 above).
-// Load order (round 5): the tile's stream loads go out first and the solver scalars (done flag, p.Ap, uDotR)
-// after them as independent loads, so a workgroup waits for memory once. Before, the scalars came first as a
-// chain of dependent scalar loads, each behind its own wait, and every workgroup spent that chain before it
-// issued a vector load.
 template <int JAC, bool FIRST>
 __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ r, const double *__restrict__ b, const double *__restrict__ Ap,
     const double *__restrict__ dinv, double ds, const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st,
     const double *__restrict__ udr, int64_t k, TileMap tm) {
+    if (st->done) return;
     __shared__ double sh[kWaves];
-    // tile of this workgroup: XCD-banded like the SpMV's (tm), so the Ap rows a tile reads were
-    // written through the same XCD's L2; the grid sums are published by tile (order-independent)
-    const int64_t tile = tile_of_block(tm);
-    const int64_t i0 = tile * kPcgTile + 2 * threadIdx.x;
-    dv2 ro[kPcgPL], a[kPcgPL], d[kPcgPL];
-#pragma unroll
-    for (int pl = 0; pl < kPcgPL; ++pl) {
-        const int64_t i = i0 + pl * kVecTile;
-        ro[pl] = dv2{0.0, 0.0};
-        a[pl] = dv2{0.0, 0.0};
-        d[pl] = dv2{ds, ds};
-        if (i + 1 < n) {
-            ro[pl] = FIRST ? ld2nt(b + i) : ld2(r + i);
-            a[pl] = ld2nt(Ap + i);
-            if (JAC == 1) d[pl] = ld2(dinv + i);
-        }
-    }
-    const int32_t done = st->done;
     const double pTAp = rank_sum(pap, nparts, 1, 0);         // np.dot(p, Ap)  :113 (K1's grid sum)
-    const double urk = udr[k];
-    if (done) {   // uniform: stopped earlier (the loads above are consumed so they stay ahead of the test)
-#pragma unroll
-        for (int pl = 0; pl < kPcgPL; ++pl) __asm__ volatile("" ::"v"(ro[pl]), "v"(a[pl]), "v"(d[pl]));
-        return;
-    }
     if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
@@ -217,36 +171,41 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         }
         return;
     }
-    const double alpha = urk / pTAp;                         // :118
+    const double alpha = udr[k] / pTAp;                      // :118
     // K3 (x update) runs iff this K2 did: it tests `live`, written by the previous kernel, never its
     // own done flag, which its first workgroup may set while later ones are still starting
     if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
-    const uint32_t ticket = gridsum_ticket(gs, tile);        // thread 0 (its first element is < n)
+    // tile of this workgroup: XCD-banded like the SpMV's (tm), so the Ap rows a tile reads were
+    // written through the same XCD's L2; the grid sums are published by tile (order-independent)
+    const int64_t tile = tile_of_block(tm);
+    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+    uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
-#pragma unroll
-    for (int pl = 0; pl < kPcgPL; ++pl) {
-        const int64_t i = i0 + pl * kVecTile;
-        if (i + 1 < n) {
-            dv2 rn;
-            rn.x = ro[pl].x - alpha * a[pl].x;               // r = r - alpha*Ap  :122
-            rn.y = ro[pl].y - alpha * a[pl].y;
-            double u0 = rn.x, u1 = rn.y;
-            if (JAC) {
-                u0 = d[pl].x * rn.x;                         // u = precond.applyRight(r)  :123
-                u1 = d[pl].y * rn.y;
-            }
-            st2(r + i, rn);
-            rr = fma(rn.x, rn.x, rr);
-            rr = fma(rn.y, rn.y, rr);
-            ur = fma(u0, rn.x, ur);
-            ur = fma(u1, rn.y, ur);
-        } else if (i < n) {   // odd tail element
-            const double rn = (FIRST ? b[i] : r[i]) - alpha * Ap[i];
-            const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
-            r[i] = rn;
-            rr = fma(rn, rn, rr);
-            ur = fma(u0, rn, ur);
+    if (i + 1 < n) {
+        const dv2 ro = FIRST ? ld2nt(b + i) : ld2(r + i), a = ld2nt(Ap + i);
+        dv2 d{ds, ds};
+        if (JAC == 1) d = ld2(dinv + i);
+        ticket = gridsum_ticket(gs, tile);
+        dv2 rn;
+        rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
+        rn.y = ro.y - alpha * a.y;
+        double u0 = rn.x, u1 = rn.y;
+        if (JAC) {
+            u0 = d.x * rn.x;                                 // u = precond.applyRight(r)  :123
+            u1 = d.y * rn.y;
         }
+        st2(r + i, rn);
+        rr = fma(rn.x, rn.x, rr);
+        rr = fma(rn.y, rn.y, rr);
+        ur = fma(u0, rn.x, ur);
+        ur = fma(u1, rn.y, ur);
+    } else if (i < n) {   // odd tail element
+        ticket = gridsum_ticket(gs, tile);
+        const double rn = (FIRST ? b[i] : r[i]) - alpha * Ap[i];
+        const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
+        r[i] = rn;
+        rr = rn * rn;
+        ur = u0 * rn;
     }
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
@@ -281,29 +240,26 @@ __device__ __forceinline__ double pcg_catch_up(double xj, const PRing *pr, int q
 // (K2's expression on the same partials), the convergence test, beta. Returns false when the
 // solve stopped at this iteration; x (which K3 owns) is then still advanced over the tile.
 // pr != nullptr: the q = pcg_pending(k) deferred x updates are applied first.
-// udrk = udr[k] and tau = st->tauNormB, loaded by the caller with its other scalars (one round trip)
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
-                                             double pTAp, double rr, double ur, double udrk, double tau, PcgState *st,
+                                             double pTAp, double rr, double ur, PcgState *st,
                                              double *__restrict__ udr, double *__restrict__ hist, int64_t k,
                                              int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
-                                             int64_t tile, int64_t tile_elems, int pairs, const PRing *pr = nullptr,
+                                             int64_t tile, const PRing *pr = nullptr,
                                              const double *__restrict__ alphas = nullptr) {
-    alpha = udrk / pTAp;                                     // :118
+    alpha = udr[k] / pTAp;                                   // :118
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (tile == 0 && threadIdx.x == 0) {
         hist[k] = normR;                                     // reportIter  :126
         st->last_hist = normR;
     }
-    if (normR <= tau || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+        const int64_t i = tile * kVecTile + 2 * threadIdx.x;
         // deferred updates (pr): before the first flush (k < kPcgDefer) x is still the implicit x0 = 0
         const bool x0 = pr && k < kPcgDefer;
-        for (int pl = 0; pl < pairs; ++pl) {   // this lane's element pairs of the tile
-            const int64_t i = tile * tile_elems + pl * kVecTile + 2 * threadIdx.x;
-            for (int64_t j = i; j < i + 2 && j < n; ++j) {
-                double xj = x0 ? 0.0 : x[j];
-                if (pr) xj = pcg_catch_up(xj, pr, pcg_pending(k), k, alphas, j);
-                x[j] = xj + alpha * p[j];                    // :121
-            }
+        for (int64_t j = i; j < i + 2 && j < n; ++j) {
+            double xj = x0 ? 0.0 : x[j];
+            if (pr) xj = pcg_catch_up(xj, pr, pcg_pending(k), k, alphas, j);
+            x[j] = xj + alpha * p[j];                        // :121
         }
         if (tile == 0 && threadIdx.x == 0) {
             st->iters = k + 1;                               // handleConvergence(k, ...)
@@ -313,22 +269,20 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
         }
         return false;
     }
-    beta = ur / udrk;                                        // :134-135
+    beta = ur / udr[k];                                      // :134-135
     if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
     return true;
 }
 
 // ---- K3: x += alpha p (deferred, above), convergence test, beta, p = u + beta p (one-shot, as K2) --
 // A breakdown leaves the updates of the iterations since the last flush pending (pcg_flush_kernel).
-// FLUSH: this iteration applies the deferred x updates (k % kPcgDefer == kPcgDefer - 1, or the last
-// iteration): its own instantiation, so the three iterations in four that only update p keep the register
-// budget (and occupancy) of three streams instead of paying for the flush's seven.
-template <int JAC, bool FLUSH>
+template <int JAC>
 __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     int64_t n, double *__restrict__ x, const double *__restrict__ r, PRing pr, const double *__restrict__ dinv,
     double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts, PcgState *st,
     double *__restrict__ udr, double *__restrict__ hist, double *__restrict__ alphas, int64_t k, int64_t maxiter,
     int fail_on_maxiter, int64_t tile_base, TileMap tm) {
+    if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
     // halo exchange then overlaps the rest); tile 0 alone writes the solver state. tm: XCD bands
     // over the launch's tiles (see K2)
@@ -338,80 +292,56 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     // below reads through pr.b first; the store to pnext must stay after those loads
     double *pnext = pr.b[(k + 1) % kPcgDefer];
     const int q = pcg_pending(k);
-    const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0 (never loaded)
-    const int64_t i0 = tile * kPcgTile + 2 * threadIdx.x;
-    constexpr int NQ = FLUSH && kPcgDefer > 1 ? kPcgDefer - 1 : 1;
-    // the stream loads first, the scalars after them (see K2): r, dinv and x are not needed again this
-    // iteration (non-temporal); p is gathered by the next SpMV
-    dv2 ro[kPcgPL], po[kPcgPL], d[kPcgPL], xo[kPcgPL], pp[kPcgPL][NQ];
-#pragma unroll
-    for (int pl = 0; pl < kPcgPL; ++pl) {
-        const int64_t i = i0 + pl * kVecTile;
-        ro[pl] = po[pl] = xo[pl] = dv2{0.0, 0.0};
-        d[pl] = dv2{ds, ds};
-#pragma unroll
-        for (int t = 0; t < NQ; ++t) pp[pl][t] = dv2{0.0, 0.0};
-        if (i + 1 < n) {
-            ro[pl] = ld2nt(r + i);
-            po[pl] = ld2(pcur + i);
-            if (JAC == 1) d[pl] = ld2nt(dinv + i);
-            if (FLUSH) {
-                if (!x0) xo[pl] = ld2nt(x + i);
-#pragma unroll
-                for (int t = 1; t <= NQ; ++t)
-                    if (t <= q) pp[pl][t - 1] = ld2nt(pr.b[(k - t) % kPcgDefer] + i);
-            }
-        }
-    }
-    const int64_t live = st->live;
-    const double pTAp = rank_sum(pap, nparts, 1, 0), rr = rank_sum(rrur, nparts, 2, 0), urn = rank_sum(rrur, nparts, 2, 1);
-    const double udrk = udr[k], tau = st->tauNormB;
-    if (live != k) {   // K2 returned (stopped earlier, or breakdown at :114); uniform
-#pragma unroll
-        for (int pl = 0; pl < kPcgPL; ++pl) __asm__ volatile("" ::"v"(ro[pl]), "v"(po[pl]), "v"(d[pl]), "v"(xo[pl]));
-        return;
-    }
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, pcur, pTAp, rr, urn, udrk, tau, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta, tile, kPcgTile, kPcgPL, &pr, alphas))
+    if (!pcg_direction_scalars(n, x, pcur, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
+                               rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+                               beta, tile, &pr, alphas))
         return;
+    const bool flush = q == kPcgDefer - 1 || k == maxiter - 1;
+    const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0 (never loaded)
     if (tile == 0 && threadIdx.x == 0) {
         alphas[k] = alpha;
-        if (FLUSH) st->x_written = 1;
+        if (flush) st->x_written = 1;
     }
-#pragma unroll
-    for (int pl = 0; pl < kPcgPL; ++pl) {
-        const int64_t i = i0 + pl * kVecTile;
-        if (i + 1 < n) {
-            double u0 = ro[pl].x, u1 = ro[pl].y;
-            if (JAC) {
-                u0 = d[pl].x * ro[pl].x;
-                u1 = d[pl].y * ro[pl].y;
-            }
-            if (FLUSH) {
-                dv2 xv = xo[pl];
-#pragma unroll
-                for (int t = NQ; t >= 1; --t)
-                    if (t <= q) {
-                        const double al = alphas[k - t];
-                        xv.x = xv.x + al * pp[pl][t - 1].x;   // x = x + alpha*p  :121 (iteration k-t)
-                        xv.y = xv.y + al * pp[pl][t - 1].y;
-                    }
-                dv2 xn;
-                xn.x = xv.x + alpha * po[pl].x;              // :121
-                xn.y = xv.y + alpha * po[pl].y;
-                st2nt(x + i, xn);
-            }
-            dv2 pn;
-            pn.x = u0 + beta * po[pl].x;                     // p = u + beta*p  :138
-            pn.y = u1 + beta * po[pl].y;
-            st2(pnext + i, pn);   // (non-temporal and write-through p stores measured no faster, round 4)
-        } else if (i < n) {
-            const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
-            const double pi = pcur[i];
-            if (FLUSH) x[i] = pcg_catch_up(x0 ? 0.0 : x[i], &pr, q, k, alphas, i) + alpha * pi;
-            pnext[i] = u0 + beta * pi;
+    const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+    // r, dinv and x are not needed again this iteration (non-temporal); p is gathered by the next SpMV
+    if (i + 1 < n) {
+        const dv2 ro = ld2nt(r + i), po = ld2(pcur + i);
+        dv2 d{ds, ds};
+        if (JAC == 1) d = ld2nt(dinv + i);
+        double u0 = ro.x, u1 = ro.y;
+        if (JAC) {
+            u0 = d.x * ro.x;
+            u1 = d.y * ro.y;
         }
+        if (flush) {
+            dv2 xo{0.0, 0.0};
+            if (!x0) xo = ld2nt(x + i);
+            dv2 pp[kPcgDefer > 1 ? kPcgDefer - 1 : 1];
+#pragma unroll
+            for (int t = 1; t < kPcgDefer; ++t)
+                if (t <= q) pp[t - 1] = ld2nt(pr.b[(k - t) % kPcgDefer] + i);
+#pragma unroll
+            for (int t = kPcgDefer - 1; t >= 1; --t)
+                if (t <= q) {
+                    const double a = alphas[k - t];
+                    xo.x = xo.x + a * pp[t - 1].x;           // x = x + alpha*p  :121 (iteration k-t)
+                    xo.y = xo.y + a * pp[t - 1].y;
+                }
+            dv2 xn;
+            xn.x = xo.x + alpha * po.x;                      // :121
+            xn.y = xo.y + alpha * po.y;
+            st2nt(x + i, xn);
+        }
+        dv2 pn;
+        pn.x = u0 + beta * po.x;                             // p = u + beta*p  :138
+        pn.y = u1 + beta * po.y;
+        st2(pnext + i, pn);   // (non-temporal and write-through p stores measured no faster, round 4)
+    } else if (i < n) {
+        const double u0 = JAC == 2 ? ds * r[i] : JAC ? dinv[i] * r[i] : r[i];
+        const double pi = pcur[i];
+        if (flush) x[i] = pcg_catch_up(x0 ? 0.0 : x[i], &pr, q, k, alphas, i) + alpha * pi;
+        pnext[i] = u0 + beta * pi;
     }
 }
 
@@ -489,8 +419,8 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
     double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
     if (st->live != k) return;
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, udr[k], st->tauNormB, st, udr, hist, k, maxiter,
-                               fail_on_maxiter, alpha, beta, blockIdx.x, kVecTile, 1))
+    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
+                               beta, blockIdx.x))
         return;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
     for (int64_t j = i; j < i + 2 && j < n; ++j) {
@@ -610,12 +540,11 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     const double ds = jac == 2 ? M->dinv_value : 0.0;
     // one-shot grid of K0/K2/K3 (one 512-element tile per workgroup); K0/K1/K2 finish their dot products
     // in-launch (gridsum), so the loop's scalars are part1[0] = p.Ap and part2[0..1] = (r.r, u.r)
-    const int64_t nv = n > 0 ? (n + kVecTile - 1) / kVecTile : 1;      // general-path kernels' tiles
-    const int64_t nvP = n > 0 ? (n + kPcgTile - 1) / kPcgTile : 1;     // K0 / K2 / K3 tiles (kPcgPL pairs per lane)
+    const int64_t nv = n > 0 ? (n + kVecTile - 1) / kVecTile : 1;
     if (nv > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: vector too long for a one-shot grid");
     GridSum gs0, gs2, gs3;
-    PSK_TRY(gridsum_prepare(c, gen ? nv : nvP, 2, w.pinit, &gs0));
-    PSK_TRY(gridsum_prepare(c, nvP, 2, w.part2, &gs2));
+    PSK_TRY(gridsum_prepare(c, nv, 2, w.pinit, &gs0));
+    PSK_TRY(gridsum_prepare(c, nv, 2, w.part2, &gs2));
     PSK_TRY(gridsum_prepare(c, nv, 1, w.part3, &gs3));
     // the host-mapped done stamp the kernels write (set_done); no kernel of an earlier solve is running
     volatile int64_t *hdone = kit->hmap;
@@ -634,7 +563,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     uint64_t seq0 = 0;
     if (mbc) seq0 = mbox_next(mbc, &gs0);
     PSK_HIP(hipEventRecord(kit->ev0, s));
-    const dim3 gk((unsigned)nv), gkP((unsigned)nvP);
+    const dim3 gk((unsigned)nv);
     if (gen) {
         const unsigned nb = (unsigned)((n + kBlock - 1) / kBlock);
         if (n > 0) hipLaunchKernelGGL(pcg_gen_init_kernel, dim3(nb), dim3(kBlock), 0, s, n, bd, w.x, w.r);
@@ -642,7 +571,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         hipLaunchKernelGGL(pcg_gen_init2_kernel, gk, dim3(kBlock), 0, s, n, w.r, w.u, w.p, gs0, fin);
     } else {
 #define PSK_PCG_INIT(J, F) \
-        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gkP, dim3(kBlock), 0, s, n, bd, dinv, ds, w.p, gs0, fin)
+        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gk, dim3(kBlock), 0, s, n, bd, dinv, ds, w.p, gs0, fin)
         if (jac == 2) { if (sharded) PSK_PCG_INIT(2, false); else PSK_PCG_INIT(2, true); }
         else if (jac == 1) { if (sharded) PSK_PCG_INIT(1, false); else PSK_PCG_INIT(1, true); }
         else { if (sharded) PSK_PCG_INIT(0, false); else PSK_PCG_INIT(0, true); }
@@ -683,7 +612,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // halo overlap (sharded, Jacobi/identity): when every row a neighbour needs lies in the first ov_lo
     // or the last nv - ov_hi K3 tiles (row-block shards of a banded matrix: one grid line each side),
     // those tiles run first and the exchange of p overlaps the remaining tiles of K3
-    int64_t ov_lo = 0, ov_hi = nvP;
+    int64_t ov_lo = 0, ov_hi = nv;
     // On by default (PSK_HALO_OVERLAP=0 turns it off); DESIGN.md §6 states the rule: the overlap moves
     // no arithmetic (sharded histories are bit-identical either way) and takes the halo's latency off
     // the critical path whenever K3's interior tiles outlast the exchange, which they do at every
@@ -692,7 +621,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         const char *e = std::getenv("PSK_HALO_OVERLAP");
         return !(e && std::atoi(e) == 0);
     }();
-    const bool overlap = overlap_on && sharded && !gen && halo_split(A, kPcgTile, nvP, ov_lo, ov_hi);
+    const bool overlap = overlap_on && sharded && !gen && halo_split(A, kVecTile, nv, ov_lo, ov_hi);
     hipStream_t cs = nullptr;
     hipEvent_t ev_k3a = kit->ev_a, ev_halo = kit->ev_b;
     bool halo_pending = false;
@@ -742,7 +671,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         // K2/K3 tiles in block order: XCD bands matching the SpMV's, and bands walked in alternating
         // directions (a serpentine over SpMV, K2, K3 meant to re-read Ap, r and p from the Infinity Cache),
         // measured no faster (round 4, profiles/r4_spmv_ab.txt: band1 / band2)
-        const TileMap tm2 = tile_map_for(nvP, false);
+        const TileMap tm2 = tile_map_for(nv, false);
         if (sharded && (rc = mbc ? mbox_gather(mbc, seq1, 1, w.part1g, &w.st->done, s)
                                  : allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK)
             break;
@@ -751,7 +680,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         // the general path copied r = b in its init (pcg_gen_init_kernel): it never takes the FIRST form
         const bool first = k == 0 && !gen && dev_io;
 #define PSK_PCG_K2(J, F)                                                                                       \
-        hipLaunchKernelGGL((pcg_update_kernel<J, F>), gkP, dim3(kBlock), 0, s, n, w.r, bd, w.Ap, dinv, ds, w.part1g, \
+        hipLaunchKernelGGL((pcg_update_kernel<J, F>), gk, dim3(kBlock), 0, s, n, w.r, bd, w.Ap, dinv, ds, w.part1g, \
                            P, gs2k, w.st, w.udr, k, tm2)
         if (jac == 2) { if (first) PSK_PCG_K2(2, true); else PSK_PCG_K2(2, false); }
         else if (jac == 1) { if (first) PSK_PCG_K2(1, true); else PSK_PCG_K2(1, false); }
@@ -766,31 +695,33 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             hipLaunchKernelGGL(pcg_gen_direction_kernel, gk, dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, w.part2,
                                w.part3, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
         } else {
-            // the deferred x updates are applied on every kPcgDefer-th iteration and the last one
-            const bool flush = pcg_pending(k) == kPcgDefer - 1 || k == maxiter - 1;
             auto k3 = [&](int64_t t0, int64_t t1) {   // K3 over tiles [t0, t1)
                 if (t1 <= t0) return;
                 const dim3 g3((unsigned)(t1 - t0));
                 const TileMap tm3 = tile_map_for(t1 - t0, false);
-#define PSK_PCG_K3(J, F)                                                                                       \
-                hipLaunchKernelGGL((pcg_direction_kernel<J, F>), g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,  \
-                                   w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,                   \
-                                   ctl->fail_on_maxiter, t0, tm3)
-                if (jac == 2) { if (flush) PSK_PCG_K3(2, true); else PSK_PCG_K3(2, false); }
-                else if (jac == 1) { if (flush) PSK_PCG_K3(1, true); else PSK_PCG_K3(1, false); }
-                else { if (flush) PSK_PCG_K3(0, true); else PSK_PCG_K3(0, false); }
-#undef PSK_PCG_K3
+                if (jac == 2)
+                    hipLaunchKernelGGL(pcg_direction_kernel<2>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
+                                       ctl->fail_on_maxiter, t0, tm3);
+                else if (jac == 1)
+                    hipLaunchKernelGGL(pcg_direction_kernel<1>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
+                                       ctl->fail_on_maxiter, t0, tm3);
+                else
+                    hipLaunchKernelGGL(pcg_direction_kernel<0>, g3, dim3(kBlock), 0, s, n, w.x, w.r, w.pr, dinv, ds,
+                                       w.part1g, w.part2g, P, w.st, w.udr, w.hist, w.alphas, k, maxiter,
+                                       ctl->fail_on_maxiter, t0, tm3);
             };
             if (overlap && k + 1 < maxiter) {
                 // the tiles holding the rows the neighbours need first, then their halo exchange on the
                 // second stream while the other tiles run; the next SpMV waits for it
                 k3(0, ov_lo);
-                k3(ov_hi, nvP);
+                k3(ov_hi, nv);
                 if ((rc = halo_exchange_async(A, pn, s, cs, ev_k3a, ev_halo)) != PSK_OK) break;
                 k3(ov_lo, ov_hi);
                 halo_pending = true;
             } else {
-                k3(0, nvP);
+                k3(0, nv);
             }
         }
         if (hipGetLastError() != hipSuccess) { rc = fail(PSK_ERR_HIP, "pcg launch"); break; }
