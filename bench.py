@@ -820,6 +820,7 @@ def pcg_amg(N, m=8192, levels=5, cycles=2, iters=6, repeats=3):
     del A
     out["amg_setup_s"] = time.time() - t1
     out["level_sizes"] = M.levels()
+    out["coarse_solve"] = M.coarse_kind   # dense: streamed GEMV over A_c^-1 (dense.hip); lu: SuperLU factors
 
     def timed(fn, reps=3):
         fn()

@@ -78,6 +78,8 @@ extern "C" {
 #define PSK_PREC_ILU      2      /* triangular-solve chain: SuperLU ILU.solve ILUTPreconditioner.py:70-78,
                                     IC, Gauss-Seidel, coarse LU (psk_prec_create_trisolve) */
 #define PSK_PREC_AMG      3      /* smoothed-aggregation V-cycles  AMGPreconditioner.py:46-51 */
+#define PSK_PREC_DENSE    4      /* x = A^-1 f by a dense inverse: the AMG coarse solve spsolve(A_c, f),
+                                    VCycleManager.py:34-37 (psk_prec_create_dense_inverse) */
 
 typedef struct psk_csr  psk_csr;    /* device CSR (int32 rowptr/colidx, f64 vals), library-owned */
 typedef struct psk_prec psk_prec;   /* formed preconditioner, library-owned */
@@ -223,6 +225,13 @@ int psk_prec_create_trisolve(int64_t n, const int32_t *l_rowptr, const int32_t *
                              int32_t l_unit, const int32_t *u_rowptr, const int32_t *u_colidx,
                              const double *u_vals, int32_t u_unit, const int32_t *gather_in,
                              const int32_t *gather_out, psk_prec **out);
+/* Direct solve x = A^-1 f through the explicit inverse, formed once on the device (rocSOLVER getrf +
+ * getri, loaded at first use) and applied as one streamed GEMV per solve, with `refine` (0..4) steps of
+ * x <- x + A^-1 (f - A x) after it. Replaces spsolve(A_c, f) for the AMG coarse level
+ * (VCycleManager.py:34-37; pass it as psk_prec_create_amg's `coarse`). A is BORROWED (refinement).
+ * PSK_ERR_UNSUPPORTED when n > 32768 (8.6 GB) or rocSOLVER cannot be loaded, PSK_ERR_ARG when A is
+ * singular. The input vector of an apply must be 16-byte aligned. */
+int psk_prec_create_dense_inverse(const psk_csr *A, int32_t refine, psk_prec **out);
 /* Smoothed-aggregation AMG preconditioner over a host-built hierarchy (levels 0 = coarsest ..
  * num_levels-1 = finest, MLHierarchy.py:250-258). Arrays of num_levels handles, all BORROWED
  * (they must outlive the preconditioner): A[k] level matrices (A[num_levels-1] = the fine A),
@@ -259,6 +268,8 @@ int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out);
  * workgroups that started, not over the grid). */
 int psk_lab_occupy_begin(int32_t wgs, int32_t lds_bytes, double seconds);
 int psk_lab_occupy_end(int32_t *timed_out);
+/* Lab: occupiers per XCD (HW_REG_XCC_ID) of the last psk_lab_occupy_begin, counts[8]. */
+int psk_lab_occupy_xcc(int32_t *counts);
 int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid);
 /* Host-only: the grid plan psk_prec_create_trisolve would make for one triangular factor (CSR with its
  * diagonal; upper = 1: solved from the last row up), without any device work — out[0..6] = w, H,

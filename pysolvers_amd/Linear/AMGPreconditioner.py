@@ -8,8 +8,14 @@ pysolvers_amd/csrc/amg.hip): numIters V-cycles from x0 = v, early exit on ||v - 
 
 Level operators: SpMV (bit-identical stored-order sums) for A_k, R_k, P_k; smoothing sweeps
 x <- x + S^-1 (f - A x) with S^-1 = DInv* (Jacobi) or triu(A_k)^-1 (Gauss-Seidel, sync-free
-triangular solve); the coarsest level solves with SuperLU's factors of A_0 computed once on the
-host (the reference refactors A_0 on every call, VCycleManager.py:34-37, same factors each time).
+triangular solve); the coarsest level is spsolve(A_0, f) (VCycleManager.py:34-37; the reference
+refactors A_0 on every call, same factors each time). Since round 5 that solve is a streamed GEMV over
+A_0^-1, formed once on the device (coarse="dense", pysolvers_amd/csrc/dense.hip): one HBM-bound pass
+instead of a sparse triangular-solve chain thousands of dependency levels deep (4.84 -> ~0.4 ms at
+-FD 8192^2, A_0 16,642^2); it agrees with SuperLU's solve to ~1e-15 relative (tests pin 1e-12).
+coarse="lu" keeps SuperLU's factors of A_0 computed once on the host as two device triangular solves.
+"auto" (default) takes the dense inverse up to 32,768 unknowns and falls back to the factors when the
+inverse cannot be formed (A_0 singular, rocSOLVER absent).
 """
 import ctypes
 
@@ -27,16 +33,20 @@ from .TriangularSolve import superlu_transposed_solver
 
 
 class AMG(PreconditionerType):
-    def __init__(self, numIters=5, numLevels=2, nuPre=2, nuPost=2, smoother=GaussSeidelSmoother):
+    def __init__(self, numIters=5, numLevels=2, nuPre=2, nuPost=2, smoother=GaussSeidelSmoother, coarse="auto",
+                 coarse_refine=0):
         self.numIters = numIters
         self.numLevels = numLevels
         self.nuPre = nuPre
         self.nuPost = nuPost
         self.smoother = smoother
+        self.coarse = coarse
+        self.coarse_refine = coarse_refine
 
     def form(self, A):
         return AMGPreconditioner(A, numIters=self.numIters, numLevels=self.numLevels, nuPre=self.nuPre,
-                                 nuPost=self.nuPost, smoother=self.smoother)
+                                 nuPost=self.nuPost, smoother=self.smoother, coarse=self.coarse,
+                                 coarse_refine=self.coarse_refine)
 
 
 def coarse_factor(A_c):
@@ -56,12 +66,37 @@ def coarse_solver(A_c):
     return superlu_transposed_solver(lu), lu
 
 
+DENSE_COARSE_MAX = 32768   # kDenseMaxN (psk_internal.hpp): 8.6 GB of inverse
+
+
+class DenseInverseSolver(DeviceOperator):
+    """x = A^-1 f through A's explicit inverse on the device (psk_prec_create_dense_inverse): formed once
+    (rocSOLVER getrf/getri), each apply one streamed GEMV plus `refine` steps x += A^-1 (f - A x)."""
+
+    device_kind = N.PSK_PREC_DENSE
+
+    def __init__(self, A, refine=0):
+        self._A = A if isinstance(A, DeviceCSR) else DeviceCSR.from_scipy(sp.csr_matrix(A))   # borrowed
+        self.n = self._A.n
+        self.refine = int(refine)
+        h = ctypes.c_void_p()
+        N.check(N.lib.psk_prec_create_dense_inverse(self._A.handle, self.refine, ctypes.byref(h)),
+                "psk_prec_create_dense_inverse")
+        self._h = h
+
+    def apply(self, vec):
+        return self._device_apply(vec)
+
+
 class AMGPreconditioner(DeviceOperator, GenericPreconditioner):
     device_kind = N.PSK_PREC_AMG
 
-    def __init__(self, A, numIters=5, numLevels=2, nuPre=2, nuPost=2, smoother=GaussSeidelSmoother, tau=1.0e-8):
+    def __init__(self, A, numIters=5, numLevels=2, nuPre=2, nuPost=2, smoother=GaussSeidelSmoother, tau=1.0e-8,
+                 coarse="auto", coarse_refine=0):
         if smoother not in (GaussSeidelSmoother, JacobiSmoother):
             raise TypeError("AMG smoother must be GaussSeidelSmoother or JacobiSmoother")
+        if coarse not in ("auto", "dense", "lu"):
+            raise ValueError("AMG coarse must be 'auto', 'dense' or 'lu'")
         dA = A if isinstance(A, DeviceCSR) else DeviceCSR.from_scipy(A)
         Ah = A.to_scipy() if isinstance(A, DeviceCSR) else sp.csr_matrix(A)
         self.n = Ah.shape[0]
@@ -73,7 +108,16 @@ class AMGPreconditioner(DeviceOperator, GenericPreconditioner):
         self._P = [DeviceCSR.from_scipy(self.mlh.update(k), rectangular=True) for k in range(L - 1)]
         self._R = [DeviceCSR.from_scipy(self.mlh.downdate(k), rectangular=True) for k in range(L - 1)]
         self._S = [None] + [smoother(self.mlh.matrix(k), device_A=self._A[k]) for k in range(1, L)]
-        self._coarse, self._lu = coarse_solver(self.mlh.matrix(0))
+        self._coarse, self._lu, self.coarse_kind = None, None, "lu"
+        if coarse == "dense" or (coarse == "auto" and 0 < self._A[0].n <= DENSE_COARSE_MAX):
+            try:
+                self._coarse = DenseInverseSolver(self._A[0], refine=coarse_refine)
+                self.coarse_kind = "dense"
+            except N.PskError as e:   # singular A_0, rocSOLVER absent, out of memory: the factors instead
+                if coarse == "dense" or e.code in (N.PSK_ERR_HIP, N.PSK_ERR_RCCL):
+                    raise
+        if self._coarse is None:
+            self._coarse, self._lu = coarse_solver(self.mlh.matrix(0))
         pa, ka = N.handle_array([d.handle for d in self._A])
         pp, kp = N.handle_array([d.handle for d in self._P])
         pr, kr = N.handle_array([d.handle for d in self._R])

@@ -14,11 +14,12 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"))
 
 PSK_OK = 0
+PSK_ERR_ARG, PSK_ERR_HIP, PSK_ERR_RCCL, PSK_ERR_ALLOC, PSK_ERR_UNSUPPORTED = -1, -2, -3, -4, -5
 ABI_VERSION = 3          # include/psk.h PSK_ABI_VERSION (psk_ctl gained norm_b in 2, psk_result.exit in 3)
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_EXIT_NONE, PSK_EXIT_TOLERANCE, PSK_EXIT_ARNOLDI_BREAKDOWN, PSK_EXIT_MAXITER, PSK_EXIT_DOT_BREAKDOWN = 0, 1, 2, 3, 4
 PSK_HOST, PSK_DEVICE = 0, 1
-PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG = 0, 1, 2, 3
+PSK_PREC_IDENTITY, PSK_PREC_JACOBI, PSK_PREC_ILU, PSK_PREC_AMG, PSK_PREC_DENSE = 0, 1, 2, 3, 4
 PSK_LAYOUT_CSR, PSK_LAYOUT_SLICED, PSK_LAYOUT_SLICED_WIDE, PSK_LAYOUT_SLICED_DICT, PSK_LAYOUT_DIAG = 0, 1, 2, 3, 4
 PSK_UNIQUE_ID_BYTES = 128
 
@@ -76,11 +77,13 @@ SIGNATURES = {
     "psk_prec_destroy": (ctypes.c_int, [P]),
     "psk_prec_create_trisolve": (ctypes.c_int, [I64, P, P, P, I32, P, P, P, I32, P, P, PP]),
     "psk_prec_create_amg": (ctypes.c_int, [I32, PP, PP, PP, PP, P, I32, I32, I32, F64, PP]),
+    "psk_prec_create_dense_inverse": (ctypes.c_int, [P, I32, PP]),
     "psk_prec_trisolve_schedule": (ctypes.c_int, [P, I32, I32, ctypes.POINTER(I32), ctypes.POINTER(I64),
                                                    ctypes.POINTER(I32), ctypes.POINTER(F64), ctypes.POINTER(F64)]),
     "psk_prec_trisolve_grid_info": (ctypes.c_int, [P, I32, ctypes.POINTER(I64)]),
     "psk_lab_occupy_begin": (ctypes.c_int, [I32, I32, F64]),
     "psk_lab_occupy_end": (ctypes.c_int, [ctypes.POINTER(I32)]),
+    "psk_lab_occupy_xcc": (ctypes.c_int, [ctypes.POINTER(I32)]),
     "psk_lab_trisolve_workers": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "psk_trisolve_grid_plan": (ctypes.c_int, [I64, P, P, P, I32, ctypes.POINTER(I64)]),
     "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),

@@ -1898,6 +1898,10 @@ __global__ __launch_bounds__(1024) void occupy_kernel(uint32_t *flag, int64_t *s
     if (threadIdx.x == 0) {
         occ_lds[0] = 1;
         __hip_atomic_fetch_add(started, (int64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        // which XCD holds this occupier (HW_REG_XCC_ID, bits 3:0): psk_lab_occupy_xcc
+        const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
+        __hip_atomic_fetch_add(reinterpret_cast<uint32_t *>(timed_out) + 32 + xcc, 1u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -1968,6 +1972,14 @@ extern "C" int psk_lab_occupy_end(int32_t *timed_out) {
     PSK_HIP(hipMemcpy(&h, g_occ.dw + 64, sizeof(int32_t), hipMemcpyDeviceToHost));
     g_occ.active = false;
     if (timed_out) *timed_out = h;
+    return PSK_OK;
+}
+
+// occupiers per XCD of the last psk_lab_occupy_begin (counts[8]; after psk_lab_occupy_end)
+extern "C" int psk_lab_occupy_xcc(int32_t *counts) {
+    using namespace psk;
+    if (!counts || !g_occ.dw) return fail(PSK_ERR_ARG, "psk_lab_occupy_xcc: no occupiers yet");
+    PSK_HIP(hipMemcpy(counts, g_occ.dw + 96, 8 * sizeof(int32_t), hipMemcpyDeviceToHost));
     return PSK_OK;
 }
 

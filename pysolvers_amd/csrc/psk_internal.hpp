@@ -119,6 +119,9 @@ struct HaloPeer {
 };
 
 struct ShmComm;
+struct DenseInverse;
+// largest dense coarse inverse (psk_prec_create_dense_inverse): 32768^2 doubles = 8.6 GB
+constexpr int64_t kDenseMaxN = 32768;
 
 // Device-side exchange of the solvers' per-rank scalars through a host-shared mailbox (dist.hip,
 // psk_comm_mailbox; round 5): the kernel that finishes a rank's grid sums stores them straight into
@@ -293,6 +296,7 @@ struct psk_prec {
     double *work = nullptr;   // 2n: y, z
     int32_t *err = nullptr;
     psk::AmgHierarchy *amg = nullptr;   // PSK_PREC_AMG
+    psk::DenseInverse *dense = nullptr; // PSK_PREC_DENSE (dense.hip)
 };
 
 namespace psk {
@@ -816,10 +820,12 @@ int ilu_apply_add(const psk_prec *M, const double *v, double *x, hipStream_t s);
 int ilu_check_error(const psk_prec *M, hipStream_t s);
 int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
 void amg_free(AmgHierarchy *h);
+int dense_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
+void dense_free(DenseInverse *d);
 // preconditioners whose apply is not a single elementwise op (triangular solves, AMG): the
 // Krylov drivers take their general path for these
 inline bool prec_is_general(const psk_prec *M) {
-    return M && (M->kind == PSK_PREC_ILU || M->kind == PSK_PREC_AMG);
+    return M && (M->kind == PSK_PREC_ILU || M->kind == PSK_PREC_AMG || M->kind == PSK_PREC_DENSE);
 }
 // reports a bounded-spin timeout of any triangular solve inside M (syncs the stream)
 int prec_check_error(const psk_prec *M, hipStream_t s);

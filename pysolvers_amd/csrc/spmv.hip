@@ -601,6 +601,10 @@ constexpr int kDiagMax = 8;
 #define PSK_DIAG_TPW 2
 #endif
 constexpr int kDiagTpw = PSK_DIAG_TPW;   // slices per workgroup
+#ifndef PSK_DIAG_DPP
+#define PSK_DIAG_DPP 0
+#endif
+constexpr bool kDiagDpp = PSK_DIAG_DPP != 0;   // the -1/+1 diagonals by DPP lane shifts (lab until measured)
 struct DiagDesc {
     int32_t d[kDiagMax];   // diagonal offsets, in every row's stored order
     double v[kDiagMax];    // the value (bit pattern) of every entry on diagonal j
@@ -622,11 +626,36 @@ __device__ __forceinline__ int32_t spmv_vzero() {
     return z;
 }
 
-template <int MODE, int KM, int TPW>
+// a double moved one lane along the wave (DPP wavefront shift; both halves by the same pattern): SHR: lane l
+// receives lane l-1's value, SHL: lane l+1's; the lane with no source keeps `edge`
+template <bool SHR>
+__device__ __forceinline__ double wave_shift1(double v, double edge) {
+    constexpr int ctrl = SHR ? 0x138 : 0x130;   // wave_shr:1 / wave_shl:1
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(v), ctrl, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), ctrl, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+
+// column of row + off under the diagonal layout's mapping (diag_col with an explicit offset)
+__device__ __forceinline__ int64_t diag_col_off(const DiagDesc &dd, int64_t n, int64_t row, int64_t off) {
+    int64_t c = row + off;
+    c += c < 0 ? dd.lo : (c >= n ? dd.hi : 0);
+    return c < 0 ? 0 : (c >= dd.ncols ? dd.ncols - 1 : c);
+}
+
+// NB (round 5 lab, PSK_DIAG_DPP builds): the diagonals -1 and +1 are not gathered: lane l's x[row -/+ 1] is
+// lane l -/+ 1's x[row] (the d = 0 gather of the same wave), moved by a DPP wave shift; the two wave-edge
+// lanes load theirs (one more load instruction, its other lanes re-reading their own x[row]). Exact for
+// any mapping: the d = 0 gather of a row r >= n is diag_col(r) = the column of (r - 1) + 1. NB = 1: the
+// FD stored order (0, -m, +m, -1, +1); NB = 2: sorted (-m, -1, 0, +1, +m).
+template <int MODE, int KM, int TPW, int NB = 0>
 __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
     int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd, const double *__restrict__ x, double *__restrict__ y,
     const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
     TileMap tm, int64_t ntiles) {
+    constexpr int JD = NB == 1 ? 0 : NB == 2 ? 2 : -1, JM1 = NB == 1 ? 3 : NB == 2 ? 1 : -1,
+                  JP1 = NB == 1 ? 4 : NB == 2 ? 3 : -1;
+    static_assert(NB == 0 || KM == 5, "NB: the 5-diagonal patterns only");
     PSK_SPMV_PROF_AT(0);
     // ONE memory round trip per workgroup: the done flag (a vector load, so that waiting for it leaves the
     // loads issued after it in flight), the presence bytes and every diagonal's x (clamped addresses that do
@@ -638,7 +667,7 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
     int64_t tl[TPW];
     bool tv[TPW];
     uint32_t mk[TPW];
-    double xv[TPW][KM], eq[TPW];
+    double xv[TPW][KM], eq[TPW], xe[TPW];
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t t = grp * TPW + q;
@@ -651,9 +680,16 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
         const int64_t row = tl[q] * kSlice + tid;
 #pragma unroll
         for (int j = 0; j < KM; ++j) {
+            if (NB && (j == JM1 || j == JP1)) continue;   // from the d = 0 value of the neighbouring lane
             const int64_t c = diag_col(dd, n, row, j);
             xv[q][j] = x[c];
             if (MODE == kSpmvJacobiDot) xv[q][j] = aux_d[c] * xv[q][j];   // (DInv*q)[c], rounded
+        }
+        if (NB) {   // the wave-edge lanes' neighbours: lane 0 x[row - 1], lane 63 x[row + 1]
+            const int lane = tid & 63;
+            const int64_t c = diag_col_off(dd, n, row, lane == 0 ? -1 : (lane == 63 ? 1 : 0));
+            xe[q] = x[c];
+            if (MODE == kSpmvJacobiDot) xe[q] = aux_d[c] * xe[q];
         }
         eq[q] = 0.0;
         if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
@@ -675,8 +711,10 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
 #pragma unroll
         for (int q = 0; q < TPW; ++q) {
             __asm__ volatile("" ::"v"(mk[q]));
+            if (NB) __asm__ volatile("" ::"v"(xe[q]));
 #pragma unroll
-            for (int j = 0; j < KM; ++j) __asm__ volatile("" ::"v"(xv[q][j]));
+            for (int j = 0; j < KM; ++j)
+                if (!(NB && (j == JM1 || j == JP1))) __asm__ volatile("" ::"v"(xv[q][j]));
             if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
                 __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)), 1u, __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
@@ -690,6 +728,13 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
         __syncthreads();
     }
     double acc[TPW], yv[TPW];
+    if (NB) {
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            xv[q][JM1] = wave_shift1<true>(xv[q][JD], xe[q]);
+            xv[q][JP1] = wave_shift1<false>(xv[q][JD], xe[q]);
+        }
+    }
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t row = tl[q] * kSlice + tid;
@@ -1415,6 +1460,15 @@ static bool spmv_xcd_bands() {
     return on;
 }
 
+// PSK_SPMV_CSR_BANDS=1: the CSR tile kernel on the XCD-banded map too (A/B)
+static bool spmv_csr_bands() {
+    static const bool on = [] {
+        const char *e = std::getenv("PSK_SPMV_CSR_BANDS");
+        return e && std::atoi(e) != 0;
+    }();
+    return on;
+}
+
 // lab: the persistent diagonal-layout kernel (PSK_SPMV_PERSIST=1) and its workgroups per CU
 static bool spmv_persist() {
     static const bool on = [] {
@@ -1469,7 +1523,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     // 0.057 ms); the CSR tile kernel measured 2-3% slower with them (3163^2 and 16384^2), so it keeps
     // block order
     // rev: each XCD walks its band backwards (the PCG loop alternates directions, PSK_K23_BANDS=2)
-    const TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands(), rev != 0);
+    const TileMap tm = tile_map_for(nwg, (sliced || spmv_csr_bands()) && spmv_xcd_bands(), rev != 0);
     // compact uniform layout (FD and other 2-value stencils): slices per workgroup,
     // spmv_uniform_multi_kernel (round 4: 2 by default, PSK_SPMV_TPW=1 the one-slice kernel, 3 and 4
     // lab). Two slices per workgroup: in-loop SpMV at N = 10M 0.0657 -> 0.0611 ms, 16384^2 1.60 ->
@@ -1488,9 +1542,19 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const bool persist = spmv_persist();
         int64_t gp = std::min<int64_t>(nwgd, (int64_t)c->num_cus * spmv_persist_per_cu());
         gp = std::max<int64_t>(8, gp - gp % 8);
+        // the DPP neighbour form (PSK_DIAG_DPP builds) for the two 5-diagonal orders it is written for
+        const int nbk = !kDiagDpp || A->dg_K != 5 ? 0
+                        : (A->dg_d[0] == 0 && A->dg_d[3] == -1 && A->dg_d[4] == 1) ? 1
+                        : (A->dg_d[2] == 0 && A->dg_d[1] == -1 && A->dg_d[3] == 1) ? 2 : 0;
 #define PSK_DIAG_LAUNCH(M, KM)                                                                                     \
     do {                                                                                                           \
-        if (persist)                                                                                               \
+        if (KM == 5 && nbk == 1)                                                                                   \
+            hipExtLaunchKernelGGL((spmv_diag_kernel<M, 5, kDiagTpw, 1>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, \
+                                  dd, x, y, aux_d, aux_q, gs, done_flag, tmd, nwg);                                 \
+        else if (KM == 5 && nbk == 2)                                                                              \
+            hipExtLaunchKernelGGL((spmv_diag_kernel<M, 5, kDiagTpw, 2>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, \
+                                  dd, x, y, aux_d, aux_q, gs, done_flag, tmd, nwg);                                 \
+        else if (persist)                                                                                          \
             hipExtLaunchKernelGGL((spmv_diag_persist_kernel<M, KM, kDiagTpw>), dim3((unsigned)gp), bd, 0, s, ev0, ev1, \
                                   0, A->n, A->dg_mask, dd, x, y, aux_d, aux_q, gs, done_flag, nwgd, nwg);            \
         else                                                                                                       \
@@ -1719,6 +1783,7 @@ int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, h
     }
     if (M->kind == PSK_PREC_ILU) return ilu_apply(M, v, out, s);
     if (M->kind == PSK_PREC_AMG) return amg_apply(M, v, out, s);
+    if (M->kind == PSK_PREC_DENSE) return dense_apply(M, v, out, s);
     return fail(PSK_ERR_UNSUPPORTED, "unknown preconditioner kind");
 }
 
@@ -2136,6 +2201,7 @@ int psk_prec_destroy(psk_prec *M) {
     M->lo.release();
     M->up.release();
     if (M->amg) amg_free(M->amg);
+    if (M->dense) dense_free(M->dense);
     delete M;
     return PSK_OK;
 }

@@ -411,3 +411,68 @@ def test_grid_markstein_range_fallback(psk, scale):
     assert np.array_equal(M.apply(v), g)
     ref = spla.spsolve_triangular(T, vs, lower=False)
     assert np.all(np.isfinite(g_small)) and _rel(g_small / scale, ref / scale) <= 1e-12   # norms would under/overflow
+
+
+# ---------------------------------------------------------------------------------------------
+# dense coarse solve (round 5, pysolvers_amd/csrc/dense.hip): x = A_c^-1 f as one streamed GEMV.
+# Bar: within 1e-12 (max-norm, relative) of SuperLU's solve of the same matrix (spsolve, VCycleManager.py:36),
+# bitwise reproducible run to run, and the AMG apply with it within 1e-10 of the oracle (above).
+
+def _sa_coarse(m, L):
+    from oracle import fdlap
+    from pysolvers_amd.Linear.SmoothedAggregation import SmoothedAggregationMLHierarchy
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    return sp.csr_matrix(SmoothedAggregationMLHierarchy(sp.csr_matrix(A), numLevels=L).matrix(0))
+
+
+def _maxrel(a, b):
+    return np.max(np.abs(a - b)) / np.max(np.abs(b))
+
+
+@pytest.mark.parametrize("m,L,refine", [(64, 2, 0), (384, 3, 0), (2048, 4, 0), (2048, 4, 1)])
+def test_dense_coarse_matches_splu(psk, m, L, refine):
+    """SA coarse operators of -FD m^2: n_c = 1,024 (one column segment), ~4,800 (three) and 9,715 (five;
+    the partial last segment), with and without the refinement step."""
+    from pysolvers_amd.Linear.AMGPreconditioner import DenseInverseSolver, coarse_factor
+    Ac = _sa_coarse(m, L)
+    lu = coarse_factor(Ac)
+    D = DenseInverseSolver(Ac, refine=refine)
+    rng = np.random.default_rng(m + refine)
+    for _ in range(3):
+        f = rng.standard_normal(Ac.shape[0])
+        x = D.apply(f)
+        assert _maxrel(x, lu.solve(f, trans='T')) <= 1e-12
+        assert np.array_equal(D.apply(f).view(np.uint64), x.view(np.uint64))
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (7, 1), (2049, 2), (4097, 3)])
+def test_dense_inverse_random(psk, n, seed):
+    """Odd sizes (row pitch padding, a one-column last segment), nonsymmetric, against numpy's solve."""
+    from pysolvers_amd.Linear.AMGPreconditioner import DenseInverseSolver
+    rng = np.random.default_rng(seed)
+    A = sp.random(n, n, density=min(1.0, 6.0 / n), random_state=rng) + sp.diags(4.0 + rng.random(n))
+    A = sp.csr_matrix(A)
+    f = rng.standard_normal(n)
+    x = DenseInverseSolver(A).apply(f)
+    ref = np.linalg.solve(A.toarray(), f)
+    assert _maxrel(x, ref) <= 1e-12
+
+
+def test_dense_inverse_singular_refused(psk):
+    from pysolvers_amd import _native as N
+    from pysolvers_amd.Linear.AMGPreconditioner import DenseInverseSolver
+    A = sp.csr_matrix(np.array([[1.0, 2.0], [2.0, 4.0]]))
+    with pytest.raises(N.PskError):
+        DenseInverseSolver(A)
+
+
+def test_amg_dense_vs_lu_coarse(psk):
+    """The same hierarchy with either coarse solve: applies within 1e-12 of each other, the dense one by
+    default."""
+    from oracle import fdlap
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 1024)
+    v = np.random.default_rng(4).standard_normal(A.shape[0])
+    Md = psk.AMG(numIters=2, numLevels=4).form(A)
+    Ml = psk.AMG(numIters=2, numLevels=4, coarse="lu").form(A)
+    assert Md.coarse_kind == "dense" and Ml.coarse_kind == "lu"
+    assert _rel(Md.applyRight(v), Ml.applyRight(v)) <= 1e-12

@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--cycles", type=int, default=2)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--smoother", default="gs", choices=["gs", "jacobi"])
+    ap.add_argument("--coarse", default="auto", choices=["auto", "dense", "lu"])
     args = ap.parse_args()
     import pysolvers_amd as psk
     from pysolvers_amd import _native as N
@@ -48,7 +49,7 @@ def main():
     out = dict(side=m, n=n, levels=args.levels, cycles=args.cycles, smoother=args.smoother, iters=args.iters)
     t1 = time.time()
     sm = psk.JacobiSmoother if args.smoother == "jacobi" else psk.GaussSeidelSmoother
-    M = psk.AMG(numIters=args.cycles, numLevels=args.levels, smoother=sm).form(dA)
+    M = psk.AMG(numIters=args.cycles, numLevels=args.levels, smoother=sm, coarse=args.coarse).form(dA)
     del A
     out["amg_setup_s"] = time.time() - t1
     out["level_sizes"] = M.levels()
@@ -102,7 +103,7 @@ def main():
         if args.smoother == "gs":
             e.update(op.schedule("U"), dep_levels=op.device_info()["levels_u"])
             chosen = e["schedule"]
-            for sched in ("syncfree", "band", "grid"):
+            for sched in ("syncfree", "band", "grid", "part"):
                 try:
                     op.schedule("U", set=sched)
                 except N.PskError:
@@ -112,10 +113,16 @@ def main():
         per.append(e)
     v0 = psk.DeviceVector.from_numpy(np.random.default_rng(0).standard_normal(M.levels()[0]))
     co = M._coarse
-    per.append(dict(level=0, n=M.levels()[0], coarse_solve_ms=timed(co, v0), L=co.schedule("L"), U=co.schedule("U"),
-                    dep_levels=[co.device_info()["levels_l"], co.device_info()["levels_u"]],
-                    nnz=[co.device_info()["nnz_l"], co.device_info()["nnz_u"]]))
-    if M.levels()[0] <= 18432:   # coarse solve under each schedule it can run, then back to the chosen one
+    if M.coarse_kind == "dense":
+        n0 = M.levels()[0]
+        ms = timed(co, v0)
+        per.append(dict(level=0, n=n0, coarse="dense", coarse_solve_ms=ms,
+                        gemv_gb_s=n0 * ((n0 + 7) // 8 * 8) * 8 / (ms * 1e-3) / 1e9))
+    else:
+        per.append(dict(level=0, n=M.levels()[0], coarse="lu", coarse_solve_ms=timed(co, v0), L=co.schedule("L"),
+                        U=co.schedule("U"), dep_levels=[co.device_info()["levels_l"], co.device_info()["levels_u"]],
+                        nnz=[co.device_info()["nnz_l"], co.device_info()["nnz_u"]]))
+    if M.coarse_kind == "lu" and M.levels()[0] <= 18432:   # coarse solve under each schedule it can run, then back to the chosen one
         chosen = (co.schedule("L")["schedule"], co.schedule("U")["schedule"])
         for sched in ("syncfree", "lds"):
             co.schedule("L", set=sched)

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Lab probe of the triangular solves beside occupiers (tests/test_gpu_progress.py's setting, verbose).
 
-    python tools/progress_probe.py [--m 384] [--wgs 128] [--lds 102400] [--seconds 8] [--sched syncfree]
+    python tools/progress_probe.py [--m 384] [--wgs 128[,192,...]] [--lds 102400] [--seconds 8] [--sched syncfree]
+                                   [--factor ilu|gs]
+
+--factor gs: the Gauss-Seidel factor triu(-FD m^2) as a one-factor chain (schedules band / grid / syncfree).
 
 Prints, for an idle device and then beside `wgs` occupier workgroups: the apply's wall time, the
 enrolled workers / grid of each sync-free factor, whether the occupiers timed out, the error word, and
@@ -23,7 +26,8 @@ sys.path.insert(0, REPO)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=384)
-    ap.add_argument("--wgs", type=int, default=128)
+    ap.add_argument("--wgs", default="128")
+    ap.add_argument("--factor", default="ilu", choices=["ilu", "gs"])
     ap.add_argument("--lds", type=int, default=100 * 1024)
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--sched", default="syncfree")
@@ -33,15 +37,22 @@ def main():
     from pysolvers_amd import _native as N
     from oracle import fdlap
     A = fdlap.fd_laplacian_2d(-1.0, 1.0, a.m)
-    M = psk.RightILUT().form(psk.DeviceCSR.from_scipy(A))
-    code = {"syncfree": 0, "band": 1, "part": 4}[a.sched]
-    for f in (0, 1):
+    code = {"syncfree": 0, "band": 1, "lds": 2, "grid": 3, "part": 4}[a.sched]
+    if a.factor == "gs":
+        import scipy.sparse as sp
+        from pysolvers_amd.Linear import TriangularSolveChain
+        M = TriangularSolveChain(A.shape[0], U=sp.triu(-A).tocsr())
+        facs = (1,)
+    else:
+        M = psk.RightILUT().form(psk.DeviceCSR.from_scipy(A))
+        facs = (0, 1)
+    for f in facs:
         N.check(N.lib.psk_prec_trisolve_schedule(M.device_handle, f, code, None, None, None, None, None), "schedule")
     v = psk.DeviceVector.from_numpy(np.random.default_rng(5).standard_normal(A.shape[0]))
 
     def workers():
         out = []
-        for f in (0, 1):
+        for f in facs:
             e, g = N.I32(), N.I32()
             N.check(N.lib.psk_lab_trisolve_workers(M.device_handle, f, ctypes.byref(e), ctypes.byref(g)), "workers")
             out.append((e.value, g.value))
@@ -63,14 +74,18 @@ def main():
     ms, err = timed()
     ref = out.numpy()
     print(json.dumps({"phase": "idle2", "ms": ms, "err": err, "workers": workers()}), flush=True)
-    N.check(N.lib.psk_lab_occupy_begin(a.wgs, a.lds, a.seconds), "occupy_begin")
-    ms, err = timed()
-    to = N.I32()
-    N.check(N.lib.psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
-    y = out.numpy()
-    print(json.dumps({"phase": "occupied", "ms": ms, "err": err, "timed_out": to.value, "workers": workers(),
-                      "same_bits": None if y is None else bool(np.array_equal(y.view(np.uint64), ref.view(np.uint64)))}),
-          flush=True)
+    for wgs in (int(w) for w in a.wgs.split(",")):
+        N.check(N.lib.psk_lab_occupy_begin(wgs, a.lds, a.seconds), "occupy_begin")
+        ms, err = timed()
+        to = N.I32()
+        N.check(N.lib.psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
+        xcc = (N.I32 * 8)()
+        N.check(N.lib.psk_lab_occupy_xcc(xcc), "occupy_xcc")
+        y = out.numpy()
+        print(json.dumps({"phase": "occupied", "wgs": wgs, "xcc": list(xcc), "ms": ms, "err": err,
+                          "timed_out": to.value, "workers": workers(),
+                          "same_bits": None if y is None else bool(np.array_equal(y.view(np.uint64), ref.view(np.uint64)))}),
+              flush=True)
 
 
 if __name__ == "__main__":

@@ -17,7 +17,7 @@ import statistics
 
 def family(name):
     for key in ("pcg_init_kernel", "spmv_", "pcg_update_kernel", "pcg_direction_kernel", "gridsum_counter_check",
-                "pcg_flush", "pcg_init_finish"):
+                "pcg_flush", "pcg_init_finish", "pcg_finish_kernel"):
         if key in name:
             return key.rstrip("_")
     m = re.match(r"(?:void )?(?:psk::)?([A-Za-z0-9_]+)", name)
@@ -42,8 +42,8 @@ def main():
             cur.append(r)
     res = []
     for sv in solves:
-        # the solve ends at its counter check kernel
-        end = next((i for i, r in enumerate(sv) if r[2] == "gridsum_counter_check"), None)
+        # the solve ends at its finish kernel (state + gridsum checks; round 4: the counter check kernel)
+        end = next((i for i, r in enumerate(sv) if r[2] in ("pcg_finish_kernel", "gridsum_counter_check")), None)
         if end is None:
             continue
         sv = sv[:end + 1]
