@@ -182,11 +182,13 @@ int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
 int prec_check_error(const psk_prec *M, hipStream_t s) {
     if (!M) return PSK_OK;
     if (M->kind == PSK_PREC_ILU) return ilu_check_error(M, s);
+    if (M->kind == PSK_PREC_DENSE) return dense_check_error(M, s);
     if (M->kind == PSK_PREC_AMG) {
         const AmgHierarchy *h = M->amg;
         for (psk_prec *S : h->S)
             if (S && S->kind == PSK_PREC_ILU) PSK_TRY(ilu_check_error(S, s));
         if (h->coarse && h->coarse->kind == PSK_PREC_ILU) PSK_TRY(ilu_check_error(h->coarse, s));
+        if (h->coarse && h->coarse->kind == PSK_PREC_DENSE) PSK_TRY(dense_check_error(h->coarse, s));
     }
     return PSK_OK;
 }

@@ -42,6 +42,7 @@ struct DenseInverse {
     int64_t nrb = 0;       // row blocks
     uint64_t *part = nullptr;   // nseg * n partials (nseg > 1)
     uint32_t *cnt = nullptr;    // nrb counters (zero between launches)
+    int32_t *err = nullptr;     // set when a partial never landed (bounded wait; dense_check_error)
     double *work = nullptr;     // 2 ld: x1, r (refinement)
     const psk_csr *A = nullptr; // borrowed: the refinement's residual
     int32_t refine = 0;
@@ -49,7 +50,7 @@ struct DenseInverse {
 
 void dense_free(DenseInverse *d) {
     if (!d) return;
-    void *ptrs[] = {d->M, d->part, d->cnt, d->work};
+    void *ptrs[] = {d->M, d->part, d->cnt, d->work, d->err};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     delete d;
@@ -71,7 +72,8 @@ __global__ __launch_bounds__(kBlock) void dense_gemv_kernel(int64_t n, int64_t l
                                                             const double *__restrict__ M,
                                                             const double *__restrict__ f,
                                                             const double *add, double *y,
-                                                            uint64_t *__restrict__ part, uint32_t *__restrict__ cnt) {
+                                                            uint64_t *__restrict__ part, uint32_t *__restrict__ cnt,
+                                                            int32_t *err) {
     const int64_t b = blockIdx.x, rb = b / nseg;
     const int32_t seg = (int32_t)(b - rb * nseg);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -113,27 +115,36 @@ __global__ __launch_bounds__(kBlock) void dense_gemv_kernel(int64_t n, int64_t l
         }
         return;
     }
+    // split rows: each unit publishes its two row partials into slots armed with the gridsum sentinel
+    // (agent-scope stores, value-is-flag: no fence, which on gfx950 would write back the whole L2 per
+    // workgroup), then draws a ticket on its row block's counter; the holder of the last ticket sums the
+    // nseg partials of each row in segment order (every other unit's stores were issued before its ticket,
+    // so each poll ends), re-arms the slots and resets the counter (psk_internal.hpp "gridsum" protocol).
     if (lane == 0) {
         if (r0 < n) gridsum_put(part + (int64_t)seg * n + r0, s0);
         if (r1 < n) gridsum_put(part + (int64_t)seg * n + r1, s1);
-        __threadfence();
     }
     __syncthreads();
     __shared__ uint32_t tk;
-    if (threadIdx.x == 0)
-        tk = __hip_atomic_fetch_add(cnt + rb * kDenseCntStride, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) tk = gridsum_draw(cnt + rb * kDenseCntStride);
     __syncthreads();
     if (tk != (uint32_t)nseg - 1) return;   // not the row block's last unit
-    __threadfence();
     if (threadIdx.x == 0) gridsum_reset(cnt + rb * kDenseCntStride);
     const int64_t r = rb * kDenseRows + threadIdx.x;
     if (threadIdx.x < kDenseRows && r < n) {
         double s = 0.0;
-        for (int32_t q = 0; q < nseg; ++q)
-            s += __longlong_as_double((long long)__hip_atomic_load(part + (int64_t)q * n + r, __ATOMIC_RELAXED,
-                                                                   __HIP_MEMORY_SCOPE_AGENT));
+        for (int32_t q = 0; q < nseg; ++q) {
+            uint64_t *sl = part + (int64_t)q * n + r;
+            s += __longlong_as_double((long long)gridsum_wait(sl, err));
+            __hip_atomic_store(sl, kGridSumSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
         y[r] = ADD ? add[r] + s : s;
     }
+}
+
+__global__ void dense_arm_kernel(int64_t m, uint64_t *part) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) part[i] = kGridSumSentinel;
 }
 
 static int dense_gemv(const DenseInverse *d, int64_t n, const double *f, const double *add, double *y,
@@ -141,10 +152,10 @@ static int dense_gemv(const DenseInverse *d, int64_t n, const double *f, const d
     const dim3 grid((unsigned)(d->nrb * d->nseg));
     if (add)
         hipLaunchKernelGGL(dense_gemv_kernel<true>, grid, dim3(kBlock), 0, s, n, d->ld, d->nseg, d->M, f, add, y,
-                           d->part, d->cnt);
+                           d->part, d->cnt, d->err);
     else
         hipLaunchKernelGGL(dense_gemv_kernel<false>, grid, dim3(kBlock), 0, s, n, d->ld, d->nseg, d->M, f, add,
-                           y, d->part, d->cnt);
+                           y, d->part, d->cnt, d->err);
     PSK_HIP(hipGetLastError());
     return PSK_OK;
 }
@@ -161,6 +172,20 @@ int dense_apply(const psk_prec *P, const double *v, double *out, hipStream_t s) 
         PSK_TRY(launch_spmv(d->A, kSpmvResid, x1, r, nullptr, v, nullptr, nullptr, s));
         double *dst = it + 1 == d->refine ? out : x1;
         PSK_TRY(dense_gemv(d, n, r, x1, dst, s));   // (dst may alias add: each y[i] reads add[i] first)
+    }
+    return PSK_OK;
+}
+
+int dense_check_error(const psk_prec *P, hipStream_t s) {
+    const DenseInverse *d = P->dense;
+    if (!d || !d->err) return PSK_OK;
+    int32_t h = 0;
+    PSK_HIP(hipMemcpyAsync(&h, d->err, 4, hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    if (h) {
+        (void)hipMemsetAsync(d->err, 0, sizeof(int32_t), s);
+        (void)hipStreamSynchronize(s);
+        return fail(PSK_ERR_HIP, "dense inverse apply: a partial sum never landed (bounded wait expired)");
     }
     return PSK_OK;
 }
@@ -237,6 +262,7 @@ extern "C" int psk_prec_create_dense_inverse(const psk_csr *A, int32_t refine, p
     if (!alloc((void **)&d->M, (size_t)n * ld * sizeof(double)) ||
         (d->nseg > 1 && !alloc((void **)&d->part, (size_t)d->nseg * n * sizeof(uint64_t))) ||
         (d->nseg > 1 && !alloc((void **)&d->cnt, (size_t)d->nrb * kDenseCntStride * sizeof(uint32_t))) ||
+        !alloc((void **)&d->err, sizeof(int32_t)) ||
         (refine > 0 && !alloc((void **)&d->work, (size_t)2 * ld * sizeof(double)))) {
         delete P;
         return bail(PSK_ERR_ALLOC, "hipMalloc (" + std::to_string((double)n * ld * 8 / 1e9) + " GB inverse)");
@@ -257,6 +283,12 @@ extern "C" int psk_prec_create_dense_inverse(const psk_csr *A, int32_t refine, p
     hipStream_t s = c->stream;
     hipError_t e = hipMemsetAsync(d->M, 0, (size_t)n * ld * sizeof(double), s);
     if (e == hipSuccess && d->cnt) e = hipMemsetAsync(d->cnt, 0, (size_t)d->nrb * kDenseCntStride * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(d->err, 0, sizeof(int32_t), s);
+    if (e == hipSuccess && d->part) {
+        const int64_t m = (int64_t)d->nseg * n;
+        hipLaunchKernelGGL(dense_arm_kernel, dim3((unsigned)((m + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, m, d->part);
+        e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipMemsetAsync(info, 0, 2 * sizeof(int32_t), s);
     if (e == hipSuccess) {
         hipLaunchKernelGGL(dense_scatter_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,

@@ -821,6 +821,7 @@ int ilu_check_error(const psk_prec *M, hipStream_t s);
 int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
 void amg_free(AmgHierarchy *h);
 int dense_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
+int dense_check_error(const psk_prec *M, hipStream_t s);
 void dense_free(DenseInverse *d);
 // preconditioners whose apply is not a single elementwise op (triangular solves, AMG): the
 // Krylov drivers take their general path for these

@@ -602,9 +602,11 @@ constexpr int kDiagMax = 8;
 #endif
 constexpr int kDiagTpw = PSK_DIAG_TPW;   // slices per workgroup
 #ifndef PSK_DIAG_DPP
-#define PSK_DIAG_DPP 0
+#define PSK_DIAG_DPP 1
 #endif
-constexpr bool kDiagDpp = PSK_DIAG_DPP != 0;   // the -1/+1 diagonals by DPP lane shifts (lab until measured)
+// the -1/+1 diagonals by DPP lane shifts (default from round 5: in-loop SpMV at N = 10M 0.0587 -> 0.0550 ms,
+// 16384^2 1.44 -> 1.28 ms, same bits; profiles/r5_diag_dpp_ab.txt; -DPSK_DIAG_DPP=0 builds the gathers)
+constexpr bool kDiagDpp = PSK_DIAG_DPP != 0;
 struct DiagDesc {
     int32_t d[kDiagMax];   // diagonal offsets, in every row's stored order
     double v[kDiagMax];    // the value (bit pattern) of every entry on diagonal j
@@ -643,7 +645,7 @@ __device__ __forceinline__ int64_t diag_col_off(const DiagDesc &dd, int64_t n, i
     return c < 0 ? 0 : (c >= dd.ncols ? dd.ncols - 1 : c);
 }
 
-// NB (round 5 lab, PSK_DIAG_DPP builds): the diagonals -1 and +1 are not gathered: lane l's x[row -/+ 1] is
+// NB (round 5, PSK_DIAG_DPP): the diagonals -1 and +1 are not gathered: lane l's x[row -/+ 1] is
 // lane l -/+ 1's x[row] (the d = 0 gather of the same wave), moved by a DPP wave shift; the two wave-edge
 // lanes load theirs (one more load instruction, its other lanes re-reading their own x[row]). Exact for
 // any mapping: the d = 0 gather of a row r >= n is diag_col(r) = the column of (r - 1) + 1. NB = 1: the

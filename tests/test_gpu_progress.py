@@ -38,8 +38,10 @@ def _apply_under_occupiers(handle, v, wgs, lds=100 * 1024):
         N.check(N.lib.psk_prec_apply(handle, v.n, v._p, out._p, N.PSK_DEVICE), "psk_prec_apply")
     finally:
         N.check(N.lib.psk_lab_occupy_end(ctypes.byref(timed_out)), "psk_lab_occupy_end")
-    assert timed_out.value == 0, "the occupiers hit their time limit: the solve waited for them"
-    return out.numpy()
+    xcc = (N.I32 * 8)()
+    N.check(N.lib.psk_lab_occupy_xcc(xcc), "psk_lab_occupy_xcc")
+    assert timed_out.value == 0, "the occupiers hit their time limit: the solve waited for them (per XCD %s)" % list(xcc)
+    return out.numpy(), list(xcc)
 
 
 def psk_mod():
@@ -67,7 +69,7 @@ def test_syncfree_ilu_apply_beside_occupiers(psk):
     v = psk.DeviceVector.from_numpy(np.random.default_rng(5).standard_normal(A.shape[0]))
     ref = M.applyRight(v).numpy()
     idle = [_workers(M.device_handle, f) for f in (0, 1)]
-    out = _apply_under_occupiers(M.device_handle, v, 128)
+    out, _ = _apply_under_occupiers(M.device_handle, v, 128)
     busy = [_workers(M.device_handle, f) for f in (0, 1)]
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
     for (ei, g), (eb, g2) in zip(idle, busy):
@@ -75,26 +77,32 @@ def test_syncfree_ilu_apply_beside_occupiers(psk):
         assert 0 < eb < g, (eb, g)                   # beside the occupiers: fewer workers, still solved
 
 
-@pytest.mark.parametrize("sched", ["band", "grid"])
-def test_block_schedules_beside_occupiers(psk, sched):
-    """triu(-FD 1024^2) — the Gauss-Seidel smoother's factor (ClassicSmoothers.py:33) — on the band
+@pytest.mark.parametrize("sched,m", [("band", 1024), ("grid", 2048)])
+def test_block_schedules_beside_occupiers(psk, sched, m):
+    """triu(-FD m^2) — the Gauss-Seidel smoother's factor (ClassicSmoothers.py:33) — on the band
     schedule (blocks of the solve order) and the grid schedule (64-line bands): workgroups draw their
     blocks from a ticket counter, so a block only ever waits on blocks held by running workgroups. The
-    band grid is 2 workgroups per CU; occupiers leave 1 on half the CUs. For the grid schedule the
-    occupiers hold 31 of the 32 CUs of every XCD (workgroups are dealt to the XCDs round-robin and only
-    start on their own XCD's CUs), so at most one band per XCD runs at a time."""
+    band grid is 2 workgroups per CU; occupiers leave 1 on half the CUs. For the grid schedule (one
+    147-KiB-LDS workgroup per CU, 32 bands at 2048^2) the occupiers hold 30 of the 32 CUs of every XCD,
+    so at most 16 of the 32 bands run at a time and workgroups must be recycled.
+    (With 31 per XCD — the placement tools/progress_probe.py records — the launch does not start at all
+    until the occupiers leave: the dispatcher does not place the kernel's workgroups on the one free CU
+    of each XCD. That is a launch waiting for CUs, not a wait inside the solve; the occupiers of this test
+    never leave on their own, so the test stays at 30.)"""
     import scipy.sparse.linalg as spla
     from oracle import fdlap
     from pysolvers_amd.Linear import TriangularSolveChain
-    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 1024)
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
     U = sp.triu(A).tocsr()
     v = np.random.default_rng(9).standard_normal(A.shape[0])
     M = TriangularSolveChain(A.shape[0], U=U)
     M.schedule("U", set=sched)
     ref = M.apply(v)
     assert np.max(np.abs(ref - spla.spsolve_triangular(U, v, lower=False))) <= 1e-12 * np.max(np.abs(ref))
-    wgs = 128 if sched == "band" else 248
-    out = _apply_under_occupiers(M.device_handle, psk.DeviceVector.from_numpy(v), wgs)
+    wgs = 128 if sched == "band" else 240
+    out, xcc = _apply_under_occupiers(M.device_handle, psk.DeviceVector.from_numpy(v), wgs)
+    if sched == "grid":
+        assert max(xcc) <= 30, xcc   # every XCD kept two free CUs (the placement the docstring assumes)
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
     assert np.array_equal(M.apply(v).view(np.uint64), ref.view(np.uint64))   # counters re-armed
 
@@ -107,5 +115,5 @@ def test_amg_apply_beside_occupiers(psk):
     M = psk.AMG(numIters=2, numLevels=4, smoother=psk.GaussSeidelSmoother).form(psk.DeviceCSR.from_scipy(A))
     v = psk.DeviceVector.from_numpy(np.random.default_rng(2).standard_normal(A.shape[0]))
     ref = M.applyRight(v).numpy()
-    out = _apply_under_occupiers(M.device_handle, v, 128)
+    out, _ = _apply_under_occupiers(M.device_handle, v, 128)
     assert np.array_equal(out.view(np.uint64), ref.view(np.uint64))
