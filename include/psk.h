@@ -268,6 +268,9 @@ int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out);
  * workgroups that started, not over the grid). */
 int psk_lab_occupy_begin(int32_t wgs, int32_t lds_bytes, double seconds);
 int psk_lab_occupy_end(int32_t *timed_out);
+/* Lab: nwg workgroups of 128 threads with lds_bytes of LDS, each spinning usec; rec_out[3*i..] = start, end
+ * (s_memrealtime, 100 MHz) and XCD of workgroup i. Waits for the launch. */
+int psk_lab_dispatch_probe(int32_t nwg, int32_t lds_bytes, double usec, int64_t *rec_out);
 /* Lab: occupiers per XCD (HW_REG_XCC_ID) of the last psk_lab_occupy_begin, counts[8]. */
 int psk_lab_occupy_xcc(int32_t *counts);
 int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid);

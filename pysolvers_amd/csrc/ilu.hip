@@ -1975,6 +1975,42 @@ extern "C" int psk_lab_occupy_end(int32_t *timed_out) {
     return PSK_OK;
 }
 
+// lab: `nwg` workgroups of 128 threads holding `lds_bytes` of LDS each, each spinning `usec` and recording
+// (start, end, XCD) in s_memrealtime ticks — is a launch that needs its workgroups recycled dispatched
+// beside the occupiers? (the grid schedule's progress test)
+__global__ void dispatch_probe_kernel(uint64_t ticks, int64_t *rec) {
+    extern __shared__ unsigned char dp_lds[];
+    if (threadIdx.x == 0) {
+        dp_lds[0] = 1;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t t = t0;
+        while (t - t0 < ticks) {
+            __builtin_amdgcn_s_sleep(4);
+            t = __builtin_amdgcn_s_memrealtime();
+        }
+        rec[3 * blockIdx.x + 0] = (int64_t)t0;
+        rec[3 * blockIdx.x + 1] = (int64_t)t;
+        rec[3 * blockIdx.x + 2] = (int64_t)(__builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u);
+    }
+}
+
+extern "C" int psk_lab_dispatch_probe(int32_t nwg, int32_t lds_bytes, double usec, int64_t *rec_out) {
+    using namespace psk;
+    if (nwg < 1 || lds_bytes < 16 || lds_bytes > 160 * 1024 || usec < 0 || !rec_out)
+        return fail(PSK_ERR_ARG, "psk_lab_dispatch_probe: bad arguments");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    int64_t *rec = nullptr;
+    PSK_HIP(hipMalloc(&rec, (size_t)nwg * 3 * sizeof(int64_t)));
+    hipLaunchKernelGGL(dispatch_probe_kernel, dim3((unsigned)nwg), dim3(128), (size_t)lds_bytes, c->stream,
+                       (uint64_t)(usec * 100.0), rec);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(rec_out, rec, (size_t)nwg * 3 * sizeof(int64_t), hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(rec);   // (after the launch completed: the caller releases the occupiers afterwards)
+    return e == hipSuccess ? PSK_OK : fail(PSK_ERR_HIP, hipGetErrorString(e));
+}
+
 // occupiers per XCD of the last psk_lab_occupy_begin (counts[8]; after psk_lab_occupy_end)
 extern "C" int psk_lab_occupy_xcc(int32_t *counts) {
     using namespace psk;
@@ -2617,11 +2653,16 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     {
         const char *pe = std::getenv("PSK_TRISOLVE_PART");
         const bool force = pe && std::atoi(pe) == 1, off = pe && std::atoi(pe) == 0;
-        const int64_t strip = (n + c->num_cus - 1) / std::max(1, c->num_cus);
-        if (!off && n > kLdsMaxRows && n >= (int64_t)c->num_cus * kPartWaves &&
+        static const int nparts = [] {   // lab: PSK_PART_STRIPS = strips (default: one per CU)
+            const char *e = std::getenv("PSK_PART_STRIPS");
+            return e ? std::atoi(e) : 0;
+        }();
+        const int P = nparts > 0 ? nparts : c->num_cus;
+        const int64_t strip = (n + P - 1) / std::max(1, P);
+        if (!off && n > kLdsMaxRows && n >= (int64_t)P * kPartWaves &&
             (force || (T.schedule != kSchedGrid && strip <= kPartMaxStrip))) {
             PartPlan pp;
-            plan_part(F, nat, c->num_cus, pp);
+            plan_part(F, nat, P, pp);
             T.est_part_us = pp.est;
             const double cur = T.schedule == kSchedBand ? T.est_band_us
                                : T.schedule == kSchedLds  ? T.est_lds_us

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--m", type=int, default=384)
     ap.add_argument("--wgs", default="128")
     ap.add_argument("--factor", default="ilu", choices=["ilu", "gs"])
+    ap.add_argument("--dispatch", default="", help="NWG,LDS_BYTES,USEC: the dispatch probe kernel instead of a solve")
     ap.add_argument("--lds", type=int, default=100 * 1024)
     ap.add_argument("--seconds", type=float, default=8.0)
     ap.add_argument("--sched", default="syncfree")
@@ -35,6 +36,25 @@ def main():
     os.environ.setdefault("PSK_NO_TORCH", "1")
     import pysolvers_amd as psk
     from pysolvers_amd import _native as N
+    if a.dispatch:
+        nwg, lds, us = (float(v) for v in a.dispatch.split(","))
+        nwg, lds = int(nwg), int(lds)
+        for wgs in [0] + [int(w) for w in a.wgs.split(",")]:
+            if wgs:
+                N.check(N.lib.psk_lab_occupy_begin(wgs, a.lds, a.seconds), "occupy_begin")
+            rec = np.zeros(3 * nwg, np.int64)
+            t0 = time.perf_counter()
+            N.check(N.lib.psk_lab_dispatch_probe(nwg, lds, us, N.ptr(rec)), "dispatch_probe")
+            ms = (time.perf_counter() - t0) * 1e3
+            to = N.I32()
+            if wgs:
+                N.check(N.lib.psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
+            r = rec.reshape(nwg, 3)
+            st = (r[:, 0] - r[:, 0].min()) / 100.0   # us
+            print(json.dumps({"phase": "dispatch", "wgs": wgs, "nwg": nwg, "lds": lds, "usec": us, "ms": ms,
+                              "timed_out": to.value, "start_us_quantiles": [float(np.quantile(st, q)) for q in (0, .25, .5, .75, 1)],
+                              "per_xcd": np.bincount(r[:, 2], minlength=8).tolist()}), flush=True)
+        return
     from oracle import fdlap
     A = fdlap.fd_laplacian_2d(-1.0, 1.0, a.m)
     code = {"syncfree": 0, "band": 1, "lds": 2, "grid": 3, "part": 4}[a.sched]
