@@ -159,3 +159,28 @@ def test_native_first_level_matches_oracle_negfd1024():
     oP, oagg = amg.sa_coarsen(A, lvl=1)
     assert np.array_equal(agg, oagg)
     assert _bitwise(P, oP)
+
+
+def test_amg_coarse_option_validated_before_any_device_work():
+    """AMG(coarse=...) accepts "auto" / "dense" / "lu" (the dense coarse solve, round 5); anything else is
+    refused before a device matrix is created, so this runs without a GPU."""
+    import pysolvers_amd as psk
+    A = sp.identity(4, format="csr")
+    with pytest.raises(ValueError):
+        psk.AMG(coarse="qr").form(A)
+
+
+def test_dense_coarse_accuracy_model_on_host():
+    """What the dense coarse solve relies on, checked on the host for an SA coarse operator of -FD 256^2
+    (n_c ~ 1,000): x = A_c^-1 f through an explicit inverse agrees with SuperLU's transposed solve (the
+    reference's spsolve) far inside the 1e-12 the GPU tests pin."""
+    from oracle import fdlap
+    from pysolvers_amd.Linear.AMGPreconditioner import coarse_factor
+    from pysolvers_amd.Linear.SmoothedAggregation import SmoothedAggregationMLHierarchy
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, 256)
+    Ac = sp.csr_matrix(SmoothedAggregationMLHierarchy(sp.csr_matrix(A), numLevels=3).matrix(0))
+    lu = coarse_factor(Ac)
+    Minv = np.linalg.inv(Ac.toarray())
+    f = np.random.default_rng(0).standard_normal(Ac.shape[0])
+    xs = lu.solve(f, trans='T')
+    assert np.max(np.abs(Minv @ f - xs)) <= 1e-13 * np.max(np.abs(xs))
