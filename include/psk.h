@@ -249,8 +249,10 @@ int psk_prec_create_amg(int32_t num_levels, psk_csr *const *A, psk_csr *const *P
  * workgroup, sync-free inside it with x in LDS), 3 = grid (2-D stencil factors: one wave per band of
  * 64 lines advancing along a skewed coordinate), 4 = part (rows cut into strips of their natural
  * index, one workgroup per CU, in-strip dependencies through LDS; its layout is built when chosen or
- * when PSK_TRISOLVE_PART=1 at creation). The library picks the fastest by host cost models
- * (est_*_us); set = 0..4 forces one (PSK_ERR_UNSUPPORTED when the factor has no such layout), -1 only
+ * when PSK_TRISOLVE_PART=1 at creation), 5 = levels (round 5: ONE workgroup, a dependency level per step
+ * behind a barrier, x in an LDS ring; for factors with narrow levels and dependencies a bounded number of
+ * solve positions back; built when chosen or when PSK_TRISOLVE_LEVELS=1 at creation). The library picks the fastest by host cost models
+ * (est_*_us); set = 0..5 forces one (PSK_ERR_UNSUPPORTED when the factor has no such layout), -1 only
  * queries. Any out pointer may be NULL. */
 int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t *schedule, int64_t *blocks,
                                int32_t *ring_words, double *est_syncfree_us, double *est_band_us);

@@ -70,13 +70,15 @@ class TriangularSolveChain(DeviceOperator, GenericPreconditioner):
 
     def schedule(self, which, set=None):
         """dict(schedule, blocks, ring_words, est_syncfree_us, est_band_us) of factor `which` ('L' or
-        'U'); set='syncfree' / 'band' / 'lds' / 'grid' / 'part' forces a schedule (psk_prec_trisolve_schedule)."""
-        code = {None: -1, "syncfree": 0, "band": 1, "lds": 2, "grid": 3, "part": 4}[set]
+        'U'); set='syncfree' / 'band' / 'lds' / 'grid' / 'part' / 'levels' forces a schedule
+        (psk_prec_trisolve_schedule)."""
+        code = {None: -1, "syncfree": 0, "band": 1, "lds": 2, "grid": 3, "part": 4, "levels": 5}[set]
         sc, bl, rw, e0, e1 = N.I32(), N.I64(), N.I32(), N.F64(), N.F64()
         N.check(N.lib.psk_prec_trisolve_schedule(self._h, {"L": 0, "U": 1}[which], code, ctypes.byref(sc),
                                                  ctypes.byref(bl), ctypes.byref(rw), ctypes.byref(e0),
                                                  ctypes.byref(e1)), "psk_prec_trisolve_schedule")
-        return dict(schedule=("syncfree", "band", "lds", "grid", "part")[sc.value], blocks=bl.value, ring_words=rw.value,
+        return dict(schedule=("syncfree", "band", "lds", "grid", "part", "levels")[sc.value], blocks=bl.value,
+                    ring_words=rw.value,
                     est_syncfree_us=e0.value, est_band_us=e1.value)
 
     def grid_info(self, which):

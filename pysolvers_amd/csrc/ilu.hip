@@ -1319,12 +1319,13 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     const int32_t *gate, uint32_t *sched) {
     if (gate && __hip_atomic_load(gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;   // uniform
     extern __shared__ __align__(16) unsigned char smem[];
-    // the band this workgroup solves: drawn from the ticket counter (band b waits only on band b - 1, drawn
-    // earlier by a running workgroup; sched_next_block)
+    // the bands this workgroup solves: drawn one after the other from the ticket counter (band b waits only on
+    // band b - 1, drawn earlier by a running workgroup; sched_next_block) until they run out. A workgroup
+    // that finishes its band takes the next one itself: the launch never needs a workgroup that has not
+    // started (round 5: with one band per workgroup, a launch beside a kernel holding most CUs stalled —
+    // the dispatcher did not start its later workgroups on the CUs its finished ones freed, tests/
+    // test_gpu_progress.py, profiles/r5_progress_probe.txt)
     __shared__ int64_t s_band;
-    if (threadIdx.x == 0) s_band = sched_one_block(sched);
-    __syncthreads();
-    const int64_t band = s_band;
     double *ring = reinterpret_cast<double *>(smem);                  // [2 * kGridRing][kGridRW]
     int64_t *ctl = reinterpret_cast<int64_t *>(smem + 2 * kGridMirror);
     unsigned char *dict = smem + 2 * kGridMirror + 16;                // DICT: ndict GridDict<K> records
@@ -1342,247 +1343,370 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             for (int k = 0; k < K; ++k) ro[k] = grid_ring_off((gcode[(size_t)i * (K / 2) + k / 2] >> (16 * (k & 1))) & 0xffff);
         }
     }
-    // ctl[0]: last u of the band above present in the ring (poller -> solver)
-    // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
-    const int tid = threadIdx.x, j = tid & 63;
-    const int64_t y0 = band * kGridLanes;
-    const int64_t ylast = (y0 + kGridLanes - 1 < H - 1) ? y0 + kGridLanes - 1 : H - 1;
-    const int64_t u_lo = grid_g(sigma2, phase, y0), u_hi = (w - 1) + grid_g(sigma2, phase, ylast);
-    const int S = (int)(u_hi - u_lo + 1);
-    int min_ud = 1 << 30, max_ud = 0;
-    for (int e = 0; e < pe; ++e) {
-        const int ud = ext.delta[e] >> 6;
-        min_ud = ud < min_ud ? ud : min_ud;
-        max_ud = ud > max_ud ? ud : max_ud;
-    }
-    const bool has_ext = band > 0 && pe > 0;
-    for (int i = tid; i < 2 * kGridRing * kGridRW; i += 2 * kGridLanes) ring[i] = 0.0;
-    if (tid == 0) {
-        ctl[0] = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;
-        ctl[1] = u_lo - 1;
-    }
-    __syncthreads();
-#ifdef PSK_GRID_PROF
-    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
-    unsigned long long n_wait = 0, c_wait = 0;
-#endif
-    if (tid >= kGridLanes) {
-        // ---------------- poller: u positions [u_lo - max_ud, u_hi - min_ud] of lines y0-maxyd .. y0-1
-        if (!has_ext) return;
-        const int64_t ua = u_lo - max_ud, ub = u_hi - min_ud;
-        for (int64_t base = ua; base <= ub; base += kGridLanes) {
-            const int64_t u = base + j;
-            double *row_lo = ring + (size_t)((u - u_lo) & (kGridRing - 1)) * kGridRW + (8 - maxyd);
-            double *row_hi = row_lo + kGridRing * kGridRW;
-            // ring capacity: row (u - u_lo) last held u - kGridRing, which the solver reads until it passes
-            // that position + max_ud
-            int64_t spins = 0;
-            while (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
-                   base + kGridLanes - 1 - kGridRing + max_ud) {
-                if (++spins > kMaxSpins) { atomicExch(err, (2 << 24) | (int)band); return; }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            uint32_t pending = 0;   // lines of this lane's u still to fetch
-            for (int L = 0; L < maxyd; ++L) {
-                const int64_t yl = y0 - maxyd + L, xl = u - grid_g(sigma2, phase, yl), q = yl * w + xl - off;
-                const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q >= 0 && q < n;
-                if (valid) {
-                    pending |= 1u << L;
-                } else {
-                    row_lo[L] = 0.0;
-                    row_hi[L] = 0.0;
+    const int64_t nbands = (H + kGridLanes - 1) / kGridLanes;
+    auto run_band = [&](const int64_t band) {
+        // ctl[0]: last u of the band above present in the ring (poller -> solver)
+        // ctl[1]: last u the solver has finished (solver -> poller, ring capacity)
+        const int tid = threadIdx.x, j = tid & 63;
+        const int64_t y0 = band * kGridLanes;
+        const int64_t ylast = (y0 + kGridLanes - 1 < H - 1) ? y0 + kGridLanes - 1 : H - 1;
+        const int64_t u_lo = grid_g(sigma2, phase, y0), u_hi = (w - 1) + grid_g(sigma2, phase, ylast);
+        const int S = (int)(u_hi - u_lo + 1);
+        int min_ud = 1 << 30, max_ud = 0;
+        for (int e = 0; e < pe; ++e) {
+            const int ud = ext.delta[e] >> 6;
+            min_ud = ud < min_ud ? ud : min_ud;
+            max_ud = ud > max_ud ? ud : max_ud;
+        }
+        const bool has_ext = band > 0 && pe > 0;
+        for (int i = tid; i < 2 * kGridRing * kGridRW; i += 2 * kGridLanes) ring[i] = 0.0;
+        if (tid == 0) {
+            ctl[0] = has_ext ? u_lo - max_ud - 1 : INT64_MAX / 2;
+            ctl[1] = u_lo - 1;
+        }
+        __syncthreads();
+    #ifdef PSK_GRID_PROF
+        const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+        unsigned long long n_wait = 0, c_wait = 0;
+    #endif
+        if (tid >= kGridLanes) {
+            // ---------------- poller: u positions [u_lo - max_ud, u_hi - min_ud] of lines y0-maxyd .. y0-1
+            if (!has_ext) return;
+            const int64_t ua = u_lo - max_ud, ub = u_hi - min_ud;
+            for (int64_t base = ua; base <= ub; base += kGridLanes) {
+                const int64_t u = base + j;
+                double *row_lo = ring + (size_t)((u - u_lo) & (kGridRing - 1)) * kGridRW + (8 - maxyd);
+                double *row_hi = row_lo + kGridRing * kGridRW;
+                // ring capacity: row (u - u_lo) last held u - kGridRing, which the solver reads until it passes
+                // that position + max_ud
+                int64_t spins = 0;
+                while (__hip_atomic_load(&ctl[1], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) <
+                       base + kGridLanes - 1 - kGridRing + max_ud) {
+                    if (++spins > kMaxSpins) { atomicExch(err, (2 << 24) | (int)band); return; }
+                    __builtin_amdgcn_s_sleep(2);
+                }
+                uint32_t pending = 0;   // lines of this lane's u still to fetch
+                for (int L = 0; L < maxyd; ++L) {
+                    const int64_t yl = y0 - maxyd + L, xl = u - grid_g(sigma2, phase, yl), q = yl * w + xl - off;
+                    const bool valid = u <= ub && yl >= 0 && xl >= 0 && xl < w && q >= 0 && q < n;
+                    if (valid) {
+                        pending |= 1u << L;
+                    } else {
+                        row_lo[L] = 0.0;
+                        row_hi[L] = 0.0;
+                    }
+                }
+                spins = 0;
+                while (true) {
+                    for (int L = 0; L < maxyd; ++L)
+                        if (pending & (1u << L)) {
+                            const int64_t yl = y0 - maxyd + L, q = yl * w + (u - grid_g(sigma2, phase, yl)) - off;
+                            const double v = load_pub(x + (upper ? n - 1 - q : q));
+                            if (!is_sentinel(v)) {
+                                row_lo[L] = v;
+                                row_hi[L] = v;
+                                pending &= ~(1u << L);
+                            }
+                        }
+                    // ready prefix of this chunk: lanes 0..r-1 have every line
+                    const uint64_t notready = __ballot(pending != 0);
+                    const int r = notready ? __builtin_ctzll(notready) : kGridLanes;
+                    __builtin_amdgcn_s_waitcnt(0xc07f);   // ring writes before the announcement
+                    if (j == 0 && r > 0)
+                        __hip_atomic_store(&ctl[0], base + r - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (!notready) break;
+                    if (++spins > kMaxSpins) { atomicExch(err, (3 << 24) | (int)band); return; }
+                    __builtin_amdgcn_s_sleep(1);
                 }
             }
-            spins = 0;
-            while (true) {
-                for (int L = 0; L < maxyd; ++L)
-                    if (pending & (1u << L)) {
-                        const int64_t yl = y0 - maxyd + L, q = yl * w + (u - grid_g(sigma2, phase, yl)) - off;
-                        const double v = load_pub(x + (upper ? n - 1 - q : q));
-                        if (!is_sentinel(v)) {
-                            row_lo[L] = v;
-                            row_hi[L] = v;
-                            pending &= ~(1u << L);
-                        }
-                    }
-                // ready prefix of this chunk: lanes 0..r-1 have every line
-                const uint64_t notready = __ballot(pending != 0);
-                const int r = notready ? __builtin_ctzll(notready) : kGridLanes;
-                __builtin_amdgcn_s_waitcnt(0xc07f);   // ring writes before the announcement
-                if (j == 0 && r > 0)
-                    __hip_atomic_store(&ctl[0], base + r - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (!notready) break;
-                if (++spins > kMaxSpins) { atomicExch(err, (3 << 24) | (int)band); return; }
-                __builtin_amdgcn_s_sleep(1);
-            }
-        }
-        return;
-    }
-    // ---------------- solver
-    const int64_t y = y0 + j;
-    // lane j's line holds grid positions [y*w, y*w + w) of [off, n + off) (the first `off` positions of
-    // the first line are empty: a partial line leading the solve order); it is active for steps
-    // [s_beg, s_end): x = s - gy in [x_lo, x_hi), gy = g(y) - g(y0) (the line's first step in the band)
-    const int64_t x_lo = y * w < off ? off - y * w : 0;
-    const int64_t x_hi = n + off - y * w < w ? n + off - y * w : w;
-    const bool live = y < H && x_hi > x_lo;
-    const int64_t gy = grid_g(sigma2, phase, y) - u_lo;
-    const int s_beg = (int)(gy + (live ? x_lo : 0)), s_end = live ? (int)(gy + x_hi) : s_beg;
-    const uint32_t s_len = (uint32_t)(s_end - s_beg);
-    // byte offset of step s's row: rb8 + rs8 * s (32-bit: n <= kGridMaxRows; step indices < 2^23, so a
-    // 24-bit multiply), q = y*w + s - gy - off; a line-less lane reads out of range (loads 0)
-    const int64_t qb = y * w - gy - off;
-    const uint32_t rb8 = live ? (uint32_t)((upper ? n - 1 - qb : qb) * 8) : kBufOOB - 8;
-    const int32_t rs8 = live ? (upper ? -8 : 8) : 0;
-    const bool pub = j >= kGridLanes - maxyd;   // the lines the band below reads: agent-scope stores
-    const uint32_t lane8 = (uint32_t)(8 + j) * 8;
-    const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
-                                 band * S_full * GridStep<K>::kBytes;
-    // the index stream of this band: a buffer with the step in the scalar offset
-    const __amdgpu_buffer_rsrc_t ridx = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<uint32_t *>(DICT ? gidx + band * S_full * kGridLanes : gidx), (short)0,
-        DICT ? (int)(uint32_t)(S_full * kGridLanes * 4) : 0, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rrhs = grid_rsrc(rhs, n), rx = grid_rsrc(x, n);
-    // steps up to s_ok need nothing more from the band above (uniform)
-    int s_ok = has_ext ? -max_ud - 1 + min_ud : INT32_MAX / 2;
-    uint64_t rbad = 0;   // MK: lanes with a step's right-hand side outside the Markstein range (div_markstein)
-    struct Slot {
-        uint32_t idx;   // DICT: the record index
-        uint32_t code[K / 2];
-        double cf[K], d, b;
-    };
-    auto fetch = [&](int s, Slot &sl) {
-        const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
-        const int sa = __builtin_elementwise_max(__builtin_elementwise_min(s, s_end - 1), s_beg);
-        sl.b = grid_bload(rrhs, rb8 + (uint32_t)__mul24(rs8, sa));
-        if (DICT) {
-            sl.idx = __builtin_amdgcn_raw_buffer_load_b32(ridx, (uint32_t)j * 4, (uint32_t)sc * (kGridLanes * 4), 0);
             return;
         }
-        const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
-        const uint32_t *pc = reinterpret_cast<const uint32_t *>(st + GridStep<K>::kCode) + j * (K / 2);
-#pragma unroll
-        for (int k = 0; k < K / 2; ++k) sl.code[k] = pc[k];
-        const dv2 *pf = reinterpret_cast<const dv2 *>(st + GridStep<K>::kCoef) + j * (K / 2);
-#pragma unroll
-        for (int k = 0; k < K; k += 2) {
-            const dv2 c = pf[k / 2];
-            sl.cf[k] = c.x;
-            sl.cf[k + 1] = c.y;
+        // ---------------- solver
+        const int64_t y = y0 + j;
+        // lane j's line holds grid positions [y*w, y*w + w) of [off, n + off) (the first `off` positions of
+        // the first line are empty: a partial line leading the solve order); it is active for steps
+        // [s_beg, s_end): x = s - gy in [x_lo, x_hi), gy = g(y) - g(y0) (the line's first step in the band)
+        const int64_t x_lo = y * w < off ? off - y * w : 0;
+        const int64_t x_hi = n + off - y * w < w ? n + off - y * w : w;
+        const bool live = y < H && x_hi > x_lo;
+        const int64_t gy = grid_g(sigma2, phase, y) - u_lo;
+        const int s_beg = (int)(gy + (live ? x_lo : 0)), s_end = live ? (int)(gy + x_hi) : s_beg;
+        const uint32_t s_len = (uint32_t)(s_end - s_beg);
+        // byte offset of step s's row: rb8 + rs8 * s (32-bit: n <= kGridMaxRows; step indices < 2^23, so a
+        // 24-bit multiply), q = y*w + s - gy - off; a line-less lane reads out of range (loads 0)
+        const int64_t qb = y * w - gy - off;
+        const uint32_t rb8 = live ? (uint32_t)((upper ? n - 1 - qb : qb) * 8) : kBufOOB - 8;
+        const int32_t rs8 = live ? (upper ? -8 : 8) : 0;
+        const bool pub = j >= kGridLanes - maxyd;   // the lines the band below reads: agent-scope stores
+        const uint32_t lane8 = (uint32_t)(8 + j) * 8;
+        const unsigned char *pstep = reinterpret_cast<const unsigned char *>(grec) +
+                                     band * S_full * GridStep<K>::kBytes;
+        // the index stream of this band: a buffer with the step in the scalar offset
+        const __amdgpu_buffer_rsrc_t ridx = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<uint32_t *>(DICT ? gidx + band * S_full * kGridLanes : gidx), (short)0,
+            DICT ? (int)(uint32_t)(S_full * kGridLanes * 4) : 0, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rrhs = grid_rsrc(rhs, n), rx = grid_rsrc(x, n);
+        // steps up to s_ok need nothing more from the band above (uniform)
+        int s_ok = has_ext ? -max_ud - 1 + min_ud : INT32_MAX / 2;
+        uint64_t rbad = 0;   // MK: lanes with a step's right-hand side outside the Markstein range (div_markstein)
+        struct Slot {
+            uint32_t idx;   // DICT: the record index
+            uint32_t code[K / 2];
+            double cf[K], d, b;
+        };
+        auto fetch = [&](int s, Slot &sl) {
+            const int sc = s < S ? s : S - 1;   // past the end: re-read the last step (unused)
+            const int sa = __builtin_elementwise_max(__builtin_elementwise_min(s, s_end - 1), s_beg);
+            sl.b = grid_bload(rrhs, rb8 + (uint32_t)__mul24(rs8, sa));
+            if (DICT) {
+                sl.idx = __builtin_amdgcn_raw_buffer_load_b32(ridx, (uint32_t)j * 4, (uint32_t)sc * (kGridLanes * 4), 0);
+                return;
+            }
+            const unsigned char *st = pstep + (int64_t)sc * GridStep<K>::kBytes;
+            const uint32_t *pc = reinterpret_cast<const uint32_t *>(st + GridStep<K>::kCode) + j * (K / 2);
+    #pragma unroll
+            for (int k = 0; k < K / 2; ++k) sl.code[k] = pc[k];
+            const dv2 *pf = reinterpret_cast<const dv2 *>(st + GridStep<K>::kCoef) + j * (K / 2);
+    #pragma unroll
+            for (int k = 0; k < K; k += 2) {
+                const dv2 c = pf[k / 2];
+                sl.cf[k] = c.x;
+                sl.cf[k + 1] = c.y;
+            }
+            sl.d = reinterpret_cast<const double *>(st + GridStep<K>::kDiag)[j];
+        };
+        auto lookup = [&](uint32_t idx, GridRec<K> &rc) {   // DICT: the record of a step, from LDS
+            const unsigned char *rec = dict + idx * GridDict<K>::kBytes;
+    #pragma unroll
+            for (int k = 0; k < K; k += 2) {
+                const dv2 c = *reinterpret_cast<const dv2 *>(rec + 8 * k);
+                rc.cf[k] = c.x;
+                rc.cf[k + 1] = c.y;
+            }
+            const dv2 dd = *reinterpret_cast<const dv2 *>(rec + GridDict<K>::kDg);
+            rc.d = dd.x;
+            rc.rd = dd.y;
+    #pragma unroll
+            for (int k = 0; k < K; ++k) rc.off[k] = reinterpret_cast<const uint32_t *>(rec + GridDict<K>::kOff)[k];
+        };
+        // the ring values of step t are requested right after step t-1's ring write (one wave: the LDS
+        // queue is in order, so they see it), and the step's other work — the x stores, the prefetch D
+        // steps ahead, the dictionary lookup two steps ahead — runs while they are in flight: the chain
+        // per step is the LDS round trip and the arithmetic, not the step's whole instruction stream
+        auto wait_ext = [&](int t) {
+            if (t > s_ok && t < S) {   // uniform: the band above not yet in the ring
+    #ifdef PSK_GRID_PROF
+                const unsigned long long tw = __builtin_amdgcn_s_memtime();
+    #endif
+                int64_t spins = 0;
+                do {
+                    const int known = __builtin_amdgcn_readfirstlane(
+                        (int)(__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - u_lo));
+                    s_ok = known + min_ud;   // ext_known >= u - min_ud  <=>  t <= known + min_ud
+                    if (t <= s_ok) break;
+                    if (++spins > kMaxSpins) { atomicExch(err, (1 << 24) | (int)band); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                } while (true);
+    #ifdef PSK_GRID_PROF
+                n_wait += 1;
+                c_wait += __builtin_amdgcn_s_memtime() - tw;
+    #endif
+            }
+        };
+        auto request = [&](int t, const Slot &sl, const GridRec<K> &rec, double *v) {
+            const uint32_t base = lane8 + (uint32_t)(t & (kGridRing - 1)) * (kGridRW * 8);   // lower copy, row t
+    #pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const uint32_t ro = DICT ? rec.off[k] : grid_ring_off((sl.code[k >> 1] >> (16 * (k & 1))) & 0xffff);
+                v[k] = *reinterpret_cast<const double *>(smem + base + ro);
+            }
+        };
+        auto solve = [&](int s, const Slot &sl, const GridRec<K> &rec, const double *v) -> double {
+            double acc = 0.0;
+    #pragma unroll
+            for (int k = 0; k < K; ++k) acc = fma(DICT ? rec.cf[k] : sl.cf[k], v[k], acc);   // stored order; padding adds +-0
+            double r = sl.b - acc;
+            const double d = DICT ? rec.d : sl.d;
+            if (DICT && MK) {   // a select, not a branch, on `unit` (the chain stays branch-free)
+                const double q = div_markstein(r, d, rec.rd, rbad);
+                r = unit ? r : q;
+            } else if (!unit) {
+                r = r / d;
+            }
+            // both copies of the row (the mirror is kGridMirror bytes above)
+            const uint32_t base = lane8 + (uint32_t)(s & (kGridRing - 1)) * (kGridRW * 8);
+            *reinterpret_cast<double *>(smem + base) = r;
+            *reinterpret_cast<double *>(smem + base + kGridMirror) = r;
+            return r;
+        };
+        auto store_x = [&](int s, double r) {   // the lines the band below reads are published
+            const bool act = (uint32_t)(s - s_beg) < s_len;
+            const uint32_t o = rb8 + (uint32_t)__mul24(rs8, s);
+            grid_bstore<0x10>(rx, act && pub ? o : kBufOOB, r);
+            grid_bstore<0>(rx, act && !pub ? o : kBufOOB, r);
+        };
+        static_assert(D >= 3 && D % 2 == 0, "the lookup runs two steps ahead; step parity = slot parity");
+        Slot buf[D];
+    #pragma unroll
+        for (int i = 0; i < D; ++i) fetch(i, buf[i]);
+        GridRec<K> rq[2] = {};   // DICT: rq[t & 1] = the record of step t
+        if (DICT) {
+            lookup(buf[0].idx, rq[0]);
+            lookup(buf[1].idx, rq[1]);
         }
-        sl.d = reinterpret_cast<const double *>(st + GridStep<K>::kDiag)[j];
-    };
-    auto lookup = [&](uint32_t idx, GridRec<K> &rc) {   // DICT: the record of a step, from LDS
-        const unsigned char *rec = dict + idx * GridDict<K>::kBytes;
-#pragma unroll
-        for (int k = 0; k < K; k += 2) {
-            const dv2 c = *reinterpret_cast<const dv2 *>(rec + 8 * k);
-            rc.cf[k] = c.x;
-            rc.cf[k + 1] = c.y;
+        double vn[K];
+        wait_ext(0);
+        request(0, buf[0], rq[0], vn);
+        for (int s0 = 0; s0 < S; s0 += D) {   // D even: step s0 + i has the parity of i
+    #pragma unroll
+            for (int i = 0; i < D; ++i) {
+                const int s = s0 + i;
+                const double r = solve(s, buf[i], rq[i & 1], vn);
+                __asm__ volatile("" ::: "memory");   // the ring write before the next step's reads
+                wait_ext(s + 1);
+                request(s + 1, buf[(i + 1) % D], rq[(i + 1) & 1], vn);
+                store_x(s, r);
+                __asm__ volatile("" ::: "memory");
+                fetch(s + D, buf[i]);
+                if (DICT) lookup(buf[(i + 2) % D].idx, rq[i & 1]);   // step s + 2's record
+                // issued HERE: left to itself the machine scheduler sank the lookup into the next step,
+                // next to the ring reads that need it (two LDS round trips on the chain)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if (j == 0)   // progress for the poller's ring capacity
+                __hip_atomic_store(&ctl[1], u_lo + s0 + D - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
-        const dv2 dd = *reinterpret_cast<const dv2 *>(rec + GridDict<K>::kDg);
-        rc.d = dd.x;
-        rc.rd = dd.y;
-#pragma unroll
-        for (int k = 0; k < K; ++k) rc.off[k] = reinterpret_cast<const uint32_t *>(rec + GridDict<K>::kOff)[k];
-    };
-    // the ring values of step t are requested right after step t-1's ring write (one wave: the LDS
-    // queue is in order, so they see it), and the step's other work — the x stores, the prefetch D
-    // steps ahead, the dictionary lookup two steps ahead — runs while they are in flight: the chain
-    // per step is the LDS round trip and the arithmetic, not the step's whole instruction stream
-    auto wait_ext = [&](int t) {
-        if (t > s_ok && t < S) {   // uniform: the band above not yet in the ring
-#ifdef PSK_GRID_PROF
-            const unsigned long long tw = __builtin_amdgcn_s_memtime();
-#endif
-            int64_t spins = 0;
-            do {
-                const int known = __builtin_amdgcn_readfirstlane(
-                    (int)(__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) - u_lo));
-                s_ok = known + min_ud;   // ext_known >= u - min_ud  <=>  t <= known + min_ud
-                if (t <= s_ok) break;
-                if (++spins > kMaxSpins) { atomicExch(err, (1 << 24) | (int)band); break; }
-                __builtin_amdgcn_s_sleep(1);
-            } while (true);
-#ifdef PSK_GRID_PROF
-            n_wait += 1;
-            c_wait += __builtin_amdgcn_s_memtime() - tw;
-#endif
+        if (j == 0) __hip_atomic_store(&ctl[1], INT64_MAX / 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (MK && !unit && rbad != 0 && j == 0) atomicOr(rflag, 1);
+    #ifdef PSK_GRID_PROF
+        if (j == 0 && band < 8192) {
+            g_grid_prof[band * 8 + 0] = t_start;
+            g_grid_prof[band * 8 + 1] = __builtin_amdgcn_s_memtime();
+            g_grid_prof[band * 8 + 2] = n_wait;
+            g_grid_prof[band * 8 + 3] = c_wait;
         }
+    #endif
     };
-    auto request = [&](int t, const Slot &sl, const GridRec<K> &rec, double *v) {
-        const uint32_t base = lane8 + (uint32_t)(t & (kGridRing - 1)) * (kGridRW * 8);   // lower copy, row t
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const uint32_t ro = DICT ? rec.off[k] : grid_ring_off((sl.code[k >> 1] >> (16 * (k & 1))) & 0xffff);
-            v[k] = *reinterpret_cast<const double *>(smem + base + ro);
-        }
-    };
-    auto solve = [&](int s, const Slot &sl, const GridRec<K> &rec, const double *v) -> double {
-        double acc = 0.0;
-#pragma unroll
-        for (int k = 0; k < K; ++k) acc = fma(DICT ? rec.cf[k] : sl.cf[k], v[k], acc);   // stored order; padding adds +-0
-        double r = sl.b - acc;
-        const double d = DICT ? rec.d : sl.d;
-        if (DICT && MK) {   // a select, not a branch, on `unit` (the chain stays branch-free)
-            const double q = div_markstein(r, d, rec.rd, rbad);
-            r = unit ? r : q;
-        } else if (!unit) {
-            r = r / d;
-        }
-        // both copies of the row (the mirror is kGridMirror bytes above)
-        const uint32_t base = lane8 + (uint32_t)(s & (kGridRing - 1)) * (kGridRW * 8);
-        *reinterpret_cast<double *>(smem + base) = r;
-        *reinterpret_cast<double *>(smem + base + kGridMirror) = r;
-        return r;
-    };
-    auto store_x = [&](int s, double r) {   // the lines the band below reads are published
-        const bool act = (uint32_t)(s - s_beg) < s_len;
-        const uint32_t o = rb8 + (uint32_t)__mul24(rs8, s);
-        grid_bstore<0x10>(rx, act && pub ? o : kBufOOB, r);
-        grid_bstore<0>(rx, act && !pub ? o : kBufOOB, r);
-    };
-    static_assert(D >= 3 && D % 2 == 0, "the lookup runs two steps ahead; step parity = slot parity");
-    Slot buf[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) fetch(i, buf[i]);
-    GridRec<K> rq[2] = {};   // DICT: rq[t & 1] = the record of step t
-    if (DICT) {
-        lookup(buf[0].idx, rq[0]);
-        lookup(buf[1].idx, rq[1]);
+    for (;;) {
+        __syncthreads();   // the previous band's waves are done with the ring (and the dictionary is in LDS)
+        if (threadIdx.x == 0) s_band = sched_next_block(sched, nbands);
+        __syncthreads();
+        const int64_t band = s_band;
+        if (band >= nbands) break;
+        run_band(band);
     }
-    double vn[K];
-    wait_ext(0);
-    request(0, buf[0], rq[0], vn);
-    for (int s0 = 0; s0 < S; s0 += D) {   // D even: step s0 + i has the parity of i
+}
+
+// ---- levels schedule (round 5): one workgroup, level-synchronous, x in an LDS ring -------------------
+// For factors with few rows per dependency level and dependencies a bounded number of solve positions
+// back (the SA level-1 operator of -FD 8192^2: 131k rows, 1706 levels of <= 109 rows, every dependency
+// <= 4294 positions back): step s solves lane t's row of one level (a level wider than the workgroup takes
+// several steps), reading its dependencies from the ring (slot = solve position mod R, checked on the host:
+// a slot is rewritten only in a step after its last reader), then a barrier. A hop between levels is an
+// LDS round trip plus a barrier instead of a device-scope publication seen by a polling load (sync-free,
+// ~1 us per level). Records are field-major per step, loaded D steps ahead into registers; the barrier
+// waits for LDS only (lgkmcnt), so those loads stay in flight across it. Per-row arithmetic: fma over the
+// stored entries in stored order from 0.0, padding entries (-0.0 x 0.0) add exactly nothing, then
+// (b - acc) / d: the band and grid kernels' bits.
+constexpr uint32_t kLevelIdle = 0x07FFFFFFu;
+constexpr int kLevelMaxK = 16, kLevelMaxW = 256, kLevelD = 4;
+constexpr int64_t kLevelMaxR = 16384;   // ring slots: 128 KiB of LDS (+ the padding slot)
+template <int KM, int D>
+__global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int R, int64_t n, int unit,
+                                                            const uint32_t *__restrict__ rc,
+                                                            const uint64_t *__restrict__ sl,
+                                                            const double *__restrict__ cf,
+                                                            const double *__restrict__ dg,
+                                                            const double *__restrict__ bp, double *__restrict__ x) {
+    static_assert(KM % 4 == 0, "slots are loaded four per 8-byte word, coefficients two per 16-byte load");
+    extern __shared__ double lv_ring[];   // R + 1 slots; slot R stays 0.0 (padding entries)
+    const int t = threadIdx.x, W = blockDim.x;
+    for (int i = t; i <= R; i += W) lv_ring[i] = 0.0;
+    __syncthreads();
+    struct Rec {
+        uint32_t rc;
+        uint64_t sw[KM / 4];
+        double c[KM];
+        double d, b;
+    };
+    (void)R;
+    // every load is unconditional, branch-free and independent of the others (an address computed from a
+    // loaded count would make the wave wait for that load at once; a predicated load becomes a branch,
+    // after which the compiler waits for ALL outstanding loads): entries past a row's count are stored
+    // padding (slot R, coefficient -0.0), the diagonal is stored as 1.0 for a unit factor
+    const __amdgpu_buffer_rsrc_t rrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(rc), (short)0,
+                                                                         (int)(uint32_t)(nsteps * W * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(sl), (short)0,
+                                                                         (int)(uint32_t)(nsteps * W * (KM / 4) * 8),
+                                                                         0x00020000);
+    const __amdgpu_buffer_rsrc_t rcf = grid_rsrc(cf, nsteps * W * KM), rdg = grid_rsrc(dg, nsteps * W),
+                                 rbp = grid_rsrc(bp, nsteps * W), rx = grid_rsrc(x, n);
+    auto fetch = [&](int64_t s, Rec &r) {
+        const uint32_t sc = (uint32_t)(s < nsteps ? s : nsteps - 1);   // past the end: the last step (unused)
+        const uint32_t p = sc * (uint32_t)W + (uint32_t)t;
+        r.rc = __builtin_amdgcn_raw_buffer_load_b32(rrc, p * 4, 0, 0);
+        r.d = grid_bload(rdg, p * 8);
+        r.b = grid_bload(rbp, p * 8);
+#pragma unroll
+        for (int k4 = 0; k4 < KM / 4; ++k4)
+            r.sw[k4] = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(
+                                                        rsl, ((sc * (KM / 4) + k4) * (uint32_t)W + (uint32_t)t) * 8, 0, 0));
+#pragma unroll
+        for (int k2 = 0; k2 < KM / 2; ++k2) {
+            const auto v4 = __builtin_amdgcn_raw_buffer_load_b128(rcf, ((sc * (KM / 2) + k2) * (uint32_t)W + (uint32_t)t) * 16,
+                                                                  0, 0);
+            r.c[2 * k2] = __longlong_as_double((long long)((uint64_t)v4[0] | ((uint64_t)v4[1] << 32)));
+            r.c[2 * k2 + 1] = __longlong_as_double((long long)((uint64_t)v4[2] | ((uint64_t)v4[3] << 32)));
+        }
+    };
+    // The loop starts D steps early with zeroed records (idle: nothing stored), so that every record load
+    // is issued inside the loop: loads issued before it (a prologue) would be merged into the loop
+    // header's wait state and make the compiler wait for ALL loads at every iteration.
+    Rec buf[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+        buf[i].rc = kLevelIdle;
+#pragma unroll
+        for (int k4 = 0; k4 < KM / 4; ++k4) buf[i].sw[k4] = 0;
+#pragma unroll
+        for (int k = 0; k < KM; ++k) buf[i].c[k] = 0.0;
+        buf[i].d = 1.0;
+        buf[i].b = 0.0;
+    }
+    uint32_t rbase = (uint32_t)((int64_t)R - (int64_t)D * W % R) & (uint32_t)(R - 1);   // (s * W) mod R at s = -D
+    for (int64_t s0 = -D; s0 < nsteps; s0 += D) {   // nsteps: a multiple of D (the host pads idle steps)
 #pragma unroll
         for (int i = 0; i < D; ++i) {
-            const int s = s0 + i;
-            const double r = solve(s, buf[i], rq[i & 1], vn);
-            __asm__ volatile("" ::: "memory");   // the ring write before the next step's reads
-            wait_ext(s + 1);
-            request(s + 1, buf[(i + 1) % D], rq[(i + 1) & 1], vn);
-            store_x(s, r);
-            __asm__ volatile("" ::: "memory");
+            const int64_t s = s0 + i;
+            double acc = 0.0;
+#pragma unroll
+            for (int k = 0; k < KM; ++k) {
+                const uint32_t slot = (uint32_t)(buf[i].sw[k >> 2] >> (16 * (k & 3))) & 0xFFFFu;
+                acc = fma(buf[i].c[k], lv_ring[slot], acc);
+            }
+            double r = buf[i].b - acc;
+            if (!unit) r = r / buf[i].d;   // (uniform)
+            lv_ring[(rbase + (uint32_t)t) & (uint32_t)(R - 1)] = r;
+            const uint32_t row = buf[i].rc & kLevelIdle;
+            grid_bstore<0>(rx, row != kLevelIdle ? row * 8u : kBufOOB, r);   // idle lanes: out of range, dropped
             fetch(s + D, buf[i]);
-            if (DICT) lookup(buf[(i + 2) % D].idx, rq[i & 1]);   // step s + 2's record
-            // issued HERE: left to itself the machine scheduler sank the lookup into the next step,
-            // next to the ring reads that need it (two LDS round trips on the chain)
-            __builtin_amdgcn_sched_barrier(0);
+            rbase = (rbase + (uint32_t)W) & (uint32_t)(R - 1);
+            // the step's ring writes before the next step's reads (LDS-only fences: the prefetch loads stay
+            // in flight across the barrier)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            __builtin_amdgcn_s_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
         }
-        if (j == 0)   // progress for the poller's ring capacity
-            __hip_atomic_store(&ctl[1], u_lo + s0 + D - 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    if (j == 0) __hip_atomic_store(&ctl[1], INT64_MAX / 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (MK && !unit && rbad != 0 && j == 0) atomicOr(rflag, 1);
-#ifdef PSK_GRID_PROF
-    if (j == 0 && band < 8192) {
-        g_grid_prof[band * 8 + 0] = t_start;
-        g_grid_prof[band * 8 + 1] = __builtin_amdgcn_s_memtime();
-        g_grid_prof[band * 8 + 2] = n_wait;
-        g_grid_prof[band * 8 + 3] = c_wait;
-    }
-#endif
+}
+
+// right-hand side into step order: bp[p] = rhs[idx ? idx[row] : row] (0 on idle lanes)
+__global__ void levels_gather_kernel(int64_t np, const uint32_t *__restrict__ rc, const double *__restrict__ rhs,
+                                     const int32_t *__restrict__ idx, double *__restrict__ bp) {
+    const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= np) return;
+    const uint32_t row = rc[p] & kLevelIdle;
+    bp[p] = row == kLevelIdle ? 0.0 : rhs[idx ? idx[row] : row];
 }
 
 // x = sentinel on the rows the grid schedule publishes — lines y with y mod 64 >= 64 - maxyd, the ones
@@ -1667,6 +1791,7 @@ static unsigned grid_fill_blocks(const TriFactor &T) {
 // the output of one factor before its solve: the sentinel where the schedule's waits read it (the grid
 // schedule: only its published lines; every other schedule: every row)
 static int fill_factor_output(const TriFactor &T, int64_t n, double *x, hipStream_t s) {
+    if (T.schedule == kSchedLevel) return PSK_OK;   // nothing polls: one workgroup, dependencies through LDS
     if (T.schedule == kSchedGrid) {
         if (T.grid_pe == 0 || T.grid_maxyd == 0) return PSK_OK;   // no band waits on another
         hipLaunchKernelGGL(grid_fill_published_kernel, dim3(grid_fill_blocks(T)), dim3(kBlock), 0, s, n, T.grid_w,
@@ -1696,6 +1821,24 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         const int32_t *ord = T.order;
         void *args[] = {&nn, &rp, &ci, &va, &dg, &rhs, &rhs_idx, &x, &err, &ord};
         PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(kLdsThreads), args, (size_t)n * sizeof(double), s));
+        return PSK_OK;
+    }
+    if (T.schedule == kSchedLevel) {
+        int64_t ns = T.lv_steps;
+        const int64_t np = ns * T.lv_W;
+        hipLaunchKernelGGL(levels_gather_kernel, dim3((unsigned)((np + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, np,
+                           T.lv_rc, rhs, rhs_idx, T.lv_b);
+        PSK_HIP(hipGetLastError());
+        const void *k = T.lv_KM == 4    ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<4, kLevelD>)
+                        : T.lv_KM == 8  ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<8, kLevelD>)
+                        : T.lv_KM == 12 ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<12, kLevelD>)
+                                        : reinterpret_cast<const void *>(&sptrsv_levels_kernel<16, kLevelD>);
+        int R = T.lv_R, unit = T.diag ? 0 : 1;
+        const uint32_t *lrc = T.lv_rc;
+        const uint64_t *lsl = T.lv_sl;
+        const double *lcf = T.lv_cf, *ldg = T.lv_dg, *lb = T.lv_b;
+        void *args[] = {&ns, &R, &nn, &unit, &lrc, &lsl, &lcf, &ldg, &lb, &x};
+        PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(T.lv_W), args, (size_t)(R + 1) * sizeof(double), s));
         return PSK_OK;
     }
     if (T.schedule == kSchedPart) {
@@ -1824,7 +1967,10 @@ static int ilu_apply_impl(const psk_prec *M, const double *v, double *out, bool 
     const unsigned fb = (unsigned)((n + kBlock - 1) / kBlock);
     double *y = M->work, *z = M->work + n;
     const int nbuf = (M->lo.present ? 1 : 0) + (M->up.present ? 1 : 0);
-    const bool grid_any = (M->lo.present && M->lo.schedule == kSchedGrid) || (M->up.present && M->up.schedule == kSchedGrid);
+    // factors whose schedule fills (or needs) no sentinel of its own: the grid schedule's published lines only,
+    // none for the levels schedule
+    auto own_fill = [](const TriFactor &T) { return T.schedule == kSchedGrid || T.schedule == kSchedLevel; };
+    const bool grid_any = (M->lo.present && own_fill(M->lo)) || (M->up.present && own_fill(M->up));
     if (nbuf > 0 && !grid_any) {
         hipLaunchKernelGGL(fill_sentinel_kernel, dim3((unsigned)((nbuf * n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
                            s, nbuf * n, y);   // y and z are contiguous
@@ -2040,7 +2186,7 @@ namespace psk {
 void TriFactor::release() {
     void *ptrs[] = {rowptr, colidx, vals,   diag,    order,     rec_row,  rec_end,  rec_c,  rec_v,   rec_d,
                     gd_code, gd_coef, gd_diag, gd_idx, gd_dict, part_seg, part_rp, part_code, part_row, part_va,
-                    grid_flag, sched};
+                    grid_flag, sched, lv_rc,    lv_sl,    lv_cf,  lv_dg,   lv_b};
     for (void *p : ptrs)
         if (p) (void)hipFree(p);
     *this = TriFactor();
@@ -2109,6 +2255,8 @@ void build_grid_dict(const unsigned char *gb, int64_t nsteps, int64_t SB, int K,
 // FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
 constexpr double kHopUs = 0.36, kRowUs = 0.61, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
 constexpr double kLdsLevelUs = 0.15, kLdsBytesPerUs = 40e3;   // LDS schedule (provisional)
+// levels schedule (provisional until measured): a step's barrier + LDS round trip, one CU's record stream
+constexpr double kLevelStepUs = 0.30, kLevelBytesPerUs = 60e3;
 constexpr double kNarrowLevelUs = 0.8;    // narrow band local level (FD 8192^2 Gauss-Seidel: 12.6 ms / 16128 levels)
 
 struct HostFactor {
@@ -2645,6 +2793,83 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         }
         if (T.grid_dict_n > 0) std::vector<double>().swap(gcoef);   // the records are not uploaded
     }
+    // levels schedule (sptrsv_levels_kernel): one workgroup of W = 64..256 lanes, one level (or a W-row
+    // piece of one) per step, x in an LDS ring. Eligible: at most 16 entries per row, every dependency
+    // within the ring (a slot is rewritten only in a step after its last reader), records < 4 GB.
+    // PSK_TRISOLVE_LEVELS=0 never plans it, =1 builds it and selects it whenever eligible.
+    std::vector<uint32_t> lrc;
+    std::vector<uint64_t> lsl;
+    std::vector<double> lcf, ldg;
+    bool lv_forced = false;
+    {
+        const char *le = std::getenv("PSK_TRISOLVE_LEVELS");
+        const bool force = le && std::atoi(le) == 1, off = le && std::atoi(le) == 0;
+        if (!off && n > 0 && n < (int64_t)kLevelIdle && kmax <= kLevelMaxK) {
+            std::vector<int64_t> lw((size_t)nlev, 0);
+            for (int64_t i = 0; i < n; ++i) lw[(size_t)lev[(size_t)i]]++;
+            int64_t wmax = 1;
+            for (int64_t w : lw) wmax = std::max(wmax, w);
+            const int W = (int)std::min<int64_t>(kLevelMaxW, (wmax + 63) / 64 * 64);
+            // positions: level by level in `order`, each level padded to whole steps of W
+            std::vector<int64_t> pos((size_t)n);
+            int64_t steps = 0;
+            {
+                int64_t q = 0;
+                for (int64_t L = 0; L < nlev; ++L) {
+                    const int64_t cntL = lw[(size_t)L], st = (cntL + W - 1) / W;
+                    for (int64_t j = 0; j < cntL; ++j) pos[(size_t)order[(size_t)(q + j)]] = steps * W + j;
+                    q += cntL;
+                    steps += st;
+                }
+            }
+            steps = (steps + kLevelD - 1) / kLevelD * kLevelD;   // the kernel's loop: whole groups of D steps
+            int64_t need = W;
+            for (int64_t i = 0; i < n; ++i) {
+                const int64_t si = pos[(size_t)i] / W;
+                for (int32_t j = F.rp[(size_t)i]; j < F.rp[(size_t)i + 1]; ++j)
+                    need = std::max(need, (si + 1) * W - pos[(size_t)F.ci[(size_t)j]]);
+            }
+            int64_t R = 64;
+            while (R < need) R <<= 1;
+            const int KM = kmax <= 4 ? 4 : kmax <= 8 ? 8 : kmax <= 12 ? 12 : 16;
+            const bool fits = R <= kLevelMaxR && steps * W * KM * 8 < ((int64_t)1 << 32);
+            if (fits) {
+                T.est_level_us = (double)steps * kLevelStepUs +
+                                 (double)steps * W * (20.0 + 10.0 * KM) / kLevelBytesPerUs;
+                const double cur = T.schedule == kSchedBand ? T.est_band_us
+                                   : T.schedule == kSchedLds  ? T.est_lds_us
+                                   : T.schedule == kSchedGrid ? T.est_grid_us
+                                                              : T.est_syncfree_us;
+                if (force || T.est_level_us < cur) {
+                    lv_forced = force;
+                    T.schedule = kSchedLevel;
+                    T.lv_steps = steps;
+                    T.lv_W = W;
+                    T.lv_R = (int)R;
+                    T.lv_KM = KM;
+                    const size_t NP = (size_t)steps * W;
+                    lrc.assign(NP, kLevelIdle);
+                    lsl.assign(NP * (KM / 4), (uint64_t)R * 0x0001000100010001ull);
+                    lcf.assign(NP * KM, -0.0);
+                    ldg.assign(NP, 1.0);
+                    for (int64_t i = 0; i < n; ++i) {
+                        const int64_t p = pos[(size_t)i], st = p / W, t = p % W;
+                        const int32_t a = F.rp[(size_t)i], e = F.rp[(size_t)i + 1];
+                        lrc[(size_t)p] = (uint32_t)i | ((uint32_t)(e - a) << 27);
+                        for (int32_t j = a; j < e; ++j) {
+                            const int k = j - a;
+                            const uint64_t slot = (uint64_t)(pos[(size_t)F.ci[(size_t)j]] & (R - 1));
+                            uint64_t &w = lsl[((size_t)st * (KM / 4) + (size_t)(k / 4)) * W + (size_t)t];
+                            w = (w & ~((uint64_t)0xFFFF << (16 * (k % 4)))) | (slot << (16 * (k % 4)));
+                            // coefficient pairs (2k2, 2k2 + 1) of lane t: one 16-byte load
+                            lcf[(((size_t)st * (KM / 2) + (size_t)(k / 2)) * W + (size_t)t) * 2 + (size_t)(k % 2)] = ova[(size_t)j];
+                        }
+                        if (!dg.empty()) ldg[(size_t)p] = dg[(size_t)i];
+                    }
+                }
+            }
+        }
+    }
     // partitioned schedule: planned for factors too large for one CU and not solved by the grid
     // schedule (PSK_TRISOLVE_PART=0 disables it, =1 builds it and selects it whatever the estimate)
     std::vector<int64_t> pseg;
@@ -2659,15 +2884,16 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         }();
         const int P = nparts > 0 ? nparts : c->num_cus;
         const int64_t strip = (n + P - 1) / std::max(1, P);
-        if (!off && n > kLdsMaxRows && n >= (int64_t)P * kPartWaves &&
+        if (!off && !lv_forced && n > kLdsMaxRows && n >= (int64_t)P * kPartWaves &&
             (force || (T.schedule != kSchedGrid && strip <= kPartMaxStrip))) {
             PartPlan pp;
             plan_part(F, nat, P, pp);
             T.est_part_us = pp.est;
-            const double cur = T.schedule == kSchedBand ? T.est_band_us
-                               : T.schedule == kSchedLds  ? T.est_lds_us
-                               : T.schedule == kSchedGrid ? T.est_grid_us
-                                                          : T.est_syncfree_us;
+            const double cur = T.schedule == kSchedBand  ? T.est_band_us
+                               : T.schedule == kSchedLds   ? T.est_lds_us
+                               : T.schedule == kSchedGrid  ? T.est_grid_us
+                               : T.schedule == kSchedLevel ? T.est_level_us
+                                                           : T.est_syncfree_us;
             if (force || pp.est < cur) {
                 T.schedule = kSchedPart;
                 T.part_P = pp.P;
@@ -2698,9 +2924,9 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (const char *ve = std::getenv("PSK_TRISOLVE_VERBOSE"))   // development: the cost model's view
         if (std::atoi(ve))
             std::fprintf(stderr, "psk trisolve %s n=%lld levels=%lld est_us syncfree=%.0f band=%.0f lds=%.0f grid=%.0f "
-                                 "part=%.0f -> schedule %d\n",
+                                 "part=%.0f levels=%.0f -> schedule %d\n",
                          upper ? "U" : "L", (long long)n, (long long)nlev, T.est_syncfree_us, T.est_band_us,
-                         T.est_lds_us, T.est_grid_us, T.est_part_us, T.schedule);
+                         T.est_lds_us, T.est_grid_us, T.est_part_us, T.est_level_us, T.schedule);
     T.present = true;
     T.upper = upper;
     T.nnz = (int64_t)F.ci.size();
@@ -2765,6 +2991,11 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (rc == PSK_OK) rc = upload(&T.part_code, pcode);
     if (rc == PSK_OK) rc = upload(&T.part_row, prow);
     if (rc == PSK_OK) rc = upload(&T.part_va, pva);
+    if (rc == PSK_OK) rc = upload(&T.lv_rc, lrc);
+    if (rc == PSK_OK) rc = upload(&T.lv_sl, lsl);
+    if (rc == PSK_OK) rc = upload(&T.lv_cf, lcf);
+    if (rc == PSK_OK) rc = upload(&T.lv_dg, ldg);
+    if (rc == PSK_OK) rc = upload(&T.lv_b, std::vector<double>(lrc.size(), 0.0));
     return rc;
 }
 
@@ -2871,8 +3102,11 @@ extern "C" int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t se
     if (set == kSchedPart && T.part_P == 0)
         return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: partitioned layout not built for this factor "
                                          "(built when chosen, or with PSK_TRISOLVE_PART=1 at creation)");
-    if (set >= kSchedSyncFree && set <= kSchedPart) T.schedule = set;
-    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1, 0, 1, 2, 3 or 4");
+    if (set == kSchedLevel && T.lv_steps == 0)
+        return fail(PSK_ERR_UNSUPPORTED, "psk_prec_trisolve_schedule: levels layout not built for this factor "
+                                         "(built when chosen, or with PSK_TRISOLVE_LEVELS=1 at creation)");
+    if (set >= kSchedSyncFree && set <= kSchedLevel) T.schedule = set;
+    else if (set != -1) return fail(PSK_ERR_ARG, "psk_prec_trisolve_schedule: set must be -1 or 0..5");
     if (schedule) *schedule = T.schedule;
     if (blocks) *blocks = T.band_nblocks;
     if (ring_words) *ring_words = T.ring_words;

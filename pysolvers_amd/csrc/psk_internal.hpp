@@ -236,7 +236,8 @@ struct AmgHierarchy;
 //    (sptrsv_part_kernel).
 // `schedule` picks one (kSchedSyncFree / kSchedBand / kSchedLds / kSchedGrid / kSchedPart), chosen by host
 // cost models.
-enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4 };
+enum TriSchedule : int { kSchedSyncFree = 0, kSchedBand = 1, kSchedLds = 2, kSchedGrid = 3, kSchedPart = 4,
+                         kSchedLevel = 5 };
 constexpr int kGridMaxPE = 8;   // distinct dependency patterns reaching into the band above
 struct GridExt {
     int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
@@ -279,7 +280,19 @@ struct TriFactor {
     int32_t *part_rp = nullptr, *part_code = nullptr, *part_row = nullptr;
     double *part_va = nullptr;
     int part_P = 0;
+    // levels layout (round 5, sptrsv_levels_kernel): ONE workgroup of lv_W lanes, a dependency level (or a
+    // lv_W-row piece of one) per step behind a barrier, x in an LDS ring of lv_R slots indexed by step
+    // position. Per step s and lane t (field-major, coalesced): lv_rc = row | (entries << 27) (0x07FFFFFF:
+    // idle lane), lv_sl = ring slots of the entries, two uint16 per word (padding: slot lv_R, which holds
+    // 0.0), lv_cf = coefficients in stored order (padding -0.0), lv_dg = diagonal (nullptr: unit),
+    // lv_b = the right-hand side gathered into step order before each solve
+    uint32_t *lv_rc = nullptr;
+    uint64_t *lv_sl = nullptr;
+    double *lv_cf = nullptr, *lv_dg = nullptr, *lv_b = nullptr;
+    int64_t lv_steps = 0;
+    int lv_W = 0, lv_R = 0, lv_KM = 0;
     double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0;
+    double est_level_us = -1.0;
     void release();
 };
 }  // namespace psk

@@ -476,3 +476,79 @@ def test_amg_dense_vs_lu_coarse(psk):
     Ml = psk.AMG(numIters=2, numLevels=4, coarse="lu").form(A)
     assert Md.coarse_kind == "dense" and Ml.coarse_kind == "lu"
     assert _rel(Md.applyRight(v), Ml.applyRight(v)) <= 1e-12
+
+
+# ---------------------------------------------------------------------------------------------
+# levels schedule (round 5, ilu.hip sptrsv_levels_kernel): one workgroup, a dependency level per step
+# behind a barrier, x in an LDS ring. Bars: bit-identical to the band and grid schedules (the same per-row
+# arithmetic: fma over the stored entries in stored order from 0.0, then (b - acc) / d), 1e-12 against
+# scipy on random chains with permutations, and the SA level-1 Gauss-Seidel factor it is planned for.
+
+@pytest.mark.parametrize("m", [96, 256])
+def test_levels_schedule_matches_band_and_grid_bitwise(psk, monkeypatch, m):
+    from oracle import fdlap
+    from pysolvers_amd.Linear import TriangularSolveChain
+    monkeypatch.setenv("PSK_TRISOLVE_LEVELS", "1")   # build the levels layout at creation
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    U = sp.triu(A).tocsr()
+    v = np.random.default_rng(m).standard_normal(A.shape[0])
+    M = TriangularSolveChain(A.shape[0], U=U)
+    assert M.schedule("U")["schedule"] == "levels"
+    y = M.apply(v)
+    assert _rel(y, spla.spsolve_triangular(U, v, lower=False)) <= 1e-12
+    for sched in ("band", "grid"):
+        M.schedule("U", set=sched)
+        assert np.array_equal(M.apply(v).view(np.uint64), y.view(np.uint64)), sched
+    M.schedule("U", set="levels")
+    assert np.array_equal(M.apply(v).view(np.uint64), y.view(np.uint64))   # run to run
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (37, 1), (2000, 2), (20000, 5)])
+def test_levels_schedule_random_chain(psk, monkeypatch, n, seed):
+    """Random unit / non-unit factors with gather permutations (the ILU chain's shape), rows of 0..16
+    entries, forced onto the levels schedule."""
+    from pysolvers_amd.Linear import TriangularSolveChain
+    monkeypatch.setenv("PSK_TRISOLVE_LEVELS", "1")
+    rng = np.random.default_rng(seed)
+    dens = min(1.0, 4.0 / max(n, 1))
+    Lo = sp.tril(sp.random(n, n, density=dens, random_state=rng), k=-1).tocsr() * 0.1
+    Up = sp.triu(sp.random(n, n, density=dens, random_state=rng), k=1).tocsr() * 0.1
+    dl, du = 1.0 + rng.random(n), 1.0 + rng.random(n)
+    gin, gout = rng.permutation(n), rng.permutation(n)
+    v = rng.standard_normal(n)
+    for l_unit, u_unit in ((True, False), (False, True), (False, False)):
+        L = (Lo + sp.diags(dl)).tocsr()
+        U = (Up + sp.diags(du)).tocsr()
+        Ld = (Lo + sp.eye(n)).tocsr() if l_unit else L
+        Ud = (Up + sp.eye(n)).tocsr() if u_unit else U
+        ref = spla.spsolve_triangular(Ud, spla.spsolve_triangular(Ld, v[gin], lower=True), lower=False)[gout]
+        M = TriangularSolveChain(n, L=L, l_unit=l_unit, U=U, u_unit=u_unit, gather_in=gin, gather_out=gout)
+        levels_used = [M.schedule(f)["schedule"] == "levels" for f in ("L", "U")]
+        assert _rel(M.apply(v), ref) <= 1e-12
+        if n <= 2000:   # (larger random factors may reach further back than the 16384-slot ring: not eligible)
+            assert all(levels_used)
+
+
+def test_levels_schedule_sa_level1(psk, monkeypatch):
+    """Level 1 of the SA hierarchy of -FD 1024^2 (5 levels, 2167 rows): the Gauss-Seidel factor triu(A_1)
+    is the kind the levels schedule is planned for (at -FD 8192^2: 131k rows, 1706 levels; narrow levels,
+    dependencies a bounded number of positions back); forced, against the sync-free schedule (lane-tree
+    row sums: not bitwise) and scipy."""
+    from pysolvers_amd.Linear import TriangularSolveChain
+    monkeypatch.setenv("PSK_TRISOLVE_LEVELS", "1")
+    A1 = _sa_level(1024, 5, 1)
+    U = sp.triu(A1).tocsr()
+    v = np.random.default_rng(3).standard_normal(A1.shape[0])
+    M = TriangularSolveChain(A1.shape[0], U=U)
+    assert M.schedule("U")["schedule"] == "levels"
+    y = M.apply(v)
+    assert _rel(y, spla.spsolve_triangular(U, v, lower=False)) <= 1e-12
+    M.schedule("U", set="syncfree")
+    assert _rel(M.apply(v), y) <= 1e-13
+
+
+def _sa_level(m, L, k):
+    from oracle import fdlap
+    from pysolvers_amd.Linear.SmoothedAggregation import SmoothedAggregationMLHierarchy
+    A = -fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    return sp.csr_matrix(SmoothedAggregationMLHierarchy(sp.csr_matrix(A), numLevels=L).matrix(k))

@@ -34,7 +34,7 @@ def child(path, reps):
     out = psk.DeviceVector(A.shape[0])
     res = {"n": A.shape[0], "levels": M.device_info()["levels_u"], "planned": M.schedule("U")["schedule"]}
     ref = None
-    for sched in ("syncfree", "part", "band"):
+    for sched in ("syncfree", "part", "band", "levels"):
         try:
             M.schedule("U", set=sched)
         except N.PskError:
@@ -61,6 +61,8 @@ def main():
     ap.add_argument("--strips", default="256,64,32,16")
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--child", default="")
+    ap.add_argument("--use-levels", type=int, default=0,
+                    help="1: PSK_TRISOLVE_LEVELS=1 (the levels schedule) instead of the part sweep")
     a = ap.parse_args()
     if a.child:
         child(a.child, a.reps)
@@ -73,8 +75,9 @@ def main():
         A = -fdlap.fd_laplacian_2d(-1.0, 1.0, a.side)
         Ak = sp.csr_matrix(SmoothedAggregationMLHierarchy(sp.csr_matrix(A), numLevels=a.levels).matrix(a.level))
         np.savez(path, data=Ak.data, indices=Ak.indices, indptr=Ak.indptr, shape=np.array(Ak.shape))
-    for P in a.strips.split(","):
-        env = dict(os.environ, PSK_TRISOLVE_PART="1", PSK_PART_STRIPS=P)
+    for P in (["0"] if a.use_levels else a.strips.split(",")):
+        env = dict(os.environ, PSK_TRISOLVE_LEVELS="1") if a.use_levels else \
+            dict(os.environ, PSK_TRISOLVE_PART="1", PSK_PART_STRIPS=P)
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", path, "--reps", str(a.reps)],
                            env=env, capture_output=True, text=True, timeout=300)
         line = p.stdout.strip().splitlines()[-1] if p.returncode == 0 and p.stdout.strip() else None
