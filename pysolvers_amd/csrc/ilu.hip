@@ -1367,6 +1367,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
         __syncthreads();
     #ifdef PSK_GRID_PROF
         const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+        const unsigned long long rt_start = __builtin_amdgcn_s_memrealtime();
         unsigned long long n_wait = 0, c_wait = 0;
     #endif
         if (tid >= kGridLanes) {
@@ -1584,6 +1585,10 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
             g_grid_prof[band * 8 + 1] = __builtin_amdgcn_s_memtime();
             g_grid_prof[band * 8 + 2] = n_wait;
             g_grid_prof[band * 8 + 3] = c_wait;
+            g_grid_prof[band * 8 + 4] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;   // XCD
+            g_grid_prof[band * 8 + 5] = blockIdx.x;
+            g_grid_prof[band * 8 + 6] = rt_start;                                       // 100 MHz, device-wide
+            g_grid_prof[band * 8 + 7] = __builtin_amdgcn_s_memrealtime();
         }
     #endif
     };

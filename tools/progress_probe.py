@@ -102,10 +102,18 @@ def main():
         xcc = (N.I32 * 8)()
         N.check(N.lib.psk_lab_occupy_xcc(xcc), "occupy_xcc")
         y = out.numpy()
-        print(json.dumps({"phase": "occupied", "wgs": wgs, "xcc": list(xcc), "ms": ms, "err": err,
-                          "timed_out": to.value, "workers": workers(),
-                          "same_bits": None if y is None else bool(np.array_equal(y.view(np.uint64), ref.view(np.uint64)))}),
-              flush=True)
+        rec = {"phase": "occupied", "wgs": wgs, "xcc": list(xcc), "ms": ms, "err": err, "timed_out": to.value,
+               "workers": workers(),
+               "same_bits": None if y is None else bool(np.array_equal(y.view(np.uint64), ref.view(np.uint64)))}
+        if a.sched == "grid" and hasattr(N.lib, "psk_grid_prof_read"):   # a -DPSK_GRID_PROF lab build
+            nb = (a.m + 63) // 64
+            buf = (ctypes.c_ulonglong * (8 * nb))()
+            N.lib.psk_grid_prof_read(buf, nb)
+            b = np.frombuffer(buf, dtype=np.uint64).reshape(nb, 8).astype(np.int64)
+            t0 = b[:, 6].min()
+            rec["bands"] = [{"band": i, "xcd": int(b[i, 4]), "wg": int(b[i, 5]), "start_us": (b[i, 6] - t0) / 100.0,
+                             "end_us": (b[i, 7] - t0) / 100.0} for i in range(nb)]
+        print(json.dumps(rec), flush=True)
 
 
 if __name__ == "__main__":
