@@ -41,6 +41,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <queue>
 #include <vector>
 
 namespace psk {
@@ -1602,34 +1603,34 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
     }
 }
 
-// ---- levels schedule (round 5): one workgroup, level-synchronous, x in an LDS ring -------------------
-// For factors with few rows per dependency level and dependencies a bounded number of solve positions
-// back (the SA level-1 operator of -FD 8192^2: 131k rows, 1706 levels of <= 109 rows, every dependency
-// <= 4294 positions back): step s solves lane t's row of one level (a level wider than the workgroup takes
-// several steps), reading its dependencies from the ring (slot = solve position mod R, checked on the host:
-// a slot is rewritten only in a step after its last reader), then a barrier. A hop between levels is an
-// LDS round trip plus a barrier instead of a device-scope publication seen by a polling load (sync-free,
-// ~1 us per level). Records are field-major per step, loaded D steps ahead into registers; the barrier
-// waits for LDS only (lgkmcnt), so those loads stay in flight across it. Per-row arithmetic: fma over the
-// stored entries in stored order from 0.0, padding entries (-0.0 x 0.0) add exactly nothing, then
-// (b - acc) / d: the band and grid kernels' bits.
-constexpr uint32_t kLevelIdle = 0x07FFFFFFu;
+// ---- levels schedule (round 5): one workgroup, level-synchronous, x in LDS slots ---------------------------
+// For factors with few rows per dependency level (the SA level-1 operator of -FD 8192^2: 131k rows, 1706
+// levels of <= 109 rows): step s solves lane t's row of one level (a level wider than the workgroup takes
+// several steps), reading its dependencies from LDS, then a barrier. A hop between levels is an LDS round
+// trip plus a barrier instead of a device-scope publication seen by a polling load (sync-free, ~1 us per
+// level). Each value lives in an LDS slot the host assigned it (interval allocation: a slot is reused only
+// in a step after its last reader), so dependencies any number of levels back are fine as long as the
+// values alive at once fit the LDS. Records are field-major per step, loaded D steps ahead into registers;
+// the barrier waits for LDS only (lgkmcnt), so those loads stay in flight across it. Per-row arithmetic:
+// fma over the stored entries in stored order from 0.0, padding entries (-0.0 x 0.0) add exactly nothing,
+// then (b - acc) / d: the band and grid kernels' bits.
+constexpr uint32_t kLevelIdle = 0xFFFFFFFFu;   // row field of an idle lane
 constexpr int kLevelMaxK = 16, kLevelMaxW = 256, kLevelD = 4;
-constexpr int64_t kLevelMaxR = 16384;   // ring slots: 128 KiB of LDS (+ the padding slot)
+constexpr int64_t kLevelMaxSlots = 18432;     // live values + the zero and trash slots: <= 144 KiB of LDS
 template <int KM, int D>
 __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int R, int64_t n, int unit,
-                                                            const uint32_t *__restrict__ rc,
+                                                            const uint64_t *__restrict__ rc,
                                                             const uint64_t *__restrict__ sl,
                                                             const double *__restrict__ cf,
                                                             const double *__restrict__ dg,
                                                             const double *__restrict__ bp, double *__restrict__ x) {
     static_assert(KM % 4 == 0, "slots are loaded four per 8-byte word, coefficients two per 16-byte load");
-    extern __shared__ double lv_ring[];   // R + 1 slots; slot R stays 0.0 (padding entries)
+    extern __shared__ double lv_ring[];   // R + 2 slots: R live values, R = 0.0 (padding), R + 1 = trash
     const int t = threadIdx.x, W = blockDim.x;
-    for (int i = t; i <= R; i += W) lv_ring[i] = 0.0;
+    for (int i = t; i <= R + 1; i += W) lv_ring[i] = 0.0;
     __syncthreads();
     struct Rec {
-        uint32_t rc;
+        uint64_t rc;
         uint64_t sw[KM / 4];
         double c[KM];
         double d, b;
@@ -1639,8 +1640,8 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
     // loaded count would make the wave wait for that load at once; a predicated load becomes a branch,
     // after which the compiler waits for ALL outstanding loads): entries past a row's count are stored
     // padding (slot R, coefficient -0.0), the diagonal is stored as 1.0 for a unit factor
-    const __amdgpu_buffer_rsrc_t rrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint32_t *>(rc), (short)0,
-                                                                         (int)(uint32_t)(nsteps * W * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(rc), (short)0,
+                                                                         (int)(uint32_t)(nsteps * W * 8), 0x00020000);
     const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t *>(sl), (short)0,
                                                                          (int)(uint32_t)(nsteps * W * (KM / 4) * 8),
                                                                          0x00020000);
@@ -1649,7 +1650,7 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
     auto fetch = [&](int64_t s, Rec &r) {
         const uint32_t sc = (uint32_t)(s < nsteps ? s : nsteps - 1);   // past the end: the last step (unused)
         const uint32_t p = sc * (uint32_t)W + (uint32_t)t;
-        r.rc = __builtin_amdgcn_raw_buffer_load_b32(rrc, p * 4, 0, 0);
+        r.rc = __builtin_bit_cast(uint64_t, __builtin_amdgcn_raw_buffer_load_b64(rrc, p * 8, 0, 0));
         r.d = grid_bload(rdg, p * 8);
         r.b = grid_bload(rbp, p * 8);
 #pragma unroll
@@ -1670,7 +1671,7 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
     Rec buf[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-        buf[i].rc = kLevelIdle;
+        buf[i].rc = (uint64_t)kLevelIdle | ((uint64_t)(R + 1) << 40);
 #pragma unroll
         for (int k4 = 0; k4 < KM / 4; ++k4) buf[i].sw[k4] = 0;
 #pragma unroll
@@ -1678,7 +1679,6 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
         buf[i].d = 1.0;
         buf[i].b = 0.0;
     }
-    uint32_t rbase = (uint32_t)((int64_t)R - (int64_t)D * W % R) & (uint32_t)(R - 1);   // (s * W) mod R at s = -D
     for (int64_t s0 = -D; s0 < nsteps; s0 += D) {   // nsteps: a multiple of D (the host pads idle steps)
 #pragma unroll
         for (int i = 0; i < D; ++i) {
@@ -1691,11 +1691,10 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
             }
             double r = buf[i].b - acc;
             if (!unit) r = r / buf[i].d;   // (uniform)
-            lv_ring[(rbase + (uint32_t)t) & (uint32_t)(R - 1)] = r;
-            const uint32_t row = buf[i].rc & kLevelIdle;
+            lv_ring[(uint32_t)(buf[i].rc >> 40) & 0xFFFFu] = r;
+            const uint32_t row = (uint32_t)buf[i].rc;
             grid_bstore<0>(rx, row != kLevelIdle ? row * 8u : kBufOOB, r);   // idle lanes: out of range, dropped
             fetch(s + D, buf[i]);
-            rbase = (rbase + (uint32_t)W) & (uint32_t)(R - 1);
             // the step's ring writes before the next step's reads (LDS-only fences: the prefetch loads stay
             // in flight across the barrier)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
@@ -1706,11 +1705,11 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
 }
 
 // right-hand side into step order: bp[p] = rhs[idx ? idx[row] : row] (0 on idle lanes)
-__global__ void levels_gather_kernel(int64_t np, const uint32_t *__restrict__ rc, const double *__restrict__ rhs,
+__global__ void levels_gather_kernel(int64_t np, const uint64_t *__restrict__ rc, const double *__restrict__ rhs,
                                      const int32_t *__restrict__ idx, double *__restrict__ bp) {
     const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= np) return;
-    const uint32_t row = rc[p] & kLevelIdle;
+    const uint32_t row = (uint32_t)rc[p];
     bp[p] = row == kLevelIdle ? 0.0 : rhs[idx ? idx[row] : row];
 }
 
@@ -1839,11 +1838,11 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
                         : T.lv_KM == 12 ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<12, kLevelD>)
                                         : reinterpret_cast<const void *>(&sptrsv_levels_kernel<16, kLevelD>);
         int R = T.lv_R, unit = T.diag ? 0 : 1;
-        const uint32_t *lrc = T.lv_rc;
+        const uint64_t *lrc = T.lv_rc;
         const uint64_t *lsl = T.lv_sl;
         const double *lcf = T.lv_cf, *ldg = T.lv_dg, *lb = T.lv_b;
         void *args[] = {&ns, &R, &nn, &unit, &lrc, &lsl, &lcf, &ldg, &lb, &x};
-        PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(T.lv_W), args, (size_t)(R + 1) * sizeof(double), s));
+        PSK_HIP(hipLaunchKernel(k, dim3(1), dim3(T.lv_W), args, (size_t)(R + 2) * sizeof(double), s));
         return PSK_OK;
     }
     if (T.schedule == kSchedPart) {
@@ -1891,7 +1890,9 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         uint32_t *sch = T.sched;
         void *args[] = {&nn, &w, &H, &sg, &gph, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext, &gi,
                         &gdd, &nd, &flag, &nogate, &sch};
-        const unsigned nb = (unsigned)((H + kGridLanes - 1) / kGridLanes);
+        // one workgroup per band, at most one per CU (a workgroup holds ~147 KiB of LDS); workgroups draw bands
+        // until they run out, so fewer workgroups than bands still solve every band
+        const unsigned nb = (unsigned)std::min<int64_t>((H + kGridLanes - 1) / kGridLanes, c->num_cus);
         const size_t lds = grid_lds_bytes(T.grid_K, T.grid_dict_n);
         PSK_HIP(hipLaunchKernel(k, dim3(nb), dim3(2 * kGridLanes), args, lds, s));
         if (dict) {   // conditional IEEE re-solve (div_markstein): no-ops unless a step was out of range
@@ -1904,7 +1905,9 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
             }
             void *fargs[] = {&nn, &w, &H, &sg, &gph, &goff, &sfull, &upper, &pe_, &myd, &unit, &rhs, &x, &err, &gr, &ext,
                              &gi, &gdd, &nd, &noflag, &gate, &sch};
-            PSK_HIP(hipLaunchKernel(kf, dim3(nb), dim3(2 * kGridLanes), fargs, lds, s));
+            // one workgroup: a no-op unless the gate is set (then it solves every band itself, a rare path), and
+            // a launch that needs no more than one free CU to complete
+            PSK_HIP(hipLaunchKernel(kf, dim3(1), dim3(2 * kGridLanes), fargs, lds, s));
             hipLaunchKernelGGL(grid_flag_reset_kernel, dim3(1), dim3(1), 0, s, T.grid_flag);
             PSK_HIP(hipGetLastError());
         }
@@ -2799,11 +2802,10 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
         if (T.grid_dict_n > 0) std::vector<double>().swap(gcoef);   // the records are not uploaded
     }
     // levels schedule (sptrsv_levels_kernel): one workgroup of W = 64..256 lanes, one level (or a W-row
-    // piece of one) per step, x in an LDS ring. Eligible: at most 16 entries per row, every dependency
-    // within the ring (a slot is rewritten only in a step after its last reader), records < 4 GB.
+    // piece of one) per step, x in host-assigned LDS slots. Eligible: at most 16 entries per row, the values
+    // alive at once (written, a reader still to come) within kLevelMaxSlots, records < 4 GB.
     // PSK_TRISOLVE_LEVELS=0 never plans it, =1 builds it and selects it whenever eligible.
-    std::vector<uint32_t> lrc;
-    std::vector<uint64_t> lsl;
+    std::vector<uint64_t> lrc, lsl;
     std::vector<double> lcf, ldg;
     bool lv_forced = false;
     {
@@ -2828,19 +2830,44 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
                 }
             }
             steps = (steps + kLevelD - 1) / kLevelD * kLevelD;   // the kernel's loop: whole groups of D steps
-            int64_t need = W;
-            for (int64_t i = 0; i < n; ++i) {
-                const int64_t si = pos[(size_t)i] / W;
+            // slot of every value: the step of its last reader, then greedy interval allocation in step order
+            std::vector<int64_t> last((size_t)n, -1);
+            for (int64_t i = 0; i < n; ++i)
                 for (int32_t j = F.rp[(size_t)i]; j < F.rp[(size_t)i + 1]; ++j)
-                    need = std::max(need, (si + 1) * W - pos[(size_t)F.ci[(size_t)j]]);
+                    last[(size_t)F.ci[(size_t)j]] = std::max(last[(size_t)F.ci[(size_t)j]], pos[(size_t)i] / W);
+            std::vector<int32_t> by_pos((size_t)steps * W, -1), slot((size_t)n, -1);
+            for (int64_t i = 0; i < n; ++i) by_pos[(size_t)pos[(size_t)i]] = (int32_t)i;
+            std::priority_queue<std::pair<int64_t, int32_t>, std::vector<std::pair<int64_t, int32_t>>,
+                                std::greater<std::pair<int64_t, int32_t>>> live;   // (last reader step, slot)
+            std::vector<int32_t> freed;
+            int32_t nslots = 0;
+            bool fits = true;
+            for (int64_t st = 0; st < steps && fits; ++st) {
+                while (!live.empty() && live.top().first < st) {   // its last reader ran in an earlier step
+                    freed.push_back(live.top().second);
+                    live.pop();
+                }
+                for (int64_t t = 0; t < W; ++t) {
+                    const int32_t i = by_pos[(size_t)(st * W + t)];
+                    if (i < 0 || last[(size_t)i] < 0) continue;   // idle lane / nobody reads it: the trash slot
+                    int32_t sl;
+                    if (!freed.empty()) {
+                        sl = freed.back();
+                        freed.pop_back();
+                    } else {
+                        sl = nslots++;
+                    }
+                    slot[(size_t)i] = sl;
+                    live.push({last[(size_t)i], sl});
+                }
+                fits = nslots + 2 <= kLevelMaxSlots;
             }
-            int64_t R = 64;
-            while (R < need) R <<= 1;
             const int KM = kmax <= 4 ? 4 : kmax <= 8 ? 8 : kmax <= 12 ? 12 : 16;
-            const bool fits = R <= kLevelMaxR && steps * W * KM * 8 < ((int64_t)1 << 32);
+            fits = fits && steps * W * KM * 8 < ((int64_t)1 << 32);
             if (fits) {
+                const int64_t R = nslots, zero = R, trash = R + 1;
                 T.est_level_us = (double)steps * kLevelStepUs +
-                                 (double)steps * W * (20.0 + 10.0 * KM) / kLevelBytesPerUs;
+                                 (double)steps * W * (24.0 + 10.0 * KM) / kLevelBytesPerUs;
                 const double cur = T.schedule == kSchedBand ? T.est_band_us
                                    : T.schedule == kSchedLds  ? T.est_lds_us
                                    : T.schedule == kSchedGrid ? T.est_grid_us
@@ -2853,19 +2880,20 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
                     T.lv_R = (int)R;
                     T.lv_KM = KM;
                     const size_t NP = (size_t)steps * W;
-                    lrc.assign(NP, kLevelIdle);
-                    lsl.assign(NP * (KM / 4), (uint64_t)R * 0x0001000100010001ull);
+                    lrc.assign(NP, (uint64_t)kLevelIdle | ((uint64_t)trash << 40));
+                    lsl.assign(NP * (KM / 4), (uint64_t)zero * 0x0001000100010001ull);
                     lcf.assign(NP * KM, -0.0);
                     ldg.assign(NP, 1.0);
                     for (int64_t i = 0; i < n; ++i) {
                         const int64_t p = pos[(size_t)i], st = p / W, t = p % W;
                         const int32_t a = F.rp[(size_t)i], e = F.rp[(size_t)i + 1];
-                        lrc[(size_t)p] = (uint32_t)i | ((uint32_t)(e - a) << 27);
+                        const uint64_t ws = slot[(size_t)i] >= 0 ? (uint64_t)slot[(size_t)i] : (uint64_t)trash;
+                        lrc[(size_t)p] = (uint64_t)(uint32_t)i | (ws << 40);
                         for (int32_t j = a; j < e; ++j) {
                             const int k = j - a;
-                            const uint64_t slot = (uint64_t)(pos[(size_t)F.ci[(size_t)j]] & (R - 1));
+                            const uint64_t ds = (uint64_t)slot[(size_t)F.ci[(size_t)j]];   // read: it has a reader
                             uint64_t &w = lsl[((size_t)st * (KM / 4) + (size_t)(k / 4)) * W + (size_t)t];
-                            w = (w & ~((uint64_t)0xFFFF << (16 * (k % 4)))) | (slot << (16 * (k % 4)));
+                            w = (w & ~((uint64_t)0xFFFF << (16 * (k % 4)))) | (ds << (16 * (k % 4)));
                             // coefficient pairs (2k2, 2k2 + 1) of lane t: one 16-byte load
                             lcf[(((size_t)st * (KM / 2) + (size_t)(k / 2)) * W + (size_t)t) * 2 + (size_t)(k % 2)] = ova[(size_t)j];
                         }

@@ -281,12 +281,13 @@ struct TriFactor {
     double *part_va = nullptr;
     int part_P = 0;
     // levels layout (round 5, sptrsv_levels_kernel): ONE workgroup of lv_W lanes, a dependency level (or a
-    // lv_W-row piece of one) per step behind a barrier, x in an LDS ring of lv_R slots indexed by step
-    // position. Per step s and lane t (field-major, coalesced): lv_rc = row | (entries << 27) (0x07FFFFFF:
-    // idle lane), lv_sl = ring slots of the entries, two uint16 per word (padding: slot lv_R, which holds
-    // 0.0), lv_cf = coefficients in stored order (padding -0.0), lv_dg = diagonal (nullptr: unit),
-    // lv_b = the right-hand side gathered into step order before each solve
-    uint32_t *lv_rc = nullptr;
+    // lv_W-row piece of one) per step behind a barrier, x in lv_R LDS slots the host assigns (a value's slot
+    // is free again after the step of its last reader; slot lv_R holds 0.0, slot lv_R + 1 takes the values
+    // nobody reads). Per step s and lane t (field-major, coalesced): lv_rc = row | (write slot << 40)
+    // (row 0xFFFFFFFF: idle lane), lv_sl = slots of the entries, four uint16 per word (padding: slot lv_R),
+    // lv_cf = coefficients in stored order (padding -0.0), two per 16 bytes, lv_dg = diagonal (1.0 for a
+    // unit factor), lv_b = the right-hand side gathered into step order before each solve
+    uint64_t *lv_rc = nullptr;
     uint64_t *lv_sl = nullptr;
     double *lv_cf = nullptr, *lv_dg = nullptr, *lv_b = nullptr;
     int64_t lv_steps = 0;
