@@ -2263,8 +2263,8 @@ void build_grid_dict(const unsigned char *gb, int64_t nsteps, int64_t SB, int K,
 // FD 2048^2 Gauss-Seidel: 3.9 ms for ~4100 levels) and ~2.7 us without (AMG level 3 at 8192^2).
 constexpr double kHopUs = 0.36, kRowUs = 0.61, kBandLevelRingUs = 1.0, kBandLevelMemUs = 2.7;
 constexpr double kLdsLevelUs = 0.15, kLdsBytesPerUs = 40e3;   // LDS schedule (provisional)
-// levels schedule (provisional until measured): a step's barrier + LDS round trip, one CU's record stream
-constexpr double kLevelStepUs = 0.30, kLevelBytesPerUs = 60e3;
+// levels schedule: a step's barrier + LDS round trip, one CU's record stream (1708 steps, 31.5 MB: measured 0.615 ms)
+constexpr double kLevelStepUs = 0.30, kLevelBytesPerUs = 200e3;   // fitted: AMG level 1 of -FD 8192^2, 0.615 ms
 constexpr double kNarrowLevelUs = 0.8;    // narrow band local level (FD 8192^2 Gauss-Seidel: 12.6 ms / 16128 levels)
 
 struct HostFactor {
