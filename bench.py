@@ -103,7 +103,7 @@ def main():
     ap.add_argument("--config4", type=int, default=1, help="also time configs[4] (PCG+AMG, -FD 8192^2) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
     ap.add_argument("--gmres", type=int, default=1, help="also time GMRES(30)+Jacobi Arnoldi steps at 4096^2 on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r4_pmc_traffic_%d.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r5_pmc_traffic_%d.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same build; %%d = the side")
     args = ap.parse_args()
 
@@ -484,8 +484,11 @@ def median(v):
 
 def spmv_kernel_label(layout, mode):
     """Descriptive name of the SpMV kernel a layout runs when no PMC profile of the build names it."""
-    return ("spmv_kernel<%d> (CSR layout)" % mode) if layout == 0 else \
-        ("spmv_uniform(_multi)_kernel / spmv_sliced_kernel <MODE=%d> (%s layout)" % (mode, LAYOUT_NAMES[layout]))
+    if layout == 0:
+        return "spmv_kernel<%d> (CSR layout)" % mode
+    if LAYOUT_NAMES.get(layout) == "diag":
+        return "spmv_diag_kernel<%d, ...> (diag layout)" % mode
+    return "spmv_uniform(_multi)_kernel / spmv_sliced_kernel <MODE=%d> (%s layout)" % (mode, LAYOUT_NAMES[layout])
 
 
 def lib_sha256():

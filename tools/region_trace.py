@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """The headline regions' SpMV launches in a rocprofv3 --kernel-trace CSV of `bench.py` (evidence tool).
 
-    python tools/region_trace.py run_kernel_trace.csv [--kernel spmv_uniform_multi_kernel<1] \
+    python tools/region_trace.py run_kernel_trace.csv [--kernel spmv_diag_kernel<1] \
         [--workgroups 19541] [--warmup 5] [--steps 20] [--regions 5]
 
 bench.py's first launches of the in-loop SpMV at the headline size are the warmup solve's (`--warmup`
@@ -19,7 +19,7 @@ import statistics
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel", default="spmv_uniform_multi_kernel<1,")
+    ap.add_argument("--kernel", default="spmv_diag_kernel<1,")
     ap.add_argument("--workgroups", type=int, default=19541)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
