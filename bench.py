@@ -176,10 +176,34 @@ def main():
     # the ranks' dot products: device-side stores into a host-shared mailbox (default; one node) or RCCL
     # all-gathers (PSK_DOT_TRANSPORT=rccl); the halo of p always goes over the transport above
     dots = os.environ.get("PSK_DOT_TRANSPORT", "mailbox")
+    dots_note = None
     if world > 1 and dots == "mailbox":
         obj = [("/psk_mb_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         N.check(N.lib.psk_comm_mailbox(comm, obj[0]), "psk_comm_mailbox")
+        # self-check (known values through the solvers' kernel stores and gather, bounded waits); every
+        # rank's verdict is shared, so all fall back to RCCL all-gathers together when any rank failed
+        rc = N.lib.psk_comm_mailbox_check(comm, 8)
+        import torch
+        flag = torch.tensor([0 if rc == 0 else 1], dtype=torch.int32)
+        dist.all_reduce(flag)
+        if int(flag.item()) != 0:
+            dots_note = "mailbox self-check failed on %d rank(s): RCCL all-gathers used" % int(flag.item())
+            N.lib.psk_comm_destroy(comm)
+            comm = ctypes.c_void_p()
+            if transport == "host":
+                obj = [("/psk_bench_%d_%s" % (os.getpid(), os.urandom(6).hex())).encode() if rank == 0 else None]
+                dist.broadcast_object_list(obj, src=0)
+                N.check(N.lib.psk_comm_init_host(world, rank, obj[0], ctypes.byref(comm)), "psk_comm_init_host")
+            else:
+                uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES)()
+                if rank == 0:
+                    N.check(N.lib.psk_comm_unique_id(uid), "psk_comm_unique_id")
+                obj = [bytes(uid)]
+                dist.broadcast_object_list(obj, src=0)
+                uid = (ctypes.c_uint8 * N.PSK_UNIQUE_ID_BYTES).from_buffer_copy(obj[0])
+                N.check(N.lib.psk_comm_init(world, rank, uid, ctypes.byref(comm)), "psk_comm_init")
+            dots = "rccl"
 
     # ---- the headline: the metric's N = 10M system on `world` GPUs ----------------------------------
     m = args.side
@@ -221,7 +245,8 @@ def main():
                        if world > 1 else "single GPU",
                        "transport": {"halo": "rccl send/recv" if transport == "rccl" else "host-shm rehearsal",
                                      "dots": "mailbox (kernel stores to host-shared memory)" if dots == "mailbox"
-                                     else ("rccl allgather" if transport == "rccl" else "host-shm allgather")}
+                                     else ("rccl allgather" if transport == "rccl" else "host-shm allgather"),
+                                     "dots_note": dots_note}
                        if world > 1 else None},
             "repeats": {"regions": len(regions), "value_is": "median region",
                         "it_s": [args.steps / r[0] for r in regions],
@@ -237,7 +262,10 @@ def main():
                          "csr_bytes_per_launch": bspmv,
                          "csr_count_over_time_GBps": csr_eq,
                          "csr_count_note": "SURVEY §8d's CSR byte count (12 nnz + 4(n+1) + 16n) over the same time: "
-                                           "NOT a bandwidth — the layout streams fewer bytes than CSR"},
+                                           "NOT a bandwidth — the layout streams fewer bytes than CSR",
+                         "bound_note": ("diag layout, 17 B/row: the launch is bound by one memory round trip per "
+                                        "workgroup (latency), not by HBM bandwidth; pcg_iteration_roofline prices the "
+                                        "whole iteration (DESIGN.md §4)") if lname == "diag" else None},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter, "vector_bytes_per_row": vb,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},

@@ -343,6 +343,10 @@ int psk_comm_init_host(int32_t nranks, int32_t rank, const char *name, psk_comm 
  * instead of ncclAllGather (the halo of p stays on RCCL / the host transport). Same bits as the
  * all-gather: every rank still sums the P values in rank order. Replaces nothing in the reference. */
 int psk_comm_mailbox(psk_comm *c, const char *name);
+/* Self-check of the attached mailbox (collective over c's ranks): `rounds` exchanges of known values
+ * through the same kernel stores and gather the solvers use; PSK_ERR_RCCL when a value is wrong or never
+ * arrives (bounded wait). bench.py runs it before a multi-GPU run and falls back to RCCL all-gathers. */
+int psk_comm_mailbox_check(psk_comm *c, int32_t rounds);
 int psk_comm_destroy(psk_comm *c);
 /* Rank `rank`'s row block of FDLaplacian2D(a,b,m): rows [row_begin,row_end) split on
  * whole grid lines; local columns are [owned | halo_lo | halo_hi]. */

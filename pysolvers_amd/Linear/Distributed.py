@@ -78,6 +78,11 @@ class Communicator:
         N.check(N.lib.psk_comm_mailbox(self._h, name), "psk_comm_mailbox")
         self.mailbox = name
 
+    def check_mailbox(self, rounds=4):
+        """psk_comm_mailbox_check (collective): known values through the mailbox exchange; raises on a wrong
+        or missing value (bounded waits)."""
+        N.check(N.lib.psk_comm_mailbox_check(self._h, int(rounds)), "psk_comm_mailbox_check")
+
     @property
     def handle(self):
         return self._h

@@ -100,6 +100,7 @@ SIGNATURES = {
     "psk_comm_init_dry": (ctypes.c_int, [I32, I32, PP]),
     "psk_comm_init_host": (ctypes.c_int, [I32, I32, ctypes.c_char_p, PP]),
     "psk_comm_mailbox": (ctypes.c_int, [P, ctypes.c_char_p]),
+    "psk_comm_mailbox_check": (ctypes.c_int, [P, I32]),
     "psk_csr_create_fd2d_dist": (ctypes.c_int, [F64, F64, I64, P, PP, ctypes.POINTER(I64),
                                                 ctypes.POINTER(I64)]),
     "psk_csr_create_dist": (ctypes.c_int, [I64, P, P, P, P, P, PP]),

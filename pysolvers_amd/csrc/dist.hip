@@ -492,6 +492,45 @@ int psk_comm_mailbox(psk_comm *c, const char *name) {
     return PSK_OK;
 }
 
+// mailbox self-check: each rank stores (rank*4096 + r, -(rank*4096 + r)) into exchange r the way a
+// solver's grid-sum finisher does, gathers the P pairs and verifies them (bounded waits: a value that
+// never arrives is reported, not waited for). Collective: every rank of c, the same rounds.
+__global__ void mbox_check_put_kernel(GridSum gs, double v) {
+    if (threadIdx.x == 0) {
+        const double r[2] = {v, -v};
+        gridsum_mail<2>(gs, r);
+    }
+}
+
+extern "C" int psk_comm_mailbox_check(psk_comm *c, int32_t rounds) {
+    if (!c || !c->mb || rounds < 1) return fail(PSK_ERR_ARG, "psk_comm_mailbox_check: no mailbox attached");
+    Context *cx;
+    PSK_TRY(ctx(&cx));
+    const int P = c->nranks;
+    DevBuf rb;
+    struct Release {
+        DevBuf &b;
+        ~Release() { b.release(); }
+    } rel{rb};
+    PSK_TRY(rb.ensure((size_t)P * 2 * sizeof(double)));
+    std::vector<double> h((size_t)P * 2);
+    for (int r = 0; r < rounds; ++r) {
+        GridSum gs{};
+        const uint64_t seq = mbox_next(c, &gs);
+        hipLaunchKernelGGL(mbox_check_put_kernel, dim3(1), dim3(64), 0, cx->stream, gs, (double)(c->rank * 4096 + r));
+        PSK_HIP(hipGetLastError());
+        PSK_TRY(mbox_gather(c, seq, 2, rb.as<double>(), nullptr, cx->stream));
+        PSK_HIP(hipMemcpyAsync(h.data(), rb.p, h.size() * sizeof(double), hipMemcpyDeviceToHost, cx->stream));
+        PSK_HIP(hipStreamSynchronize(cx->stream));
+        PSK_TRY(gridsum_check(cx));   // a wait that expired (bit 8)
+        for (int q = 0; q < P; ++q)
+            if (h[2 * q] != (double)(q * 4096 + r) || h[2 * q + 1] != -(double)(q * 4096 + r))
+                return fail(PSK_ERR_RCCL, "psk_comm_mailbox_check: rank " + std::to_string(q) + "'s value of exchange " +
+                                              std::to_string(r) + " is wrong");
+    }
+    return PSK_OK;
+}
+
 int psk_comm_destroy(psk_comm *c) {
     if (!c) return PSK_OK;
     mbox_close(c);

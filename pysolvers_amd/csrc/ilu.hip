@@ -1615,7 +1615,7 @@ __global__ __launch_bounds__(2 * kGridLanes) void sptrsv_grid_kernel(
 // fma over the stored entries in stored order from 0.0, padding entries (-0.0 x 0.0) add exactly nothing,
 // then (b - acc) / d: the band and grid kernels' bits.
 constexpr uint32_t kLevelIdle = 0xFFFFFFFFu;   // row field of an idle lane
-constexpr int kLevelMaxK = 16, kLevelMaxW = 256, kLevelD = 4;
+constexpr int kLevelMaxK = 16, kLevelMaxW = 256, kLevelD = 4, kLevelPad = 8;   // D: steps loaded ahead (PSK_LEVELS_D=8: lab)
 constexpr int64_t kLevelMaxSlots = 18432;     // live values + the zero and trash slots: <= 144 KiB of LDS
 template <int KM, int D>
 __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int R, int64_t n, int unit,
@@ -1684,10 +1684,15 @@ __global__ __launch_bounds__(256) void sptrsv_levels_kernel(int64_t nsteps, int 
         for (int i = 0; i < D; ++i) {
             const int64_t s = s0 + i;
             double acc = 0.0;
+            // the step's widest row (bits 56..60 of every lane's record word, uniform): the fma chain stops
+            // there instead of running through every padding entry (which would add exactly nothing)
+            const int ks = __builtin_amdgcn_readfirstlane((int)(buf[i].rc >> 56) & 31);
 #pragma unroll
             for (int k = 0; k < KM; ++k) {
-                const uint32_t slot = (uint32_t)(buf[i].sw[k >> 2] >> (16 * (k & 3))) & 0xFFFFu;
-                acc = fma(buf[i].c[k], lv_ring[slot], acc);
+                if (k < ks) {
+                    const uint32_t slot = (uint32_t)(buf[i].sw[k >> 2] >> (16 * (k & 3))) & 0xFFFFu;
+                    acc = fma(buf[i].c[k], lv_ring[slot], acc);
+                }
             }
             double r = buf[i].b - acc;
             if (!unit) r = r / buf[i].d;   // (uniform)
@@ -1833,10 +1838,18 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         hipLaunchKernelGGL(levels_gather_kernel, dim3((unsigned)((np + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, np,
                            T.lv_rc, rhs, rhs_idx, T.lv_b);
         PSK_HIP(hipGetLastError());
-        const void *k = T.lv_KM == 4    ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<4, kLevelD>)
-                        : T.lv_KM == 8  ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<8, kLevelD>)
-                        : T.lv_KM == 12 ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<12, kLevelD>)
-                                        : reinterpret_cast<const void *>(&sptrsv_levels_kernel<16, kLevelD>);
+        static const bool d8 = [] {
+            const char *e = std::getenv("PSK_LEVELS_D");
+            return e && std::atoi(e) == 8;
+        }();
+        const void *k = d8 ? (T.lv_KM == 4    ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<4, 8>)
+                              : T.lv_KM == 8  ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<8, 8>)
+                              : T.lv_KM == 12 ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<12, 8>)
+                                              : reinterpret_cast<const void *>(&sptrsv_levels_kernel<16, 8>))
+                           : (T.lv_KM == 4    ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<4, kLevelD>)
+                              : T.lv_KM == 8  ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<8, kLevelD>)
+                              : T.lv_KM == 12 ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<12, kLevelD>)
+                                              : reinterpret_cast<const void *>(&sptrsv_levels_kernel<16, kLevelD>));
         int R = T.lv_R, unit = T.diag ? 0 : 1;
         const uint64_t *lrc = T.lv_rc;
         const uint64_t *lsl = T.lv_sl;
@@ -2829,7 +2842,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
                     steps += st;
                 }
             }
-            steps = (steps + kLevelD - 1) / kLevelD * kLevelD;   // the kernel's loop: whole groups of D steps
+            steps = (steps + kLevelPad - 1) / kLevelPad * kLevelPad;   // the kernel's loop: whole groups of D steps
             // slot of every value: the step of its last reader, then greedy interval allocation in step order
             std::vector<int64_t> last((size_t)n, -1);
             for (int64_t i = 0; i < n; ++i)
@@ -2888,7 +2901,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
                         const int64_t p = pos[(size_t)i], st = p / W, t = p % W;
                         const int32_t a = F.rp[(size_t)i], e = F.rp[(size_t)i + 1];
                         const uint64_t ws = slot[(size_t)i] >= 0 ? (uint64_t)slot[(size_t)i] : (uint64_t)trash;
-                        lrc[(size_t)p] = (uint64_t)(uint32_t)i | (ws << 40);
+                        lrc[(size_t)p] = (uint64_t)(uint32_t)i | (ws << 40) | (lrc[(size_t)p] & ((uint64_t)31 << 56));
                         for (int32_t j = a; j < e; ++j) {
                             const int k = j - a;
                             const uint64_t ds = (uint64_t)slot[(size_t)F.ci[(size_t)j]];   // read: it has a reader
@@ -2898,6 +2911,15 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
                             lcf[(((size_t)st * (KM / 2) + (size_t)(k / 2)) * W + (size_t)t) * 2 + (size_t)(k % 2)] = ova[(size_t)j];
                         }
                         if (!dg.empty()) ldg[(size_t)p] = dg[(size_t)i];
+                    }
+                    // every lane's word carries its step's widest row (the kernel's fma chain length)
+                    for (int64_t st = 0; st < steps; ++st) {
+                        uint64_t ks = 0;
+                        for (int64_t t = 0; t < W; ++t) {
+                            const uint32_t row = (uint32_t)lrc[(size_t)(st * W + t)];
+                            if (row != kLevelIdle) ks = std::max<uint64_t>(ks, (uint64_t)(F.rp[row + 1] - F.rp[row]));
+                        }
+                        for (int64_t t = 0; t < W; ++t) lrc[(size_t)(st * W + t)] |= ks << 56;
                     }
                 }
             }

@@ -44,6 +44,8 @@ def _worker(rank, world, port, name, kind, out_dir, mailbox=False):
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % port, rank=rank, world_size=world)
     N.check(N.lib.psk_set_device(0), "psk_set_device")
     comm = Communicator.from_torch_distributed(transport="host", mailbox=mailbox)
+    if mailbox:
+        comm.check_mailbox(4)   # psk_comm_mailbox_check: known values through the exchange first
     A = _matrix(name)
     b, _ = fdlap.manufactured_rhs(A, 12345)
     if kind == "fd":
