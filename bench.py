@@ -468,8 +468,8 @@ class PcgSystem:
         sync; per region the max over ranks of (wall time, mean SpMV launch time). events: libpsk
         records HIP events around every SpMV launch (the roofline's kernel time)."""
         N = self.N
-        if warmup > 0:
-            r = self.run(warmup, False)
+        if warmup > 0:   # the same path as the timed regions (the timing events are created here, not in region 1)
+            r = self.run(warmup, events)
             assert r.iters == warmup, r.iters
         out = []
         for _ in range(max(1, repeats)):
