@@ -55,7 +55,7 @@ def spmv_bytes(n, nnz):
     return 12 * nnz + 4 * (n + 1) + 16 * n
 
 
-PCG_VEC_BYTES_PER_ROW = 74   # K2 (r, Ap, dinv in; r out) + K3 (r, p, dinv in; p out; x and p_{k-3..k-1} every 4th iteration), Jacobi
+PCG_VEC_BYTES_PER_ROW = 73   # K2 (r, Ap, dinv in; r out) + K3 (r, p, dinv in; p out; x and p_{k-7..k-1} every 8th iteration), Jacobi
 LAYOUT_NAMES = {0: "csr", 1: "sliced", 2: "sliced_wide", 3: "sliced_dict", 4: "diag"}   # PSK_LAYOUT_*
 
 
@@ -67,10 +67,10 @@ def pcg_iter_bytes(n, nnz, jacobi=True):
 
 def vec_bytes_per_row(N, M):
     """K2 + K3 bytes per row, averaged over iterations: K2 24 (r, Ap read, r written); K3 reads r and
-    p_k and writes p_{k+1} every iteration, and x (read + write) with p_{k-3}, p_{k-2}, p_{k-1} every
-    4th iteration only (the deferred x update, pcg.hip kPcgDefer) = 24 + 40/4; + 16 for a streamed
-    DInv (K2 and K3 read it). 58 when the Jacobi diagonal is one scalar (psk_prec_jacobi_uniform),
-    74 otherwise."""
+    p_k and writes p_{k+1} every iteration, and x (read + write) with p_{k-7} .. p_{k-1} every 8th
+    iteration only (the deferred x update, pcg.hip kPcgDefer) = 24 + 72/8; + 16 for a streamed
+    DInv (K2 and K3 read it). 57 when the Jacobi diagonal is one scalar (psk_prec_jacobi_uniform),
+    73 otherwise."""
     u = N.I32()
     N.check(N.lib.psk_prec_jacobi_uniform(M, ctypes.byref(u), None), "psk_prec_jacobi_uniform")
     return PCG_VEC_BYTES_PER_ROW - (16 if u.value else 0)

@@ -217,9 +217,10 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
 // by element). A flush applies the pending updates in iteration order, x = ((x + a_{k-q} p_{k-q}) + ...)
 // + a_k p_k, the reference's two roundings per update in its order (PCGSolver.py:121), so x is
 // bit-identical to updating every iteration. x traffic per iteration: 16 B/row updated every
-// iteration, 8 (kPcgDefer + 1) / kPcgDefer deferred (12 at 2, 10 at 4).
+// iteration, 8 (kPcgDefer + 1) / kPcgDefer deferred (12 at 2, 10 at 4, 9 at 8). Round 5 A/B
+// (profiles/r5_pcg_defer_ab.txt, same bits): 8 = 4 at N = 10M, +2.2% at 16384^2; 2 and 3 slower.
 #ifndef PSK_PCG_DEFER
-#define PSK_PCG_DEFER 4
+#define PSK_PCG_DEFER 8
 #endif
 constexpr int kPcgDefer = PSK_PCG_DEFER;
 static_assert(kPcgDefer >= 1 && kPcgDefer <= 8, "kPcgDefer");
