@@ -276,6 +276,10 @@ int psk_lab_dispatch_probe(int32_t nwg, int32_t lds_bytes, double usec, int64_t 
 /* Lab: occupiers per XCD (HW_REG_XCC_ID) of the last psk_lab_occupy_begin, counts[8]. */
 int psk_lab_occupy_xcc(int32_t *counts);
 int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid);
+/* Lab / tests (round 5): the PCG loop's fused K3 + SpMV launch (diagonal layout, unsharded, Jacobi with one
+ * DInv value or none) on (1) or off (0, the separate K3 and SpMV launches; same bits). Returns the previous
+ * setting (initially PSK_PCG_FUSED, default off: measured no faster, profiles/r5_pcg_fused_ab.txt). */
+int psk_lab_pcg_fused(int32_t on);
 /* Host-only: the grid plan psk_prec_create_trisolve would make for one triangular factor (CSR with its
  * diagonal; upper = 1: solved from the last row up), without any device work — out[0..6] = w, H,
  * sigma2, phase, off, steps per band, record width K. PSK_ERR_UNSUPPORTED when it is not a 2-D stencil. */

@@ -85,6 +85,7 @@ SIGNATURES = {
     "psk_lab_occupy_end": (ctypes.c_int, [ctypes.POINTER(I32)]),
     "psk_lab_occupy_xcc": (ctypes.c_int, [ctypes.POINTER(I32)]),
     "psk_lab_dispatch_probe": (ctypes.c_int, [I32, I32, F64, P]),
+    "psk_lab_pcg_fused": (ctypes.c_int, [I32]),
     "psk_lab_trisolve_workers": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "psk_trisolve_grid_plan": (ctypes.c_int, [I64, P, P, P, I32, ctypes.POINTER(I64)]),
     "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),

@@ -15,6 +15,7 @@
 // u is never stored: K2 and K3 both recompute u_i = DInv_i * r_i (one rounding, as np.multiply).
 // Elementwise updates use two roundings (-ffp-contract=off), exactly as numpy's x + alpha*p.
 #include "psk_internal.hpp"
+#include "pcg_state.hpp"
 
 #include <cstdlib>
 
@@ -24,40 +25,6 @@
 
 
 namespace psk {
-
-struct PcgState {
-    int32_t done;      // 0 running, 1 converged, 2 breakdown
-    int32_t brk_kind;  // 1: dot(u,r)==0 at start, 2: dot(p,Ap)==0
-    int64_t iters;
-    double resid;
-    double normB;
-    double tauNormB;
-    int64_t live;      // k of the last K2 that ran to completion (no breakdown); -1 before the loop
-    int64_t *hdone;    // host-mapped stamp of the iteration that set `done` (nullptr: none), see set_done
-    int64_t hgen;      // this solve's generation in the stamp's high bits (kStampGenShift)
-    double last_hist;  // the latest reported ||r_k|| (resid_recursive without copying the history back)
-    int32_t x_written; // 1 once x has been stored (Jacobi/identity: x0 = 0 is implicit until the first flush)
-    int32_t pad;
-};
-
-// done = v != 0, and the host-mapped stamp the solve loop polls: k + 2 for a kernel of iteration k, 1
-// for the init (0 = running) — a system-scope store drained before the kernel ends, so once an event
-// recorded after this kernel has completed the host reads the word directly, with no per-chunk
-// device-to-host copy (a blit kernel) on the solver's stream. The stamp lets the host act on the state
-// as of the chunk it waited for, not a later one its GPU has already run: every rank of a sharded
-// solve then stops after the same chunk and enqueues the same collectives.
-// The word is shared by every solve on the device; each solve tags its stamps with its own generation
-// (high bits), so a kernel still queued from an earlier solve that failed on the host side cannot leave a
-// stamp the next solve's poll would act on.
-constexpr int kStampGenShift = 40;
-constexpr int64_t kStampMask = ((int64_t)1 << kStampGenShift) - 1;
-__device__ __forceinline__ void set_done(PcgState *st, int32_t v, int64_t stamp) {
-    st->done = v;
-    if (st->hdone) {
-        __hip_atomic_store(st->hdone, st->hgen | stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __threadfence_system();
-    }
-}
 
 // the solver state after the init sums bb = b.b and ur = u.r (PCGSolver.py:86-105)
 __device__ __forceinline__ void pcg_init_state(double bb, double ur, double tau, PcgState *st, double *udr,
@@ -209,70 +176,6 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     }
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
-}
-
-// Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
-// p_j lives in ring buffer j mod kPcgDefer; K3 of iteration k reads p_k and writes p_{k+1} over
-// p_{k+1-kPcgDefer}, which the last flush consumed (or, on a flush, which this K3 reads first, element
-// by element). A flush applies the pending updates in iteration order, x = ((x + a_{k-q} p_{k-q}) + ...)
-// + a_k p_k, the reference's two roundings per update in its order (PCGSolver.py:121), so x is
-// bit-identical to updating every iteration. x traffic per iteration: 16 B/row updated every
-// iteration, 8 (kPcgDefer + 1) / kPcgDefer deferred (12 at 2, 10 at 4, 9 at 8). Round 5 A/B
-// (profiles/r5_pcg_defer_ab.txt, same bits): 8 = 4 at N = 10M, +2.2% at 16384^2; 2 and 3 slower.
-#ifndef PSK_PCG_DEFER
-#define PSK_PCG_DEFER 8
-#endif
-constexpr int kPcgDefer = PSK_PCG_DEFER;
-static_assert(kPcgDefer >= 1 && kPcgDefer <= 8, "kPcgDefer");
-struct PRing {
-    double *b[kPcgDefer];
-};
-// iterations whose x update is still pending when K3 of iteration k runs: k - q .. k - 1
-__host__ __device__ inline int pcg_pending(int64_t k) { return (int)(k % kPcgDefer); }
-
-// x[j] with the pending updates of iterations k - q .. k - 1 applied (ring: their p; alphas[i] = a_i)
-__device__ __forceinline__ double pcg_catch_up(double xj, const PRing *pr, int q, int64_t k,
-                                               const double *__restrict__ alphas, int64_t j) {
-    for (int t = q; t >= 1; --t) xj = xj + alphas[k - t] * pr->b[(k - t) % kPcgDefer][j];   // :121
-    return xj;
-}
-
-// K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
-// (K2's expression on the same partials), the convergence test, beta. Returns false when the
-// solve stopped at this iteration; x (which K3 owns) is then still advanced over the tile.
-// pr != nullptr: the q = pcg_pending(k) deferred x updates are applied first.
-__device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
-                                             double pTAp, double rr, double ur, PcgState *st,
-                                             double *__restrict__ udr, double *__restrict__ hist, int64_t k,
-                                             int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
-                                             int64_t tile, const PRing *pr = nullptr,
-                                             const double *__restrict__ alphas = nullptr) {
-    alpha = udr[k] / pTAp;                                   // :118
-    const double normR = sqrt(rr);                           // self.norm(r)  :125
-    if (tile == 0 && threadIdx.x == 0) {
-        hist[k] = normR;                                     // reportIter  :126
-        st->last_hist = normR;
-    }
-    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
-        const int64_t i = tile * kVecTile + 2 * threadIdx.x;
-        // deferred updates (pr): before the first flush (k < kPcgDefer) x is still the implicit x0 = 0
-        const bool x0 = pr && k < kPcgDefer;
-        for (int64_t j = i; j < i + 2 && j < n; ++j) {
-            double xj = x0 ? 0.0 : x[j];
-            if (pr) xj = pcg_catch_up(xj, pr, pcg_pending(k), k, alphas, j);
-            x[j] = xj + alpha * p[j];                        // :121
-        }
-        if (tile == 0 && threadIdx.x == 0) {
-            st->iters = k + 1;                               // handleConvergence(k, ...)
-            st->resid = normR;
-            st->x_written = 1;
-            set_done(st, 1, k + 2);
-        }
-        return false;
-    }
-    beta = ur / udr[k];                                      // :134-135
-    if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
-    return true;
 }
 
 // ---- K3: x += alpha p (deferred, above), convergence test, beta, p = u + beta p (one-shot, as K2) --
@@ -628,6 +531,10 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     bool halo_pending = false;
     if (overlap) PSK_TRY(comm_stream(c, &cs));
 
+    // K3(k) fused into the SpMV of k + 1 (spmv.hip, pcg_fused_kernel): the SpMV launches once, at k = 0; p.Ap
+    // alternates between two result words (launch k reads p_k.Ap_k while it sums p_{k+1}.Ap_{k+1})
+    const bool fused = !gen && !sharded && pcg_fused_eligible(A, jac);
+    double *papb[2] = {w.part1, w.part1 + 32};
     int64_t launched = 0;
     int rc = PSK_OK;
     for (int64_t k = 0; k < maxiter && rc == PSK_OK; ++k) {
@@ -665,9 +572,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
         }
         // a timed launch records its events in its own dispatch (kernel start / end)
+        // (fused: the timed launch is the fused one of the same k)
         uint64_t seq1 = 0;
-        if ((rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s,
-                              timed ? ta[slot] : nullptr, timed ? tb[slot] : nullptr, 0, mbc ? &seq1 : nullptr)) != PSK_OK)
+        if ((!fused || k == 0) &&
+            (rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, fused ? papb[0] : w.part1, &w.st->done, s,
+                              timed && !fused ? ta[slot] : nullptr, timed && !fused ? tb[slot] : nullptr, 0,
+                              mbc ? &seq1 : nullptr)) != PSK_OK)
             break;
         // K2/K3 tiles in block order: XCD bands matching the SpMV's, and bands walked in alternating
         // directions (a serpentine over SpMV, K2, K3 meant to re-read Ap, r and p from the Infinity Cache),
@@ -680,8 +590,9 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         const uint64_t seq2 = mbc ? mbox_next(mbc, &gs2k) : 0;
         // the general path copied r = b in its init (pcg_gen_init_kernel): it never takes the FIRST form
         const bool first = k == 0 && !gen && dev_io;
+        const double *pap_k = fused ? papb[k & 1] : w.part1g;
 #define PSK_PCG_K2(J, F)                                                                                       \
-        hipLaunchKernelGGL((pcg_update_kernel<J, F>), gk, dim3(kBlock), 0, s, n, w.r, bd, w.Ap, dinv, ds, w.part1g, \
+        hipLaunchKernelGGL((pcg_update_kernel<J, F>), gk, dim3(kBlock), 0, s, n, w.r, bd, w.Ap, dinv, ds, pap_k,     \
                            P, gs2k, w.st, w.udr, k, tm2)
         if (jac == 2) { if (first) PSK_PCG_K2(2, true); else PSK_PCG_K2(2, false); }
         else if (jac == 1) { if (first) PSK_PCG_K2(1, true); else PSK_PCG_K2(1, false); }
@@ -695,6 +606,12 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             hipLaunchKernelGGL(pcg_dot_kernel, gk, dim3(kBlock), 0, s, n, w.u, w.r, gs3, w.st);
             hipLaunchKernelGGL(pcg_gen_direction_kernel, gk, dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, w.part2,
                                w.part3, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
+        } else if (fused) {
+            const PcgFusedK fk{w.x, w.r, w.pr, ds, papb[k & 1], w.part2g, w.st, w.udr, w.hist, w.alphas, w.Ap, k, maxiter,
+                               ctl->fail_on_maxiter};
+            if ((rc = launch_pcg_fused(A, jac, fk, papb[(k + 1) & 1], s, timed ? ta[slot] : nullptr,
+                                       timed ? tb[slot] : nullptr)) != PSK_OK)
+                break;
         } else {
             auto k3 = [&](int64_t t0, int64_t t1) {   // K3 over tiles [t0, t1)
                 if (t1 <= t0) return;
@@ -808,7 +725,9 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         }
         if (ctl->time_kernels) {
             double tot = 0.0;
-            const int64_t cnt = nk < (int64_t)spmv_ms.size() ? nk : (int64_t)spmv_ms.size();
+            // fused: launch k of the last iteration only ran the convergence test (not a sample)
+            const int64_t nrun = fused && nk > 0 ? nk - 1 : nk;
+            const int64_t cnt = nrun < (int64_t)spmv_ms.size() ? nrun : (int64_t)spmv_ms.size();
             int64_t nt = 0;
             for (int64_t i = 0; i < cnt; i += ctl->time_kernels, ++nt) tot += spmv_ms[(size_t)i];
             res->spmv_launches = nt;

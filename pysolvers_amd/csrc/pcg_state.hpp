@@ -1,0 +1,127 @@
+// pcg_state.hpp — the PCG solver state and the K3 scalar logic (PCGSolver.py:113-138), shared by pcg.hip
+// (the loop, K0/K2/K3) and spmv.hip (the fused K3 + SpMV launch of the diagonal layout).
+#pragma once
+#include "psk_internal.hpp"
+
+namespace psk {
+
+struct PcgState {
+    int32_t done;      // 0 running, 1 converged, 2 breakdown
+    int32_t brk_kind;  // 1: dot(u,r)==0 at start, 2: dot(p,Ap)==0
+    int64_t iters;
+    double resid;
+    double normB;
+    double tauNormB;
+    int64_t live;      // k of the last K2 that ran to completion (no breakdown); -1 before the loop
+    int64_t *hdone;    // host-mapped stamp of the iteration that set `done` (nullptr: none), see set_done
+    int64_t hgen;      // this solve's generation in the stamp's high bits (kStampGenShift)
+    double last_hist;  // the latest reported ||r_k|| (resid_recursive without copying the history back)
+    int32_t x_written; // 1 once x has been stored (Jacobi/identity: x0 = 0 is implicit until the first flush)
+    int32_t pad;
+};
+
+// done = v != 0, and the host-mapped stamp the solve loop polls: k + 2 for a kernel of iteration k, 1
+// for the init (0 = running) — a system-scope store drained before the kernel ends, so once an event
+// recorded after this kernel has completed the host reads the word directly, with no per-chunk
+// device-to-host copy (a blit kernel) on the solver's stream. The stamp lets the host act on the state
+// as of the chunk it waited for, not a later one its GPU has already run: every rank of a sharded
+// solve then stops after the same chunk and enqueues the same collectives.
+// The word is shared by every solve on the device; each solve tags its stamps with its own generation
+// (high bits), so a kernel still queued from an earlier solve that failed on the host side cannot leave a
+// stamp the next solve's poll would act on.
+constexpr int kStampGenShift = 40;
+constexpr int64_t kStampMask = ((int64_t)1 << kStampGenShift) - 1;
+__device__ __forceinline__ void set_done(PcgState *st, int32_t v, int64_t stamp) {
+    st->done = v;
+    if (st->hdone) {
+        __hip_atomic_store(st->hdone, st->hgen | stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
+}
+
+// Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
+// p_j lives in ring buffer j mod kPcgDefer; K3 of iteration k reads p_k and writes p_{k+1} over
+// p_{k+1-kPcgDefer}, which the last flush consumed (or, on a flush, which this K3 reads first, element
+// by element). A flush applies the pending updates in iteration order, x = ((x + a_{k-q} p_{k-q}) + ...)
+// + a_k p_k, the reference's two roundings per update in its order (PCGSolver.py:121), so x is
+// bit-identical to updating every iteration. x traffic per iteration: 16 B/row updated every
+// iteration, 8 (kPcgDefer + 1) / kPcgDefer deferred (12 at 2, 10 at 4, 9 at 8). Round 5 A/B
+// (profiles/r5_pcg_defer_ab.txt, same bits): 8 = 4 at N = 10M, +2.2% at 16384^2; 2 and 3 slower.
+#ifndef PSK_PCG_DEFER
+#define PSK_PCG_DEFER 8
+#endif
+constexpr int kPcgDefer = PSK_PCG_DEFER;
+static_assert(kPcgDefer >= 1 && kPcgDefer <= 8, "kPcgDefer");
+struct PRing {
+    double *b[kPcgDefer];
+};
+// iterations whose x update is still pending when K3 of iteration k runs: k - q .. k - 1
+__host__ __device__ inline int pcg_pending(int64_t k) { return (int)(k % kPcgDefer); }
+
+// x[j] with the pending updates of iterations k - q .. k - 1 applied (ring: their p; alphas[i] = a_i)
+__device__ __forceinline__ double pcg_catch_up(double xj, const PRing *pr, int q, int64_t k,
+                                               const double *__restrict__ alphas, int64_t j) {
+    for (int t = q; t >= 1; --t) xj = xj + alphas[k - t] * pr->b[(k - t) % kPcgDefer][j];   // :121
+    return xj;
+}
+
+// K3 prologue shared by the Jacobi/identity and general-preconditioner variants: alpha again
+// (K2's expression on the same partials), the convergence test, beta. Returns false when the
+// solve stopped at this iteration; x (which K3 owns) is then still advanced over the tile.
+// pr != nullptr: the q = pcg_pending(k) deferred x updates are applied first.
+__device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
+                                             double pTAp, double rr, double ur, PcgState *st,
+                                             double *__restrict__ udr, double *__restrict__ hist, int64_t k,
+                                             int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
+                                             int64_t tile, const PRing *pr = nullptr,
+                                             const double *__restrict__ alphas = nullptr) {
+    alpha = udr[k] / pTAp;                                   // :118
+    const double normR = sqrt(rr);                           // self.norm(r)  :125
+    if (tile == 0 && threadIdx.x == 0) {
+        hist[k] = normR;                                     // reportIter  :126
+        st->last_hist = normR;
+    }
+    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+        const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+        // deferred updates (pr): before the first flush (k < kPcgDefer) x is still the implicit x0 = 0
+        const bool x0 = pr && k < kPcgDefer;
+        for (int64_t j = i; j < i + 2 && j < n; ++j) {
+            double xj = x0 ? 0.0 : x[j];
+            if (pr) xj = pcg_catch_up(xj, pr, pcg_pending(k), k, alphas, j);
+            x[j] = xj + alpha * p[j];                        // :121
+        }
+        if (tile == 0 && threadIdx.x == 0) {
+            st->iters = k + 1;                               // handleConvergence(k, ...)
+            st->resid = normR;
+            st->x_written = 1;
+            set_done(st, 1, k + 2);
+        }
+        return false;
+    }
+    beta = ur / udr[k];                                      // :134-135
+    if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
+    return true;
+}
+
+// the fused K3(k) + SpMV(k+1) launch of the PCG loop (spmv.hip, pcg_fused_kernel)
+struct PcgFusedK {
+    double *x;
+    const double *r;
+    PRing pr;
+    double ds;             // the one DInv value (JAC 2)
+    const double *pap;     // p_k.Ap_k: the previous launch's grid sum
+    const double *rrur;    // K2(k)'s [r.r, u.r]
+    PcgState *st;
+    double *udr, *hist, *alphas, *Ap;
+    int64_t k, maxiter;
+    int32_t fail_on_maxiter;
+};
+
+// the diagonal layout in the 5-diagonal DPP order, unsharded, jac 0 (none) or 2 (one DInv value);
+// off by default (measured no faster); PSK_PCG_FUSED=1 or psk_lab_pcg_fused(1) turns it on
+bool pcg_fused_eligible(const psk_csr *A, int jac);
+// iteration k's launch: p.Ap of p_{k+1} into pap_out[0]; ev0/ev1 (optional) bracket the dispatch
+int launch_pcg_fused(const psk_csr *A, int jac, const PcgFusedK &a, double *pap_out, hipStream_t s, hipEvent_t ev0,
+                     hipEvent_t ev1);
+
+}  // namespace psk

@@ -14,10 +14,12 @@
 // length is exact. Optional epilogues fuse the dot products the Krylov loops need next (p.Ap for
 // PCG, q_0.u for GMRES, ||b-Ax||^2 for the true residual), reduced deterministically by gridsum.
 #include "psk_internal.hpp"
+#include "pcg_state.hpp"
 
 #include <hip/hip_ext.h>
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cstdlib>
 #include <cmath>
@@ -772,6 +774,186 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
         spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
     }
     PSK_SPMV_PROF_AT(2);
+}
+
+// ---- PCG K3 fused into the next SpMV (round 5; diagonal layout, 5 diagonals, unsharded, Jacobi with one DInv
+// value or no preconditioner): one launch per iteration k does K3(k) and K1(k+1) of pcg.hip —
+//   alpha, ||r||, the convergence test, beta (pcg_direction_scalars), x's deferred updates on a flush,
+//   p_{k+1} = u + beta p_k (PCGSolver.py:138), Ap_{k+1} = A p_{k+1} (:111) and p_{k+1}.Ap_{k+1} (:113).
+// A row needs p_{k+1} at its stencil columns, rows the neighbouring workgroups own: each workgroup
+// recomputes them from r and p_k (the same two roundings, so the same bits as the p_{k+1} their owners
+// store), the -1/+1 columns by DPP lane shifts as in spmv_diag_kernel. Per row it reads the presence byte,
+// r and p_k (the ±m rows again through L2) and writes p_{k+1} and Ap: 33 B/row, against 24 (K3) + 17 (SpMV)
+// and one launch boundary in two. p.Ap has the bits of the unfused pair (same slices, same per-row sums).
+// Measured (profiles/r5_pcg_fused_ab.txt): no faster than the separate launches — 0.093 ms per launch at
+// N = 10M against SpMV 0.056 + K3 0.037 (PCG 6390 vs 6540 it/s), 2.36 vs 1.30 + ~1.05 ms at 16384^2 — also
+// with one slice per workgroup (59 VGPRs, 8 workgroups per CU) or a 64-VGPR cap (spills: 2x slower). Kept as
+// the PSK_PCG_FUSED=1 / psk_lab_pcg_fused path, bit-identical to the default (tests/test_gpu_parity.py).
+template <int JAC, int NB, bool FLUSH>
+__global__ __launch_bounds__(kBlock) void pcg_fused_kernel(int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd,
+                                                           PcgFusedK a, GridSum gs, TileMap tm, int64_t ntiles) {
+    constexpr int TPW = 2, KM = 5;
+    static_assert(NB == 1 || NB == 2, "the DPP orders of spmv_diag_kernel");
+    constexpr int JD = NB == 1 ? 0 : 2, JM1 = NB == 1 ? 3 : 1, JP1 = NB == 1 ? 4 : 3;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t grp = tile_of_block(tm), k = a.k;
+    const double *__restrict__ r = a.r;
+    const double *pk = a.pr.b[k % kPcgDefer];
+    // NOT __restrict__: on a flush, p_{k+1}'s buffer is p_{k+1-kPcgDefer}'s, read below first (pcg.hip K3)
+    double *pnext = a.pr.b[(k + 1) % kPcgDefer];
+    // the solver scalars are loaded first: vector loads return in order, so waiting for them (below) does
+    // not wait for the gathers issued after them; every stream and gather load then goes out before any wait
+    const int64_t live = a.st->live;
+    const double tau_nb = a.st->tauNormB, udr_k = a.udr[k], pTAp = a.pap[0], rr = a.rrur[0], ur = a.rrur[1];
+    int64_t tl[TPW];
+    bool tv[TPW];
+    uint32_t mk[TPW];
+    double rv[TPW][KM], pv[TPW][KM], re[TPW], pe[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t t = grp * TPW + q;
+        tv[q] = t < ntiles;
+        tl[q] = tv[q] ? t : ntiles - 1;
+        mk[q] = __builtin_nontemporal_load(mask + tl[q] * kSlice + tid);
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j == JM1 || j == JP1) continue;
+            const int64_t c = diag_col(dd, n, row, j);
+            rv[q][j] = r[c];
+            pv[q][j] = pk[c];
+        }
+        const int64_t c = diag_col_off(dd, n, row, lane == 0 ? -1 : (lane == 63 ? 1 : 0));
+        re[q] = r[c];
+        pe[q] = pk[c];
+    }
+    // a flush: x and the pending iterations' p at this workgroup's rows (uniform branches)
+    const int qp = pcg_pending(k);
+    const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0
+    double xo[TPW], pp[TPW][kPcgDefer > 1 ? kPcgDefer - 1 : 1];
+    if (FLUSH) {
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            const int64_t row = tl[q] * kSlice + tid, rc = row < n ? row : n - 1;
+            xo[q] = x0 ? 0.0 : __builtin_nontemporal_load(a.x + rc);
+#pragma unroll
+            for (int t = 1; t < kPcgDefer; ++t)
+                pp[q][t - 1] = t <= qp ? __builtin_nontemporal_load(a.pr.b[(k - t) % kPcgDefer] + rc) : 0.0;
+        }
+    }
+    const bool pub = spmv_publishes<kSpmvDot>(gs);
+    uint32_t ticket[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        ticket[q] = 0;
+        if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
+            ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+    }
+    // K2(k) returned (stopped earlier, or a p.Ap breakdown): nothing to do; otherwise pcg_direction_scalars'
+    // expressions, inline (PCGSolver.py:118-136); converged now: x advanced over this workgroup's rows with
+    // the pending updates (pcg_catch_up) and the state written (handleConvergence)
+    double alpha = 0.0, beta = 0.0;
+    bool go = live == k;
+    if (go) {
+        const double normR = sqrt(rr);                                                      // :125
+        alpha = udr_k / pTAp;                                                               // :118
+        if (grp == 0 && tid == 0) {
+            a.hist[k] = normR;                                                              // reportIter  :126
+            a.st->last_hist = normR;
+        }
+        if (normR <= tau_nb || (!a.fail_on_maxiter && k == a.maxiter - 1)) {               // :129-131
+#pragma unroll
+            for (int q = 0; q < TPW; ++q) {
+                const int64_t row = tl[q] * kSlice + tid;
+                if (!tv[q] || row >= n) continue;
+                const double xj = pcg_catch_up(x0 ? 0.0 : a.x[row], &a.pr, qp, k, a.alphas, row);
+                a.x[row] = xj + alpha * pk[row];                                            // :121
+            }
+            if (grp == 0 && tid == 0) {
+                a.st->iters = k + 1;
+                a.st->resid = normR;
+                a.st->x_written = 1;
+                set_done(a.st, 1, k + 2);
+            }
+            go = false;
+        } else {
+            beta = ur / udr_k;                                                              // :134-135
+            if (grp == 0 && tid == 0) {
+                a.udr[k + 1] = ur;                                                          // :136
+                a.alphas[k] = alpha;
+                if (FLUSH) a.st->x_written = 1;
+            }
+        }
+    }
+    if (!go) {   // uniform over the grid: every workgroup hands its tickets back, nobody reduces
+#pragma unroll
+        for (int q = 0; q < TPW; ++q) {
+            __asm__ volatile("" ::"v"(mk[q]), "v"(re[q]), "v"(pe[q]));
+#pragma unroll
+            for (int j = 0; j < KM; ++j)
+                if (j != JM1 && j != JP1) __asm__ volatile("" ::"v"(rv[q][j]), "v"(pv[q][j]));
+            if (FLUSH) {
+                __asm__ volatile("" ::"v"(xo[q]));
+#pragma unroll
+                for (int t = 1; t < kPcgDefer; ++t) __asm__ volatile("" ::"v"(pp[q][t - 1]));
+            }
+            if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
+                __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)), 1u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+    }
+    __shared__ GridSumTile<1> gsl[TPW];
+    if (pub) {
+        if (tid < TPW) gsl[tid].cnt = 0;
+        if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
+        __syncthreads();
+    }
+    double pn[TPW][KM], acc[TPW], yv[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j == JM1 || j == JP1) continue;
+            const double u = JAC == 2 ? a.ds * rv[q][j] : rv[q][j];   // u = precond.applyRight(r)  :123
+            pn[q][j] = u + beta * pv[q][j];                          // p = u + beta*p  :138
+        }
+        const double ue = JAC == 2 ? a.ds * re[q] : re[q];
+        const double pne = ue + beta * pe[q];
+        pn[q][JM1] = wave_shift1<true>(pn[q][JD], pne);
+        pn[q][JP1] = wave_shift1<false>(pn[q][JD], pne);
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        const bool has = tv[q] && row < n;
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {   // stored order, rounded product (spmv_diag_kernel)
+            const double t = sum + dd.v[j] * pn[q][j];
+            sum = ((mk[q] >> j) & 1u) ? t : sum;
+        }
+        yv[q] = spmv_row_value<kSpmvDot>(has, sum, pn[q][JD], acc[q]);
+    }
+    if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        const bool has = tv[q] && row < n;
+        if (FLUSH && has) {
+            double xn = xo[q];
+#pragma unroll
+            for (int t = kPcgDefer - 1; t >= 1; --t)
+                if (t <= qp) xn = xn + a.alphas[k - t] * pp[q][t - 1];   // x = x + alpha*p  :121 (iteration k-t)
+            xn = xn + alpha * pv[q][JD];                                   // :121
+            __builtin_nontemporal_store(xn, a.x + row);
+        }
+        if (has) pnext[row] = pn[q][JD];
+        spmv_store_row<kSpmvDot>(has, row, yv[q], a.Ap);
+    }
 }
 
 // Persistent form of spmv_diag_kernel (round 5 lab, PSK_SPMV_PERSIST=1): one resident grid, each workgroup
@@ -1672,6 +1854,58 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     return PSK_OK;
 }
 
+// the DPP neighbour order of a 5-diagonal layout (spmv_diag_kernel's NB): 1 FD stored, 2 sorted, 0 neither
+static int diag_nb(const psk_csr *A) {
+    if (!kDiagDpp || !A->dg_mask || A->dg_K != 5) return 0;
+    if (A->dg_d[0] == 0 && A->dg_d[3] == -1 && A->dg_d[4] == 1) return 1;
+    if (A->dg_d[2] == 0 && A->dg_d[1] == -1 && A->dg_d[3] == 1) return 2;
+    return 0;
+}
+
+static std::atomic<int> g_pcg_fused{-1};   // -1: PSK_PCG_FUSED not read yet
+static bool pcg_fused_on() {
+    int v = g_pcg_fused.load();
+    if (v < 0) {
+        const char *e = std::getenv("PSK_PCG_FUSED");
+        int expect = -1;
+        g_pcg_fused.compare_exchange_strong(expect, e && std::atoi(e) != 0 ? 1 : 0);
+        v = g_pcg_fused.load();
+    }
+    return v != 0;
+}
+
+bool pcg_fused_eligible(const psk_csr *A, int jac) {
+    return pcg_fused_on() && !A->comm && A->n > 0 && (jac == 0 || jac == 2) && diag_nb(A) != 0;
+}
+
+int launch_pcg_fused(const psk_csr *A, int jac, const PcgFusedK &a, double *pap_out, hipStream_t s, hipEvent_t ev0,
+                     hipEvent_t ev1) {
+    if (!pcg_fused_eligible(A, jac)) return fail(PSK_ERR_ARG, "launch_pcg_fused: not eligible");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    const int nb = diag_nb(A);
+    const int64_t nwg = (A->n + kSlice - 1) / kSlice, nwgd = (nwg + 1) / 2;
+    GridSum gs;
+    PSK_TRY(gridsum_prepare(c, nwg, 1, pap_out, &gs));
+    const DiagDesc dd = diag_desc(A);
+    const TileMap tmd = tile_map_for(nwgd, spmv_xcd_bands());
+    const bool flush = pcg_pending(a.k) == kPcgDefer - 1 || a.k == a.maxiter - 1;
+#define PSK_FUSED(J, NB, F)                                                                                         \
+    hipExtLaunchKernelGGL((pcg_fused_kernel<J, NB, F>), dim3((unsigned)nwgd), dim3(kBlock), 0, s, ev0, ev1, 0, A->n, \
+                          A->dg_mask, dd, a, gs, tmd, nwg)
+#define PSK_FUSED_J(J)                                                                                              \
+    do {                                                                                                            \
+        if (nb == 1) { if (flush) PSK_FUSED(J, 1, true); else PSK_FUSED(J, 1, false); }                             \
+        else { if (flush) PSK_FUSED(J, 2, true); else PSK_FUSED(J, 2, false); }                                    \
+    } while (0)
+    if (jac == 2) PSK_FUSED_J(2);
+    else PSK_FUSED_J(0);
+#undef PSK_FUSED_J
+#undef PSK_FUSED
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
 // ---------------------------------------------------------------------------------------------
 // FDLaplacian2D on the device (examples/FDLaplacian2D.py:5-23). Row k = m*iy + ix stores
 // [diag, -m, +m, -1, +1] minus absent neighbours; rowptr in closed form
@@ -2221,3 +2455,10 @@ int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, 
 }
 
 }  // extern "C"
+
+// lab / tests: the fused K3 + SpMV launch of the PCG loop on (1) or off (0); returns the previous setting
+extern "C" int psk_lab_pcg_fused(int32_t on) {
+    const int prev = psk::pcg_fused_on() ? 1 : 0;
+    psk::g_pcg_fused.store(on ? 1 : 0);
+    return prev;
+}
