@@ -232,6 +232,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle": {"iters": sys_.settle_iters(), "note": "one untimed solve before the warm-up iterations (~0.3 s: "
+                                                             "GPU clocks settle; same count on every rank)"},
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "strong",
@@ -424,6 +426,7 @@ class PcgSystem:
         self.N = N
         t0 = time.time()
         n, _ = fd_sizes(m)
+        self.n = n
         self.A = ctypes.c_void_p()
         if comm is not None:
             rb, re_ = ctypes.c_int64(), ctypes.c_int64()
@@ -468,6 +471,13 @@ class PcgSystem:
         sync; per region the max over ranks of (wall time, mean SpMV launch time). events: libpsk
         records HIP events around every SpMV launch (the roofline's kernel time)."""
         N = self.N
+        # one untimed settle solve of ~0.3 s first (a count from n alone, so every rank runs the same): without
+        # it the GPU's clocks were still rising through the first timed regions (round 5: regions 6033 -> 6282
+        # it/s and the SpMV launch 0.061 -> 0.056 ms in order)
+        settle = self.settle_iters()
+        if settle > 0:
+            r = self.run(settle, False)
+            assert r.iters == settle, r.iters
         if warmup > 0:   # the same path as the timed regions (the timing events are created here, not in region 1)
             r = self.run(warmup, events)
             assert r.iters == warmup, r.iters
@@ -489,6 +499,10 @@ class PcgSystem:
                 dt, spmv_ms = float(t[0]), float(t[1])
             out.append((dt, spmv_ms, res.spmv_launches))
         return out
+
+    def settle_iters(self):
+        """Iterations of the settle solve: ~0.3 s at the measured rates (2000 at N = 10M, 74 at 16384^2)."""
+        return max(20, min(5000, int(2e10 / max(1, self.n))))
 
     def layout(self):
         N = self.N

@@ -2,10 +2,11 @@
 """The headline regions' SpMV launches in a rocprofv3 --kernel-trace CSV of `bench.py` (evidence tool).
 
     python tools/region_trace.py run_kernel_trace.csv [--kernel spmv_diag_kernel<1] \
-        [--workgroups 19541] [--warmup 5] [--steps 20] [--regions 5]
+        [--workgroups 19541] [--settle 1999] [--warmup 5] [--steps 20] [--regions 5]
 
-bench.py's first launches of the in-loop SpMV at the headline size are the warmup solve's (`--warmup`
-iterations), then the timed regions (`--regions` x `--steps`). Prints the mean duration over exactly those
+bench.py's first launches of the in-loop SpMV at the headline size are the settle solve's (`--settle`
+iterations: PcgSystem.settle_iters, 1999 at N = 10M) and the warmup solve's (`--warmup` iterations), then the
+timed regions (`--regions` x `--steps`). Prints the mean duration over exactly those
 timed launches, per region, and over every launch of the kernel at that grid in the whole run (what a
 `--stats` summary averages), so the bench line's `roofline.avg_launch_ms` (HIP events on every 8th launch of
 the median region) can be compared with the profiler on the same launches.
@@ -21,6 +22,7 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--kernel", default="spmv_diag_kernel<1,")
     ap.add_argument("--workgroups", type=int, default=19541)
+    ap.add_argument("--settle", type=int, default=1999)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--regions", type=int, default=5)
@@ -37,7 +39,8 @@ def main():
         launches.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]) - int(r["Start_Timestamp"])))
     launches.sort()
     durs = [d for _, d in launches]
-    timed = durs[a.warmup:a.warmup + a.steps * a.regions]
+    skip = a.settle + a.warmup
+    timed = durs[skip:skip + a.steps * a.regions]
     per_region = [statistics.mean(timed[i * a.steps:(i + 1) * a.steps]) / 1e3 for i in range(a.regions)
                   if timed[i * a.steps:(i + 1) * a.steps]]
     print(json.dumps({"kernel": a.kernel, "workgroups": a.workgroups, "launches_in_trace": len(durs),
