@@ -232,8 +232,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "settle": {"iters": sys_.settle_iters(), "note": "one untimed solve before the warm-up iterations (~0.3 s: "
-                                                             "GPU clocks settle; same count on every rank)"},
+            "settle": {"iters": sys_.settle_iters(), "note": "one untimed solve (~0.3 s; same count on every rank) after "
+                                                             "the warm-up iterations, right before the first timed region"},
             "ms_per_step": dt * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "strong",
@@ -471,16 +471,18 @@ class PcgSystem:
         sync; per region the max over ranks of (wall time, mean SpMV launch time). events: libpsk
         records HIP events around every SpMV launch (the roofline's kernel time)."""
         N = self.N
-        # one untimed settle solve of ~0.3 s first (a count from n alone, so every rank runs the same): without
-        # it the GPU's clocks were still rising through the first timed regions (round 5: regions 6033 -> 6282
-        # it/s and the SpMV launch 0.061 -> 0.056 ms in order)
+        if warmup > 0:   # the same path as the timed regions (the timing events are created here, not in region 1)
+            r = self.run(warmup, events)
+            assert r.iters == warmup, r.iters
+        # then one untimed settle solve of ~0.3 s (a count from n alone, so every rank runs the same), right
+        # before the first region: without it the first regions ran slower (round 5: 6033 -> 6282 it/s in order,
+        # the SpMV launch 0.061 -> 0.056 ms), and a short solve (W = 5) between it and region 1 still left
+        # region 1 ~2% slow (a candidate cause: it writes 6 of the 8 p ring buffers, a 20-iteration one all 8)
+        # (profiles/r5_region_order_probe.txt)
         settle = self.settle_iters()
         if settle > 0:
             r = self.run(settle, False)
             assert r.iters == settle, r.iters
-        if warmup > 0:   # the same path as the timed regions (the timing events are created here, not in region 1)
-            r = self.run(warmup, events)
-            assert r.iters == warmup, r.iters
         out = []
         for _ in range(max(1, repeats)):
             barrier()

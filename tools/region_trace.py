@@ -4,8 +4,8 @@
     python tools/region_trace.py run_kernel_trace.csv [--kernel spmv_diag_kernel<1] \
         [--workgroups 19541] [--settle 1999] [--warmup 5] [--steps 20] [--regions 5]
 
-bench.py's first launches of the in-loop SpMV at the headline size are the settle solve's (`--settle`
-iterations: PcgSystem.settle_iters, 1999 at N = 10M) and the warmup solve's (`--warmup` iterations), then the
+bench.py's first launches of the in-loop SpMV at the headline size are the warmup solve's (`--warmup`
+iterations) and the settle solve's (`--settle` iterations: PcgSystem.settle_iters, 1999 at N = 10M), then the
 timed regions (`--regions` x `--steps`). Prints the mean duration over exactly those
 timed launches, per region, and over every launch of the kernel at that grid in the whole run (what a
 `--stats` summary averages), so the bench line's `roofline.avg_launch_ms` (HIP events on every 8th launch of
