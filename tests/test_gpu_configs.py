@@ -9,8 +9,9 @@ from it are crossed at size) on the device vs the oracle GMRES(m) driven by the 
 
 configs[4]: PCG + AMG(numIters=2, 5 levels) on -FDLaplacian2D 8192^2 (FDBratu2D.py:15 sign): the
 hierarchy's level sizes, every device operator against the host scipy operators bit for bit, each
-coarse operator against R_k (A_{k+1} P_k) recomputed on the host (MLHierarchy.py:54), and a few PCG
-iterations (run-to-run bitwise). At -FD 2048^2 (4.2M rows) one AMG apply and two PCG+AMG iterations
+coarse operator against R_k (A_{k+1} P_k) recomputed on the host (MLHierarchy.py:54), a few PCG
+iterations (run-to-run bitwise), the apply's linearity, and after 6 iterations the reported (recursive)
+residual against the true residual of the returned x. At -FD 2048^2 (4.2M rows) one AMG apply and two PCG+AMG iterations
 are compared with the oracle's V-cycle (oracle/amg.py) over the same hierarchy.
 """
 import numpy as np
@@ -97,6 +98,16 @@ def test_configs4_amg_hierarchy_and_pcg_fd8192(psk):
     assert st1.iters() == st2.iters() == 3 and st1.success()
     assert np.array_equal(st1.info["hist"], st2.info["hist"]) and np.array_equal(st1.soln(), st2.soln())
     assert np.all(np.isfinite(st1.info["hist"])) and st1.info["hist"][-1] < np.linalg.norm(b)
+    # full-size property past the oracle's reach: the recursive residual the loop reports (PCGSolver.py:122,
+    # 125) and the true residual of the returned x agree within 1e-10 ||b|| after 6 PCG+AMG iterations
+    ctl6 = _ctl(maxiter=6, tau=0.0, failOnMaxiter=False)
+    s6 = psk.PCG(control=ctl6, precond=psk.AMG(numIters=2, numLevels=5)).makeSolver()
+    s6.precond = M
+    s6.freezePrec()
+    st6 = s6.solve(dA, b)
+    assert st6.iters() == 6 and np.array_equal(st6.info["hist"][:3], st1.info["hist"])
+    r6 = b - psk.mvmult(dA, st6.soln())
+    assert abs(np.linalg.norm(r6) - st6.info["hist"][-1]) <= RTOL_RESID * np.linalg.norm(b)
     # size-independent property at full size: the V-cycle apply (x = copy(v), VCycleSolver.py:69, then
     # cycles of smoothing / restriction / prolongation, no convergence snapshot for random v) is
     # linear in v, so M(u + 2 v) = M(u) + 2 M(v) up to rounding

@@ -61,6 +61,26 @@ def test_fd16384_pcg_jacobi_vs_oracle(unsharded):
     assert np.linalg.norm(unsharded["x3"] - ref["soln"]) <= RTOL * np.linalg.norm(ref["soln"])
 
 
+def test_fd16384_true_residual_after_50_iterations(unsharded):
+    """Full-size property past the oracle's reach (its 16384^2 iterations take seconds each): after 50
+    PCG+Jacobi iterations the recursive residual the loop reports, ||r_50|| (PCGSolver.py:122,125), and
+    the true residual of the returned x, ||b - A x_50|| (one device SpMV, bit-exact to csr_matvec), agree
+    within 1e-10 ||b||; a wrong or missing x update (the deferred flushes at k = 7, 15, ..., 47 and the
+    final catch-up at k = 49) would leave an O(||b||) gap."""
+    import pysolvers_amd as psk
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, M)
+    b = unsharded["b"]
+    st = psk.PCG(control=_ctl(psk, 50), precond=psk.Jacobi()).makeSolver().solve(dA, b)
+    assert st.iters() == 50 and len(st.info["hist"]) == 50
+    x = st.soln()
+    r = b - psk.mvmult(dA, x)
+    del dA, x
+    nb = np.linalg.norm(b)
+    h = st.info["hist"]
+    assert h[-1] < 0.5 * nb                                           # the iteration made progress
+    assert abs(np.linalg.norm(r) - h[-1]) <= RTOL * nb
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
