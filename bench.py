@@ -259,7 +259,7 @@ def main():
                          **pmc,
                          "algorithmic_bytes_per_launch": blay, "avg_launch_ms": spmv_ms_med,
                          "launches": spmv_launches, "layout": lname,
-                         "timing": "HIP events libpsk records on its own stream around every %d-th SpMV launch "
+                         "timing": "HIP events libpsk records on its own stream around every %d-th SpMV launch (iteration 0's runs inside the fused init launch on the diagonal layout) "
                                    "of the median timed region (rank 0's events; max over ranks at N > 1)" % EVENT_STRIDE,
                          "csr_bytes_per_launch": bspmv,
                          "csr_count_over_time_GBps": csr_eq,

@@ -26,89 +26,54 @@
 
 namespace psk {
 
-// the solver state after the init sums bb = b.b and ur = u.r (PCGSolver.py:86-105)
-__device__ __forceinline__ void pcg_init_state(double bb, double ur, double tau, PcgState *st, double *udr,
-                                               int64_t *hdone, int64_t hgen, int32_t x_written) {
-    const double normB = sqrt(bb);                 // self.norm(b)   :86
-    st->normB = normB;
-    st->tauNormB = tau * normB;
-    st->iters = 0;
-    st->resid = 0.0;
-    st->brk_kind = 0;
-    st->live = -1;
-    st->hdone = hdone;
-    st->hgen = hgen;
-    st->last_hist = normB;
-    st->x_written = x_written;
-    udr[0] = ur;
-    if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
-        st->iters = 1;
-        set_done(st, 1, 1);
-    } else if (ur == 0.0) {                        // :104-105
-        st->brk_kind = 1;
-        st->iters = 0;
-        set_done(st, 2, 1);
-    } else {
-        st->done = 0;
-    }
-}
-
-// fused init finish: runs once, in thread 0 of the workgroup that completes the init's grid sums
-struct PcgInitFin {
-    double tau;
-    PcgState *st;
-    double *udr;
-    int64_t *hdone;
-    int64_t hgen;
-    int32_t x_written;
-    __device__ void operator()(const double *r) const { pcg_init_state(r[0], r[1], tau, st, udr, hdone, hgen, x_written); }
-};
-
 // ---- K0 (Jacobi/identity): p_0 = M b; [b.b, u.r] --------------------------------------------
-// One-shot like K2 (one 512-element tile per workgroup), the two sums finished in the same launch by
-// gridsum and, unsharded, the solver state set by the workgroup that completes them (PcgInitFin; a
-// sharded solve gathers the per-rank sums and runs pcg_init_finish_kernel). x0 = 0 is not stored:
-// K3's first flush of the deferred x updates starts from the literal 0.0 (x = np.zeros_like(b) :100,
-// then x + alpha*p :121: the same roundings). r = np.copy(b) (:97) is not stored either (round 5): K2
-// of iteration 0 reads b where it would read r, and writes r. The init streams 16 B/row (was 32).
+// One-shot, the two sums finished in the same launch by gridsum and, unsharded, the solver state set by the
+// wave that completes them (PcgInitFin; a sharded solve gathers the per-rank sums and runs
+// pcg_init_finish_kernel). x0 = 0 is not stored: K3's first flush of the deferred x updates starts from the
+// literal 0.0 (x = np.zeros_like(b) :100, then x + alpha*p :121: the same roundings). r = np.copy(b) (:97) is
+// not stored either (round 5): K2 of iteration 0 reads b where it would read r, and writes r. 16 B/row.
+// Round 5: the sums run over the SpMV's 256-row gridsum tiles with one row per lane (two tiles per
+// workgroup) and the SpMV's tile epilogue (per-row products, wave totals in wave order): the diagonal
+// layout's init fused into the first SpMV (spmv.hip pcg_init_diag_kernel) then has the same bits.
 template <int JAC, bool FUSED>
 __global__ __launch_bounds__(kBlock) void pcg_init_kernel(int64_t n, const double *__restrict__ b,
                                                           const double *__restrict__ dinv, double ds,
-                                                          double *__restrict__ p, GridSum gs, PcgInitFin fin) {
-    __shared__ double sh[kWaves];
-    const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
-    uint32_t ticket = 0;
-    double bb = 0.0, ur = 0.0;
-    if (i + 1 < n) {
-        const dv2 bi = ld2nt(b + i);
-        dv2 d{ds, ds};
-        if (JAC == 1) d = ld2nt(dinv + i);
-        ticket = gridsum_ticket(gs);
-        dv2 u = bi;
-        if (JAC) {
-            u.x = d.x * bi.x;                          // p = precond.applyRight(r)  :98
-            u.y = d.y * bi.y;
-        }
-        st2(p + i, u);                                 // (r = np.copy(b) :97 is read from b by K2)
-        bb = fma(bi.x, bi.x, bb);
-        bb = fma(bi.y, bi.y, bb);
-        ur = fma(u.x, bi.x, ur);                       // uDotR = np.dot(u, r)       :102
-        ur = fma(u.y, bi.y, ur);
-    } else {
-        ticket = gridsum_ticket(gs);
-        if (i < n) {   // odd tail element
-            const double bi = b[i];
-            const double u0 = JAC == 2 ? ds * bi : JAC ? dinv[i] * bi : bi;
-            p[i] = u0;
-            bb = bi * bi;
-            ur = u0 * bi;
-        }
+                                                          double *__restrict__ p, GridSum gs, PcgInitFin fin,
+                                                          int64_t ntiles) {
+    constexpr int TPW = 2;
+    const int tid = threadIdx.x;
+    int64_t tl[TPW];
+    bool tv[TPW];
+    double acc[TPW][2];
+    uint32_t ticket[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t t = (int64_t)blockIdx.x * TPW + q;
+        tv[q] = t < ntiles;
+        tl[q] = tv[q] ? t : ntiles - 1;
+        const int64_t row = tl[q] * kBlock + tid;
+        const bool has = tv[q] && row < n;
+        const double bi = has ? __builtin_nontemporal_load(b + row) : 0.0;
+        const double d = JAC == 1 ? (has ? dinv[row] : 0.0) : ds;
+        const double u = JAC ? d * bi : bi;                     // p = precond.applyRight(r)  :98
+        if (has) p[row] = u;                                    // (r = np.copy(b) :97 is read from b by K2)
+        acc[q][0] = has ? bi * bi : 0.0;                        // self.norm(b)  :86
+        acc[q][1] = has ? u * bi : 0.0;                         // uDotR = np.dot(u, r)  :102
     }
-    const double v[2] = {block_sum(bb, sh), block_sum(ur, sh)};
+    __shared__ GridSumTile<2> gsl[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        ticket[q] = 0;
+        if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
+            ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+    }
+    if (tid < TPW) gsl[tid].cnt = 0;
+    if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
+    __syncthreads();
     if (FUSED)
-        gridsum_publish<2>(gs, v, sh, ticket, fin);
+        gridsum_tiles_publish<TPW, 2>(gs, gsl, acc, ticket, tl, tv, fin);
     else
-        gridsum_publish<2>(gs, v, sh, ticket);
+        gridsum_tiles_publish<TPW, 2>(gs, gsl, acc, ticket, tl, tv);
 }
 
 // sharded init: the per-rank sums all-gathered, added in rank order (bit-identical on every rank)
@@ -263,8 +228,18 @@ constexpr int kPcgFinishWord = 8;
 static_assert(sizeof(PcgState) % 8 == 0 && kPcgFinishWord + kPcgStateWords + 1 <= 64, "SolveKit::hmap words");
 __global__ __launch_bounds__(kBlock) void pcg_finish_kernel(const PcgState *st, const uint32_t *cnt, const int32_t *err,
                                                             int64_t *hw) {
+    // every counter (kGridSumMaxGroups + 1) loaded at once, unconditionally (indices clamped): one memory
+    // round trip instead of a dependent chain of nine
+    constexpr int kPer = (kGridSumMaxGroups + kBlock) / kBlock;
+    uint32_t v[kPer];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) {
+        const int g = (int)threadIdx.x + i * kBlock;
+        v[i] = cnt[(int64_t)(g < kGridSumMaxGroups ? g : kGridSumMaxGroups) * kGridSumCntStride];
+    }
     uint32_t any = 0;
-    for (int g = threadIdx.x; g <= kGridSumMaxGroups; g += kBlock) any |= cnt[(int64_t)g * kGridSumCntStride];
+#pragma unroll
+    for (int i = 0; i < kPer; ++i) any |= v[i];
     const bool bad = __syncthreads_or(any != 0);
     if (threadIdx.x < kPcgStateWords)
         __hip_atomic_store(hw + threadIdx.x, reinterpret_cast<const int64_t *>(st)[threadIdx.x], __ATOMIC_RELAXED,
@@ -446,15 +421,20 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     // in-launch (gridsum), so the loop's scalars are part1[0] = p.Ap and part2[0..1] = (r.r, u.r)
     const int64_t nv = n > 0 ? (n + kVecTile - 1) / kVecTile : 1;
     if (nv > INT32_MAX) return fail(PSK_ERR_UNSUPPORTED, "psk_pcg: vector too long for a one-shot grid");
+    // the init: unsharded with the diagonal layout (5 diagonals, one DInv value or none) fused into the first
+    // SpMV (spmv.hip pcg_init_diag_kernel, [p.Ap, b.b, u.r] into part1); otherwise pcg_init_kernel over the
+    // SpMV's 256-row tiles (the same bits for b.b and u.r), or the general path's init over 512-element tiles
+    const bool init_diag = !gen && !sharded && (jac == 0 || jac == 2) && pcg_init_diag_eligible(A);
+    const int64_t nsl = n > 0 ? (n + kBlock - 1) / kBlock : 1;
     GridSum gs0, gs2, gs3;
-    PSK_TRY(gridsum_prepare(c, nv, 2, w.pinit, &gs0));
+    if (!init_diag) PSK_TRY(gridsum_prepare(c, gen ? nv : nsl, 2, w.pinit, &gs0));
     PSK_TRY(gridsum_prepare(c, nv, 2, w.part2, &gs2));
     PSK_TRY(gridsum_prepare(c, nv, 1, w.part3, &gs3));
     // the host-mapped done stamp the kernels write (set_done); no kernel of an earlier solve is running
     volatile int64_t *hdone = kit->hmap;
     const int64_t hgen = (int64_t)(++kit->solve_gen & 0x7FFFFF) << kStampGenShift;
     *hdone = 0;
-    const PcgInitFin fin{ctl->tau, w.st, w.udr, const_cast<int64_t *>(hdone), hgen, gen ? 1 : 0};
+    const PcgInitFin fin{ctl->tau, w.st, w.udr, const_cast<int64_t *>(hdone), hgen, gen ? 1 : 0, 0};
     const double *bd = b;
     if (!dev_io) {   // host b staged in r (r_0 = b already: K2 of iteration 0 then reads r as usual), or, on
                      // the general path, in Ap (unused until the first SpMV; its init copies r = b)
@@ -473,9 +453,14 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         if (n > 0) hipLaunchKernelGGL(pcg_gen_init_kernel, dim3(nb), dim3(kBlock), 0, s, n, bd, w.x, w.r);
         PSK_TRY(prec_apply_dev(M, n, w.r, w.u, s));                   // p = precond.applyRight(r)  :98
         hipLaunchKernelGGL(pcg_gen_init2_kernel, gk, dim3(kBlock), 0, s, n, w.r, w.u, w.p, gs0, fin);
+    } else if (init_diag) {
+        PcgInitFin fin3 = fin;
+        fin3.off = 1;
+        PSK_TRY(launch_pcg_init_diag(A, bd, jac == 2 ? ds : 1.0, w.p, w.Ap, w.part1, fin3, s));
     } else {
+        const dim3 gi((unsigned)((nsl + 1) / 2));
 #define PSK_PCG_INIT(J, F) \
-        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gk, dim3(kBlock), 0, s, n, bd, dinv, ds, w.p, gs0, fin)
+        hipLaunchKernelGGL((pcg_init_kernel<J, F>), gi, dim3(kBlock), 0, s, n, bd, dinv, ds, w.p, gs0, fin, nsl)
         if (jac == 2) { if (sharded) PSK_PCG_INIT(2, false); else PSK_PCG_INIT(2, true); }
         else if (jac == 1) { if (sharded) PSK_PCG_INIT(1, false); else PSK_PCG_INIT(1, true); }
         else { if (sharded) PSK_PCG_INIT(0, false); else PSK_PCG_INIT(0, true); }
@@ -502,7 +487,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     int64_t tk[kTimedSlots];
     for (int i = 0; i < TP; ++i) tk[i] = -1;
     std::vector<float> spmv_ms;
-    if (ctl->time_kernels) spmv_ms.assign((size_t)maxiter, 0.0f);
+    if (ctl->time_kernels) spmv_ms.assign((size_t)maxiter, -1.0f);   // -1: not sampled
     auto harvest = [&](int slot) -> int {
         if (tk[slot] < 0) return PSK_OK;
         float ms = 0.f;
@@ -565,7 +550,8 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         }
         // every time_kernels-th SpMV between two events (sampled: an event pair costs ~5% of an
         // iteration at N = 10M)
-        const bool timed = ctl->time_kernels > 0 && k % ctl->time_kernels == 0;
+        // (init_diag: iteration 0's SpMV ran inside the init launch, not sampled)
+        const bool timed = ctl->time_kernels > 0 && k % ctl->time_kernels == 0 && !(init_diag && k == 0);
         int slot = (int)((k / (ctl->time_kernels > 0 ? ctl->time_kernels : 1)) % TP);
         if (timed) {
             if ((rc = harvest(slot)) != PSK_OK) break;
@@ -574,7 +560,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         // a timed launch records its events in its own dispatch (kernel start / end)
         // (fused: the timed launch is the fused one of the same k)
         uint64_t seq1 = 0;
-        if ((!fused || k == 0) &&
+        if ((!fused || k == 0) && !(init_diag && k == 0) &&
             (rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, fused ? papb[0] : w.part1, &w.st->done, s,
                               timed && !fused ? ta[slot] : nullptr, timed && !fused ? tb[slot] : nullptr, 0,
                               mbc ? &seq1 : nullptr)) != PSK_OK)
@@ -729,7 +715,11 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             const int64_t nrun = fused && nk > 0 ? nk - 1 : nk;
             const int64_t cnt = nrun < (int64_t)spmv_ms.size() ? nrun : (int64_t)spmv_ms.size();
             int64_t nt = 0;
-            for (int64_t i = 0; i < cnt; i += ctl->time_kernels, ++nt) tot += spmv_ms[(size_t)i];
+            for (int64_t i = 0; i < cnt; i += ctl->time_kernels)
+                if (spmv_ms[(size_t)i] >= 0.0f) {
+                    tot += spmv_ms[(size_t)i];
+                    ++nt;
+                }
             res->spmv_launches = nt;
             res->spmv_ms = nt > 0 ? tot / (double)nt : 0.0;
         }

@@ -39,6 +39,47 @@ __device__ __forceinline__ void set_done(PcgState *st, int32_t v, int64_t stamp)
     }
 }
 
+// the solver state after the init sums bb = b.b and ur = u.r (PCGSolver.py:86-105)
+__device__ __forceinline__ void pcg_init_state(double bb, double ur, double tau, PcgState *st, double *udr,
+                                               int64_t *hdone, int64_t hgen, int32_t x_written) {
+    const double normB = sqrt(bb);                 // self.norm(b)   :86
+    st->normB = normB;
+    st->tauNormB = tau * normB;
+    st->iters = 0;
+    st->resid = 0.0;
+    st->brk_kind = 0;
+    st->live = -1;
+    st->hdone = hdone;
+    st->hgen = hgen;
+    st->last_hist = normB;
+    st->x_written = x_written;
+    udr[0] = ur;
+    if (normB == 0.0) {                            // :87-88 handleConvergence(0, zeros, 0, 0)
+        st->iters = 1;
+        set_done(st, 1, 1);
+    } else if (ur == 0.0) {                        // :104-105
+        st->brk_kind = 1;
+        st->iters = 0;
+        set_done(st, 2, 1);
+    } else {
+        st->done = 0;
+    }
+}
+
+// fused init finish: runs once, in thread 0 of the workgroup that completes the init's grid sums
+struct PcgInitFin {
+    double tau;
+    PcgState *st;
+    double *udr;
+    int64_t *hdone;
+    int64_t hgen;
+    int32_t x_written;
+    int32_t off;   // b.b and u.r are sums off, off + 1 of the launch (the diagonal layout's fused init: 1)
+    __device__ void operator()(const double *r) const {
+        pcg_init_state(r[off], r[off + 1], tau, st, udr, hdone, hgen, x_written);
+    }
+};
+
 // Deferred x updates (Jacobi/identity K3): x is read and written every kPcgDefer-th iteration only.
 // p_j lives in ring buffer j mod kPcgDefer; K3 of iteration k reads p_k and writes p_{k+1} over
 // p_{k+1-kPcgDefer}, which the last flush consumed (or, on a flush, which this K3 reads first, element
@@ -102,6 +143,13 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
     if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
     return true;
 }
+
+// the PCG init fused into the first SpMV (spmv.hip, pcg_init_diag_kernel): the diagonal layout in the
+// 5-diagonal DPP order, unsharded; xs = the one DInv value (Jacobi) or 1.0 (none). [p_0.Ap_0, b.b, u.r] into
+// out3[0..2], p_0 into p, Ap_0 into Ap; fin runs on sums 1 and 2 (fin.off = 1)
+bool pcg_init_diag_eligible(const psk_csr *A);
+int launch_pcg_init_diag(const psk_csr *A, const double *b, double xs, double *p, double *Ap, double *out3,
+                         const PcgInitFin &fin, hipStream_t s);
 
 // the fused K3(k) + SpMV(k+1) launch of the PCG loop (spmv.hip, pcg_fused_kernel)
 struct PcgFusedK {

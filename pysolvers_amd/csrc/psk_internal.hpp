@@ -669,8 +669,9 @@ __device__ __forceinline__ uint32_t gridsum_tile_begin(const GridSum &gs, GridSu
     return t;
 }
 
-template <int W>
-__device__ __forceinline__ void gridsum_final_wave(const GridSum &gs) {
+// fin: see gridsum_final (run by lane 0 of the wave that finished the W sums)
+template <int W, class F = GridSumNoFin>
+__device__ __forceinline__ void gridsum_final_wave(const GridSum &gs, const F &fin = F()) {
     const bool lane0 = (threadIdx.x & 63) == 0;
     uint32_t f = 0;
     if (lane0) f = gridsum_draw(gridsum_counter(gs, kGridSumMaxGroups));
@@ -683,6 +684,7 @@ __device__ __forceinline__ void gridsum_final_wave(const GridSum &gs) {
 #pragma unroll
         for (int c = 0; c < W; ++c) gs.out[c] = r[c];
         gridsum_mail<W>(gs, r);
+        fin(r);
     }
 }
 
@@ -740,6 +742,72 @@ __device__ __forceinline__ void gridsum_tile_publish(const GridSum &gs, GridSumT
         for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
     }
     gridsum_final_wave<W>(gs);
+}
+
+// The tile epilogue of a workgroup holding TPW gridsum tiles with W sums each (the W = 1 form is the SpMV's
+// spmv_publish_multi): each wave's totals (DPP) combined in LDS in wave order per tile, every tile's slot
+// stored first, then a wave holding a group's last ticket reduces that group; fin: see gridsum_final.
+// Every thread, after the tiles' LDS counters were zeroed behind a barrier; tv[q] uniform.
+template <int TPW, int W, class F = GridSumNoFin>
+__device__ __forceinline__ void gridsum_tiles_publish(const GridSum &gs, GridSumTile<W> *L, const double (*acc)[W],
+                                                      const uint32_t *ticket, const int64_t *tl, const bool *tv,
+                                                      const F &fin = F()) {
+    const bool lane0 = (threadIdx.x & 63) == 0;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    bool mine[TPW];
+    uint32_t tk[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        mine[q] = false;
+        tk[q] = 0;
+        if (!tv[q]) continue;
+        double ws[W];
+#pragma unroll
+        for (int c = 0; c < W; ++c) ws[c] = wave_total(acc[q][c]);
+        uint32_t old = 0;
+        if (lane0) {
+#pragma unroll
+            for (int c = 0; c < W; ++c) L[q].part[wave * W + c] = ws[c];
+            if (threadIdx.x == 0) L[q].ticket = ticket[q];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            old = atomicAdd(&L[q].cnt, 1u);
+        }
+        if (__builtin_amdgcn_readfirstlane(old) != kWaves - 1) continue;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        double sum[W];
+#pragma unroll
+        for (int c = 0; c < W; ++c) {
+            sum[c] = L[q].part[c];
+#pragma unroll
+            for (int w = 1; w < kWaves; ++w) sum[c] += L[q].part[w * W + c];   // wave order
+        }
+        tk[q] = L[q].ticket;
+        if (lane0)
+#pragma unroll
+            for (int c = 0; c < W; ++c)
+                gridsum_put(gs.grp_log2 < 0 ? gs.gslots + tl[q] * W + c : gs.slots + gridsum_slot(gs, tl[q]) * W + c, sum[c]);
+        mine[q] = true;
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        if (!mine[q]) continue;
+        if (gs.grp_log2 < 0) {
+            gridsum_final_wave<W>(gs, fin);
+            continue;
+        }
+        const int64_t g = gridsum_group_of(tl[q], gs.grp_log2);
+        int64_t base;
+        const int64_t cnt = gridsum_members(gs, g, base);
+        if (tk[q] != (uint32_t)(cnt - 1)) continue;
+        double r[W];
+        gridsum_take<W, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
+        if (lane0) {
+            gridsum_reset(gridsum_counter(gs, g));
+#pragma unroll
+            for (int c = 0; c < W; ++c) gridsum_put(gs.gslots + g * W + c, r[c]);
+        }
+        gridsum_final_wave<W>(gs, fin);
+    }
 }
 
 // host: a GridSum for a one-shot launch of nt tiles (workgroups) with W (<= kGridSumMaxW) sums

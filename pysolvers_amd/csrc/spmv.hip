@@ -776,6 +776,90 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
     PSK_SPMV_PROF_AT(2);
 }
 
+// ---- the PCG init fused into the first SpMV (round 5; diagonal layout in a DPP order, unsharded, Jacobi with one
+// DInv value or none): p_0 = M b (PCGSolver.py:98) computed where this SpMV gathers it (xs * b[c]: xs = the DInv
+// value, or 1.0), Ap_0 = A p_0 (:111) and the three sums [p_0.Ap_0, b.b, u.r] (:113, :86, :102) through the
+// SpMV's tile epilogue; the wave that finishes them runs the init's state logic (PcgInitFin, sums 1 and 2), and
+// p_0 is stored for K3. One launch instead of pcg_init_kernel + the SpMV of iteration 0 (b read once, not b and
+// then p_0). b.b and u.r have pcg_init_kernel's bits (same 256-row tiles, same per-row products, wave totals in
+// wave order), p_0.Ap_0 and Ap_0 the SpMV's (p_0 = xs * b is the product pcg_init_kernel stores).
+template <int NB>
+__global__ __launch_bounds__(kBlock) void pcg_init_diag_kernel(int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd,
+                                                               const double *__restrict__ b, double xs,
+                                                               double *__restrict__ p, double *__restrict__ y,
+                                                               GridSum gs, PcgInitFin fin, TileMap tm, int64_t ntiles) {
+    constexpr int TPW = kDiagTpw, KM = 5;
+    static_assert(NB == 1 || NB == 2, "the DPP orders of spmv_diag_kernel");
+    constexpr int JD = NB == 1 ? 0 : 2, JM1 = NB == 1 ? 3 : 1, JP1 = NB == 1 ? 4 : 3;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int64_t grp = tile_of_block(tm);
+    int64_t tl[TPW];
+    bool tv[TPW];
+    uint32_t mk[TPW];
+    double xv[TPW][KM], xe[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t t = grp * TPW + q;
+        tv[q] = t < ntiles;
+        tl[q] = tv[q] ? t : ntiles - 1;
+        mk[q] = __builtin_nontemporal_load(mask + tl[q] * kSlice + tid);
+    }
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j == JM1 || j == JP1) continue;
+            xv[q][j] = b[diag_col(dd, n, row, j)];
+        }
+        xe[q] = b[diag_col_off(dd, n, row, lane == 0 ? -1 : (lane == 63 ? 1 : 0))];
+    }
+    uint32_t ticket[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        ticket[q] = 0;
+        if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
+            ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
+    }
+    __shared__ GridSumTile<3> gsl[TPW];
+    if (tid < TPW) gsl[tid].cnt = 0;
+    if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
+    __syncthreads();
+    double acc[TPW][3], yv[TPW], pv[TPW];
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        const bool has = tv[q] && row < n;
+        const double braw = xv[q][JD];   // b[row] (the d = 0 column of a row < n is the row itself)
+#pragma unroll
+        for (int j = 0; j < KM; ++j)
+            if (j != JM1 && j != JP1) xv[q][j] = xs * xv[q][j];   // u = precond.applyRight(r)  :98
+        xe[q] = xs * xe[q];
+        xv[q][JM1] = wave_shift1<true>(xv[q][JD], xe[q]);
+        xv[q][JP1] = wave_shift1<false>(xv[q][JD], xe[q]);
+        double sum = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {   // stored order, rounded product (spmv_diag_kernel)
+            const double t = sum + dd.v[j] * xv[q][j];
+            sum = ((mk[q] >> j) & 1u) ? t : sum;
+        }
+        pv[q] = xv[q][JD];
+        yv[q] = sum;
+        acc[q][0] = has ? pv[q] * sum : 0.0;    // np.dot(p, Ap)  :113 (spmv_row_value's eq * sum)
+        acc[q][1] = has ? braw * braw : 0.0;    // self.norm(b)   :86
+        acc[q][2] = has ? pv[q] * braw : 0.0;   // np.dot(u, r)   :102
+    }
+    gridsum_tiles_publish<TPW, 3>(gs, gsl, acc, ticket, tl, tv, fin);
+#pragma unroll
+    for (int q = 0; q < TPW; ++q) {
+        const int64_t row = tl[q] * kSlice + tid;
+        if (tv[q] && row < n) {
+            __builtin_nontemporal_store(yv[q], y + row);
+            p[row] = pv[q];
+        }
+    }
+}
+
 // ---- PCG K3 fused into the next SpMV (round 5; diagonal layout, 5 diagonals, unsharded, Jacobi with one DInv
 // value or no preconditioner): one launch per iteration k does K3(k) and K1(k+1) of pcg.hip —
 //   alpha, ||r||, the convergence test, beta (pcg_direction_scalars), x's deferred updates on a flush,
@@ -1872,6 +1956,28 @@ static bool pcg_fused_on() {
         v = g_pcg_fused.load();
     }
     return v != 0;
+}
+
+bool pcg_init_diag_eligible(const psk_csr *A) { return !A->comm && A->n > 0 && diag_nb(A) != 0; }
+
+int launch_pcg_init_diag(const psk_csr *A, const double *b, double xs, double *p, double *Ap, double *out3,
+                         const PcgInitFin &fin, hipStream_t s) {
+    if (!pcg_init_diag_eligible(A)) return fail(PSK_ERR_ARG, "launch_pcg_init_diag: not eligible");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    const int64_t nwg = (A->n + kSlice - 1) / kSlice, nwgd = (nwg + kDiagTpw - 1) / kDiagTpw;
+    GridSum gs;
+    PSK_TRY(gridsum_prepare(c, nwg, 3, out3, &gs));
+    const DiagDesc dd = diag_desc(A);
+    const TileMap tmd = tile_map_for(nwgd, spmv_xcd_bands());
+    if (diag_nb(A) == 1)
+        hipLaunchKernelGGL(pcg_init_diag_kernel<1>, dim3((unsigned)nwgd), dim3(kBlock), 0, s, A->n, A->dg_mask, dd, b, xs,
+                           p, Ap, gs, fin, tmd, nwg);
+    else
+        hipLaunchKernelGGL(pcg_init_diag_kernel<2>, dim3((unsigned)nwgd), dim3(kBlock), 0, s, A->n, A->dg_mask, dd, b, xs,
+                           p, Ap, gs, fin, tmd, nwg);
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
 }
 
 bool pcg_fused_eligible(const psk_csr *A, int jac) {
