@@ -84,6 +84,29 @@ def layout_bytes(N, A, n):
     return stream.value + 16 * n, LAYOUT_NAMES[lay.value]
 
 
+_PHASE = {"name": "start", "t0": time.time()}
+
+
+def progress(name):
+    """Phase marker on stderr (stdout carries only the JSON line). A daemon thread repeats the current phase
+    every 30 s, so a long host-side phase (SuperLU's ILUT at 2896^2, the AMG setup: ~50-130 s of host work on
+    the GPU box) is not mistaken for a hung run."""
+    _PHASE["name"], _PHASE["t0"] = name, time.time()
+    sys.stderr.write("bench: %s\n" % name)
+    sys.stderr.flush()
+
+
+def _heartbeat():
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(30)
+            sys.stderr.write("bench: ... %s (%.0f s)\n" % (_PHASE["name"], time.time() - _PHASE["t0"]))
+            sys.stderr.flush()
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -205,7 +228,9 @@ def main():
                 N.check(N.lib.psk_comm_init(world, rank, uid, ctypes.byref(comm)), "psk_comm_init")
             dots = "rccl"
 
+    _heartbeat()
     # ---- the headline: the metric's N = 10M system on `world` GPUs ----------------------------------
+    progress("headline N=%d" % (args.side * args.side))
     m = args.side
     n, nnz = fd_sizes(m)
     sys_ = PcgSystem(N, m, comm if world > 1 else None, world)
@@ -286,8 +311,10 @@ def main():
             out["spmv_plain_batch50"] = {"avg_launch_ms": bms.value,
                                          "achieved_GBps": blay / (bms.value * 1e-3) / 1e9,
                                          "frac": blay / (bms.value * 1e-3) / 1e9 / HBM_PEAK_GBPS, **pbb}
+            progress("fixed_overhead")
             out["fixed_overhead"] = fixed_overhead(sys_, args.steps)
             if args.general:
+                progress("general_path")
                 out["general_path"] = general_path(N, sys_.A, sys_.db, sys_.dsol, m, args.steps)
             out["spmv_csr_layout_batch50"] = csr_layout_batch(N, sys_.A, sys_.db, sys_.dsol, bspmv, reps=50)
             # the north star's "CSR SpMV" inside the PCG loop: the same solve with the CSR layout
@@ -299,6 +326,7 @@ def main():
     # ---- configs[3]'s 16384^2 system at the same N: the strong-scaling series of the >= 6x target ----
     if args.scaling_side and args.scaling_side != m:
         ms_ = args.scaling_side
+        progress("strong_scaling_%d" % ms_)
         big = PcgSystem(N, ms_, comm if world > 1 else None, world)
         reg = big.regions(args.scaling_steps, 5, 3, barrier, dist)
         if rank == 0:
@@ -320,14 +348,19 @@ def main():
 
     if rank == 0:
         if world == 1 and args.config1 and m != 4096:
+            progress("configs1_pcg_jacobi_4096")
             out["configs1_pcg_jacobi_4096"] = pcg_4096(N)
         if world == 1 and args.gmres:
+            progress("gmres30_jacobi_4096")
             out["gmres30_jacobi_4096"] = gmres_arnoldi(N)
         if world == 1 and args.config2:
+            progress("configs2_gmres30_ilut (host SuperLU ILUT first)")
             out["configs2_gmres30_ilut"] = gmres_ilut(N)
         if world == 1 and args.config4:
+            progress("configs4_pcg_amg_8192 (host SA setup first)")
             out["configs4_pcg_amg_8192"] = pcg_amg(N)
         if world == 1 and args.cpu_iters > 0:
+            progress("cpu_baseline")
             out["cpu_baseline"] = cpu_baseline(m, args.cpu_iters)
         else:
             out["cpu_baseline"] = None
