@@ -347,3 +347,28 @@ def test_diag_layout_refused(psk):
             dA.set_layout("diag")
         assert dA.layout == before
         assert np.array_equal(psk.mvmult(dA, x), A @ x)
+
+
+@pytest.mark.parametrize("prec", ["jacobi", "identity"])
+def test_pcg_init_edges_diag_vs_csr(psk, prec, monkeypatch):
+    """The PCG init fused into the first SpMV (diagonal layout, spmv.hip pcg_init_diag_kernel) against
+    pcg_init_kernel + the CSR SpMV, at the init's edges: b = 0 (PCGSolver.py:87-88, converged before any
+    iteration), maxiter 0, 1 and 2 (the loop stops before, at and right after the fused launch's first
+    consumer), a 1-line grid and a grid smaller than one 256-row tile: identical status, x and history."""
+    from oracle import fdlap
+    cases = []
+    for m in (1, 2, 9, 64):
+        A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+        b = A @ np.random.default_rng(m).random(m * m)
+        cases += [(A, b, k) for k in (0, 1, 2, 30)] + [(A, np.zeros(m * m), 5)]
+    for A, b, k in cases:
+        out = []
+        for lay in ("csr", "diag"):
+            monkeypatch.setenv("PSK_SPMV_LAYOUT", lay)
+            ctl = _ctl(maxiter=k, tau=1e-10, failOnMaxiter=False)
+            pre = psk.Jacobi() if prec == "jacobi" else psk.IdentityPreconditionerType()
+            st = psk.PCG(control=ctl, precond=pre).makeSolver().solve(A, b)
+            out.append((st.iters(), bool(st.success()), st.soln(), np.asarray(st.info["hist"])))
+        (i1, s1, x1, h1), (i2, s2, x2, h2) = out
+        assert (i1, s1) == (i2, s2), (A.shape, k)
+        assert np.array_equal(x1, x2) and np.array_equal(h1, h2), (A.shape, k)
