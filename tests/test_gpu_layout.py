@@ -368,7 +368,9 @@ def test_pcg_init_edges_diag_vs_csr(psk, prec, monkeypatch):
             ctl = _ctl(maxiter=k, tau=1e-10, failOnMaxiter=False)
             pre = psk.Jacobi() if prec == "jacobi" else psk.IdentityPreconditionerType()
             st = psk.PCG(control=ctl, precond=pre).makeSolver().solve(A, b)
-            out.append((st.iters(), bool(st.success()), st.soln(), np.asarray(st.info["hist"])))
+            h = st.info.get("hist")   # absent where the reference reports no iteration (b = 0, maxiter 0)
+            out.append((st.iters(), bool(st.success()), st.soln(), None if h is None else np.asarray(h)))
         (i1, s1, x1, h1), (i2, s2, x2, h2) = out
         assert (i1, s1) == (i2, s2), (A.shape, k)
-        assert np.array_equal(x1, x2) and np.array_equal(h1, h2), (A.shape, k)
+        assert np.array_equal(x1, x2), (A.shape, k)
+        assert (h1 is None) == (h2 is None) and (h1 is None or np.array_equal(h1, h2)), (A.shape, k)
