@@ -117,7 +117,11 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         const dv2 ro = FIRST ? ld2nt(b + i) : ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2(dinv + i);
+#if defined(PSK_LAB_K2_NOSUM) || defined(PSK_LAB_K2_NOPUB)
+        ticket = 0;
+#else
         ticket = gridsum_ticket(gs, tile);
+#endif
         dv2 rn;
         rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
         rn.y = ro.y - alpha * a.y;
@@ -132,13 +136,30 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
+#if defined(PSK_LAB_K2_NOSUM) || defined(PSK_LAB_K2_NOPUB)
+        ticket = 0;
+#else
         ticket = gridsum_ticket(gs, tile);
+#endif
         const double rn = (FIRST ? b[i] : r[i]) - alpha * Ap[i];
         const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
         rr = rn * rn;
         ur = u0 * rn;
     }
+#ifdef PSK_LAB_K2_NOSUM   // development probe (scripts/build_variant.sh): no grid sums at all — wrong scalars
+    if (rr == 1.2345e-300 && ur == 1.0) r[0] = 0.0;   // keeps the sums live; probe only
+    if (blockIdx.x == 0 && threadIdx.x == 0) gs.out[0] = gs.out[1] = 1.0;   // nonzero scalars: the loop runs on
+    (void)ticket;
+    return;
+#endif
+#ifdef PSK_LAB_K2_NOPUB      // development probe: the block sums, no slot store / ticket reduction — wrong scalars
+    const double vp[2] = {block_sum(rr, sh), block_sum(ur, sh)};
+    if (vp[0] == 1.2345e-300 && threadIdx.x == 0) r[0] = vp[1];
+    if (blockIdx.x == 0 && threadIdx.x == 0) gs.out[0] = gs.out[1] = 1.0;
+    (void)ticket;
+    return;
+#endif
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
 }
