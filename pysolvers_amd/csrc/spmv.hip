@@ -776,6 +776,304 @@ __global__ __launch_bounds__(kBlock) void spmv_diag_kernel(
     PSK_SPMV_PROF_AT(2);
 }
 
+// ---- Pair-row diagonal SpMV (round 6): 16-B accesses, two CONTIGUOUS rows per lane ---------------------
+// spmv_diag_kernel gives each lane one row of a slice: every x gather, the y store and the aux loads move 8 B
+// per lane, the rate the guide puts at 0.54-0.70x of 16-B accesses (MI355X_MICROARCH.md, L2 table). Here a
+// lane owns rows (2l, 2l+1) of a 128-row half-slice, so x[row + d] for both rows is ONE 16-B load (8-B aligned
+// when d is odd; the rare pair whose two columns are not adjacent after the shard mapping — it straddles
+// column 0, n or the halo — is loaded element-wise), as are y, aux_q and aux_d; the presence bytes are one
+// 2-B load. The -1/+1 diagonals: row 2l's +1 and row 2l+1's -1 are the lane's own pair, row 2l's -1 and row
+// 2l+1's +1 come from the neighbouring lanes by DPP wave shifts (NB orders only). H half-slices per wave:
+//   H = 2: a wave owns a whole 256-row slice = one gridsum tile (4 slices per workgroup): it publishes its
+//          tile's slot itself — no LDS combine, no workgroup barrier; the halves' edge columns come from each
+//          other by readlane, so one edge load per wave;
+//   H = 1: two waves per slice (2 slices per workgroup), the tile's four wave totals combined in LDS as
+//          spmv_publish_multi does.
+// Bits: y as spmv_diag_kernel (each row summed from 0.0 in stored order). p.Ap: the tile sum of the one-row
+// kernels is ((T0 + T1) + T2) + T3 over their wave totals T_w = wave_total over 64 rows; a lane here holds
+// the first level of that tree (a_{2l} + a_{2l+1}), and diag_pair_totals runs the remaining levels in the same
+// operand pairs, so p.Ap is bit-identical to the CSR, sliced and one-row diagonal kernels.
+
+// 16-B accesses at 8-B alignment (x + row + d with d odd; aux arrays that are column views)
+typedef double dv2u __attribute__((ext_vector_type(2), aligned(8)));
+__device__ __forceinline__ dv2 ldu2(const double *p) {
+    const dv2u v = *reinterpret_cast<const dv2u *>(p);
+    return dv2{v.x, v.y};
+}
+__device__ __forceinline__ dv2 ldu2nt(const double *p) {
+    const dv2u v = __builtin_nontemporal_load(reinterpret_cast<const dv2u *>(p));
+    return dv2{v.x, v.y};
+}
+__device__ __forceinline__ void stu2(double *p, dv2 v) { *reinterpret_cast<dv2u *>(p) = dv2u{v.x, v.y}; }
+__device__ __forceinline__ void stu2nt(double *p, dv2 v) {
+    __builtin_nontemporal_store(dv2u{v.x, v.y}, reinterpret_cast<dv2u *>(p));
+}
+
+// the wave totals of the two 64-row halves of a 128-row half-slice whose lane l holds v = a_{2l} + a_{2l+1}:
+// wave_total's levels after its first (quad_perm [1,0,3,2] on a_{2l}, a_{2l+1}) in the same operand pairs —
+//   quad sums: lanes 2j, 2j+1 of the pair layout hold the one-row layout's quad j;
+//   wave_total's row_ror 4 then row_ror 8 leave ((Q0 + Q3) + (Q2 + Q1)) in lane 0 of each 16-lane row: here a
+//   row's four quads are lanes 8r..8r+7, so row_half_mirror puts Q0 + Q3 in lane 8r and Q2 + Q1 in lane 8r+4,
+//   and row_shl 4 adds the latter to the former;
+//   the four row totals of a one-row wave (its lanes 0/16/32/48) are lanes 0/8/16/24 (first half) and
+//   32/40/48/56 (second half), added in that order.
+__device__ __forceinline__ double lane_f64(double x, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(x), l),
+                            __builtin_amdgcn_readlane(__double2loint(x), l));
+}
+__device__ __forceinline__ void diag_pair_totals(double v, double &t0, double &t1) {
+    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f64<0x141>(v);   // row_half_mirror
+    v += dpp_f64<0x104>(v);   // row_shl:4
+    t0 = ((lane_f64(v, 0) + lane_f64(v, 8)) + lane_f64(v, 16)) + lane_f64(v, 24);
+    t1 = ((lane_f64(v, 32) + lane_f64(v, 40)) + lane_f64(v, 48)) + lane_f64(v, 56);
+}
+
+// x at the columns of rows r, r + 1 on diagonal offset d (the diag_col mapping): one 16-B load at the pair's
+// first column when the two columns are adjacent and in range. The rare pair that is not (it straddles column
+// 0 or n, or a shard's halo) is marked in `fix` and re-read element-wise by diag_pair_fix once every load of
+// the wave has been issued and waited for: a fix-up branch between the loads put a vmcnt wait (the pair load
+// and the element loads share their destination registers) in front of every later gather
+struct PairFix {
+    int64_t c0, c1;   // the clamped columns (diag_col's clamp)
+    bool bad;         // not one 16-B pair
+};
+__device__ __forceinline__ dv2 diag_pair_x(const DiagDesc &dd, int64_t n, int64_t r, int64_t d,
+                                           const double *__restrict__ x, PairFix &f) {
+    int64_t c0 = r + d, c1 = c0 + 1;
+    c0 += c0 < 0 ? dd.lo : (c0 >= n ? dd.hi : 0);
+    c1 += c1 < 0 ? dd.lo : (c1 >= n ? dd.hi : 0);
+    f.bad = !(c1 == c0 + 1 && c0 >= 0 && c1 < dd.ncols);
+    f.c0 = c0 < 0 ? 0 : (c0 >= dd.ncols ? dd.ncols - 1 : c0);
+    f.c1 = c1 < 0 ? 0 : (c1 >= dd.ncols ? dd.ncols - 1 : c1);
+    const int64_t a = c0 < 0 ? 0 : (c0 > dd.ncols - 2 ? dd.ncols - 2 : c0);   // ncols >= 2 (host check)
+    return ldu2(x + a);
+}
+__device__ __forceinline__ void diag_pair_fix(dv2 &v, const PairFix &f, const double *__restrict__ x) {
+    if (f.bad) {
+        v.x = x[f.c0];
+        v.y = x[f.c1];
+    }
+}
+
+// 8 workgroups per CU (<= 64 VGPRs) where that does not spill: the H = 2 forms of the modes with aux loads keep
+// more in flight and are left at 4
+template <int MODE, int NB, int H>
+__global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kSpmvDot) ? 4 : 8) void spmv_diagp_kernel(
+    int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd, const double *__restrict__ x, double *__restrict__ y,
+    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
+    TileMap tm, int64_t ntiles) {
+    constexpr int KM = 5;
+    static_assert(NB == 1 || NB == 2, "the 5-diagonal DPP orders");
+    static_assert(H == 1 || H == 2, "half-slices per wave");
+    constexpr int JD = NB == 1 ? 0 : 2, JM1 = NB == 1 ? 3 : 1, JP1 = NB == 1 ? 4 : 3;
+    constexpr int GD = NB == 1 ? 0 : 1;   // the d = 0 pair among the three gathered diagonals
+    constexpr int TPB = H == 2 ? kWaves : kWaves / 2;   // slices (gridsum tiles) per workgroup
+    constexpr bool JX = MODE == kSpmvJacobiDot;           // gathers of (DInv * q)[c]
+    constexpr bool EQ = MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot;
+    const int32_t dnv = (done ? done : &g_spmv_never_done)[spmv_vzero()];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t grp = tile_of_block(tm);
+    const int64_t t = grp * TPB + (H == 2 ? wave : wave >> 1);   // this wave's slice
+    const bool tv = t < ntiles;                                   // wave-uniform
+    const int64_t tl = tv ? t : ntiles - 1;
+    const int64_t r0 = tl * kSlice + (H == 2 ? 0 : 128 * (wave & 1));   // first row of the wave's first half
+    uint32_t mk[H];
+    dv2 xv[H][3], dg[H][3], eq[H];
+    PairFix fx[H][3];
+    double xe, de = 1.0;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+        const int64_t row = r0 + 128 * h + 2 * lane;
+        mk[h] = __builtin_nontemporal_load(reinterpret_cast<const uint16_t *>(mask + row));   // padded slices
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+        const int64_t row = r0 + 128 * h + 2 * lane;
+        int g = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j == JM1 || j == JP1) continue;   // from the d = 0 pair (own lane and neighbours)
+            xv[h][g] = diag_pair_x(dd, n, row, dd.d[j], x, fx[h][g]);
+            if (JX) dg[h][g] = diag_pair_x(dd, n, row, dd.d[j], aux_d, fx[h][g]);
+            ++g;
+        }
+        eq[h] = dv2{0.0, 0.0};
+        if (EQ) eq[h] = ldu2(aux_q + (row + 1 < n ? row : (n >= 2 ? n - 2 : 0)));   // n >= 2 (host check)
+    }
+    {   // the wave's edge columns: lane 0 x[first row - 1], lane 63 x[last row + 1]; the other lanes re-read
+        // their own x[row] (one load instruction, no branch)
+        const int64_t er = lane == 0 ? r0 - 1 : (lane == 63 ? r0 + 128 * H : r0 + 2 * lane);
+        const int64_t c = diag_col_off(dd, n, er, 0);
+        xe = x[c];
+        if (JX) de = aux_d[c];
+    }
+    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
+    const bool pub = PUB && spmv_publishes<MODE>(gs);
+    const bool drawer = H == 2 || (wave & 1) == 0;   // the wave that draws its slice's ticket
+    uint32_t ticket = 0;
+    if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0)
+        ticket = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)));
+    if (__builtin_amdgcn_readfirstlane(dnv) != 0) {   // uniform: the solve has stopped; tickets handed back
+#pragma unroll
+        for (int h = 0; h < H; ++h) {
+            __asm__ volatile("" ::"v"(mk[h]));
+#pragma unroll
+            for (int g = 0; g < 3; ++g) {
+                __asm__ volatile("" ::"v"(xv[h][g].x), "v"(xv[h][g].y));
+                if (JX) __asm__ volatile("" ::"v"(dg[h][g].x), "v"(dg[h][g].y));
+            }
+            if (EQ) __asm__ volatile("" ::"v"(eq[h].x), "v"(eq[h].y));
+        }
+        __asm__ volatile("" ::"v"(xe), "v"(de));
+        if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0)
+            __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    __shared__ GridSumTile<1> gsl[H == 1 ? TPB : 1];
+    if (H == 1 && pub) {
+        if (threadIdx.x < TPB) gsl[threadIdx.x].cnt = 0;
+        __syncthreads();
+    }
+    if (pub && threadIdx.x == 0 && blockIdx.x == 0 && (gs.nt + TPB - 1) / TPB != gridDim.x) atomicOr(gs.err, 2);
+    // the rare pairs that are not one 16-B load, then (DInv*q)[c] products (JX), all after every load was issued
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+#pragma unroll
+        for (int g = 0; g < 3; ++g) {
+            diag_pair_fix(xv[h][g], fx[h][g], x);
+            if (JX) {
+                diag_pair_fix(dg[h][g], fx[h][g], aux_d);
+                xv[h][g].x = dg[h][g].x * xv[h][g].x;   // (DInv*q)[c], rounded
+                xv[h][g].y = dg[h][g].y * xv[h][g].y;
+            }
+        }
+    if (JX) xe = de * xe;
+    // the +-1 neighbours: g = GD is the d = 0 pair (x[row], x[row + 1]) of every lane
+    double xl[H], xr[H];   // x[row - 1] of the lane's first row, x[row + 2] of its second
+    if constexpr (H == 2) {
+        const double a63 = lane_f64(xv[0][GD].y, 63), b0 = lane_f64(xv[1][GD].x, 0);
+        xl[0] = wave_shift1<true>(xv[0][GD].y, xe);                    // lane 0: the loaded x[r0 - 1]
+        xr[0] = wave_shift1<false>(xv[0][GD].x, b0);                   // lane 63: row 128 = half 1's lane 0
+        xl[1] = wave_shift1<true>(xv[1][GD].y, a63);                   // lane 0: row 127 = half 0's lane 63
+        xr[1] = wave_shift1<false>(xv[1][GD].x, xe);                   // lane 63: the loaded x[r0 + 256]
+    } else {
+        xl[0] = wave_shift1<true>(xv[0][GD].y, xe);
+        xr[0] = wave_shift1<false>(xv[0][GD].x, xe);
+    }
+    double acc[H];
+    dv2 yv[H];
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+        const int64_t row = r0 + 128 * h + 2 * lane;
+        // the five diagonals' x of each row in j order (stored order)
+        double c0[KM], c1[KM];
+        int g = 0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {
+            if (j == JM1) {
+                c0[j] = xl[h];
+                c1[j] = xv[h][GD].x;
+            } else if (j == JP1) {
+                c0[j] = xv[h][GD].y;
+                c1[j] = xr[h];
+            } else {
+                c0[j] = xv[h][g].x;
+                c1[j] = xv[h][g].y;
+                ++g;
+            }
+        }
+        const uint32_t m0 = mk[h] & 0xffu, m1 = mk[h] >> 8;
+        double s0 = 0.0, s1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM; ++j) {   // stored order, rounded product; absent diagonals by a select
+            const double u0 = s0 + dd.v[j] * c0[j], u1 = s1 + dd.v[j] * c1[j];
+            s0 = ((m0 >> j) & 1u) ? u0 : s0;
+            s1 = ((m1 >> j) & 1u) ? u1 : s1;
+        }
+        const bool has0 = tv && row < n, has1 = tv && row + 1 < n;
+        double e0 = eq[h].x, e1 = eq[h].y;
+        if (EQ && row + 1 >= n) {   // the last pair of an odd n: aux_q was loaded one row early
+            e0 = eq[h].y;
+            e1 = 0.0;
+        }
+        if (MODE == kSpmvDot) {   // x[row]: the d = 0 gather when the row stores its diagonal
+            const bool f0 = (m0 >> JD) & 1u, f1 = (m1 >> JD) & 1u;
+            e0 = f0 ? c0[JD] : 0.0;
+            e1 = f1 ? c1[JD] : 0.0;
+            if (!f0 && has0) e0 = x[row];   // rare: a row without its diagonal
+            if (!f1 && has1) e1 = x[row + 1];
+        }
+        double a0, a1;
+        yv[h].x = spmv_row_value<MODE>(has0, s0, e0, a0);
+        yv[h].y = spmv_row_value<MODE>(has1, s1, e1, a1);
+        acc[h] = a0 + a1;   // wave_total's first level
+    }
+    if (pub && tv) {
+        double w[2 * H];
+#pragma unroll
+        for (int h = 0; h < H; ++h) diag_pair_totals(acc[h], w[2 * h], w[2 * h + 1]);
+        bool reduce = false;
+        uint32_t tk = 0;
+        double s = 0.0;
+        if (H == 2) {   // the wave is the tile
+            s = ((w[0] + w[1]) + w[2]) + w[3];
+            tk = __builtin_amdgcn_readfirstlane(ticket);
+            reduce = true;
+        } else {        // two waves per tile: the later one publishes
+            GridSumTile<1> &L = gsl[wave >> 1];
+            const int hb = wave & 1;
+            uint32_t old = 0;
+            if (lane == 0) {
+                L.part[2 * hb] = w[0];
+                L.part[2 * hb + 1] = w[1];
+                if (hb == 0) L.ticket = ticket;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+                old = atomicAdd(&L.cnt, 1u);
+            }
+            if (__builtin_amdgcn_readfirstlane(old) == 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+                s = ((L.part[0] + L.part[1]) + L.part[2]) + L.part[3];
+                tk = L.ticket;
+                reduce = true;
+            }
+        }
+        if (reduce) {
+            if (gs.grp_log2 < 0) {
+                if (lane == 0) gridsum_put(gs.gslots + tl, s);
+                gridsum_final_wave<1>(gs);
+            } else {
+                if (lane == 0) gridsum_put(gs.slots + gridsum_slot(gs, tl), s);
+                const int64_t g = gridsum_group_of(tl, gs.grp_log2);
+                int64_t base;
+                const int64_t cnt = gridsum_members(gs, g, base);
+                if (tk == (uint32_t)(cnt - 1)) {
+                    double r[1];
+                    gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
+                    if (lane == 0) {
+                        gridsum_reset(gridsum_counter(gs, g));
+                        gridsum_put(gs.gslots + g, r[0]);
+                    }
+                    gridsum_final_wave<1>(gs);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int h = 0; h < H; ++h) {   // y after the dot epilogue (spmv_row_value)
+        const int64_t row = r0 + 128 * h + 2 * lane;
+        if (!tv || row >= n) continue;
+        if (row + 1 < n) {
+            if (MODE == kSpmvResid || MODE == kSpmvAdd) stu2(y + row, yv[h]);
+            else stu2nt(y + row, yv[h]);
+        } else {
+            spmv_store_row<MODE>(true, row, yv[h].x, y);
+        }
+    }
+}
+
 // ---- the PCG init fused into the first SpMV (round 5; diagonal layout in a DPP order, unsharded, Jacobi with one
 // DInv value or none): p_0 = M b (PCGSolver.py:98) computed where this SpMV gathers it (xs * b[c]: xs = the DInv
 // value, or 1.0), Ap_0 = A p_0 (:111) and the three sums [p_0.Ap_0, b.b, u.r] (:113, :86, :102) through the
@@ -1738,6 +2036,15 @@ static bool spmv_csr_bands() {
 }
 
 // lab: the persistent diagonal-layout kernel (PSK_SPMV_PERSIST=1) and its workgroups per CU
+// the pair-row diagonal kernel: 0 off (spmv_diag_kernel), 1 or 2 half-slices per wave (PSK_DIAG_PAIR)
+static int diag_pair_h() {
+    static const int v = [] {
+        const char *e = std::getenv("PSK_DIAG_PAIR");
+        const int h = e ? std::atoi(e) : 2;
+        return h == 0 || h == 1 ? h : 2;
+    }();
+    return v;
+}
 static bool spmv_persist() {
     static const bool on = [] {
         const char *e = std::getenv("PSK_SPMV_PERSIST");
@@ -1814,9 +2121,21 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const int nbk = !kDiagDpp || A->dg_K != 5 ? 0
                         : (A->dg_d[0] == 0 && A->dg_d[3] == -1 && A->dg_d[4] == 1) ? 1
                         : (A->dg_d[2] == 0 && A->dg_d[1] == -1 && A->dg_d[3] == 1) ? 2 : 0;
+        // round 6: the pair-row kernel (16-B accesses) for the two DPP orders
+        const int pairh = (nbk != 0 && A->n >= 2 && dd.ncols >= 2) ? diag_pair_h() : 0;
+        const int64_t nwgp = pairh ? (nwg + (pairh == 2 ? 4 : 2) - 1) / (pairh == 2 ? 4 : 2) : 1;
+        const dim3 gdp((unsigned)nwgp);
+        const TileMap tmp = tile_map_for(nwgp, spmv_xcd_bands(), rev != 0);
+#define PSK_DIAGP(M, NB, H)                                                                                        \
+    hipExtLaunchKernelGGL((spmv_diagp_kernel<M, NB, H>), gdp, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, x, y, aux_d, \
+                          aux_q, gs, done_flag, tmp, nwg)
 #define PSK_DIAG_LAUNCH(M, KM)                                                                                     \
     do {                                                                                                           \
-        if (KM == 5 && nbk == 1)                                                                                   \
+        if (KM == 5 && pairh == 2 && nbk == 1) PSK_DIAGP(M, 1, 2);                                                 \
+        else if (KM == 5 && pairh == 2 && nbk == 2) PSK_DIAGP(M, 2, 2);                                            \
+        else if (KM == 5 && pairh == 1 && nbk == 1) PSK_DIAGP(M, 1, 1);                                            \
+        else if (KM == 5 && pairh == 1 && nbk == 2) PSK_DIAGP(M, 2, 1);                                            \
+        else if (KM == 5 && nbk == 1)                                                                              \
             hipExtLaunchKernelGGL((spmv_diag_kernel<M, 5, kDiagTpw, 1>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, \
                                   dd, x, y, aux_d, aux_q, gs, done_flag, tmd, nwg);                                 \
         else if (KM == 5 && nbk == 2)                                                                              \
@@ -1847,6 +2166,7 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         }
 #undef PSK_DIAG_MODE
 #undef PSK_DIAG_LAUNCH
+#undef PSK_DIAGP
         PSK_HIP(hipGetLastError());
         return PSK_OK;
     }

@@ -374,3 +374,30 @@ def test_pcg_init_edges_diag_vs_csr(psk, prec, monkeypatch):
         assert (i1, s1) == (i2, s2), (A.shape, k)
         assert np.array_equal(x1, x2), (A.shape, k)
         assert (h1 is None) == (h2 is None) and (h1 is None or np.array_equal(h1, h2)), (A.shape, k)
+
+
+def test_fd_pair_kernel_two_level_sums(psk, monkeypatch):
+    """The pair-row diagonal kernel (spmv_diagp_kernel: two contiguous rows per lane, 16-B accesses) at a size
+    whose fused dot products take the two-level gridsum (1887 tiles, odd n, odd line length): PCG+Jacobi
+    (kSpmvDot), GMRES+Jacobi (kSpmvJacobiDot, kSpmvPlainDot, kSpmvResid) and PCG with no preconditioner give the
+    CSR layout's trajectories bit for bit — the kernel's wave totals follow wave_total's operand pairs."""
+    from oracle import fdlap
+    m = 695
+    A = fdlap.fd_laplacian_2d(-1.0, 1.0, m)
+    b = A @ np.random.default_rng(17).random(m * m)
+    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
+    assert dA.layout == "diag"
+    runs = {}
+    for lay in ("diag", "csr"):
+        dA.set_layout(lay)
+        runs[lay] = [
+            psk.PCG(control=_ctl(maxiter=60, tau=0.0, failOnMaxiter=False), precond=psk.Jacobi()).makeSolver()
+            .solve(dA, b),
+            psk.PCG(control=_ctl(maxiter=45, tau=0.0, failOnMaxiter=False)).makeSolver().solve(dA, b),
+            psk.GMRES(control=_ctl(maxiter=25, tau=1e-30, failOnMaxiter=False), precond=psk.Jacobi()).makeSolver()
+            .solve(dA, b),
+        ]
+    for d, c in zip(runs["diag"], runs["csr"]):
+        assert d.iters() == c.iters() and d.success() == c.success()
+        assert np.array_equal(d.soln(), c.soln())
+        assert np.array_equal(d.info["hist"], c.info["hist"])
