@@ -84,27 +84,86 @@ def layout_bytes(N, A, n):
     return stream.value + 16 * n, LAYOUT_NAMES[lay.value]
 
 
-_PHASE = {"name": "start", "t0": time.time()}
+class Liveness:
+    """Progress that advances only when work completes, and a watchdog on it (round 6).
+
+    `tick` is called when a libpsk call returns (bench wraps N.check), when a timed region or solve ends, and
+    at host setup sub-steps; `phase` names what runs now and whether it is GPU work ("gpu": libpsk calls
+    return every few seconds at most) or one long host call ("host": SuperLU's spilu at 2896^2, the SA setup,
+    the CPU oracle). A daemon thread prints, every `beat_s`, the phase, the progress counter and the age of its
+    last advance; when the counter has not advanced for the phase's limit it prints the stuck phase and ends
+    the process with exit code 3 (no restart, no re-exec) instead of leaving a stalled device call to the
+    driver's time limit. The printed line changes only with the counter and its age, so a stall reads as one."""
+
+    def __init__(self, gpu_stall_s=150.0, host_stall_s=420.0, beat_s=30.0, clock=time.monotonic, write=None,
+                 exit_fn=None):
+        self.gpu_stall_s, self.host_stall_s, self.beat_s = gpu_stall_s, host_stall_s, beat_s
+        self.clock = clock
+        self.write = write or (lambda msg: (sys.stderr.write(msg + "\n"), sys.stderr.flush()))
+        self.exit_fn = exit_fn or os._exit
+        self.t_start = clock()
+        self.name, self.kind, self.count, self.what = "start", "host", 0, "start"
+        self.t_last = self.t_phase = self.t_start
+
+    def phase(self, name, kind="gpu"):
+        self.name, self.kind = name, kind
+        self.t_phase = self.clock()
+        self.tick("phase " + name)
+        self.write("bench: %s (%s phase, t=%.1f s)" % (name, kind, self.t_phase - self.t_start))
+
+    def tick(self, what=""):
+        self.count += 1
+        self.what = what
+        self.t_last = self.clock()
+
+    def limit(self):
+        return self.gpu_stall_s if self.kind == "gpu" else self.host_stall_s
+
+    def line(self):
+        now = self.clock()
+        return "bench: %s [%s] progress %d, last: %s %.0f s ago (phase %.0f s)" % (
+            self.name, self.kind, self.count, self.what, now - self.t_last, now - self.t_phase)
+
+    def stalled(self):
+        """The watchdog's verdict now: None, or the message it ends the run with."""
+        age = self.clock() - self.t_last
+        if age <= self.limit():
+            return None
+        return ("bench: WATCHDOG: no progress in %s phase '%s' for %.0f s (limit %.0f s; last advance: %s, "
+                "progress %d): exiting with code 3" % (self.kind, self.name, age, self.limit(), self.what, self.count))
+
+    def start(self):
+        import threading
+
+        def run():
+            while True:
+                time.sleep(self.beat_s)
+                self.write(self.line())
+                msg = self.stalled()
+                if msg:
+                    self.write(msg)
+                    self.exit_fn(3)
+                    return
+        threading.Thread(target=run, daemon=True).start()
 
 
-def progress(name):
-    """Phase marker on stderr (stdout carries only the JSON line). A daemon thread repeats the current phase
-    every 30 s, so a long host-side phase (SuperLU's ILUT at 2896^2, the AMG setup: ~50-130 s of host work on
-    the GPU box) is not mistaken for a hung run."""
-    _PHASE["name"], _PHASE["t0"] = name, time.time()
-    sys.stderr.write("bench: %s\n" % name)
-    sys.stderr.flush()
+LIVE = Liveness()
 
 
-def _heartbeat():
-    import threading
+def progress(name, kind="gpu"):
+    """Phase marker on stderr (stdout carries only the JSON line), with the watchdog's phase kind."""
+    LIVE.phase(name, kind)
 
-    def beat():
-        while True:
-            time.sleep(30)
-            sys.stderr.write("bench: ... %s (%.0f s)\n" % (_PHASE["name"], time.time() - _PHASE["t0"]))
-            sys.stderr.flush()
-    threading.Thread(target=beat, daemon=True).start()
+
+def _watch_libpsk(N):
+    """Every libpsk call that returns through N.check (bench's own calls and the pysolvers_amd classes') is a
+    progress tick: a kernel that never finishes blocks inside its call and stops the counter."""
+    check = N.check
+
+    def checked(rc, where):
+        LIVE.tick(where)
+        return check(rc, where)
+    N.check = checked
 
 
 def main():
@@ -129,6 +188,7 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r5_pmc_traffic_%d.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same build; %%d = the side")
     args = ap.parse_args()
+    LIVE.write("bench: start (pid %d, python %s)" % (os.getpid(), sys.version.split()[0]))
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # launched as `python bench.py --gpus N` (no torchrun): start the N ranks ourselves. Nothing in
@@ -152,7 +212,11 @@ def main():
     # called into it after the profiler had finalised it (profiles/r4_exit_fault.txt).
     if world == 1:
         os.environ.setdefault("PSK_NO_TORCH", "1")
+    LIVE.start()   # from here a stall of more than the phase's limit ends the run (exit 3) with its phase named
+    progress("start-up: load libpsk (HIP runtime)", "host")
     from pysolvers_amd import _native as N
+    _watch_libpsk(N)
+    progress("start-up: device selection")
     # one GPU per rank: LOCAL_RANK when every GPU is visible to every rank; a launcher that narrows
     # visibility per rank leaves one device (ordinal 0) per process
     ndev = N.device_count()
@@ -163,6 +227,7 @@ def main():
 
     dist = None
     if world > 1:
+        progress("start-up: torch.distributed (gloo control plane)", "host")
         import torch.distributed as dist
         # control plane only. Gloo's C++ connection log goes to fd 1; keep stdout for the ONE JSON
         # line the driver parses by pointing fd 1 at stderr while the group connects
@@ -228,7 +293,6 @@ def main():
                 N.check(N.lib.psk_comm_init(world, rank, uid, ctypes.byref(comm)), "psk_comm_init")
             dots = "rccl"
 
-    _heartbeat()
     # ---- the headline: the metric's N = 10M system on `world` GPUs ----------------------------------
     progress("headline N=%d" % (args.side * args.side))
     m = args.side
@@ -354,13 +418,13 @@ def main():
             progress("gmres30_jacobi_4096")
             out["gmres30_jacobi_4096"] = gmres_arnoldi(N)
         if world == 1 and args.config2:
-            progress("configs2_gmres30_ilut (host SuperLU ILUT first)")
+            progress("configs2_gmres30_ilut (host SuperLU ILUT first)", "host")
             out["configs2_gmres30_ilut"] = gmres_ilut(N)
         if world == 1 and args.config4:
-            progress("configs4_pcg_amg_8192 (host SA setup first)")
+            progress("configs4_pcg_amg_8192 (host SA setup first)", "host")
             out["configs4_pcg_amg_8192"] = pcg_amg(N)
         if world == 1 and args.cpu_iters > 0:
-            progress("cpu_baseline")
+            progress("cpu_baseline", "host")
             out["cpu_baseline"] = cpu_baseline(m, args.cpu_iters)
         else:
             out["cpu_baseline"] = None
@@ -525,6 +589,7 @@ class PcgSystem:
             N.check(N.lib.psk_synchronize(), "sync")
             barrier()
             dt = time.perf_counter() - t0
+            LIVE.tick("timed region")
             assert res.iters == steps and res.success == 1, (res.iters, res.success)
             spmv_ms = res.spmv_ms
             if dist is not None:
@@ -611,7 +676,7 @@ def cpu_baseline(m, iters):
     marks = []
     with threadpool_limits(limits=1):
         st = krylov.pcg(A, b, maxiter=iters + 1, tau=0.0, fail_on_maxiter=False, precond=krylov.jacobi_form(A),
-                        on_iter=lambda k: marks.append(time.perf_counter()))
+                        on_iter=lambda k: (marks.append(time.perf_counter()), LIVE.tick("oracle iteration")))
         marks.append(time.perf_counter())
     assert st["iters"] == iters + 1
     per = [marks[k + 1] - marks[k] for k in range(1, iters + 1)]
@@ -838,6 +903,7 @@ def gmres_ilut(N, m=2896, restart=30, steps=60, repeats=3):
         out["error"] = "reference ILUT factorization failed: %s" % e
         return out
     out["ilut_setup_s"] = time.time() - t
+    progress("configs2_gmres30_ilut: device solves")
     info = M.device_info()
     out.update(nnz_L=info["nnz_l"], nnz_U=info["nnz_u"], levels_L=info["levels_l"], levels_U=info["levels_u"],
                schedules=trisolve_schedules(N, M.device_handle))
@@ -899,6 +965,7 @@ def pcg_amg(N, m=8192, levels=5, cycles=2, iters=6, repeats=3):
     M = psk.AMG(numIters=cycles, numLevels=levels, smoother=psk.GaussSeidelSmoother).form(dA)
     del A
     out["amg_setup_s"] = time.time() - t1
+    progress("configs4_pcg_amg_8192: device solves")
     out["level_sizes"] = M.levels()
     out["coarse_solve"] = M.coarse_kind   # dense: streamed GEMV over A_c^-1 (dense.hip); lu: SuperLU factors
 

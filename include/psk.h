@@ -261,25 +261,6 @@ int psk_prec_trisolve_schedule(psk_prec *M, int32_t which, int32_t set, int32_t 
  * >> 1)), leading empty positions off, steps per 64-line band, dictionary records (0 = per-step
  * records). PSK_ERR_UNSUPPORTED when the factor is not a 2-D stencil. No compute (diagnostics, tests). */
 int psk_prec_trisolve_grid_info(const psk_prec *M, int32_t which, int64_t *out);
-/* Lab / tests of the triangular solves' forward progress (round 5; replaces nothing in the reference).
- * psk_lab_occupy_begin starts `wgs` workgroups of 1024 threads holding `lds_bytes` of LDS each on a
- * stream of their own, spinning until psk_lab_occupy_end releases them behind everything enqueued on the
- * solver's stream so far (or `seconds` pass: *timed_out = 1); a solve enqueued in between can use only
- * what they leave free. psk_lab_trisolve_workers: the workgroups the last sync-free launch of factor
- * `which` enrolled and the grid it was launched with (the sync-free schedule deals its rows over the
- * workgroups that started, not over the grid). */
-int psk_lab_occupy_begin(int32_t wgs, int32_t lds_bytes, double seconds);
-int psk_lab_occupy_end(int32_t *timed_out);
-/* Lab: nwg workgroups of 128 threads with lds_bytes of LDS, each spinning usec; rec_out[3*i..] = start, end
- * (s_memrealtime, 100 MHz) and XCD of workgroup i. Waits for the launch. */
-int psk_lab_dispatch_probe(int32_t nwg, int32_t lds_bytes, double usec, int64_t *rec_out);
-/* Lab: occupiers per XCD (HW_REG_XCC_ID) of the last psk_lab_occupy_begin, counts[8]. */
-int psk_lab_occupy_xcc(int32_t *counts);
-int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid);
-/* Lab / tests (round 5): the PCG loop's fused K3 + SpMV launch (diagonal layout, unsharded, Jacobi with one
- * DInv value or none) on (1) or off (0, the separate K3 and SpMV launches; same bits). Returns the previous
- * setting (initially PSK_PCG_FUSED, default off: measured no faster, profiles/r5_pcg_fused_ab.txt). */
-int psk_lab_pcg_fused(int32_t on);
 /* Host-only: the grid plan psk_prec_create_trisolve would make for one triangular factor (CSR with its
  * diagonal; upper = 1: solved from the last row up), without any device work — out[0..6] = w, H,
  * sigma2, phase, off, steps per band, record width K. PSK_ERR_UNSUPPORTED when it is not a 2-D stencil. */

@@ -81,12 +81,6 @@ SIGNATURES = {
     "psk_prec_trisolve_schedule": (ctypes.c_int, [P, I32, I32, ctypes.POINTER(I32), ctypes.POINTER(I64),
                                                    ctypes.POINTER(I32), ctypes.POINTER(F64), ctypes.POINTER(F64)]),
     "psk_prec_trisolve_grid_info": (ctypes.c_int, [P, I32, ctypes.POINTER(I64)]),
-    "psk_lab_occupy_begin": (ctypes.c_int, [I32, I32, F64]),
-    "psk_lab_occupy_end": (ctypes.c_int, [ctypes.POINTER(I32)]),
-    "psk_lab_occupy_xcc": (ctypes.c_int, [ctypes.POINTER(I32)]),
-    "psk_lab_dispatch_probe": (ctypes.c_int, [I32, I32, F64, P]),
-    "psk_lab_pcg_fused": (ctypes.c_int, [I32]),
-    "psk_lab_trisolve_workers": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "psk_trisolve_grid_plan": (ctypes.c_int, [I64, P, P, P, I32, ctypes.POINTER(I64)]),
     "psk_prec_info": (ctypes.c_int, [P, ctypes.POINTER(I32)] + [ctypes.POINTER(I64)] * 5),
     "psk_mm_info": (ctypes.c_int, [ctypes.c_char_p] + [ctypes.POINTER(I64)] * 3),
@@ -110,6 +104,34 @@ SIGNATURES = {
     "psk_csr_halo_pack": (ctypes.c_int, [P, P, P]),
     "psk_fd2d_dist_plan": (ctypes.c_int, [I64, I32, I32] + [ctypes.POINTER(I64)] * 5),
 }
+
+
+# include/psk_lab.h: libpsk_lab.so (tests / lab tools only; not part of the product library)
+LAB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libpsk_lab.so")
+LAB_SIGNATURES = {
+    "psk_lab_occupy_begin": (ctypes.c_int, [I32, I32, F64]),
+    "psk_lab_occupy_end": (ctypes.c_int, [ctypes.POINTER(I32)]),
+    "psk_lab_occupy_xcc": (ctypes.c_int, [ctypes.POINTER(I32)]),
+    "psk_lab_dispatch_probe": (ctypes.c_int, [I32, I32, F64, P]),
+    "psk_lab_trisolve_workers": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
+}
+_lab = None
+
+
+def load_lab():
+    """libpsk_lab.so (include/psk_lab.h), loaded once: a separate library linked against the libpsk.so this
+    module loaded (it shares libpsk's device context, streams and handles)."""
+    global _lab
+    if _lab is None:
+        if not os.path.exists(LAB_PATH):
+            raise ImportError("libpsk_lab.so not found at %s (make -C pysolvers_amd/csrc)" % LAB_PATH)
+        lab = ctypes.CDLL(LAB_PATH)
+        for name, (res, args) in LAB_SIGNATURES.items():
+            fn = getattr(lab, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lab = lab
+    return _lab
 
 
 def prec_info(h):

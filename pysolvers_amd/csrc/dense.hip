@@ -258,7 +258,26 @@ extern "C" int psk_prec_create_dense_inverse(const psk_csr *A, int32_t refine, p
         *out = P;
         return PSK_OK;
     }
-    auto alloc = [&](void **p, size_t bytes) { return hipMalloc(p, bytes) == hipSuccess; };
+    // a failed hipMalloc leaves HIP's sticky error set: cleared here, so the caller's fallback (AMG auto mode: the
+    // SuperLU factors) does not read it as its own launch error
+    auto alloc = [&](void **p, size_t bytes) {
+        if (hipMalloc(p, bytes) == hipSuccess) return true;
+        *p = nullptr;
+        (void)hipGetLastError();
+        return false;
+    };
+    {   // never more than half of what the device has free (the inverse is 8 n^2 bytes, allocated silently)
+        size_t fr = 0, tot = 0;
+        if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+            (void)hipGetLastError();
+            fr = 0;
+        }
+        if ((double)n * ld * 8.0 > 0.5 * (double)fr) {
+            delete P;
+            return bail(PSK_ERR_ALLOC, "the " + std::to_string((double)n * ld * 8 / 1e9) +
+                                           " GB inverse exceeds half of the free device memory");
+        }
+    }
     if (!alloc((void **)&d->M, (size_t)n * ld * sizeof(double)) ||
         (d->nseg > 1 && !alloc((void **)&d->part, (size_t)d->nseg * n * sizeof(uint64_t))) ||
         (d->nseg > 1 && !alloc((void **)&d->cnt, (size_t)d->nrb * kDenseCntStride * sizeof(uint32_t))) ||
@@ -299,7 +318,8 @@ extern "C" int psk_prec_create_dense_inverse(const psk_csr *A, int32_t refine, p
     const Rocsolver &rs = rocsolver();
     if (!rs.err.empty()) return done(PSK_ERR_UNSUPPORTED, rs.err);
     rb_handle h = nullptr;
-    if (rs.create(&h) != 0) return done(PSK_ERR_HIP, "rocblas_create_handle");
+    // rocBLAS/rocSOLVER failures are reported as unsupported, so auto mode falls back to the factors
+    if (rs.create(&h) != 0) return done(PSK_ERR_UNSUPPORTED, "rocblas_create_handle");
     int st = rs.set_stream(h, s);
     // column-major view of the row-major image: A^T; its inverse read row-major is A^-1
     if (st == 0) st = rs.getrf(h, (int32_t)n, (int32_t)n, d->M, (int32_t)ld, ipiv, info);
@@ -308,7 +328,7 @@ extern "C" int psk_prec_create_dense_inverse(const psk_csr *A, int32_t refine, p
     e = hipMemcpyAsync(hinfo, info, sizeof(hinfo), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     rs.destroy(h);
-    if (st != 0) return done(PSK_ERR_HIP, "rocSOLVER getrf/getri status " + std::to_string(st));
+    if (st != 0) return done(PSK_ERR_UNSUPPORTED, "rocSOLVER getrf/getri status " + std::to_string(st));
     if (e != hipSuccess) return done(PSK_ERR_HIP, hipGetErrorString(e));
     if (hinfo[0] != 0 || hinfo[1] != 0)
         return done(PSK_ERR_ARG, "singular matrix (getrf info " + std::to_string(hinfo[0]) + ", getri info " +

@@ -153,6 +153,9 @@ __global__ void mbox_gather_kernel(uint64_t *mine, int P, int W, double *__restr
         recv[q * W + c] = __longlong_as_double((long long)v);
         __hip_atomic_store(p, kMbSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
+    // the re-arms are visible system-wide before this rank's next mailbox stores (a later kernel's), whatever the
+    // other ranks' progress: exchange e + 4 reuses this slot
+    __threadfence_system();
 }
 
 int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s) {

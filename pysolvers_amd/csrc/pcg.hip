@@ -83,7 +83,9 @@ __global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgSt
 }
 
 // ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
-// One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses). JAC: Jacobi
+// One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses); round 6 measured one tile
+// per WAVE (four per workgroup, no barrier, the workgroup form's sums re-created by one wave: the same bits) 1-2%
+// slower at N = 10M and 16384^2 (profiles/r6_k2_wave_ab.txt). JAC: Jacobi
 // preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
 // diagonal matrices such as stencils: the same products, 8 B/row less per kernel).
 // FIRST (iteration 0): r_0 = b is read from b (the init does not copy it, K0 above).
@@ -117,11 +119,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         const dv2 ro = FIRST ? ld2nt(b + i) : ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2(dinv + i);
-#if defined(PSK_LAB_K2_NOSUM) || defined(PSK_LAB_K2_NOPUB)
-        ticket = 0;
-#else
         ticket = gridsum_ticket(gs, tile);
-#endif
         dv2 rn;
         rn.x = ro.x - alpha * a.x;                           // r = r - alpha*Ap  :122
         rn.y = ro.y - alpha * a.y;
@@ -136,30 +134,13 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         ur = fma(u0, rn.x, ur);
         ur = fma(u1, rn.y, ur);
     } else if (i < n) {   // odd tail element
-#if defined(PSK_LAB_K2_NOSUM) || defined(PSK_LAB_K2_NOPUB)
-        ticket = 0;
-#else
         ticket = gridsum_ticket(gs, tile);
-#endif
         const double rn = (FIRST ? b[i] : r[i]) - alpha * Ap[i];
         const double u0 = JAC == 2 ? ds * rn : JAC ? dinv[i] * rn : rn;
         r[i] = rn;
         rr = rn * rn;
         ur = u0 * rn;
     }
-#ifdef PSK_LAB_K2_NOSUM   // development probe (scripts/build_variant.sh): no grid sums at all — wrong scalars
-    if (rr == 1.2345e-300 && ur == 1.0) r[0] = 0.0;   // keeps the sums live; probe only
-    if (blockIdx.x == 0 && threadIdx.x == 0) gs.out[0] = gs.out[1] = 1.0;   // nonzero scalars: the loop runs on
-    (void)ticket;
-    return;
-#endif
-#ifdef PSK_LAB_K2_NOPUB      // development probe: the block sums, no slot store / ticket reduction — wrong scalars
-    const double vp[2] = {block_sum(rr, sh), block_sum(ur, sh)};
-    if (vp[0] == 1.2345e-300 && threadIdx.x == 0) r[0] = vp[1];
-    if (blockIdx.x == 0 && threadIdx.x == 0) gs.out[0] = gs.out[1] = 1.0;
-    (void)ticket;
-    return;
-#endif
     const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
 }
@@ -537,10 +518,6 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     bool halo_pending = false;
     if (overlap) PSK_TRY(comm_stream(c, &cs));
 
-    // K3(k) fused into the SpMV of k + 1 (spmv.hip, pcg_fused_kernel): the SpMV launches once, at k = 0; p.Ap
-    // alternates between two result words (launch k reads p_k.Ap_k while it sums p_{k+1}.Ap_{k+1})
-    const bool fused = !gen && !sharded && pcg_fused_eligible(A, jac);
-    double *papb[2] = {w.part1, w.part1 + 32};
     int64_t launched = 0;
     int rc = PSK_OK;
     for (int64_t k = 0; k < maxiter && rc == PSK_OK; ++k) {
@@ -579,12 +556,10 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             tk[slot] = k;
         }
         // a timed launch records its events in its own dispatch (kernel start / end)
-        // (fused: the timed launch is the fused one of the same k)
         uint64_t seq1 = 0;
-        if ((!fused || k == 0) && !(init_diag && k == 0) &&
-            (rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, fused ? papb[0] : w.part1, &w.st->done, s,
-                              timed && !fused ? ta[slot] : nullptr, timed && !fused ? tb[slot] : nullptr, 0,
-                              mbc ? &seq1 : nullptr)) != PSK_OK)
+        if (!(init_diag && k == 0) &&
+            (rc = launch_spmv(A, kSpmvDot, pk, w.Ap, nullptr, nullptr, w.part1, &w.st->done, s, timed ? ta[slot] : nullptr,
+                              timed ? tb[slot] : nullptr, 0, mbc ? &seq1 : nullptr)) != PSK_OK)
             break;
         // K2/K3 tiles in block order: XCD bands matching the SpMV's, and bands walked in alternating
         // directions (a serpentine over SpMV, K2, K3 meant to re-read Ap, r and p from the Infinity Cache),
@@ -597,7 +572,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         const uint64_t seq2 = mbc ? mbox_next(mbc, &gs2k) : 0;
         // the general path copied r = b in its init (pcg_gen_init_kernel): it never takes the FIRST form
         const bool first = k == 0 && !gen && dev_io;
-        const double *pap_k = fused ? papb[k & 1] : w.part1g;
+        const double *pap_k = w.part1g;
 #define PSK_PCG_K2(J, F)                                                                                       \
         hipLaunchKernelGGL((pcg_update_kernel<J, F>), gk, dim3(kBlock), 0, s, n, w.r, bd, w.Ap, dinv, ds, pap_k,     \
                            P, gs2k, w.st, w.udr, k, tm2)
@@ -613,12 +588,6 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             hipLaunchKernelGGL(pcg_dot_kernel, gk, dim3(kBlock), 0, s, n, w.u, w.r, gs3, w.st);
             hipLaunchKernelGGL(pcg_gen_direction_kernel, gk, dim3(kBlock), 0, s, n, w.x, w.u, w.p, w.part1, w.part2,
                                w.part3, w.st, w.udr, w.hist, k, maxiter, ctl->fail_on_maxiter);
-        } else if (fused) {
-            const PcgFusedK fk{w.x, w.r, w.pr, ds, papb[k & 1], w.part2g, w.st, w.udr, w.hist, w.alphas, w.Ap, k, maxiter,
-                               ctl->fail_on_maxiter};
-            if ((rc = launch_pcg_fused(A, jac, fk, papb[(k + 1) & 1], s, timed ? ta[slot] : nullptr,
-                                       timed ? tb[slot] : nullptr)) != PSK_OK)
-                break;
         } else {
             auto k3 = [&](int64_t t0, int64_t t1) {   // K3 over tiles [t0, t1)
                 if (t1 <= t0) return;
@@ -714,15 +683,16 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
             if (res->status == PSK_MAXITER) res->resid = maxiter > 0 ? res->resid_recursive : hs.normB;
             bool x_written = hs.x_written != 0;
             // a dot(p,Ap) breakdown at k: the iterations since the last flush deferred their x updates
+            bool more = !dev_io;   // work enqueued after the sync: the caller's x is ready only after another sync
             if (!gen && hs.done == 2 && hs.brk_kind != 1 && pcg_pending(hs.iters) > 0 && n > 0) {
                 hipLaunchKernelGGL(pcg_flush_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n,
                                    w.x, w.pr, w.alphas, (int64_t)hs.iters);
                 if (hipGetLastError() != hipSuccess) rc = fail(PSK_ERR_HIP, "pcg flush");
                 x_written = true;
+                more = true;   // also when an earlier flush had already stored x
             }
             // no iteration stored x (b = 0, dot(u,r) = 0 at the start, maxiter = 0, or a dot(p,Ap)
             // breakdown at k = 0): the solution is x0 = 0
-            bool more = x_written != (hs.x_written != 0) || !dev_io;   // work enqueued after the sync
             if (rc == PSK_OK && !x_written && n > 0) {
                 if (hipMemsetAsync(w.x, 0, (size_t)n * 8, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "x zero");
                 more = true;
@@ -732,9 +702,7 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         }
         if (ctl->time_kernels) {
             double tot = 0.0;
-            // fused: launch k of the last iteration only ran the convergence test (not a sample)
-            const int64_t nrun = fused && nk > 0 ? nk - 1 : nk;
-            const int64_t cnt = nrun < (int64_t)spmv_ms.size() ? nrun : (int64_t)spmv_ms.size();
+            const int64_t cnt = nk < (int64_t)spmv_ms.size() ? nk : (int64_t)spmv_ms.size();
             int64_t nt = 0;
             for (int64_t i = 0; i < cnt; i += ctl->time_kernels)
                 if (spmv_ms[(size_t)i] >= 0.0f) {

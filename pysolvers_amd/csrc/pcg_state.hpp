@@ -1,5 +1,5 @@
 // pcg_state.hpp — the PCG solver state and the K3 scalar logic (PCGSolver.py:113-138), shared by pcg.hip
-// (the loop, K0/K2/K3) and spmv.hip (the fused K3 + SpMV launch of the diagonal layout).
+// (the loop, K0/K2/K3) and spmv.hip (the PCG init fused into the first SpMV of the diagonal layout).
 #pragma once
 #include "psk_internal.hpp"
 
@@ -150,26 +150,5 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
 bool pcg_init_diag_eligible(const psk_csr *A);
 int launch_pcg_init_diag(const psk_csr *A, const double *b, double xs, double *p, double *Ap, double *out3,
                          const PcgInitFin &fin, hipStream_t s);
-
-// the fused K3(k) + SpMV(k+1) launch of the PCG loop (spmv.hip, pcg_fused_kernel)
-struct PcgFusedK {
-    double *x;
-    const double *r;
-    PRing pr;
-    double ds;             // the one DInv value (JAC 2)
-    const double *pap;     // p_k.Ap_k: the previous launch's grid sum
-    const double *rrur;    // K2(k)'s [r.r, u.r]
-    PcgState *st;
-    double *udr, *hist, *alphas, *Ap;
-    int64_t k, maxiter;
-    int32_t fail_on_maxiter;
-};
-
-// the diagonal layout in the 5-diagonal DPP order, unsharded, jac 0 (none) or 2 (one DInv value);
-// off by default (measured no faster); PSK_PCG_FUSED=1 or psk_lab_pcg_fused(1) turns it on
-bool pcg_fused_eligible(const psk_csr *A, int jac);
-// iteration k's launch: p.Ap of p_{k+1} into pap_out[0]; ev0/ev1 (optional) bracket the dispatch
-int launch_pcg_fused(const psk_csr *A, int jac, const PcgFusedK &a, double *pap_out, hipStream_t s, hipEvent_t ev0,
-                     hipEvent_t ev1);
 
 }  // namespace psk

@@ -243,6 +243,11 @@ struct GridExt {
     int32_t delta[kGridMaxPE];  // pattern code: ud * 64 + yd (steps back, lines back)
     int32_t yd[kGridMaxPE];     // lines back
 };
+// words of a factor's scheduling array (TriFactor::sched, ilu.hip): block tickets, publication counters, the
+// exit count and the workers the last sync-free launch enrolled, each on its own 256-B line
+constexpr int kSchedTicket = 0, kSchedPub = 64, kSchedExit = 128, kSchedLast = 192, kSchedWords = 256;
+// the grid of a sync-free triangular-solve launch (ilu.hip)
+int syncfree_grid(const Context *c);
 struct TriFactor {
     bool present = false, upper = false;
     int64_t nnz = 0;

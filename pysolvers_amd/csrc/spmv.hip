@@ -606,6 +606,12 @@ constexpr int kDiagTpw = PSK_DIAG_TPW;   // slices per workgroup
 #ifndef PSK_DIAG_DPP
 #define PSK_DIAG_DPP 1
 #endif
+// the pair-row kernel's QUAD tickets (round 6): one gridsum ticket per workgroup of four slices instead of one per
+// slice, the groups of the four slices reduced by the waves of the quad's last workgroup (same bits)
+#ifndef PSK_DIAG_QUAD
+#define PSK_DIAG_QUAD 0
+#endif
+constexpr bool kDiagQuad = PSK_DIAG_QUAD != 0;
 // the -1/+1 diagonals by DPP lane shifts (default from round 5: in-loop SpMV at N = 10M 0.0587 -> 0.0550 ms,
 // 16384^2 1.44 -> 1.28 ms, same bits; profiles/r5_diag_dpp_ab.txt; -DPSK_DIAG_DPP=0 builds the gathers)
 constexpr bool kDiagDpp = PSK_DIAG_DPP != 0;
@@ -879,6 +885,12 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
     const bool tv = t < ntiles;                                   // wave-uniform
     const int64_t tl = tv ? t : ntiles - 1;
     const int64_t r0 = tl * kSlice + (H == 2 ? 0 : 128 * (wave & 1));   // first row of the wave's first half
+#ifdef PSK_LAB_DIAGP_TFIRST   // lab probe: the ticket drawn before the loads
+    uint32_t ticket = 0;
+    if (MODE != kSpmvPlain && MODE != kSpmvAdd && spmv_publishes<MODE>(gs) && tv && (H == 2 || (wave & 1) == 0) &&
+        gs.grp_log2 >= 0 && lane == 0)
+        ticket = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)));
+#endif
     uint32_t mk[H];
     dv2 xv[H][3], dg[H][3], eq[H];
     PairFix fx[H][3];
@@ -910,11 +922,23 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
         if (JX) de = aux_d[c];
     }
     constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
+#ifdef PSK_LAB_DIAGP_NOEPI   // lab probe: no dot epilogue at all (wrong p.Ap)
+    const bool pub = false;
+#else
     const bool pub = PUB && spmv_publishes<MODE>(gs);
+#endif
     const bool drawer = H == 2 || (wave & 1) == 0;   // the wave that draws its slice's ticket
+    // QUAD (H = 2, two-level sums): ONE ticket per workgroup, on the counter of its first slice's group (below)
+    const bool quad = kDiagQuad && H == 2 && pub && gs.grp_log2 >= 0;   // kernel-uniform
+    const int64_t qctr = quad ? gridsum_group_of(grp * TPB, gs.grp_log2) : 0;
+#ifndef PSK_LAB_DIAGP_TFIRST
     uint32_t ticket = 0;
-    if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0)
+    if (quad) {
+        if (wave == 0 && lane == 0) ticket = gridsum_draw(gridsum_counter(gs, qctr));
+    } else if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0) {
         ticket = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)));
+    }
+#endif
     if (__builtin_amdgcn_readfirstlane(dnv) != 0) {   // uniform: the solve has stopped; tickets handed back
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -927,9 +951,9 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
             if (EQ) __asm__ volatile("" ::"v"(eq[h].x), "v"(eq[h].y));
         }
         __asm__ volatile("" ::"v"(xe), "v"(de));
-        if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0)
-            __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+        if (quad ? (wave == 0 && lane == 0) : (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0))
+            __hip_atomic_fetch_sub(gridsum_counter(gs, quad ? qctr : gridsum_group_of(tl, gs.grp_log2)), 1u,
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     __shared__ GridSumTile<1> gsl[H == 1 ? TPB : 1];
@@ -1011,7 +1035,34 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
         yv[h].y = spmv_row_value<MODE>(has1, s1, e1, a1);
         acc[h] = a0 + a1;   // wave_total's first level
     }
-    if (pub && tv) {
+    if (quad) {
+        // every slice's slot first (no wait of any kind), then the workgroup's ticket through LDS: when it is the
+        // last of its quad (the TPB groups its slices belong to have the same member workgroups, the quad's), wave
+        // q reduces group (first group + q) — the same members, order and bits as one ticket per slice
+        if (tv) {
+            double w[4];
+            diag_pair_totals(acc[0], w[0], w[1]);
+            diag_pair_totals(acc[H - 1], w[2], w[3]);
+            const double s = ((w[0] + w[1]) + w[2]) + w[3];
+            if (lane == 0) gridsum_put(gs.slots + gridsum_slot(gs, tl), s);
+        }
+        __shared__ uint32_t wtk;
+        if (wave == 0 && lane == 0) wtk = ticket;
+        __syncthreads();
+        int64_t base;
+        const int64_t nq = gridsum_members(gs, qctr, base);   // workgroups of the quad
+        if (wtk == (uint32_t)(nq - 1)) {
+            if (wave == 0 && lane == 0) gridsum_reset(gridsum_counter(gs, qctr));
+            const int64_t g = gridsum_group_of(t, gs.grp_log2);   // t unclamped: the group of a missing slice too
+            const int64_t cnt = g < gs.ngroups ? gridsum_members(gs, g, base) : 0;
+            if (cnt > 0) {
+                double r[1];
+                gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
+                if (lane == 0) gridsum_put(gs.gslots + g, r[0]);
+                gridsum_final_wave<1>(gs);
+            }
+        }
+    } else if (pub && tv) {
         double w[2 * H];
 #pragma unroll
         for (int h = 0; h < H; ++h) diag_pair_totals(acc[h], w[2 * h], w[2 * h + 1]);
@@ -1049,6 +1100,10 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
                 const int64_t g = gridsum_group_of(tl, gs.grp_log2);
                 int64_t base;
                 const int64_t cnt = gridsum_members(gs, g, base);
+#ifdef PSK_LAB_DIAGP_NORED   // lab probe: slots stored, the group's last ticket only resets the counter (wrong p.Ap)
+                if (tk == (uint32_t)(cnt - 1) && lane == 0) gridsum_reset(gridsum_counter(gs, g));
+                tk = 0xffffffffu;
+#endif
                 if (tk == (uint32_t)(cnt - 1)) {
                     double r[1];
                     gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
@@ -1158,284 +1213,10 @@ __global__ __launch_bounds__(kBlock) void pcg_init_diag_kernel(int64_t n, const 
     }
 }
 
-// ---- PCG K3 fused into the next SpMV (round 5; diagonal layout, 5 diagonals, unsharded, Jacobi with one DInv
-// value or no preconditioner): one launch per iteration k does K3(k) and K1(k+1) of pcg.hip —
-//   alpha, ||r||, the convergence test, beta (pcg_direction_scalars), x's deferred updates on a flush,
-//   p_{k+1} = u + beta p_k (PCGSolver.py:138), Ap_{k+1} = A p_{k+1} (:111) and p_{k+1}.Ap_{k+1} (:113).
-// A row needs p_{k+1} at its stencil columns, rows the neighbouring workgroups own: each workgroup
-// recomputes them from r and p_k (the same two roundings, so the same bits as the p_{k+1} their owners
-// store), the -1/+1 columns by DPP lane shifts as in spmv_diag_kernel. Per row it reads the presence byte,
-// r and p_k (the ±m rows again through L2) and writes p_{k+1} and Ap: 33 B/row, against 24 (K3) + 17 (SpMV)
-// and one launch boundary in two. p.Ap has the bits of the unfused pair (same slices, same per-row sums).
-// Measured (profiles/r5_pcg_fused_ab.txt): no faster than the separate launches — 0.093 ms per launch at
-// N = 10M against SpMV 0.056 + K3 0.037 (PCG 6390 vs 6540 it/s), 2.36 vs 1.30 + ~1.05 ms at 16384^2 — also
-// with one slice per workgroup (59 VGPRs, 8 workgroups per CU) or a 64-VGPR cap (spills: 2x slower). Kept as
-// the PSK_PCG_FUSED=1 / psk_lab_pcg_fused path, bit-identical to the default (tests/test_gpu_parity.py).
-template <int JAC, int NB, bool FLUSH>
-__global__ __launch_bounds__(kBlock) void pcg_fused_kernel(int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd,
-                                                           PcgFusedK a, GridSum gs, TileMap tm, int64_t ntiles) {
-    constexpr int TPW = 2, KM = 5;
-    static_assert(NB == 1 || NB == 2, "the DPP orders of spmv_diag_kernel");
-    constexpr int JD = NB == 1 ? 0 : 2, JM1 = NB == 1 ? 3 : 1, JP1 = NB == 1 ? 4 : 3;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int64_t grp = tile_of_block(tm), k = a.k;
-    const double *__restrict__ r = a.r;
-    const double *pk = a.pr.b[k % kPcgDefer];
-    // NOT __restrict__: on a flush, p_{k+1}'s buffer is p_{k+1-kPcgDefer}'s, read below first (pcg.hip K3)
-    double *pnext = a.pr.b[(k + 1) % kPcgDefer];
-    // the solver scalars are loaded first: vector loads return in order, so waiting for them (below) does
-    // not wait for the gathers issued after them; every stream and gather load then goes out before any wait
-    const int64_t live = a.st->live;
-    const double tau_nb = a.st->tauNormB, udr_k = a.udr[k], pTAp = a.pap[0], rr = a.rrur[0], ur = a.rrur[1];
-    int64_t tl[TPW];
-    bool tv[TPW];
-    uint32_t mk[TPW];
-    double rv[TPW][KM], pv[TPW][KM], re[TPW], pe[TPW];
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-        const int64_t t = grp * TPW + q;
-        tv[q] = t < ntiles;
-        tl[q] = tv[q] ? t : ntiles - 1;
-        mk[q] = __builtin_nontemporal_load(mask + tl[q] * kSlice + tid);
-    }
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-        const int64_t row = tl[q] * kSlice + tid;
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            if (j == JM1 || j == JP1) continue;
-            const int64_t c = diag_col(dd, n, row, j);
-            rv[q][j] = r[c];
-            pv[q][j] = pk[c];
-        }
-        const int64_t c = diag_col_off(dd, n, row, lane == 0 ? -1 : (lane == 63 ? 1 : 0));
-        re[q] = r[c];
-        pe[q] = pk[c];
-    }
-    // a flush: x and the pending iterations' p at this workgroup's rows (uniform branches)
-    const int qp = pcg_pending(k);
-    const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0
-    double xo[TPW], pp[TPW][kPcgDefer > 1 ? kPcgDefer - 1 : 1];
-    if (FLUSH) {
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            const int64_t row = tl[q] * kSlice + tid, rc = row < n ? row : n - 1;
-            xo[q] = x0 ? 0.0 : __builtin_nontemporal_load(a.x + rc);
-#pragma unroll
-            for (int t = 1; t < kPcgDefer; ++t)
-                pp[q][t - 1] = t <= qp ? __builtin_nontemporal_load(a.pr.b[(k - t) % kPcgDefer] + rc) : 0.0;
-        }
-    }
-    const bool pub = spmv_publishes<kSpmvDot>(gs);
-    uint32_t ticket[TPW];
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-        ticket[q] = 0;
-        if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
-            ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
-    }
-    // K2(k) returned (stopped earlier, or a p.Ap breakdown): nothing to do; otherwise pcg_direction_scalars'
-    // expressions, inline (PCGSolver.py:118-136); converged now: x advanced over this workgroup's rows with
-    // the pending updates (pcg_catch_up) and the state written (handleConvergence)
-    double alpha = 0.0, beta = 0.0;
-    bool go = live == k;
-    if (go) {
-        const double normR = sqrt(rr);                                                      // :125
-        alpha = udr_k / pTAp;                                                               // :118
-        if (grp == 0 && tid == 0) {
-            a.hist[k] = normR;                                                              // reportIter  :126
-            a.st->last_hist = normR;
-        }
-        if (normR <= tau_nb || (!a.fail_on_maxiter && k == a.maxiter - 1)) {               // :129-131
-#pragma unroll
-            for (int q = 0; q < TPW; ++q) {
-                const int64_t row = tl[q] * kSlice + tid;
-                if (!tv[q] || row >= n) continue;
-                const double xj = pcg_catch_up(x0 ? 0.0 : a.x[row], &a.pr, qp, k, a.alphas, row);
-                a.x[row] = xj + alpha * pk[row];                                            // :121
-            }
-            if (grp == 0 && tid == 0) {
-                a.st->iters = k + 1;
-                a.st->resid = normR;
-                a.st->x_written = 1;
-                set_done(a.st, 1, k + 2);
-            }
-            go = false;
-        } else {
-            beta = ur / udr_k;                                                              // :134-135
-            if (grp == 0 && tid == 0) {
-                a.udr[k + 1] = ur;                                                          // :136
-                a.alphas[k] = alpha;
-                if (FLUSH) a.st->x_written = 1;
-            }
-        }
-    }
-    if (!go) {   // uniform over the grid: every workgroup hands its tickets back, nobody reduces
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            __asm__ volatile("" ::"v"(mk[q]), "v"(re[q]), "v"(pe[q]));
-#pragma unroll
-            for (int j = 0; j < KM; ++j)
-                if (j != JM1 && j != JP1) __asm__ volatile("" ::"v"(rv[q][j]), "v"(pv[q][j]));
-            if (FLUSH) {
-                __asm__ volatile("" ::"v"(xo[q]));
-#pragma unroll
-                for (int t = 1; t < kPcgDefer; ++t) __asm__ volatile("" ::"v"(pp[q][t - 1]));
-            }
-            if (pub && tv[q] && gs.grp_log2 >= 0 && tid == 0)
-                __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)), 1u, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    __shared__ GridSumTile<1> gsl[TPW];
-    if (pub) {
-        if (tid < TPW) gsl[tid].cnt = 0;
-        if (tid == 0 && blockIdx.x == 0 && (gs.nt + TPW - 1) / TPW != gridDim.x) atomicOr(gs.err, 2);
-        __syncthreads();
-    }
-    double pn[TPW][KM], acc[TPW], yv[TPW];
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {
-            if (j == JM1 || j == JP1) continue;
-            const double u = JAC == 2 ? a.ds * rv[q][j] : rv[q][j];   // u = precond.applyRight(r)  :123
-            pn[q][j] = u + beta * pv[q][j];                          // p = u + beta*p  :138
-        }
-        const double ue = JAC == 2 ? a.ds * re[q] : re[q];
-        const double pne = ue + beta * pe[q];
-        pn[q][JM1] = wave_shift1<true>(pn[q][JD], pne);
-        pn[q][JP1] = wave_shift1<false>(pn[q][JD], pne);
-    }
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-        const int64_t row = tl[q] * kSlice + tid;
-        const bool has = tv[q] && row < n;
-        double sum = 0.0;
-#pragma unroll
-        for (int j = 0; j < KM; ++j) {   // stored order, rounded product (spmv_diag_kernel)
-            const double t = sum + dd.v[j] * pn[q][j];
-            sum = ((mk[q] >> j) & 1u) ? t : sum;
-        }
-        yv[q] = spmv_row_value<kSpmvDot>(has, sum, pn[q][JD], acc[q]);
-    }
-    if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
-#pragma unroll
-    for (int q = 0; q < TPW; ++q) {
-        const int64_t row = tl[q] * kSlice + tid;
-        const bool has = tv[q] && row < n;
-        if (FLUSH && has) {
-            double xn = xo[q];
-#pragma unroll
-            for (int t = kPcgDefer - 1; t >= 1; --t)
-                if (t <= qp) xn = xn + a.alphas[k - t] * pp[q][t - 1];   // x = x + alpha*p  :121 (iteration k-t)
-            xn = xn + alpha * pv[q][JD];                                   // :121
-            __builtin_nontemporal_store(xn, a.x + row);
-        }
-        if (has) pnext[row] = pn[q][JD];
-        spmv_store_row<kSpmvDot>(has, row, yv[q], a.Ap);
-    }
-}
+// (Round 5 also built K3 fused into the next SpMV — pcg_fused_kernel, 33 B/row in one launch instead of 24 + 17 in
+// two, bit-identical — and a persistent form of spmv_diag_kernel; both measured no faster (profiles/
+// r5_pcg_fused_ab.txt, r5_diag_tpw_ab.txt) and were removed from the product library in round 6.)
 
-// Persistent form of spmv_diag_kernel (round 5 lab, PSK_SPMV_PERSIST=1): one resident grid, each workgroup
-// walking units of TPW slices of its XCD's band, the next unit's presence bytes and x gathers issued before
-// the current unit's dot epilogue and y stores, so a workgroup keeps its memory pipeline full instead of
-// ending after one unit and waiting for the dispatcher to start the next (the one-shot kernel at N = 10M:
-// ~4 us per workgroup, starts spread over 55 us, tools/spmv_probe.py). Same tiles, same per-tile gridsum
-// slots and tickets: the same bits. Tickets of a unit are drawn after the previous unit's reductions, so a
-// workgroup never holds an unpublished ticket while it waits.
-template <int MODE, int KM, int TPW>
-__global__ __launch_bounds__(kBlock) void spmv_diag_persist_kernel(
-    int64_t n, const uint8_t *__restrict__ mask, DiagDesc dd, const double *__restrict__ x, double *__restrict__ y,
-    const double *__restrict__ aux_d, const double *__restrict__ aux_q, GridSum gs, const int32_t *__restrict__ done,
-    int64_t nunits, int64_t ntiles) {
-    if (*(done ? done : &g_spmv_never_done) != 0) return;   // uniform
-    const int tid = threadIdx.x;
-    // XCD band: workgroups are dealt round-robin over the 8 XCDs; XCD k walks units [s, e) with its Gk workgroups
-    const int64_t b = blockIdx.x, G = gridDim.x;
-    const int k = (int)(b & 7);
-    const int64_t j = b >> 3, Gk = (G - k + 7) >> 3;
-    const int64_t a = nunits >> 3, rr = nunits & 7;
-    const int64_t s0 = k * a + (k < rr ? k : rr), e0 = s0 + a + (k < rr ? 1 : 0);
-    constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
-    const bool pub = PUB && spmv_publishes<MODE>(gs);
-    __shared__ GridSumTile<1> gsl[TPW];
-    uint32_t mk[TPW];
-    double xv[TPW][KM], eq[TPW];
-    auto load = [&](int64_t u) {
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            const int64_t t0 = u * TPW + q, t = t0 < ntiles ? t0 : ntiles - 1;
-            const int64_t row = t * kSlice + tid;
-            mk[q] = __builtin_nontemporal_load(mask + row);   // padded to whole slices
-            eq[q] = 0.0;
-            if (MODE == kSpmvResid || MODE == kSpmvAdd || MODE == kSpmvJacobiDot || MODE == kSpmvPlainDot)
-                eq[q] = aux_q[row < n ? row : 0];
-#pragma unroll
-            for (int jj = 0; jj < KM; ++jj) {
-                const int64_t c = diag_col(dd, n, row, jj);
-                xv[q][jj] = x[c];
-                if (MODE == kSpmvJacobiDot) xv[q][jj] = aux_d[c] * xv[q][jj];
-            }
-        }
-    };
-    int64_t u = s0 + j;
-    if (u < e0) load(u);
-    for (; u < e0; u += Gk) {
-        int64_t tl[TPW];
-        bool tv[TPW];
-        uint32_t ticket[TPW];
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            const int64_t t = u * TPW + q;
-            tv[q] = t < ntiles;
-            tl[q] = tv[q] ? t : ntiles - 1;
-        }
-        if (pub) {
-            __syncthreads();   // every wave is past the previous unit's LDS combine
-            if (tid < TPW) gsl[tid].cnt = 0;
-            __syncthreads();
-#pragma unroll
-            for (int q = 0; q < TPW; ++q) {
-                ticket[q] = 0;
-                if (tv[q] && gs.grp_log2 >= 0 && tid == 0)
-                    ticket[q] = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl[q], gs.grp_log2)));
-            }
-        }
-        double acc[TPW], yv[TPW];
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            const int64_t row = tl[q] * kSlice + tid;
-            const bool has = tv[q] && row < n;
-            double sum = 0.0;
-#pragma unroll
-            for (int jj = 0; jj < KM; ++jj)
-                if ((mk[q] >> jj) & 1u) sum = sum + dd.v[jj] * xv[q][jj];   // stored order, rounded product
-            double e = eq[q];
-            if (MODE == kSpmvDot) {
-                double d = 0.0;
-                bool found = false;
-#pragma unroll
-                for (int jj = 0; jj < KM; ++jj)
-                    if (jj == dd.jd && ((mk[q] >> jj) & 1u)) {
-                        d = xv[q][jj];
-                        found = true;
-                    }
-                if (!found && has) d = x[row];
-                e = d;
-            }
-            yv[q] = spmv_row_value<MODE>(has, sum, e, acc[q]);
-        }
-        if (u + Gk < e0) load(u + Gk);   // the next unit's loads fly during this unit's epilogue
-        if (pub) spmv_publish_multi<TPW>(gs, gsl, acc, ticket, tl, tv);
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) {
-            const int64_t row = tl[q] * kSlice + tid;
-            spmv_store_row<MODE>(tv[q] && row < n, row, yv[q], y);
-        }
-    }
-}
 
 // Diagonal-layout detection: row `row`'s stored entries must be, in order, entries of strictly increasing
 // diagonals j with column diag_col's mapping and value v_j; the presence byte is written (0 past n) and
@@ -2035,7 +1816,6 @@ static bool spmv_csr_bands() {
     return on;
 }
 
-// lab: the persistent diagonal-layout kernel (PSK_SPMV_PERSIST=1) and its workgroups per CU
 // the pair-row diagonal kernel: 0 off (spmv_diag_kernel), 1 or 2 half-slices per wave (PSK_DIAG_PAIR)
 static int diag_pair_h() {
     static const int v = [] {
@@ -2045,22 +1825,6 @@ static int diag_pair_h() {
     }();
     return v;
 }
-static bool spmv_persist() {
-    static const bool on = [] {
-        const char *e = std::getenv("PSK_SPMV_PERSIST");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
-static int spmv_persist_per_cu() {
-    static const int v = [] {
-        const char *e = std::getenv("PSK_SPMV_PERSIST_PER_CU");
-        const int t = e ? std::atoi(e) : 8;
-        return t >= 1 && t <= 16 ? t : 8;
-    }();
-    return v;
-}
-
 static int spmv_tpw() {
     static const int v = [] {
         const char *e = std::getenv("PSK_SPMV_TPW");
@@ -2114,9 +1878,6 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         const int64_t nwgd = (nwg + kDiagTpw - 1) / kDiagTpw;
         const dim3 gdd((unsigned)(nwgd > 0 ? nwgd : 1));
         const TileMap tmd = tile_map_for(nwgd, spmv_xcd_bands(), rev != 0);
-        const bool persist = spmv_persist();
-        int64_t gp = std::min<int64_t>(nwgd, (int64_t)c->num_cus * spmv_persist_per_cu());
-        gp = std::max<int64_t>(8, gp - gp % 8);
         // the DPP neighbour form (PSK_DIAG_DPP builds) for the two 5-diagonal orders it is written for
         const int nbk = !kDiagDpp || A->dg_K != 5 ? 0
                         : (A->dg_d[0] == 0 && A->dg_d[3] == -1 && A->dg_d[4] == 1) ? 1
@@ -2141,9 +1902,6 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
         else if (KM == 5 && nbk == 2)                                                                              \
             hipExtLaunchKernelGGL((spmv_diag_kernel<M, 5, kDiagTpw, 2>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, \
                                   dd, x, y, aux_d, aux_q, gs, done_flag, tmd, nwg);                                 \
-        else if (persist)                                                                                          \
-            hipExtLaunchKernelGGL((spmv_diag_persist_kernel<M, KM, kDiagTpw>), dim3((unsigned)gp), bd, 0, s, ev0, ev1, \
-                                  0, A->n, A->dg_mask, dd, x, y, aux_d, aux_q, gs, done_flag, nwgd, nwg);            \
         else                                                                                                       \
             hipExtLaunchKernelGGL((spmv_diag_kernel<M, KM, kDiagTpw>), gdd, bd, 0, s, ev0, ev1, 0, A->n, A->dg_mask, dd, \
                                   x, y, aux_d, aux_q, gs, done_flag, tmd, nwg);                                     \
@@ -2266,18 +2024,6 @@ static int diag_nb(const psk_csr *A) {
     return 0;
 }
 
-static std::atomic<int> g_pcg_fused{-1};   // -1: PSK_PCG_FUSED not read yet
-static bool pcg_fused_on() {
-    int v = g_pcg_fused.load();
-    if (v < 0) {
-        const char *e = std::getenv("PSK_PCG_FUSED");
-        int expect = -1;
-        g_pcg_fused.compare_exchange_strong(expect, e && std::atoi(e) != 0 ? 1 : 0);
-        v = g_pcg_fused.load();
-    }
-    return v != 0;
-}
-
 bool pcg_init_diag_eligible(const psk_csr *A) { return !A->comm && A->n > 0 && diag_nb(A) != 0; }
 
 int launch_pcg_init_diag(const psk_csr *A, const double *b, double xs, double *p, double *Ap, double *out3,
@@ -2296,38 +2042,6 @@ int launch_pcg_init_diag(const psk_csr *A, const double *b, double xs, double *p
     else
         hipLaunchKernelGGL(pcg_init_diag_kernel<2>, dim3((unsigned)nwgd), dim3(kBlock), 0, s, A->n, A->dg_mask, dd, b, xs,
                            p, Ap, gs, fin, tmd, nwg);
-    PSK_HIP(hipGetLastError());
-    return PSK_OK;
-}
-
-bool pcg_fused_eligible(const psk_csr *A, int jac) {
-    return pcg_fused_on() && !A->comm && A->n > 0 && (jac == 0 || jac == 2) && diag_nb(A) != 0;
-}
-
-int launch_pcg_fused(const psk_csr *A, int jac, const PcgFusedK &a, double *pap_out, hipStream_t s, hipEvent_t ev0,
-                     hipEvent_t ev1) {
-    if (!pcg_fused_eligible(A, jac)) return fail(PSK_ERR_ARG, "launch_pcg_fused: not eligible");
-    Context *c;
-    PSK_TRY(ctx(&c));
-    const int nb = diag_nb(A);
-    const int64_t nwg = (A->n + kSlice - 1) / kSlice, nwgd = (nwg + 1) / 2;
-    GridSum gs;
-    PSK_TRY(gridsum_prepare(c, nwg, 1, pap_out, &gs));
-    const DiagDesc dd = diag_desc(A);
-    const TileMap tmd = tile_map_for(nwgd, spmv_xcd_bands());
-    const bool flush = pcg_pending(a.k) == kPcgDefer - 1 || a.k == a.maxiter - 1;
-#define PSK_FUSED(J, NB, F)                                                                                         \
-    hipExtLaunchKernelGGL((pcg_fused_kernel<J, NB, F>), dim3((unsigned)nwgd), dim3(kBlock), 0, s, ev0, ev1, 0, A->n, \
-                          A->dg_mask, dd, a, gs, tmd, nwg)
-#define PSK_FUSED_J(J)                                                                                              \
-    do {                                                                                                            \
-        if (nb == 1) { if (flush) PSK_FUSED(J, 1, true); else PSK_FUSED(J, 1, false); }                             \
-        else { if (flush) PSK_FUSED(J, 2, true); else PSK_FUSED(J, 2, false); }                                    \
-    } while (0)
-    if (jac == 2) PSK_FUSED_J(2);
-    else PSK_FUSED_J(0);
-#undef PSK_FUSED_J
-#undef PSK_FUSED
     PSK_HIP(hipGetLastError());
     return PSK_OK;
 }
@@ -2882,9 +2596,3 @@ int psk_prec_info(const psk_prec *M, int32_t *kind, int64_t *n, int64_t *nnz_l, 
 
 }  // extern "C"
 
-// lab / tests: the fused K3 + SpMV launch of the PCG loop on (1) or off (0); returns the previous setting
-extern "C" int psk_lab_pcg_fused(int32_t on) {
-    const int prev = psk::pcg_fused_on() ? 1 : 0;
-    psk::g_pcg_fused.store(on ? 1 : 0);
-    return prev;
-}

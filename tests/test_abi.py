@@ -32,6 +32,19 @@ def test_library_exports_all_symbols():
     assert sorted(N.SIGNATURES) == _declared()
 
 
+def test_lab_entry_points_only_in_the_lab_library():
+    """psk_lab_* (include/psk_lab.h) live in libpsk_lab.so, not in the product library or its header."""
+    from pysolvers_amd import _native as N
+    txt = re.sub(r"/\*.*?\*/", "", open(os.path.join(REPO, "include", "psk_lab.h")).read(), flags=re.S)
+    lab_names = sorted(set(re.findall(r"\b(psk_lab_[a-z0-9_]+)\s*\(", txt)))
+    assert lab_names and sorted(N.LAB_SIGNATURES) == lab_names
+    assert not [n for n in _declared() if n.startswith("psk_lab_")]
+    prod = ctypes.CDLL(N.LIB_PATH)
+    assert not [n for n in lab_names if hasattr(prod, n)]
+    lab = N.load_lab()
+    assert all(hasattr(lab, n) for n in lab_names)
+
+
 def test_library_basic_calls_without_gpu():
     from pysolvers_amd import _native as N
     assert N.lib.psk_abi_version() == N.ABI_VERSION == 3

@@ -439,35 +439,6 @@ def test_pcg_run_to_run_bitwise(psk):
     assert np.array_equal(s1.info["hist"], s2.info["hist"])
 
 
-@pytest.mark.parametrize("m", [24, 257, 1100])
-def test_pcg_fused_launch_bitwise(psk, m):
-    """The PCG loop's fused K3 + SpMV launch (diagonal layout; spmv.hip pcg_fused_kernel, which recomputes
-    p_{k+1} at the neighbouring workgroups' rows) and the separate K3 and SpMV launches give the same bits:
-    x, the history and the status, for stops on either side of a deferred-x flush (maxiter 1..17, with
-    and without failOnMaxiter), and to convergence; Jacobi (one DInv value) and no preconditioner."""
-    from pysolvers_amd import _native as N
-    dA = psk.DeviceCSR.fd_laplacian_2d(-1.0, 1.0, m)
-    assert dA.layout == "diag"
-    b = psk.mvmult(dA, np.random.default_rng(m).random(m * m))
-    cases = [(it, fail) for it in (1, 2, 7, 8, 9, 16, 17) for fail in (False, True)]
-    cases = [(it, 0.0, fail) for it, fail in cases] + [(20000, 1e-8, True)]
-    prev = N.lib.psk_lab_pcg_fused(1)
-    try:
-        for prec in (psk.Jacobi, None):
-            for maxiter, tau, fail in cases:
-                out = []
-                for on in (1, 0):
-                    N.lib.psk_lab_pcg_fused(on)
-                    kw = {"precond": prec()} if prec else {}
-                    st = psk.PCG(control=_ctl(maxiter=maxiter, tau=tau, failOnMaxiter=fail), **kw).makeSolver().solve(dA, b)
-                    out.append((st.iters(), bool(st.success()), st.soln(), np.asarray(st.info["hist"])))
-                (i1, s1, x1, h1), (i0, s0, x0, h0) = out
-                assert (i1, s1) == (i0, s0), (maxiter, fail, prec)
-                assert np.array_equal(x1, x0) and np.array_equal(h1, h0), (maxiter, fail, prec)
-    finally:
-        N.lib.psk_lab_pcg_fused(prev)
-
-
 # ---------------------------------------------------------------------------------------------
 # ILUT apply (RightILUTPreconditioner.applyRight = SuperLU ILU.solve) on the device
 

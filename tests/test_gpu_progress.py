@@ -1,4 +1,7 @@
-"""Forward progress of the spin-waiting triangular-solve schedules when their grid cannot be co-resident
+"""(The psk_lab_* entry points are libpsk_lab.so's, include/psk_lab.h: a library of their own linked against
+libpsk.so, round 6.)
+
+Forward progress of the spin-waiting triangular-solve schedules when their grid cannot be co-resident
 (ADVICE r4): a co-running kernel (psk_lab_occupy_begin, on a stream of its own) holds part
 of the CUs while the solve runs, and is released only BEHIND the solve on the solver's stream — so the
 solve has to complete on whatever the occupiers leave. It must, bit-identical to the unloaded solve, with
@@ -32,14 +35,14 @@ def _apply_under_occupiers(handle, v, wgs, lds=100 * 1024):
     the whole device, the occupiers' stream included, which would make the test wait for them."""
     from pysolvers_amd import _native as N
     out = psk_mod().DeviceVector(v.n)
-    N.check(N.lib.psk_lab_occupy_begin(wgs, lds, 30.0), "psk_lab_occupy_begin")
+    N.check(N.load_lab().psk_lab_occupy_begin(wgs, lds, 30.0), "psk_lab_occupy_begin")
     timed_out = N.I32()
     try:
         N.check(N.lib.psk_prec_apply(handle, v.n, v._p, out._p, N.PSK_DEVICE), "psk_prec_apply")
     finally:
-        N.check(N.lib.psk_lab_occupy_end(ctypes.byref(timed_out)), "psk_lab_occupy_end")
+        N.check(N.load_lab().psk_lab_occupy_end(ctypes.byref(timed_out)), "psk_lab_occupy_end")
     xcc = (N.I32 * 8)()
-    N.check(N.lib.psk_lab_occupy_xcc(xcc), "psk_lab_occupy_xcc")
+    N.check(N.load_lab().psk_lab_occupy_xcc(xcc), "psk_lab_occupy_xcc")
     assert timed_out.value == 0, "the occupiers hit their time limit: the solve waited for them (per XCD %s)" % list(xcc)
     return out.numpy(), list(xcc)
 
@@ -52,7 +55,7 @@ def psk_mod():
 def _workers(handle, which):
     from pysolvers_amd import _native as N
     e, g = N.I32(), N.I32()
-    N.check(N.lib.psk_lab_trisolve_workers(handle, which, ctypes.byref(e), ctypes.byref(g)), "workers")
+    N.check(N.load_lab().psk_lab_trisolve_workers(handle, which, ctypes.byref(e), ctypes.byref(g)), "workers")
     return e.value, g.value
 
 

@@ -41,14 +41,14 @@ def main():
         nwg, lds = int(nwg), int(lds)
         for wgs in [0] + [int(w) for w in a.wgs.split(",")]:
             if wgs:
-                N.check(N.lib.psk_lab_occupy_begin(wgs, a.lds, a.seconds), "occupy_begin")
+                N.check(N.load_lab().psk_lab_occupy_begin(wgs, a.lds, a.seconds), "occupy_begin")
             rec = np.zeros(3 * nwg, np.int64)
             t0 = time.perf_counter()
-            N.check(N.lib.psk_lab_dispatch_probe(nwg, lds, us, N.ptr(rec)), "dispatch_probe")
+            N.check(N.load_lab().psk_lab_dispatch_probe(nwg, lds, us, N.ptr(rec)), "dispatch_probe")
             ms = (time.perf_counter() - t0) * 1e3
             to = N.I32()
             if wgs:
-                N.check(N.lib.psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
+                N.check(N.load_lab().psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
             r = rec.reshape(nwg, 3)
             st = (r[:, 0] - r[:, 0].min()) / 100.0   # us
             print(json.dumps({"phase": "dispatch", "wgs": wgs, "nwg": nwg, "lds": lds, "usec": us, "ms": ms,
@@ -74,7 +74,7 @@ def main():
         out = []
         for f in facs:
             e, g = N.I32(), N.I32()
-            N.check(N.lib.psk_lab_trisolve_workers(M.device_handle, f, ctypes.byref(e), ctypes.byref(g)), "workers")
+            N.check(N.load_lab().psk_lab_trisolve_workers(M.device_handle, f, ctypes.byref(e), ctypes.byref(g)), "workers")
             out.append((e.value, g.value))
         return out
 
@@ -95,12 +95,12 @@ def main():
     ref = out.numpy()
     print(json.dumps({"phase": "idle2", "ms": ms, "err": err, "workers": workers()}), flush=True)
     for wgs in (int(w) for w in a.wgs.split(",")):
-        N.check(N.lib.psk_lab_occupy_begin(wgs, a.lds, a.seconds), "occupy_begin")
+        N.check(N.load_lab().psk_lab_occupy_begin(wgs, a.lds, a.seconds), "occupy_begin")
         ms, err = timed()
         to = N.I32()
-        N.check(N.lib.psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
+        N.check(N.load_lab().psk_lab_occupy_end(ctypes.byref(to)), "occupy_end")
         xcc = (N.I32 * 8)()
-        N.check(N.lib.psk_lab_occupy_xcc(xcc), "occupy_xcc")
+        N.check(N.load_lab().psk_lab_occupy_xcc(xcc), "occupy_xcc")
         y = out.numpy()
         rec = {"phase": "occupied", "wgs": wgs, "xcc": list(xcc), "ms": ms, "err": err, "timed_out": to.value,
                "workers": workers(),
