@@ -299,7 +299,8 @@ def main():
     n, nnz = fd_sizes(m)
     sys_ = PcgSystem(N, m, comm if world > 1 else None, world)
     regions = sys_.regions(args.steps, args.warmup, args.repeats, barrier, dist)
-    dt, spmv_ms_med, spmv_launches = regions[sorted(range(len(regions)), key=lambda i: regions[i][0])[len(regions) // 2]]
+    imed = sorted(range(len(regions)), key=lambda i: regions[i][0])[len(regions) // 2]
+    dt, spmv_ms_med, spmv_launches = regions[imed]
 
     out = None
     if rank == 0:
@@ -383,6 +384,8 @@ def main():
             out["spmv_csr_layout_batch50"] = csr_layout_batch(N, sys_.A, sys_.db, sys_.dsol, bspmv, reps=50)
             # the north star's "CSR SpMV" inside the PCG loop: the same solve with the CSR layout
             out["csr_layout_in_loop"] = csr_in_loop(sys_, bspmv, args.steps)
+        if world > 1:
+            out["comm"] = comm_breakdown(sys_.comm[imed], dt / args.steps, spmv_ms_med, world)
         if transport == "host" and world > 1:
             out["rehearsal"] = "PSK_BENCH_TRANSPORT=host: all ranks on one GPU, host shared-memory collectives; not a measurement"
     sys_.free()
@@ -394,7 +397,8 @@ def main():
         big = PcgSystem(N, ms_, comm if world > 1 else None, world)
         reg = big.regions(args.scaling_steps, 5, 3, barrier, dist)
         if rank == 0:
-            dtb, smsb, _ = reg[sorted(range(len(reg)), key=lambda i: reg[i][0])[len(reg) // 2]]
+            imb = sorted(range(len(reg)), key=lambda i: reg[i][0])[len(reg) // 2]
+            dtb, smsb, _ = reg[imb]
             bl, lname, lay = big.layout()
             pm = pmc_traffic(args.traffic_json % ms_, ms_, world, mode=1, sliced=lay != N.PSK_LAYOUT_CSR)
             nb_, _ = fd_sizes(ms_)
@@ -408,6 +412,9 @@ def main():
                 "spmv_frac": bl / (smsb * 1e-3) / 1e9 / HBM_PEAK_GBPS, **pm,
                 "pcg_iteration_frac_of_aggregate_peak":
                     (bl * world + vbb * nb_) * args.scaling_steps / dtb / 1e9 / (HBM_PEAK_GBPS * world)}
+            if world > 1:
+                out["strong_scaling_%d" % ms_]["comm"] = comm_breakdown(big.comm[imb], dtb / args.scaling_steps, smsb,
+                                                                        world)
         big.free()
 
     if rank == 0:
@@ -434,6 +441,25 @@ def main():
         barrier()
         N.lib.psk_comm_destroy(comm)
         dist.destroy_process_group()
+
+
+def comm_breakdown(comm, t_iter_s, spmv_ms, world):
+    """The N > 1 line's own explanation of its iteration time: libpsk times, at the sampled
+    iterations (every EVENT_STRIDE-th), this rank's p.Ap scalar gather (the mailbox gather kernel, whose duration
+    is the wait for the slowest rank plus the transport; or the RCCL all-gather) and the halo exchange of p
+    (pack + send/recv on the stream that runs it: the second stream when it overlaps K3); each is the max over
+    ranks of the per-rank means. PCG has two such gathers per iteration (p.Ap after the SpMV, (r.r, u.r) after
+    K2, the same shape), so the exposed-communication estimate is 2 x gather, plus the halo when it does not
+    overlap K3 (PSK_HALO_OVERLAP=0)."""
+    gat, halo, samples = comm
+    overlap = os.environ.get("PSK_HALO_OVERLAP", "1") != "0"
+    exposed = 2 * gat + (0.0 if overlap else halo)
+    return {"ranks": world, "samples_per_rank": samples, "iteration_us": t_iter_s * 1e6,
+            "spmv_us_max_rank": spmv_ms * 1e3, "gather_us_max_rank": gat * 1e3, "halo_us_max_rank": halo * 1e3,
+            "halo_overlapped_with_K3": overlap, "exposed_comm_est_us": exposed * 1e3,
+            "exposed_comm_share_of_iteration": exposed * 1e-3 / t_iter_s if t_iter_s > 0 else None,
+            "timing": "HIP events libpsk records on every %d-th iteration of the median region (psk_result "
+                      "gather_ms / halo_ms, ABI 4); max over ranks" % EVENT_STRIDE}
 
 
 def _dump_maps(path):
@@ -581,6 +607,7 @@ class PcgSystem:
             r = self.run(settle, False)
             assert r.iters == settle, r.iters
         out = []
+        self.comm = []   # per region, N > 1: (p.Ap gather ms, halo exchange ms), each the max over ranks
         for _ in range(max(1, repeats)):
             barrier()
             N.check(N.lib.psk_synchronize(), "sync")
@@ -591,13 +618,14 @@ class PcgSystem:
             dt = time.perf_counter() - t0
             LIVE.tick("timed region")
             assert res.iters == steps and res.success == 1, (res.iters, res.success)
-            spmv_ms = res.spmv_ms
+            spmv_ms, gat, halo = res.spmv_ms, res.gather_ms, res.halo_ms
             if dist is not None:
                 import torch
-                t = torch.tensor([dt, spmv_ms], dtype=torch.float64)
+                t = torch.tensor([dt, spmv_ms, gat, halo], dtype=torch.float64)
                 dist.all_reduce(t, op=dist.ReduceOp.MAX)
-                dt, spmv_ms = float(t[0]), float(t[1])
+                dt, spmv_ms, gat, halo = (float(v) for v in t)
             out.append((dt, spmv_ms, res.spmv_launches))
+            self.comm.append((gat, halo, res.comm_samples))
         return out
 
     def settle_iters(self):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define PSK_ABI_VERSION 3
+#define PSK_ABI_VERSION 4
 
 /* return codes */
 #define PSK_OK               0
@@ -114,6 +114,14 @@ typedef struct psk_result {
     char    msg[256];         /* SolveStatus.msg() */
     int32_t exit;             /* PSK_EXIT_* (ABI 3) */
     int32_t reserved;
+    /* ABI 4, sharded PCG with ctl.time_kernels: the iterations whose SpMV is timed also time, on this rank,
+     * the scalar exchange after that SpMV (p.Ap: the mailbox gather kernel — its duration is the wait for the
+     * slowest rank plus the transport — or the RCCL all-gather) and the halo exchange of p that feeds the
+     * next SpMV (pack + send/recv, on the stream that runs it: the second stream when overlapped with K3).
+     * Means over the samples; 0 when unsharded or untimed. */
+    double  gather_ms;
+    double  halo_ms;
+    int64_t comm_samples;
 } psk_result;
 
 /* ---- library / device ---------------------------------------------------------------- */

@@ -15,7 +15,7 @@ LIB_PATH = os.environ.get("PSK_LIBRARY", os.path.join(_HERE, "_lib", "libpsk.so"
 
 PSK_OK = 0
 PSK_ERR_ARG, PSK_ERR_HIP, PSK_ERR_RCCL, PSK_ERR_ALLOC, PSK_ERR_UNSUPPORTED = -1, -2, -3, -4, -5
-ABI_VERSION = 3          # include/psk.h PSK_ABI_VERSION (psk_ctl gained norm_b in 2, psk_result.exit in 3)
+ABI_VERSION = 4          # include/psk.h PSK_ABI_VERSION (psk_ctl.norm_b in 2, psk_result.exit in 3, comm timing in 4)
 PSK_CONVERGED, PSK_MAXITER, PSK_BREAKDOWN, PSK_TRUE_RESID_FAIL = 0, 1, 2, 3
 PSK_EXIT_NONE, PSK_EXIT_TOLERANCE, PSK_EXIT_ARNOLDI_BREAKDOWN, PSK_EXIT_MAXITER, PSK_EXIT_DOT_BREAKDOWN = 0, 1, 2, 3, 4
 PSK_HOST, PSK_DEVICE = 0, 1
@@ -38,7 +38,8 @@ class PskResult(ctypes.Structure):
                 ("resid", ctypes.c_double), ("resid_recursive", ctypes.c_double),
                 ("norm_b", ctypes.c_double), ("loop_ms", ctypes.c_double), ("spmv_ms", ctypes.c_double),
                 ("spmv_launches", ctypes.c_int64), ("hist_len", ctypes.c_int64), ("msg", ctypes.c_char * 256),
-                ("exit", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("exit", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("gather_ms", ctypes.c_double), ("halo_ms", ctypes.c_double), ("comm_samples", ctypes.c_int64)]
 
 
 # name -> (restype, argtypes); this is the full list of symbols include/psk.h declares

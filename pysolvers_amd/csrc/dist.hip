@@ -9,6 +9,8 @@
 // all-reduce would leave the order of the rank sum to RCCL's algorithm choice).
 #include "psk_internal.hpp"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -68,10 +70,14 @@ int halo_exchange(psk_csr *A, double *x, hipStream_t s) {
 
 // The halo exchange on the second stream `cs`, after the work already enqueued on `s` (event ev_a);
 // ev_b marks its completion for the consumer (the next SpMV waits on it).
-int halo_exchange_async(psk_csr *A, double *x, hipStream_t s, hipStream_t cs, hipEvent_t ev_a, hipEvent_t ev_b) {
+// t0 / t1 (optional, timing): recorded on `cs` around the exchange itself
+int halo_exchange_async(psk_csr *A, double *x, hipStream_t s, hipStream_t cs, hipEvent_t ev_a, hipEvent_t ev_b,
+                        hipEvent_t t0, hipEvent_t t1) {
     PSK_HIP(hipEventRecord(ev_a, s));
     PSK_HIP(hipStreamWaitEvent(cs, ev_a, 0));
+    if (t0) PSK_HIP(hipEventRecord(t0, cs));
     PSK_TRY(halo_exchange(A, x, cs));
+    if (t1) PSK_HIP(hipEventRecord(t1, cs));
     PSK_HIP(hipEventRecord(ev_b, cs));
     return PSK_OK;
 }
@@ -158,7 +164,8 @@ __global__ void mbox_gather_kernel(uint64_t *mine, int P, int W, double *__restr
     __threadfence_system();
 }
 
-int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s) {
+int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s, hipEvent_t ev0,
+                hipEvent_t ev1) {
     Context *cx;
     PSK_TRY(ctx(&cx));
     if (!cx->gs_err) {   // the error word gridsum_check reports (allocated with the first grid sum)
@@ -167,8 +174,9 @@ int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *d
     }
     Mailbox &m = *c->mb;
     if (W < 1 || W > kMbW) return fail(PSK_ERR_ARG, "mbox_gather: bad width");
-    hipLaunchKernelGGL(mbox_gather_kernel, dim3(1), dim3(64), 0, s, m.dev + mb_index(m, m.rank, (int64_t)(seq % kMbRing), 0, 0),
-                       m.P, W, recv, done, cx->gs_err);
+    // ev0 / ev1 (optional, timing): recorded by the dispatch itself around the kernel (its wait for the ranks)
+    hipExtLaunchKernelGGL(mbox_gather_kernel, dim3(1), dim3(64), 0, s, ev0, ev1, 0,
+                          m.dev + mb_index(m, m.rank, (int64_t)(seq % kMbRing), 0, 0), m.P, W, recv, done, cx->gs_err);
     PSK_HIP(hipGetLastError());
     return PSK_OK;
 }

@@ -487,9 +487,15 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
     const int TP = kTimedSlots;
     hipEvent_t *ta = kit->ta, *tb = kit->tb;
     int64_t tk[kTimedSlots];
-    for (int i = 0; i < TP; ++i) tk[i] = -1;
+    bool tgat[kTimedSlots], thalo[kTimedSlots];   // sharded: the slot's gather / halo events were recorded
+    for (int i = 0; i < TP; ++i) {
+        tk[i] = -1;
+        tgat[i] = thalo[i] = false;
+    }
     std::vector<float> spmv_ms;
     if (ctl->time_kernels) spmv_ms.assign((size_t)maxiter, -1.0f);   // -1: not sampled
+    double gat_sum = 0.0, halo_sum = 0.0;
+    int64_t gat_n = 0, halo_n = 0;
     auto harvest = [&](int slot) -> int {
         if (tk[slot] < 0) return PSK_OK;
         float ms = 0.f;
@@ -497,6 +503,20 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         PSK_HIP(hipEventElapsedTime(&ms, ta[slot], tb[slot]));
         spmv_ms[(size_t)tk[slot]] = ms;
         tk[slot] = -1;
+        if (tgat[slot]) {
+            PSK_HIP(hipEventSynchronize(kit->gb[slot]));
+            PSK_HIP(hipEventElapsedTime(&ms, kit->ga[slot], kit->gb[slot]));
+            gat_sum += ms;
+            ++gat_n;
+            tgat[slot] = false;
+        }
+        if (thalo[slot]) {
+            PSK_HIP(hipEventSynchronize(kit->hb[slot]));
+            PSK_HIP(hipEventElapsedTime(&ms, kit->ha[slot], kit->hb[slot]));
+            halo_sum += ms;
+            ++halo_n;
+            thalo[slot] = false;
+        }
         return PSK_OK;
     };
 
@@ -540,20 +560,27 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         // p_k and the buffer K3 writes p_{k+1} into (Jacobi/identity: a ring of kPcgDefer; general: in place)
         double *pk = gen ? w.p : w.pr.b[k % kPcgDefer];
         double *pn = gen ? w.p : w.pr.b[(k + 1) % kPcgDefer];
-        if (halo_pending) {   // exchanged during the previous K3
-            if (hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess) { rc = fail(PSK_ERR_HIP, "halo wait"); break; }
-            halo_pending = false;
-        } else if (A->comm && (rc = halo_exchange(A, pk, s)) != PSK_OK) {
-            break;
-        }
         // every time_kernels-th SpMV between two events (sampled: an event pair costs ~5% of an
-        // iteration at N = 10M)
+        // iteration at N = 10M); sharded, the same iterations time this rank's p.Ap gather and the halo
+        // exchange of the iteration (ABI 4: psk_result.gather_ms / halo_ms)
         // (init_diag: iteration 0's SpMV ran inside the init launch, not sampled)
         const bool timed = ctl->time_kernels > 0 && k % ctl->time_kernels == 0 && !(init_diag && k == 0);
         int slot = (int)((k / (ctl->time_kernels > 0 ? ctl->time_kernels : 1)) % TP);
         if (timed) {
             if ((rc = harvest(slot)) != PSK_OK) break;
             tk[slot] = k;
+        }
+        if (halo_pending) {   // exchanged during the previous K3
+            if (hipStreamWaitEvent(s, ev_halo, 0) != hipSuccess) { rc = fail(PSK_ERR_HIP, "halo wait"); break; }
+            halo_pending = false;
+        } else if (A->comm) {
+            const bool th = timed && !A->comm->dry && !A->peers.empty();
+            if (th && hipEventRecord(kit->ha[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
+            if ((rc = halo_exchange(A, pk, s)) != PSK_OK) break;
+            if (th) {
+                if (hipEventRecord(kit->hb[slot], s) != hipSuccess) { rc = fail(PSK_ERR_HIP, "event"); break; }
+                thalo[slot] = true;
+            }
         }
         // a timed launch records its events in its own dispatch (kernel start / end)
         uint64_t seq1 = 0;
@@ -565,9 +592,18 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
         // directions (a serpentine over SpMV, K2, K3 meant to re-read Ap, r and p from the Infinity Cache),
         // measured no faster (round 4, profiles/r4_spmv_ab.txt: band1 / band2)
         const TileMap tm2 = tile_map_for(nv, false);
-        if (sharded && (rc = mbc ? mbox_gather(mbc, seq1, 1, w.part1g, &w.st->done, s)
-                                 : allgather(A, w.part1, w.part1g, 1, s)) != PSK_OK)
-            break;
+        if (sharded) {
+            hipEvent_t g0 = timed ? kit->ga[slot] : nullptr, g1 = timed ? kit->gb[slot] : nullptr;
+            if (mbc) {
+                rc = mbox_gather(mbc, seq1, 1, w.part1g, &w.st->done, s, g0, g1);
+            } else {
+                if (g0 && hipEventRecord(g0, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
+                if (rc == PSK_OK) rc = allgather(A, w.part1, w.part1g, 1, s);
+                if (rc == PSK_OK && g1 && hipEventRecord(g1, s) != hipSuccess) rc = fail(PSK_ERR_HIP, "event");
+            }
+            if (rc != PSK_OK) break;
+            if (timed) tgat[slot] = true;
+        }
         GridSum gs2k = gs2;   // this iteration's mailbox slot (sharded with a mailbox)
         const uint64_t seq2 = mbc ? mbox_next(mbc, &gs2k) : 0;
         // the general path copied r = b in its init (pcg_gen_init_kernel): it never takes the FIRST form
@@ -611,7 +647,10 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
                 // second stream while the other tiles run; the next SpMV waits for it
                 k3(0, ov_lo);
                 k3(ov_hi, nv);
-                if ((rc = halo_exchange_async(A, pn, s, cs, ev_k3a, ev_halo)) != PSK_OK) break;
+                if ((rc = halo_exchange_async(A, pn, s, cs, ev_k3a, ev_halo, timed ? kit->ha[slot] : nullptr,
+                                              timed ? kit->hb[slot] : nullptr)) != PSK_OK)
+                    break;
+                if (timed) thalo[slot] = true;
                 k3(ov_lo, ov_hi);
                 halo_pending = true;
             } else {
@@ -711,6 +750,9 @@ extern "C" int psk_pcg(const psk_csr *Ac, const psk_prec *M, const double *b, do
                 }
             res->spmv_launches = nt;
             res->spmv_ms = nt > 0 ? tot / (double)nt : 0.0;
+            res->gather_ms = gat_n > 0 ? gat_sum / (double)gat_n : 0.0;
+            res->halo_ms = halo_n > 0 ? halo_sum / (double)halo_n : 0.0;
+            res->comm_samples = gat_n;
         }
     }
     // a solve that failed on the host side leaves no kernel of its own running behind the next solve

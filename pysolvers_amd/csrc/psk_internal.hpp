@@ -69,6 +69,8 @@ struct SolveKit {
     hipEvent_t ev_a = nullptr, ev_b = nullptr; // halo overlap hand-offs (no timing)
     bool timed_ready = false;
     hipEvent_t ta[kTimedSlots] = {}, tb[kTimedSlots] = {};   // sampled SpMV intervals (timing)
+    // sharded solves (ABI 4): the sampled iterations' p.Ap gather and halo exchange (timing)
+    hipEvent_t ga[kTimedSlots] = {}, gb[kTimedSlots] = {}, ha[kTimedSlots] = {}, hb[kTimedSlots] = {};
 };
 constexpr size_t kStageBytes = 4096;
 struct Context {
@@ -877,7 +879,8 @@ int to_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStr
 int from_device_vec(const double *src, int32_t loc, int64_t n, double *dst, hipStream_t s);
 int halo_exchange(psk_csr *A, double *x_local, hipStream_t s);
 // the exchange on stream cs after the work enqueued on s (ev_a), completion recorded in ev_b
-int halo_exchange_async(psk_csr *A, double *x, hipStream_t s, hipStream_t cs, hipEvent_t ev_a, hipEvent_t ev_b);
+int halo_exchange_async(psk_csr *A, double *x, hipStream_t s, hipStream_t cs, hipEvent_t ev_a, hipEvent_t ev_b,
+                        hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // rows sent to peers confined to the first lo / the tiles from hi on (of nv tiles of `tile` rows)
 bool halo_split(const psk_csr *A, int64_t tile, int64_t nv, int64_t &lo, int64_t &hi);
 // recv[q*count + i] = rank q's send[i]: no arithmetic, so every rank holds the same bits and
@@ -887,7 +890,8 @@ int allgather(psk_csr *A, const double *send, double *recv, int64_t count, hipSt
 // gather of that exchange into recv[q*W + c] on s (skipped on the device when *done is set: the producer
 // did not run either); returns the exchange number
 uint64_t mbox_next(psk_comm *c, GridSum *gs);
-int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s);
+int mbox_gather(psk_comm *c, uint64_t seq, int W, double *recv, const int32_t *done, hipStream_t s,
+                hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 
 // SpMV launch (defined in spmv.hip); modes below
 enum SpmvMode : int {

@@ -46,6 +46,8 @@ int solve_kit(Context *c, bool timed, SolveKit **out) {
             // profiler's kernel time, profiles/r4_headline_regions_rocprof.json)
             PSK_HIP(hipEventCreateWithFlags(&k.ta[i], hipEventDisableSystemFence));
             PSK_HIP(hipEventCreateWithFlags(&k.tb[i], hipEventDisableSystemFence));
+            for (hipEvent_t *e : {&k.ga[i], &k.gb[i], &k.ha[i], &k.hb[i]})
+                PSK_HIP(hipEventCreateWithFlags(e, hipEventDisableSystemFence));
         }
         k.timed_ready = true;
     }
@@ -309,6 +311,7 @@ int psk_shutdown_ex(int32_t flags) {
             for (int i = 0; i < kTimedSlots; ++i) {
                 (void)hipEventDestroy(k.ta[i]);
                 (void)hipEventDestroy(k.tb[i]);
+                for (hipEvent_t e : {k.ga[i], k.gb[i], k.ha[i], k.hb[i]}) (void)hipEventDestroy(e);
             }
         k = SolveKit{};
         for (uint64_t *p : c.gs_retired) (void)hipFree(p);

@@ -47,7 +47,7 @@ def test_lab_entry_points_only_in_the_lab_library():
 
 def test_library_basic_calls_without_gpu():
     from pysolvers_amd import _native as N
-    assert N.lib.psk_abi_version() == N.ABI_VERSION == 3
+    assert N.lib.psk_abi_version() == N.ABI_VERSION == 4
     n = N.device_count()
     assert n >= 0
     assert isinstance(N.lib.psk_last_error(), bytes)
