@@ -185,7 +185,7 @@ def main():
     ap.add_argument("--config4", type=int, default=1, help="also time configs[4] (PCG+AMG, -FD 8192^2) on rank 0")
     ap.add_argument("--config1", type=int, default=1, help="also time configs[1] (PCG+Jacobi 4096^2) on rank 0")
     ap.add_argument("--gmres", type=int, default=1, help="also time GMRES(30)+Jacobi Arnoldi steps at 4096^2 on rank 0")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r5_pmc_traffic_%d.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "r6_pmc_traffic_%d.json"),
                     help="PMC traffic summary (tools/pmc_summary.py) of the same build; %%d = the side")
     args = ap.parse_args()
     LIVE.write("bench: start (pid %d, python %s)" % (os.getpid(), sys.version.split()[0]))
@@ -356,8 +356,9 @@ def main():
                          "csr_count_note": "SURVEY §8d's CSR byte count (12 nnz + 4(n+1) + 16n) over the same time: "
                                            "NOT a bandwidth — the layout streams fewer bytes than CSR",
                          "bound_note": ("diag layout, 17 B/row: the launch is bound by one memory round trip per "
-                                        "workgroup (latency), not by HBM bandwidth; pcg_iteration_roofline prices the "
-                                        "whole iteration (DESIGN.md §4)") if lname == "diag" else None},
+                                        "wave (latency) and its dot epilogue, not by HBM bandwidth; "
+                                        "pcg_iteration_roofline prices the whole iteration (DESIGN.md §4)")
+                         if lname == "diag" else None},
             "pcg_iteration_roofline": {"bytes_per_iteration": biter, "vector_bytes_per_row": vb,
                                        "achieved_GBps": biter * it_s / 1e9,
                                        "frac_of_aggregate_peak": biter * it_s / 1e9 / (HBM_PEAK_GBPS * world)},
@@ -657,7 +658,7 @@ def spmv_kernel_label(layout, mode):
     if layout == 0:
         return "spmv_kernel<%d> (CSR layout)" % mode
     if LAYOUT_NAMES.get(layout) == "diag":
-        return "spmv_diag_kernel<%d, ...> (diag layout)" % mode
+        return "spmv_diagp_kernel<%d, ...> (diag layout, two rows per lane)" % mode
     return "spmv_uniform(_multi)_kernel / spmv_sliced_kernel <MODE=%d> (%s layout)" % (mode, LAYOUT_NAMES[layout])
 
 
@@ -790,7 +791,7 @@ def pmc_traffic(path, m, world, mode, sliced):
         return {"traffic": None, "traffic_note": "%s is for another side / rank count" % src}
     if d.get("libpsk_sha256") != lib_sha256():
         return {"traffic": None, "traffic_note": "%s was captured with another libpsk.so build" % src}
-    pat = re.compile((r"psk::spmv_(uniform_multi|uniform|sliced|diag)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
+    pat = re.compile((r"psk::spmv_(uniform_multi|uniform|sliced|diag|diagp)_kernel<%d," if sliced else r"psk::spmv_kernel<%d>") % mode)
     hits = [k for k in d["kernels"] if pat.search(k)]
     if len(hits) != 1:
         return {"traffic": None, "traffic_note": "%s holds %d SpMV kernels of mode %d" % (src, len(hits), mode)}

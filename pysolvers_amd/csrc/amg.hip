@@ -111,11 +111,8 @@ static int amg_smooth(const AmgHierarchy *h, const Context *c, int lev, const do
     double *r = h->r[lev].as<double>(), *t = h->t[lev].as<double>();
     for (int it = 0; it < nu; ++it) {
         PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, s));
-        static const bool fuse = [] {   // PSK_AMG_FUSE=0: separate gather and add (A/B only)
-            const char *e = std::getenv("PSK_AMG_FUSE");
-            return !(e && std::atoi(e) == 0);
-        }();
-        if (fuse && h->S[lev] && h->S[lev]->kind == PSK_PREC_ILU) {   // Gauss-Seidel: x += U^-1 r in the last gather
+        // (round 3: x += U^-1 r fused into the solve's last gather, profiles/r3_amg_fuse_ab.txt)
+        if (h->S[lev] && h->S[lev]->kind == PSK_PREC_ILU) {   // Gauss-Seidel: x += U^-1 r in the last gather
             PSK_TRY(ilu_apply_add(h->S[lev], r, x, s));
             continue;
         }

@@ -1785,7 +1785,6 @@ int syncfree_grid(const Context *c) {
                                                          0) != hipSuccess)
             api = 2;
         per_cu = std::max(1, std::min(api, 8) - 1);
-        if (const char *e = std::getenv("PSK_SYNCFREE_PER_CU")) per_cu = std::max(1, std::atoi(e));   // experiments
     }
     return c->num_cus * per_cu;
 }
@@ -1818,10 +1817,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
     const double *va = T.vals, *dg = T.diag;
     (void)rp;
     if (T.schedule == kSchedLds) {
-        static const int depth = [] {
-            const char *e = std::getenv("PSK_LDS_DEPTH");
-            return e ? std::atoi(e) : kLdsDepth;
-        }();
+        constexpr int depth = kLdsDepth;
         const void *k = depth <= 1   ? reinterpret_cast<const void *>(&sptrsv_lds_kernel<1>)
                         : depth == 2 ? reinterpret_cast<const void *>(&sptrsv_lds_kernel<2>)
                                      : reinterpret_cast<const void *>(&sptrsv_lds_kernel<3>);   // 4 spills
@@ -1836,10 +1832,7 @@ static int launch_factor(const Context *c, int64_t n, const TriFactor &T, const 
         hipLaunchKernelGGL(levels_gather_kernel, dim3((unsigned)((np + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, np,
                            T.lv_rc, rhs, rhs_idx, T.lv_b);
         PSK_HIP(hipGetLastError());
-        static const bool d8 = [] {
-            const char *e = std::getenv("PSK_LEVELS_D");
-            return e && std::atoi(e) == 8;
-        }();
+        constexpr bool d8 = false;   // 8 steps of prefetch: measured no faster than 4 (round 5)
         const void *k = d8 ? (T.lv_KM == 4    ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<4, 8>)
                               : T.lv_KM == 8  ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<8, 8>)
                               : T.lv_KM == 12 ? reinterpret_cast<const void *>(&sptrsv_levels_kernel<12, 8>)
@@ -2371,11 +2364,8 @@ void plan_grid(const HostFactor &F, GridPlan &g) {
         }
         if (sigma > 8) return false;
         // half a step less skew when the dependencies that need sigma occur on every other line only
-        // (PSK_GRID_HALF_SKEW=0: integer skews only)
-        static const bool half = [] {
-            const char *e = std::getenv("PSK_GRID_HALF_SKEW");
-            return !(e && std::atoi(e) == 0);
-        }();
+        // (round 4: AMG level 3 2.67 -> 2.20 ms, profiles/r4_half_skew_ab.txt)
+        constexpr bool half = true;
         if (half && sigma >= 2 && (try_skew(o, 2 * sigma - 1, 0) || try_skew(o, 2 * sigma - 1, 1))) return true;
         return try_skew(o, 2 * sigma, 0);
     };
@@ -2561,7 +2551,6 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     bool band_ok = false;
     std::vector<int64_t> cands = {(int64_t)c->num_cus, 2 * (int64_t)c->num_cus, 4 * (int64_t)c->num_cus,
                                   8 * (int64_t)c->num_cus};
-    if (const char *e = std::getenv("PSK_BAND_BLOCKS")) cands = {std::max<int64_t>(1, std::atoll(e))};   // experiments
     for (int64_t nb : cands) {
         if (n == 0 || kmax > 8) break;
         const int64_t B = std::max<int64_t>(64, (n + nb - 1) / nb);
@@ -2593,8 +2582,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     if (n > 0 && n <= kLdsMaxRows) {
         T.est_lds_us = (double)nlev * kLdsLevelUs + (double)F.ci.size() * 12.0 / kLdsBytesPerUs;
         const double other = T.schedule == kSchedBand ? T.est_band_us : T.est_syncfree_us;
-        const char *le = std::getenv("PSK_TRISOLVE_LDS");
-        if (T.est_lds_us < other && !(le && std::atoi(le) == 0)) T.schedule = kSchedLds;
+        if (T.est_lds_us < other) T.schedule = kSchedLds;
     }
     // grid schedule (2-D stencil factors): records in solve order
     GridPlan gp;
@@ -2605,10 +2593,9 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     std::vector<double> gcoef, gdiag, gdict;
     std::vector<uint32_t> gidx;
     if (gp.ok) {
-        const char *ge = std::getenv("PSK_TRISOLVE_GRID");
         const double cur = T.schedule == kSchedBand ? T.est_band_us
                            : T.schedule == kSchedLds ? T.est_lds_us : T.est_syncfree_us;
-        if (gp.est < cur && !(ge && std::atoi(ge) == 0)) T.schedule = kSchedGrid;
+        if (gp.est < cur) T.schedule = kSchedGrid;
         T.grid_K = gp.K;
         T.grid_pe = gp.pe;
         T.grid_maxyd = gp.maxyd;
@@ -2777,11 +2764,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     {
         const char *pe = std::getenv("PSK_TRISOLVE_PART");
         const bool force = pe && std::atoi(pe) == 1, off = pe && std::atoi(pe) == 0;
-        static const int nparts = [] {   // lab: PSK_PART_STRIPS = strips (default: one per CU)
-            const char *e = std::getenv("PSK_PART_STRIPS");
-            return e ? std::atoi(e) : 0;
-        }();
-        const int P = nparts > 0 ? nparts : c->num_cus;
+        const int P = c->num_cus;   // one strip per CU (16-64 strips measured slower, round 5)
         const int64_t strip = (n + P - 1) / std::max(1, P);
         if (!off && !lv_forced && n > kLdsMaxRows && n >= (int64_t)P * kPartWaves &&
             (force || (T.schedule != kSchedGrid && strip <= kPartMaxStrip))) {

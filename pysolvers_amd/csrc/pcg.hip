@@ -83,9 +83,10 @@ __global__ void pcg_init_finish_kernel(const double *g, int P, double tau, PcgSt
 }
 
 // ---- K2: r update + grid sums [r.r, u.r] -------------------------------------------------
-// One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses); round 6 measured one tile
-// per WAVE (four per workgroup, no barrier, the workgroup form's sums re-created by one wave: the same bits) 1-2%
-// slower at N = 10M and 16384^2 (profiles/r6_k2_wave_ab.txt). JAC: Jacobi
+// One-shot: workgroup b owns elements [512b, 512b+512), two per lane (16-B accesses). Round 6 measured three other
+// forms of its grid sums, none better at both N = 10M and 16384^2 (profiles/r6_k2_wave_ab.txt,
+// r6_k2_gridmask_ab.txt): one tile per WAVE with the workgroup's bits (-1 to -2%), one tile per wave with DPP wave
+// totals (+1% / -2%), DPP wave totals combined in LDS instead of block_sum (+-0). JAC: Jacobi
 // preconditioner fused: 1 = DInv streamed, 2 = every DInv entry the same double `ds` (constant-
 // diagonal matrices such as stencils: the same products, 8 B/row less per kernel).
 // FIRST (iteration 0): r_0 = b is read from b (the init does not copy it, K0 above).

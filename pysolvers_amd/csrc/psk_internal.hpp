@@ -650,8 +650,8 @@ __device__ __forceinline__ void gridsum_publish(const GridSum &gs, const double 
 // with an LDS atomic; the wave that counts last adds the kWaves totals in wave order and publishes
 // the tile's ONE slot, then plays the tile's part in the ticket protocol: one write-through store
 // per tile instead of one per wave (~2 us less at N = 10M; what the remaining ~6 us of the dot
-// epilogue is — it is not per store — is recorded in profiles/r3_gridsum_lab.txt, probe builds
-// -DPSK_LAB_GS_NOTICKET / NOSTORE). No workgroup barrier at the end; the one barrier (arming the
+// epilogue is — it is not per store — is recorded in profiles/r3_gridsum_lab.txt and, for the pair-row kernel,
+// profiles/r6_diagp_epilogue_ab.txt (round-3/6 probe builds, removed from the product since)). No workgroup barrier at the end; the one barrier (arming the
 // LDS counter) sits where every wave waits for its stream loads anyway.
 template <int W>
 struct GridSumTile {
@@ -669,9 +669,6 @@ __device__ __forceinline__ uint32_t gridsum_tile_begin(const GridSum &gs, GridSu
     }
     __syncthreads();
     uint32_t t = 0;
-#if defined(PSK_LAB_GS_NOTICKET) || defined(PSK_LAB_GS_NOSTORE)
-    return t;   // development probes (scripts/build_variant.sh): no ticket, no reduction — wrong sums
-#endif
     if (gs.grp_log2 >= 0 && threadIdx.x == 0) t = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tile, gs.grp_log2)));
     return t;
 }
@@ -720,10 +717,6 @@ __device__ __forceinline__ void gridsum_tile_publish(const GridSum &gs, GridSumT
         for (int w = 1; w < kWaves; ++w) s[c] += L.part[w * W + c];   // wave order
     }
     const uint32_t tk = L.ticket;
-#ifdef PSK_LAB_GS_NOSTORE
-    if (s[0] == 1.2345e-300 && lane0) gs.out[0] = s[0];   // keeps the sums live; probe only
-    return;
-#endif
     if (gs.grp_log2 < 0) {
         if (lane0)
 #pragma unroll
@@ -734,9 +727,6 @@ __device__ __forceinline__ void gridsum_tile_publish(const GridSum &gs, GridSumT
     if (lane0)
 #pragma unroll
         for (int c = 0; c < W; ++c) gridsum_put(gs.slots + gridsum_slot(gs, tile) * W + c, s[c]);
-#ifdef PSK_LAB_GS_NOTICKET
-    return;
-#endif
     const int64_t g = gridsum_group_of(tile, gs.grp_log2);
     int64_t base;
     const int64_t cnt = gridsum_members(gs, g, base);
@@ -839,12 +829,23 @@ struct TileMap {
     int64_t a;     // tiles / 8 (0 = identity)
     int32_t r;     // tiles mod 8: classes k < r hold one more tile
     int32_t rev;   // 1: each XCD walks its band from the end (the lines its predecessor wrote last first)
+    int64_t c;     // > 0 (with a == 0): CHUNKED — XCD k takes chunks k, k + 8, ... of c consecutive tiles (round 6,
+                   // the CSR tile kernel); the tiles past the last whole 8c in block order
 };
 inline TileMap tile_map_for(int64_t ntiles, bool banded, bool rev = false) {
-    return banded && ntiles >= 64 ? TileMap{ntiles >> 3, (int32_t)(ntiles & 7), rev ? 1 : 0} : TileMap{0, 0, 0};
+    return banded && ntiles >= 64 ? TileMap{ntiles >> 3, (int32_t)(ntiles & 7), rev ? 1 : 0, 0} : TileMap{0, 0, 0, 0};
+}
+inline TileMap tile_map_chunked(int64_t ntiles, int64_t c) {
+    return c > 0 && ntiles >= 8 * c ? TileMap{0, 0, 0, c} : TileMap{0, 0, 0, 0};
 }
 __device__ __forceinline__ int64_t tile_of_block(TileMap tm) {
     const int64_t b = blockIdx.x;
+    if (tm.c > 0) {   // b = 8 j + k on XCD k (round-robin dealing): its j-th tile is in chunk (j / c) * 8 + k
+        const int64_t k = b & 7, j = b >> 3;
+        const int64_t t = ((j / tm.c) * 8 + k) * tm.c + j % tm.c;
+        const int64_t full = (int64_t)(gridDim.x / (8 * tm.c)) * 8 * tm.c;
+        return b < full ? t : b;
+    }
     if (tm.a == 0) return b;
     const int64_t k = b & 7, j = b >> 3;
     const int64_t start = k * tm.a + (k < tm.r ? k : tm.r);

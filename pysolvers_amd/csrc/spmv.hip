@@ -395,14 +395,8 @@ __device__ __forceinline__ void spmv_publish_multi(const GridSum &gs, GridSumTil
         uint32_t old = 0;
         if (lane0) {
             L[q].part[wave] = ws;
-#ifndef PSK_LAB_EARLY_TICKET
             if (threadIdx.x == 0) L[q].ticket = ticket[q];
-#endif
-#ifdef PSK_LAB_NOFENCE
-            __asm__ volatile("" ::: "memory");   // LDS operations of one wave execute in order
-#else
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-#endif
             old = atomicAdd(&L[q].cnt, 1u);
         }
         if (__builtin_amdgcn_readfirstlane(old) != kWaves - 1) continue;
@@ -551,14 +545,6 @@ __global__ __launch_bounds__(kBlock) void spmv_uniform_multi_kernel(
             if (MODE == kSpmvJacobiDot) xv[q][j] = aux_d[cl] * xv[q][j];
         }
     }
-#ifdef PSK_LAB_EARLY_TICKET
-    // the tickets' returns consumed here, once the gathers are issued (they return before the gathers):
-    // the epilogue after the y stores then needs no wait on VMEM (a wait for a returning atomic issued
-    // before the stores was a vmcnt(0) that also waited for the stores)
-    if (pub && tid == 0)
-#pragma unroll
-        for (int q = 0; q < TPW; ++q) gsl[q].ticket = ticket[q];
-#endif
 #pragma unroll
     for (int q = 0; q < TPW; ++q) {
         const int64_t row = tl[q] * kSlice + tid;
@@ -606,12 +592,6 @@ constexpr int kDiagTpw = PSK_DIAG_TPW;   // slices per workgroup
 #ifndef PSK_DIAG_DPP
 #define PSK_DIAG_DPP 1
 #endif
-// the pair-row kernel's QUAD tickets (round 6): one gridsum ticket per workgroup of four slices instead of one per
-// slice, the groups of the four slices reduced by the waves of the quad's last workgroup (same bits)
-#ifndef PSK_DIAG_QUAD
-#define PSK_DIAG_QUAD 0
-#endif
-constexpr bool kDiagQuad = PSK_DIAG_QUAD != 0;
 // the -1/+1 diagonals by DPP lane shifts (default from round 5: in-loop SpMV at N = 10M 0.0587 -> 0.0550 ms,
 // 16384^2 1.44 -> 1.28 ms, same bits; profiles/r5_diag_dpp_ab.txt; -DPSK_DIAG_DPP=0 builds the gathers)
 constexpr bool kDiagDpp = PSK_DIAG_DPP != 0;
@@ -885,12 +865,6 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
     const bool tv = t < ntiles;                                   // wave-uniform
     const int64_t tl = tv ? t : ntiles - 1;
     const int64_t r0 = tl * kSlice + (H == 2 ? 0 : 128 * (wave & 1));   // first row of the wave's first half
-#ifdef PSK_LAB_DIAGP_TFIRST   // lab probe: the ticket drawn before the loads
-    uint32_t ticket = 0;
-    if (MODE != kSpmvPlain && MODE != kSpmvAdd && spmv_publishes<MODE>(gs) && tv && (H == 2 || (wave & 1) == 0) &&
-        gs.grp_log2 >= 0 && lane == 0)
-        ticket = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)));
-#endif
     uint32_t mk[H];
     dv2 xv[H][3], dg[H][3], eq[H];
     PairFix fx[H][3];
@@ -922,23 +896,13 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
         if (JX) de = aux_d[c];
     }
     constexpr bool PUB = MODE != kSpmvPlain && MODE != kSpmvAdd;
-#ifdef PSK_LAB_DIAGP_NOEPI   // lab probe: no dot epilogue at all (wrong p.Ap)
-    const bool pub = false;
-#else
     const bool pub = PUB && spmv_publishes<MODE>(gs);
-#endif
     const bool drawer = H == 2 || (wave & 1) == 0;   // the wave that draws its slice's ticket
-    // QUAD (H = 2, two-level sums): ONE ticket per workgroup, on the counter of its first slice's group (below)
-    const bool quad = kDiagQuad && H == 2 && pub && gs.grp_log2 >= 0;   // kernel-uniform
-    const int64_t qctr = quad ? gridsum_group_of(grp * TPB, gs.grp_log2) : 0;
-#ifndef PSK_LAB_DIAGP_TFIRST
+    // (drawn after the loads: drawn before them, its return held the loads' consumption back — in-loop SpMV
+    // 0.049 -> 0.060 ms at N = 10M, profiles/r6_diagp_epilogue_ab.txt)
     uint32_t ticket = 0;
-    if (quad) {
-        if (wave == 0 && lane == 0) ticket = gridsum_draw(gridsum_counter(gs, qctr));
-    } else if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0) {
+    if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0)
         ticket = gridsum_draw(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)));
-    }
-#endif
     if (__builtin_amdgcn_readfirstlane(dnv) != 0) {   // uniform: the solve has stopped; tickets handed back
 #pragma unroll
         for (int h = 0; h < H; ++h) {
@@ -951,9 +915,9 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
             if (EQ) __asm__ volatile("" ::"v"(eq[h].x), "v"(eq[h].y));
         }
         __asm__ volatile("" ::"v"(xe), "v"(de));
-        if (quad ? (wave == 0 && lane == 0) : (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0))
-            __hip_atomic_fetch_sub(gridsum_counter(gs, quad ? qctr : gridsum_group_of(tl, gs.grp_log2)), 1u,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pub && tv && drawer && gs.grp_log2 >= 0 && lane == 0)
+            __hip_atomic_fetch_sub(gridsum_counter(gs, gridsum_group_of(tl, gs.grp_log2)), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
         return;
     }
     __shared__ GridSumTile<1> gsl[H == 1 ? TPB : 1];
@@ -1035,34 +999,7 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
         yv[h].y = spmv_row_value<MODE>(has1, s1, e1, a1);
         acc[h] = a0 + a1;   // wave_total's first level
     }
-    if (quad) {
-        // every slice's slot first (no wait of any kind), then the workgroup's ticket through LDS: when it is the
-        // last of its quad (the TPB groups its slices belong to have the same member workgroups, the quad's), wave
-        // q reduces group (first group + q) — the same members, order and bits as one ticket per slice
-        if (tv) {
-            double w[4];
-            diag_pair_totals(acc[0], w[0], w[1]);
-            diag_pair_totals(acc[H - 1], w[2], w[3]);
-            const double s = ((w[0] + w[1]) + w[2]) + w[3];
-            if (lane == 0) gridsum_put(gs.slots + gridsum_slot(gs, tl), s);
-        }
-        __shared__ uint32_t wtk;
-        if (wave == 0 && lane == 0) wtk = ticket;
-        __syncthreads();
-        int64_t base;
-        const int64_t nq = gridsum_members(gs, qctr, base);   // workgroups of the quad
-        if (wtk == (uint32_t)(nq - 1)) {
-            if (wave == 0 && lane == 0) gridsum_reset(gridsum_counter(gs, qctr));
-            const int64_t g = gridsum_group_of(t, gs.grp_log2);   // t unclamped: the group of a missing slice too
-            const int64_t cnt = g < gs.ngroups ? gridsum_members(gs, g, base) : 0;
-            if (cnt > 0) {
-                double r[1];
-                gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
-                if (lane == 0) gridsum_put(gs.gslots + g, r[0]);
-                gridsum_final_wave<1>(gs);
-            }
-        }
-    } else if (pub && tv) {
+    if (pub && tv) {
         double w[2 * H];
 #pragma unroll
         for (int h = 0; h < H; ++h) diag_pair_totals(acc[h], w[2 * h], w[2 * h + 1]);
@@ -1100,10 +1037,6 @@ __global__ __launch_bounds__(kBlock, (H == 2 && MODE != kSpmvPlain && MODE != kS
                 const int64_t g = gridsum_group_of(tl, gs.grp_log2);
                 int64_t base;
                 const int64_t cnt = gridsum_members(gs, g, base);
-#ifdef PSK_LAB_DIAGP_NORED   // lab probe: slots stored, the group's last ticket only resets the counter (wrong p.Ap)
-                if (tk == (uint32_t)(cnt - 1) && lane == 0) gridsum_reset(gridsum_counter(gs, g));
-                tk = 0xffffffffu;
-#endif
                 if (tk == (uint32_t)(cnt - 1)) {
                     double r[1];
                     gridsum_take<1, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, r);
@@ -1693,15 +1626,11 @@ static int sliced_build(psk_csr *A, hipStream_t s, bool force, bool pack, bool u
         wsum += wd[(size_t)t];
         all_pack = all_pack && wd[(size_t)(nt + t)] <= kMaxDelta16;
     }
-    const char *ue = std::getenv("PSK_SPMV_UNIFORM");
-    const bool uniform =
-        all_pack && wmax > 0 && wmax <= kSliceRegs && wmax * nt * 100 <= wsum * 101 && !(ue && std::atoi(ue) == 0);
+    const bool uniform = all_pack && wmax > 0 && wmax <= kSliceRegs && wmax * nt * 100 <= wsum * 101;
     if (uniform)
         for (int64_t t = 0; t < nt; ++t) wd[(size_t)t] = (int32_t)wmax;
-    // compact stream (PSK_SPMV_COMPACT=0: never): uniform, odd width, a 1-bit value index
-    const char *ce = std::getenv("PSK_SPMV_COMPACT");
-    const bool compact = uniform && !dict.empty() && dict.size() <= 2 && (wmax & 1) && wmax <= 15 &&
-                         !(ce && std::atoi(ce) == 0);
+    // compact stream: uniform, odd width, a 1-bit value index
+    const bool compact = uniform && !dict.empty() && dict.size() <= 2 && (wmax & 1) && wmax <= 15;
     std::vector<int64_t> off((size_t)nt + 1), woff((size_t)nt + 1);
     std::vector<int8_t> fmt((size_t)nt);
     off[0] = 0;
@@ -1798,41 +1727,27 @@ __global__ void spmv_empty_dot_kernel(GridSum gs, const int32_t *done) {
     gridsum_mail<1>(gs, z);
 }
 
-// PSK_SPMV_XCD_BANDS=0: tiles in block order (A/B runs); default: XCD-banded (psk_internal.hpp)
-static bool spmv_xcd_bands() {
-    static const bool on = [] {
-        const char *e = std::getenv("PSK_SPMV_XCD_BANDS");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return on;
-}
+// the sliced and diagonal layouts' tiles in XCD bands (psk_internal.hpp; round 3)
+static bool spmv_xcd_bands() { return true; }
 
-// PSK_SPMV_CSR_BANDS=1: the CSR tile kernel on the XCD-banded map too (A/B)
-static bool spmv_csr_bands() {
-    static const bool on = [] {
-        const char *e = std::getenv("PSK_SPMV_CSR_BANDS");
-        return e && std::atoi(e) != 0;
-    }();
-    return on;
-}
+// The CSR tile kernel's tile map (round 6): chunks of kCsrChunk consecutive tiles dealt over the
+// XCDs (tile_map_chunked), so the +-m x lines a tile gathers were fetched through the same L2 by its chunk's
+// neighbours; in the loop at N = 10M 0.1400 -> 0.1380 ms, back to back 0.1342 -> 0.1292 ms (block order: the x
+// line neighbours land on other XCDs; the whole-band map measured 0.145 ms; profiles/r6_csr_tilemap_ab.txt).
+// (-DPSK_CSR_CHUNK=0 builds block order.)
+#ifndef PSK_CSR_CHUNK
+#define PSK_CSR_CHUNK 128
+#endif
+static int64_t spmv_csr_chunk() { return PSK_CSR_CHUNK; }
 
-// the pair-row diagonal kernel: 0 off (spmv_diag_kernel), 1 or 2 half-slices per wave (PSK_DIAG_PAIR)
-static int diag_pair_h() {
-    static const int v = [] {
-        const char *e = std::getenv("PSK_DIAG_PAIR");
-        const int h = e ? std::atoi(e) : 2;
-        return h == 0 || h == 1 ? h : 2;
-    }();
-    return v;
-}
-static int spmv_tpw() {
-    static const int v = [] {
-        const char *e = std::getenv("PSK_SPMV_TPW");
-        const int t = e ? std::atoi(e) : 2;
-        return t >= 1 && t <= 4 ? t : 2;
-    }();
-    return v;
-}
+// the pair-row diagonal kernel's half-slices per wave (round 6: 2 — a wave per slice; 1 measured slower, 0 = the
+// one-row kernel: profiles/r6_diag_pair_ab.txt; -DPSK_DIAG_PAIR=0/1 builds the others)
+#ifndef PSK_DIAG_PAIR
+#define PSK_DIAG_PAIR 2
+#endif
+static int diag_pair_h() { return PSK_DIAG_PAIR; }
+// slices per workgroup of the compact uniform sliced kernel (round 4: 2)
+static int spmv_tpw() { return 2; }
 
 static int64_t spmv_tiles(const psk_csr *A) { return (A->n + A->tile_rows - 1) / A->tile_rows; }
 
@@ -1862,7 +1777,8 @@ int launch_spmv(const psk_csr *A, int mode, const double *x, double *y, const do
     // 0.057 ms); the CSR tile kernel measured 2-3% slower with them (3163^2 and 16384^2), so it keeps
     // block order
     // rev: each XCD walks its band backwards (the PCG loop alternates directions, PSK_K23_BANDS=2)
-    const TileMap tm = tile_map_for(nwg, (sliced || spmv_csr_bands()) && spmv_xcd_bands(), rev != 0);
+    TileMap tm = tile_map_for(nwg, sliced && spmv_xcd_bands(), rev != 0);
+    if (!sliced && spmv_csr_chunk() > 0) tm = tile_map_chunked(nwg, spmv_csr_chunk());
     // compact uniform layout (FD and other 2-value stencils): slices per workgroup,
     // spmv_uniform_multi_kernel (round 4: 2 by default, PSK_SPMV_TPW=1 the one-slice kernel, 3 and 4
     // lab). Two slices per workgroup: in-loop SpMV at N = 10M 0.0657 -> 0.0611 ms, 16384^2 1.60 ->
@@ -2392,12 +2308,7 @@ int psk_spmv_timed(const psk_csr *A, const double *x, double *y, int32_t reps, d
     hipEvent_t e0, e1;
     PSK_HIP(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));   // timing only (runtime.hip)
     PSK_HIP(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
-    // PSK_SPMV_TIMED_MODE=1: the PCG loop's kSpmvDot launch (dot epilogue + gridsum) instead of a
-    // plain y = A x (lab switch: separates the epilogue from the loop context)
-    static const int mode = [] {
-        const char *e = std::getenv("PSK_SPMV_TIMED_MODE");
-        return e && std::atoi(e) == 1 ? (int)kSpmvDot : (int)kSpmvPlain;
-    }();
+    constexpr int mode = kSpmvPlain;
     DevBuf part;
     if (mode == kSpmvDot) PSK_TRY(part.ensure(64));
     double *pp = mode == kSpmvDot ? part.as<double>() : nullptr;
