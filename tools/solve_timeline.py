@@ -61,6 +61,10 @@ def analyze(api_csv, kern_csv, marks_json):
             "last_kernels": [x[2].split("(")[0][-40:] for x in k[-3:]],
             "sync_calls_us": [round((e - s) / 1e3, 1) for s, e, f in syncs],
             "api_calls": len(a),
+            "first_api": [(x[2], round((x[0] - m["t0"]) / 1e3, 1), round((x[1] - x[0]) / 1e3, 1)) for x in a[:8]],
+            "last_api": [(x[2], round((x[0] - m["t0"]) / 1e3, 1), round((x[1] - x[0]) / 1e3, 1)) for x in a[-6:]],
+            "kernels": [(x[2].split("(")[0].replace("void ", "")[-44:], round((x[0] - m["t0"]) / 1e3, 1),
+                         round((x[1] - x[0]) / 1e3, 1)) for x in (k[:5] + k[-4:])],
         })
     by = {}
     for r in rows:
