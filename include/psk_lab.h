@@ -28,6 +28,10 @@ int psk_lab_dispatch_probe(int32_t nwg, int32_t lds_bytes, double usec, int64_t 
 /* Lab: occupiers per XCD (HW_REG_XCC_ID) of the last psk_lab_occupy_begin, counts[8]. */
 int psk_lab_occupy_xcc(int32_t *counts);
 int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled, int32_t *grid);
+/* Lab / tests of the AMG smoother's paired Gauss-Seidel sweeps (round 6, amg.hip gs_pair_kernel): set = 0 runs
+ * every level's sweeps one launch each (the serialized path), 1 pairs them on the levels that qualify, -1
+ * leaves the setting; *levels_on = the levels pairing now, *levels_eligible = the levels that qualify. */
+int psk_lab_amg_gs_pair(psk_prec *M, int32_t set, int32_t *levels_on, int32_t *levels_eligible);
 #ifdef __cplusplus
 }
 #endif

@@ -22,9 +22,20 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 namespace psk {
+
+// A level whose two consecutive Gauss-Seidel sweeps run as one launch (gs_pair_kernel below)
+struct GsPairLevel {
+    bool eligible = false, on = false;
+    int64_t m = 0, H = 0, nbands = 0;
+    int role[5] = {};     // A's stored diagonals in stored order: 0 = d, 1 = -m, 2 = +m, 3 = -1, 4 = +1
+    int ord = -1;         // gs_pair_kernel's ORD: role == gp_role(ord, .)
+    double v[5] = {};
+    DevBuf pub;           // [nbands][3][m] publications of each band's last owned line
+};
 
 struct AmgHierarchy {
     int L = 0, num_iters = 0, nu_pre = 0, nu_post = 0;
@@ -34,6 +45,7 @@ struct AmgHierarchy {
     psk_prec *coarse = nullptr;
     std::vector<DevBuf> x, f, r, t;   // per level (f unused on the finest level: f = v)
     DevBuf scal;                      // [0] = ||v||^2, [1] = flag (as int64), partials after
+    std::vector<GsPairLevel> gp;      // per level
 };
 
 void amg_free(AmgHierarchy *h) {
@@ -42,8 +54,575 @@ void amg_free(AmgHierarchy *h) {
     for (auto &b : h->f) b.release();
     for (auto &b : h->r) b.release();
     for (auto &b : h->t) b.release();
+    for (auto &g : h->gp) g.pub.release();
     h->scal.release();
     delete h;
+}
+
+// ---- two Gauss-Seidel sweeps in one launch (round 6) -------------------------------------------
+// For a level whose operator is a 5-point stencil on an m x H grid with one value per diagonal (A's diagonal
+// layout, its presence masks exactly the grid's; the smoother's triu(A) carries TriFactor::fd5_*), the pair
+//     x1 = x0 + U^-1 (f - A x0),   x2 = x1 + U^-1 (f - A x1)           (ClassicSmoothers.py:31-36, twice)
+// runs as ONE launch after the first residual r = f - A x0 (launch_spmv). The upper solve goes from row n - 1
+// backwards: solve-order line Y = H - 1 - iy, position a = m - 1 - ix; (Y, a) depends on (Y, a - 1) (column
+// i + 1) and (Y - 1, a) (column i + m). A band of 63 lines is one workgroup of three waves, lane j on line
+// Y0 + j, stepping a skewed wavefront (step s: position a = s - j):
+//  * wave 0, the first sweep: dx1 from its own previous step (a - 1) and lane j - 1's previous step (line above)
+//    by a DPP wave shift — no memory on the dependency chain; x1 = x0 + dx1 into an LDS ring of steps. Lane 63
+//    recomputes the next band's first line, which the second sweep's residual needs (its -m neighbour).
+//  * wave 1, the second sweep, trailing wave 0: r2 = f - A x1 from the ring (the row's five entries in A's
+//    stored order from 0.0 with rounded products, absent entries skipped: the SpMV's bits), dx2 by the same
+//    DPP recurrence, x2 = x1 + dx2 stored to x.
+//  * wave 2 polls the band above's publications (dx1, x1, dx2 of its last owned line, sentinel-armed) into
+//    LDS for the lanes 0 of waves 0 and 1.
+//  * wave 3 streams: r, x0 and f into LDS ahead of the sweeps, 16 steps x 64 lines a chunk, and x2 back out
+//    once the second sweep has passed a chunk. A line's 16 steps are 16 consecutive rows, so each load and store
+//    instruction covers four lines' 128 B with 16 lanes each; read straight by the sweep lanes (one row of 64
+//    distinct lines per instruction, ~0.1 us of the CU's address path each) the same traffic held a step to
+//    ~0.8 us (profiles/r6_gs_pair_ab.txt).
+// Every value is the serialized path's: U's off-diagonal sum formed as the factor's current schedule forms it
+// (gp_uacc: the grid / band / levels fma chain, or the sync-free / LDS / partitioned lane partials),
+// (r - acc) / d by IEEE division (the grid kernel's Markstein quotient is the IEEE one), x + dx. Bands are drawn
+// from the U factor's ticket counter (sched_next_block's protocol: a band waits only on the band drawn before
+// it), so the launch needs no co-residency; every wait is bounded and
+// reports through the smoother's error word (ilu_check_error).
+// kGpC: steps per streamed chunk; kGpNB: chunk slots per streamed array; kGpBlk: steps between progress
+// announcements and waits (the band below trails by its publication latency plus up to one of these)
+constexpr int kGpOwn = 63, kGpRing = 32, kGpRW = 66, kGpExt = 256, kGpBlk = 8, kGpC = 16, kGpNB = 3, kGpSR = 65;
+constexpr size_t kGpStage = (size_t)kGpNB * kGpC * kGpSR;   // doubles of one streamed array's slots
+constexpr size_t kGpOffRing = 4 * kGpStage * 8, kGpOffExt = kGpOffRing + (size_t)kGpRing * kGpRW * 16,
+                 kGpOffCtl = kGpOffExt + 3 * (size_t)kGpExt * 8, kGpLds = kGpOffCtl + 8 * 8;
+static_assert(kGpLds <= 160 * 1024, "one workgroup's LDS");
+// the waves' roles: the three compute waves on waves 1..3, the light polling (0) and streaming waves (4) (the
+// five waves of a workgroup share four SIMDs; wave w runs on SIMD w % 4)
+constexpr int kGpW1st = 1, kGpWRes = 2, kGpW2nd = 3, kGpWStream = 4;
+constexpr uint32_t kGpOOB = 0xFFFFFFFFu;   // a buffer offset out of range: loads 0, drops the store
+constexpr uint64_t kGpSentinel = 0x7FF4DEAD0000BEEFull;   // ilu.hip's sentinel: an sNaN payload
+constexpr int64_t kGpMaxSpins = 1ll << 22, kGpDone = INT64_MAX / 4;
+
+struct GsPairArgs {
+    int64_t n, m, H, nbands;
+    double d, a1, am;   // U = triu(A): the diagonal, the +1 and +m values
+    int mfirst;         // U stores its +m entry before its +1 entry
+    int role[5];
+    double v[5];
+    const double *f, *r;   // right-hand side; r = f - A x0
+    double *x;             // x0 in, x2 out
+    double *pub;
+    uint32_t *tick;
+    int32_t *err;
+};
+
+__device__ __forceinline__ double gp_load(const double *p) {
+    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void gp_store(double *p, double v) {
+    __hip_atomic_store(reinterpret_cast<uint64_t *>(p), (uint64_t)__double_as_longlong(v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool gp_sent(double v) { return (uint64_t)__double_as_longlong(v) == kGpSentinel; }
+__device__ __forceinline__ int64_t gp_get(const int64_t *c) {
+    return __hip_atomic_load(c, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void gp_set(int64_t *c, int64_t v) {
+    __hip_atomic_store(c, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wave-uniform: wait until *c >= want; false after the bound (error reported)
+__device__ __forceinline__ bool gp_wait(const int64_t *c, int64_t want, int32_t *err, int code, int64_t band) {
+    int64_t spins = 0;
+    while (!__builtin_amdgcn_readfirstlane((int)(gp_get(c) >= want))) {
+        if (++spins > kGpMaxSpins) {
+            if ((threadIdx.x & 63) == 0) atomicExch(err, (code << 24) | (int)(band & 0xffffff));
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
+    return true;
+}
+// buffer (bounds-checked) loads and stores: every lane issues every one of them with no branch around it, so
+// the compiler's vmcnt waits count exactly the operations in flight (ilu.hip, the grid kernel's note)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t gp_rsrc(const double *p, int64_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<double *>(p), (short)0, (int)(uint32_t)(n * 8), 0x00020000);
+}
+__device__ __forceinline__ double gp_bload(__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+}
+typedef unsigned int gp_u2 __attribute__((ext_vector_type(2)));
+template <int CPOL>   // 0x10: sc1 (agent-scope write-through: the publications), 0: plain
+__device__ __forceinline__ void gp_bstore(__amdgpu_buffer_rsrc_t r, uint32_t off, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(gp_u2, v), r, off, 0, CPOL);
+}
+// lane l <- lane l - 1 (wave_shr:1); lane 0 <- edge
+__device__ __forceinline__ double gp_shr1(double v, double edge) {
+    const int lo = __builtin_amdgcn_update_dpp(__double2loint(edge), __double2loint(v), 0x138, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), 0x138, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// lane l <- lane l + 1 (wave_shl:1); lane 63 <- 0
+__device__ __forceinline__ double gp_shl1(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xF, 0xF, false);
+    return __hiloint2double(hi, lo);
+}
+// U's off-diagonal sum of one row as the serialized schedule forms it: LANES = false, the grid / band / levels
+// kernels' fma chain over the stored order from 0.0; LANES = true, the sync-free / LDS / partitioned kernels'
+// lane partials (entry k's product in lane k, fma(v, x, 0.0)) added by the wave reduction (ilu.hip row_total:
+// with two entries the one sum p0 + p1, the other lanes' zeros adding exactly nothing)
+template <bool LANES, bool MF>
+__device__ __forceinline__ double gp_uacc(const GsPairArgs &g, bool p1, double left, bool pm, double up) {
+    if (LANES) {
+        const double q1 = p1 ? fma(g.a1, left, 0.0) : 0.0, qm = pm ? fma(g.am, up, 0.0) : 0.0;
+        return MF ? qm + q1 : q1 + qm;
+    }
+    double acc = 0.0;
+    if (MF) {
+        acc = pm ? fma(g.am, up, acc) : acc;
+        acc = p1 ? fma(g.a1, left, acc) : acc;
+    } else {
+        acc = p1 ? fma(g.a1, left, acc) : acc;
+        acc = pm ? fma(g.am, up, acc) : acc;
+    }
+    return acc;
+}
+
+#ifdef PSK_GP_PROF   // profile build (scripts/build_variant.sh gpprof -DPSK_GP_PROF): per band, s_memrealtime (100 MHz)
+// at the start, the first sweep's end and the second's end, then s_memtime cycles spent in each wave's waits:
+// ring capacity, the band above's dx1, the first sweep's progress, the band above's dx2; the XCD
+__device__ unsigned long long g_gp_prof[4096 * 16];
+extern "C" int psk_gp_prof_read(unsigned long long *out, int nbands) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gp_prof), sizeof(unsigned long long) * 16 * (size_t)nbands) ==
+                   hipSuccess ? 0 : -1;
+}
+#define GP_PROF(...) __VA_ARGS__
+#else
+#define GP_PROF(...)
+#endif
+// A's stored orders the kernel is built for (role of each stored diagonal): the reference's FD order
+// [d, -m, +m, -1, +1] (FDLaplacian2D) and column order [-m, -1, d, +1, +m] (a sorted CSR)
+__host__ __device__ constexpr int gp_role(int ord, int t) {
+    return ord == 0 ? t : (t == 0 ? 1 : t == 1 ? 3 : t == 2 ? 0 : t == 3 ? 4 : 2);
+}
+template <bool LANES, int ORD, bool MF>
+__global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
+    extern __shared__ __align__(16) unsigned char gsm[];
+    double *st_r = reinterpret_cast<double *>(gsm), *st_x = st_r + kGpStage, *st_f = st_x + kGpStage,
+           *st_o = st_f + kGpStage;   // [slot][step][line], row stride kGpSR
+    // x1 (ring1) and the second sweep's residual r2 (ring2) of step s, lane j at [s % kGpRing][j + 1]
+    double(*ring1)[kGpRW] = reinterpret_cast<double(*)[kGpRW]>(gsm + kGpOffRing);
+    double(*ring2)[kGpRW] = ring1 + kGpRing;
+    double *e1d = reinterpret_cast<double *>(gsm + kGpOffExt), *e1x = e1d + kGpExt, *e2d = e1x + kGpExt;
+    // done through step: [0] first sweep, [1] second; known through position: [2] dx1 and x1, [3] all three;
+    // chunks: [4] loaded through, [5] stored through; [6] the band; [7] residuals done through step
+    int64_t *ctl = reinterpret_cast<int64_t *>(gsm + kGpOffCtl);
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int j = threadIdx.x & 63;
+    const int64_t m = g.m, n = g.n, S = m + kGpOwn, nch = (S + kGpC - 1) / kGpC;
+    auto slot = [](int64_t c, int e, int line) { return ((int)(c % kGpNB) * kGpC + e) * kGpSR + line; };
+    for (;;) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t t = __hip_atomic_fetch_add(g.tick + kSchedTicket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((int64_t)t == g.nbands + (int64_t)gridDim.x - 1)
+                __hip_atomic_store(g.tick + kSchedTicket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ctl[6] = t;
+            ctl[0] = ctl[1] = -1;
+            ctl[2] = ctl[3] = t > 0 ? -1 : kGpDone;
+            ctl[4] = ctl[5] = ctl[7] = -1;
+        }
+        __syncthreads();
+        const int64_t b = ctl[6];
+        if (b >= g.nbands) break;
+        const int64_t Y0 = b * kGpOwn, Y = Y0 + j;
+        double *pb = g.pub + b * 3 * m;
+        bool dead = false;   // a wait ran out (error reported): finish the band without waiting
+        GP_PROF(unsigned long long wcyc[4] = {0, 0, 0, 0};
+                const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+                const unsigned long long c_start = __builtin_amdgcn_s_memtime();)
+        auto wait = [&](const int64_t *c, int64_t want, int code) {
+            GP_PROF(const unsigned long long tw = __builtin_amdgcn_s_memtime();)
+            if (!dead && !gp_wait(c, want, g.err, code, b)) dead = true;
+            GP_PROF(wcyc[(code - 5) & 3] += __builtin_amdgcn_s_memtime() - tw;)
+        };
+        if (wave == kGpW1st) {
+            // ---------------- first sweep: lanes 0..63 (lane 63: the next band's first line)
+            const bool line = Y < g.H;
+            double prev = 0.0;
+            for (int64_t s0 = 0; s0 < S; s0 += kGpBlk) {
+                const int64_t c = s0 / kGpC;
+                if (s0 % kGpC == 0) wait(&ctl[4], c, 10);   // the chunk's r and x0 in LDS
+                if (s0 > 0) {
+                    __builtin_amdgcn_s_waitcnt(0xc07f);   // the ring writes before the announcement
+                    if (j == 0) gp_set(&ctl[0], s0 - 1);
+                }
+                wait(&ctl[1], s0 + kGpBlk - kGpRing, 5);   // ring rows free
+                if (b > 0) wait(&ctl[2], (s0 + kGpBlk - 1 < m - 1) ? s0 + kGpBlk - 1 : m - 1, 6);
+                double rr[kGpBlk], xx[kGpBlk], e1[kGpBlk];
+#pragma unroll
+                for (int k = 0; k < kGpBlk; ++k) {
+                    const int e = (int)((s0 + k) % kGpC);
+                    rr[k] = st_r[slot(c, e, j)];
+                    xx[k] = st_x[slot(c, e, j)];
+                    e1[k] = e1d[(s0 + k) & (kGpExt - 1)];   // dx1 of (Y0 - 1, s): lane 0's line above
+                }
+#pragma unroll
+                for (int k = 0; k < kGpBlk; ++k) {
+                    const int64_t t = s0 + k, a = t - j;
+                    const bool act = line && (uint64_t)a < (uint64_t)m;
+                    const double up = gp_shr1(prev, e1[k]);   // dx1 of (Y - 1, a): lane j - 1, step t - 1
+                    const double acc = gp_uacc<LANES, MF>(g, a > 0, prev, Y > 0, up);
+                    const double dx = (rr[k] - acc) / g.d;
+                    const double x1 = xx[k] + dx;
+                    ring1[t & (kGpRing - 1)][j + 1] = x1;
+                    if (j == kGpOwn - 1 && act) {   // one lane: the band below's line above
+                        gp_store(pb + a, dx);
+                        gp_store(pb + m + a, x1);
+                    }
+                    prev = act ? dx : 0.0;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (j == 0) gp_set(&ctl[0], kGpDone);
+            GP_PROF(if (j == 0 && b < 4096) {
+                g_gp_prof[b * 16 + 0] = t_start;
+                g_gp_prof[b * 16 + 1] = __builtin_amdgcn_s_memrealtime();
+                g_gp_prof[b * 16 + 3] = wcyc[0];
+                g_gp_prof[b * 16 + 4] = wcyc[1];
+                g_gp_prof[b * 16 + 7] = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 7u;
+                g_gp_prof[b * 16 + 8] = __builtin_amdgcn_s_memtime() - c_start;
+            })
+        } else if (wave == kGpWRes) {
+            // ---------------- the second sweep's residual: at step t lane j forms r2 = f - A x1 of its row of step
+            // t - 1 from x1 of steps t - 2, t - 1, t of its own line (ring, then registers) and of lanes j -/+ 1 (DPP)
+            double x1p = 0.0, x1pp = 0.0;
+            for (int64_t s0 = 0; s0 < S; s0 += kGpBlk) {
+                if (s0 > 0) {
+                    __builtin_amdgcn_s_waitcnt(0xc07f);
+                    if (j == 0) gp_set(&ctl[7], s0 - 1);
+                }
+                wait(&ctl[0], (s0 + kGpBlk - 1 < S - 1) ? s0 + kGpBlk - 1 : S - 1, 14);   // ring rows through s0 + 7
+                if (b > 0) wait(&ctl[2], (s0 + kGpBlk - 2 < m - 1) ? s0 + kGpBlk - 2 : m - 1, 15);
+                double xc[kGpBlk], ff[kGpBlk], ex[kGpBlk];
+#pragma unroll
+                for (int k = 0; k < kGpBlk; ++k) {
+                    const int64_t t = s0 + k, tp = t > 0 ? t - 1 : 0;
+                    xc[k] = ring1[t & (kGpRing - 1)][j + 1];
+                    ff[k] = st_f[slot(tp / kGpC, (int)(tp % kGpC), j)];
+                    ex[k] = e1x[(t - 1) & (kGpExt - 1)];   // x1 of (Y0 - 1, t - 1)
+                }
+#pragma unroll
+                for (int k = 0; k < kGpBlk; ++k) {
+                    const int64_t t = s0 + k, ap = t - 1 - j;
+                    const double x1 = xc[k];
+                    // x1 by role (0 d, 1 -m, 2 +m, 3 -1, 4 +1) around (Y, ap)
+                    const double xr[5] = {x1p, gp_shl1(x1), gp_shr1(x1pp, ex[k]), x1, x1pp};
+                    const bool pr[5] = {true, Y < g.H - 1, Y > 0, ap < m - 1, ap > 0};
+                    double sum = 0.0;
+#pragma unroll
+                    for (int q = 0; q < 5; ++q) {   // A's stored order, rounded products, absent entries skipped
+                        const int ro = gp_role(ORD, q);
+                        const double u = sum + g.v[q] * xr[ro];
+                        sum = pr[ro] ? u : sum;
+                    }
+                    ring2[(t - 1) & (kGpRing - 1)][j + 1] = ff[k] - sum;
+                    x1pp = x1p;
+                    x1p = x1;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (j == 0) gp_set(&ctl[7], kGpDone);
+            GP_PROF(if (j == 0 && b < 4096) {
+                g_gp_prof[b * 16 + 10] = __builtin_amdgcn_s_memtime() - c_start;
+                g_gp_prof[b * 16 + 11] = wcyc[1];   // waits on the first sweep
+                g_gp_prof[b * 16 + 12] = wcyc[2];   // waits on the band above's x1
+            })
+        } else if (wave == kGpW2nd) {
+            // ---------------- second sweep: lanes 0..62, x1 and r2 from the rings
+            const bool line = j < kGpOwn && Y < g.H;
+            const int64_t S1 = m + kGpOwn - 1;
+            double prev = 0.0;
+            for (int64_t s0 = 0; s0 < S1; s0 += kGpBlk) {
+                const int64_t c = s0 / kGpC;
+                if (s0 % kGpC == 0) wait(&ctl[5], c - kGpNB, 12);   // the chunk's output slot stored
+                if (s0 > 0) {
+                    __builtin_amdgcn_s_waitcnt(0xc07f);   // the x2 slot writes before the announcement
+                    if (j == 0) gp_set(&ctl[1], s0 - 1);
+                }
+                wait(&ctl[7], (s0 + kGpBlk < S - 1) ? s0 + kGpBlk : S - 1, 7);   // r2 rows through s0 + 7
+                if (b > 0) wait(&ctl[3], (s0 + kGpBlk - 1 < m - 1) ? s0 + kGpBlk - 1 : m - 1, 8);
+                double xv[kGpBlk], rv[kGpBlk], e2[kGpBlk];
+#pragma unroll
+                for (int k = 0; k < kGpBlk; ++k) {
+                    xv[k] = ring1[(s0 + k) & (kGpRing - 1)][j + 1];
+                    rv[k] = ring2[(s0 + k) & (kGpRing - 1)][j + 1];
+                    e2[k] = e2d[(s0 + k) & (kGpExt - 1)];
+                }
+#pragma unroll
+                for (int k = 0; k < kGpBlk; ++k) {
+                    const int64_t s = s0 + k, a = s - j;
+                    const bool act = line && (uint64_t)a < (uint64_t)m;
+                    const double up = gp_shr1(prev, e2[k]);
+                    const double acc = gp_uacc<LANES, MF>(g, a > 0, prev, Y > 0, up);
+                    const double dx = (rv[k] - acc) / g.d;
+                    st_o[slot(c, (int)(s % kGpC), j)] = xv[k] + dx;   // x2
+                    if (j == kGpOwn - 1 && act) gp_store(pb + 2 * m + a, dx);
+                    prev = act ? dx : 0.0;
+                }
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            if (j == 0) gp_set(&ctl[1], kGpDone);
+            GP_PROF(if (j == 0 && b < 4096) {
+                g_gp_prof[b * 16 + 2] = __builtin_amdgcn_s_memrealtime();
+                g_gp_prof[b * 16 + 5] = wcyc[2];
+                g_gp_prof[b * 16 + 6] = wcyc[3];
+                g_gp_prof[b * 16 + 9] = __builtin_amdgcn_s_memtime() - c_start;
+            })
+        } else if (wave == kGpWStream) {
+            // ---------------- streaming: lane l -> line J = 4q + l / 16 of instruction q, step e = l % 16 of the chunk
+            const __amdgpu_buffer_rsrc_t rr = gp_rsrc(g.r, n), rx = gp_rsrc(g.x, n), rf = gp_rsrc(g.f, n);
+            const int e = j & 15;
+            auto off = [&](int64_t c, int J, bool own) {   // byte offset of line J's row at step 16c + e, or OOB
+                const int64_t s = c * kGpC + e, YJ = Y0 + J;
+                const bool ok = YJ < g.H && (uint64_t)(s - J) < (uint64_t)m && (!own || J < kGpOwn);
+                return ok ? (uint32_t)((n - 1 - YJ * m - (s - J)) * 8) : kGpOOB;
+            };
+            int64_t cl = 0, cs = 0, spins = 0;
+            while (cs < nch) {
+                bool moved = false;
+                const int64_t need = (cl - kGpNB + 1) * kGpC;   // the residual wave (behind the first sweep, reading f a
+                                                                // step late) past chunk cl - kGpNB
+                if (cl < nch && __builtin_amdgcn_readfirstlane((int)(gp_get(&ctl[7]) >= need))) {
+                    double vr[16], vx[16], vf[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int J = 4 * q + (j >> 4);
+                        const uint32_t o = off(cl, J, false);
+                        vr[q] = gp_bload(rr, o);
+                        vx[q] = gp_bload(rx, o);
+                        vf[q] = gp_bload(rf, o);
+                    }
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) {
+                        const int J = 4 * q + (j >> 4);
+                        st_r[slot(cl, e, J)] = vr[q];
+                        st_x[slot(cl, e, J)] = vx[q];
+                        st_f[slot(cl, e, J)] = vf[q];
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xc07f);
+                    if (j == 0) gp_set(&ctl[4], cl);
+                    ++cl;
+                    moved = true;
+                }
+                if (cs < cl && __builtin_amdgcn_readfirstlane((int)(gp_get(&ctl[1]) >= cs * kGpC + kGpC - 1))) {
+                    double vo[16];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) vo[q] = st_o[slot(cs, e, 4 * q + (j >> 4))];
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) gp_bstore<0>(rx, off(cs, 4 * q + (j >> 4), true), vo[q]);
+                    if (j == 0) gp_set(&ctl[5], cs);   // the slot's values are in the stores' registers
+                    ++cs;
+                    moved = true;
+                }
+                if (moved) {
+                    spins = 0;
+                } else {
+                    if (++spins > kGpMaxSpins) {
+                        if (j == 0) atomicExch(g.err, (13 << 24) | (int)(b & 0xffffff));
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+        } else if (b > 0) {
+            // ---------------- poller: the band above's dx1 / x1 (cursor c1) and dx2 (cursor c2), 64 positions a chunk
+            const double *pa = g.pub + (b - 1) * 3 * m;
+            int64_t c1 = 0, c2 = 0, k1 = -1, k2 = -1, spins = 0;
+            bool got1 = false, got2 = false;
+            while (c1 < m || c2 < m) {
+                const int64_t w1 = gp_get(&ctl[1]);   // slots of positions <= w1 have been consumed
+                bool moved = false;
+                if (c1 < m && c1 + 63 - kGpExt <= w1) {
+                    const int64_t a = c1 + j;
+                    if (!got1) {
+                        if (a >= m) {
+                            got1 = true;
+                        } else {
+                            const double d1 = gp_load(pa + a), v1 = gp_load(pa + m + a);
+                            if (!gp_sent(d1) && !gp_sent(v1)) {
+                                e1d[a & (kGpExt - 1)] = d1;
+                                e1x[a & (kGpExt - 1)] = v1;
+                                got1 = true;
+                            }
+                        }
+                    }
+                    const uint64_t nr = __ballot(!got1);
+                    const int64_t k = c1 + (nr ? __builtin_ctzll(nr) : 64) - 1;
+                    moved = k > k1;
+                    k1 = k;
+                    if (!nr) {
+                        c1 += 64;
+                        got1 = false;
+                    }
+                }
+                if (c2 < m && c2 + 63 - kGpExt <= w1) {
+                    const int64_t a = c2 + j;
+                    if (!got2) {
+                        if (a >= m) {
+                            got2 = true;
+                        } else {
+                            const double d2 = gp_load(pa + 2 * m + a);
+                            if (!gp_sent(d2)) {
+                                e2d[a & (kGpExt - 1)] = d2;
+                                got2 = true;
+                            }
+                        }
+                    }
+                    const uint64_t nr = __ballot(!got2);
+                    const int64_t k = c2 + (nr ? __builtin_ctzll(nr) : 64) - 1;
+                    moved = moved || k > k2;
+                    k2 = k;
+                    if (!nr) {
+                        c2 += 64;
+                        got2 = false;
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0xc07f);   // LDS writes before the announcements
+                if (j == 0) {
+                    gp_set(&ctl[2], k1 < m - 1 ? k1 : m - 1);
+                    gp_set(&ctl[3], (k1 < k2 ? k1 : k2) < m - 1 ? (k1 < k2 ? k1 : k2) : m - 1);
+                }
+                if (moved) {
+                    spins = 0;
+                } else {
+                    if (++spins > kGpMaxSpins) {
+                        if (j == 0) atomicExch(g.err, (9 << 24) | (int)(b & 0xffffff));
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+            }
+            if (j == 0) {
+                gp_set(&ctl[2], kGpDone);
+                gp_set(&ctl[3], kGpDone);
+            }
+        }
+    }
+}
+
+__global__ void gp_fill_kernel(int64_t n, double *p) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) reinterpret_cast<uint64_t *>(p)[i] = kGpSentinel;
+}
+
+// presence masks of A's diagonal layout == the m x H grid's (roles as GsPairLevel::role)
+struct GpRoles {
+    int role[8];
+};
+__global__ void gp_mask_check_kernel(int64_t n, int64_t m, int K, GpRoles R, const uint8_t *__restrict__ mask,
+                                     int32_t *bad) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t ix = i % m, iy = i / m, H = n / m;
+    uint32_t want = 0;
+    for (int t = 0; t < K; ++t) {
+        const int ro = R.role[t];
+        const bool p = ro == 0 || (ro == 1 && iy > 0) || (ro == 2 && iy < H - 1) || (ro == 3 && ix > 0) ||
+                       (ro == 4 && ix < m - 1);
+        want |= (uint32_t)p << t;
+    }
+    if (mask[i] != want) atomicOr(bad, 1);
+}
+
+// the pair's eligibility (host, at AMG creation): see the comment above gs_pair_kernel
+static int gs_pair_setup(psk_csr *A, psk_prec *S, GsPairLevel &g, hipStream_t s) {
+    g = GsPairLevel();
+    if (!A || !S || S->kind != PSK_PREC_ILU || S->lo.present || !S->up.present || S->up.fd5_m <= 0) return PSK_OK;
+    if (S->gather_in || S->gather_out || !S->up.sched || !S->err || A->comm || !A->dg_mask || A->dg_K != 5) return PSK_OK;
+
+    const TriFactor &U = S->up;
+    const int64_t n = A->n, m = U.fd5_m;
+    if (S->n != n || n % m != 0 || A->ncols != n || n > ((int64_t)1 << 29)) return PSK_OK;   // 32-bit byte offsets
+    auto same = [](double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; };
+    GpRoles R{};
+    int seen = 0;
+    for (int t = 0; t < 5; ++t) {
+        const int64_t d = A->dg_d[t];
+        const int ro = d == 0 ? 0 : d == -m ? 1 : d == m ? 2 : d == -1 ? 3 : d == 1 ? 4 : -1;
+        if (ro < 0 || (seen >> ro) & 1) return PSK_OK;
+        seen |= 1 << ro;
+        R.role[t] = ro;
+        g.role[t] = ro;
+        g.v[t] = A->dg_v[t];
+        if ((ro == 0 && !same(A->dg_v[t], U.fd5_d)) || (ro == 2 && !same(A->dg_v[t], U.fd5_am)) ||
+            (ro == 4 && !same(A->dg_v[t], U.fd5_a1)))
+            return PSK_OK;
+    }
+    if (m < 2) return PSK_OK;
+    for (int o = 0; o < 2 && g.ord < 0; ++o) {
+        bool same_order = true;
+        for (int t = 0; t < 5; ++t) same_order = same_order && g.role[t] == gp_role(o, t);
+        if (same_order) g.ord = o;
+    }
+    if (g.ord < 0) return PSK_OK;   // a stored order the kernel is not built for
+    DevBuf bad;
+    PSK_TRY(bad.ensure(sizeof(int32_t)));
+    PSK_HIP(hipMemsetAsync(bad.p, 0, sizeof(int32_t), s));
+    hipLaunchKernelGGL(gp_mask_check_kernel, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, n, m, 5, R,
+                       A->dg_mask, bad.as<int32_t>());
+    PSK_HIP(hipGetLastError());
+    int32_t hb = 1;
+    PSK_HIP(hipMemcpyAsync(&hb, bad.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    PSK_HIP(hipStreamSynchronize(s));
+    bad.release();
+    if (hb) return PSK_OK;
+    g.m = m;
+    g.H = n / m;
+    g.nbands = (g.H + kGpOwn - 1) / kGpOwn;
+    PSK_TRY(g.pub.ensure((size_t)(3 * m * g.nbands) * sizeof(double)));
+    g.eligible = g.on = true;
+    return PSK_OK;
+}
+
+// x <- two sweeps from x, given r = f - A x
+static int gs_pair_launch(const Context *c, const GsPairLevel &gl, const psk_prec *S, const double *f, const double *r,
+                          double *x, hipStream_t s) {
+    const TriFactor &U = S->up;
+    GsPairArgs g{};
+    g.n = gl.m * gl.H;
+    g.m = gl.m;
+    g.H = gl.H;
+    g.nbands = gl.nbands;
+    g.d = U.fd5_d;
+    g.a1 = U.fd5_a1;
+    g.am = U.fd5_am;
+    g.mfirst = U.fd5_mfirst;
+    for (int t = 0; t < 5; ++t) {
+        g.role[t] = gl.role[t];
+        g.v[t] = gl.v[t];
+    }
+    g.f = f;
+    g.r = r;
+    g.x = x;
+    g.pub = gl.pub.as<double>();
+    g.tick = U.sched;
+    g.err = S->err;
+    const int64_t np = 3 * gl.m * gl.nbands;
+    hipLaunchKernelGGL(gp_fill_kernel, dim3((unsigned)((np + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, np, g.pub);
+    PSK_HIP(hipGetLastError());
+    const int64_t grid = std::min<int64_t>(gl.nbands, (int64_t)c->num_cus);   // one workgroup per CU (its LDS)
+    // the arithmetic of the schedule the serialized sweep would run now (psk_prec_trisolve_schedule may change it)
+    const bool lanes = U.schedule == kSchedSyncFree || U.schedule == kSchedLds || U.schedule == kSchedPart;
+    const void *k = nullptr;
+#define PSK_GP_K(L, O, F) reinterpret_cast<const void *>(&gs_pair_kernel<L, O, F>)
+    if (lanes) k = gl.ord == 0 ? (g.mfirst ? PSK_GP_K(true, 0, true) : PSK_GP_K(true, 0, false))
+                               : (g.mfirst ? PSK_GP_K(true, 1, true) : PSK_GP_K(true, 1, false));
+    else k = gl.ord == 0 ? (g.mfirst ? PSK_GP_K(false, 0, true) : PSK_GP_K(false, 0, false))
+                         : (g.mfirst ? PSK_GP_K(false, 1, true) : PSK_GP_K(false, 1, false));
+#undef PSK_GP_K
+    void *args[] = {&g};
+    PSK_HIP(hipLaunchKernel(k, dim3((unsigned)grid), dim3(320), args, kGpLds, s));
+    PSK_HIP(hipGetLastError());
+    return PSK_OK;
 }
 
 __global__ void amg_add_kernel(int64_t n, double *__restrict__ x, const double *__restrict__ d) {
@@ -109,7 +688,13 @@ static int amg_smooth(const AmgHierarchy *h, const Context *c, int lev, const do
     psk_csr *A = h->A[lev];
     const int64_t n = A->n;
     double *r = h->r[lev].as<double>(), *t = h->t[lev].as<double>();
-    for (int it = 0; it < nu; ++it) {
+    int it = 0;
+    if ((size_t)lev < h->gp.size() && h->gp[lev].on)   // two sweeps per launch (gs_pair_kernel)
+        for (; it + 2 <= nu; it += 2) {
+            PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, s));
+            PSK_TRY(gs_pair_launch(c, h->gp[lev], h->S[lev], f, r, x, s));
+        }
+    for (; it < nu; ++it) {
         PSK_TRY(launch_spmv(A, kSpmvResid, x, r, nullptr, f, nullptr, nullptr, s));
         // (round 3: x += U^-1 r fused into the solve's last gather, profiles/r3_amg_fuse_ab.txt)
         if (h->S[lev] && h->S[lev]->kind == PSK_PREC_ILU) {   // Gauss-Seidel: x += U^-1 r in the last gather
@@ -173,6 +758,19 @@ int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s) {
     // the last cycle's test does not matter: converged or not (failOnMaxiter=False) x is returned
     hipLaunchKernelGGL(amg_copy_if_kernel, vgrid(n), dim3(kBlock), 0, s, n, flag, (int64_t)0, x, out);
     PSK_HIP(hipGetLastError());
+    return PSK_OK;
+}
+
+int amg_gs_pair(psk_prec *M, int set, int *on, int *eligible) {
+    if (!M || M->kind != PSK_PREC_AMG) return fail(PSK_ERR_ARG, "amg_gs_pair: not an AMG preconditioner");
+    int a = 0, e = 0;
+    for (GsPairLevel &g : M->amg->gp) {
+        if (set >= 0) g.on = g.eligible && set != 0;
+        a += g.on;
+        e += g.eligible;
+    }
+    if (on) *on = a;
+    if (eligible) *eligible = e;
     return PSK_OK;
 }
 
@@ -250,6 +848,8 @@ extern "C" int psk_prec_create_amg(int32_t num_levels, psk_csr *const *A, psk_cs
     }
     if (rc == PSK_OK) rc = h->r[L - 1].ensure((size_t)std::max<int64_t>(A[L - 1]->n, 1) * sizeof(double));
     if (rc == PSK_OK) rc = h->scal.ensure((size_t)(2 + kMaxGrid) * sizeof(double));
+    h->gp.resize(L);
+    for (int k = 1; k < L && rc == PSK_OK; ++k) rc = gs_pair_setup(h->A[k], h->S[k], h->gp[k], c->stream);
     if (rc != PSK_OK) {
         amg_free(h);
         return rc;

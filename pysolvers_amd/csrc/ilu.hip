@@ -2527,6 +2527,53 @@ static int check_perm(int64_t n, const int32_t *p, const char *what) {
     return PSK_OK;
 }
 
+// The 5-point grid signature of an upper factor (TriFactor::fd5_*): triu of a 5-point operator on an m x H grid
+// with one value per diagonal. amg.hip fuses two Gauss-Seidel sweeps of such a level into one launch.
+static void detect_fd5(int64_t n, const std::vector<int32_t> &rp, const std::vector<int32_t> &ci,
+                       const std::vector<double> &va, const std::vector<double> &dg, TriFactor &T) {
+    T.fd5_m = 0;
+    if (n < 4 || dg.empty() || rp[1] - rp[0] != 2) return;
+    const int64_t m = std::max(ci[rp[0]], ci[rp[0] + 1]);
+    if (m < 2 || n % m != 0 || n / m < 2) return;
+    auto same = [](double a, double b) { return std::memcmp(&a, &b, sizeof(double)) == 0; };
+    const double d = dg[0];
+    double a1 = 0.0, am = 0.0;
+    bool h1 = false, hm = false;
+    int mfirst = -1;
+    for (int64_t i = 0; i < n; ++i) {
+        if (!same(dg[i], d)) return;
+        const bool e1 = i % m != m - 1, em = i + m < n;
+        const int32_t a = rp[i], e = rp[i + 1];
+        if (e - a != (int)e1 + (int)em) return;
+        bool s1 = false, sm = false;
+        for (int32_t k = a; k < e; ++k) {
+            const int64_t c = ci[k];
+            if (e1 && !s1 && c == i + 1) {
+                s1 = true;
+                if (!h1) a1 = va[k], h1 = true;
+                else if (!same(va[k], a1)) return;
+            } else if (em && !sm && c == i + m) {
+                sm = true;
+                if (!hm) am = va[k], hm = true;
+                else if (!same(va[k], am)) return;
+            } else {
+                return;
+            }
+        }
+        if (e1 && em) {
+            const int f = ci[a] == i + m;
+            if (mfirst < 0) mfirst = f;
+            else if (f != mfirst) return;
+        }
+    }
+    if (!h1 || !hm || mfirst < 0) return;
+    T.fd5_m = m;
+    T.fd5_d = d;
+    T.fd5_a1 = a1;
+    T.fd5_am = am;
+    T.fd5_mfirst = mfirst;
+}
+
 // Build, schedule and upload one factor.
 static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int32_t *ci, const double *va, bool upper,
                        bool unit, const std::vector<int32_t> &nat, TriFactor &T) {
@@ -2535,6 +2582,7 @@ static int make_factor(const Context *c, int64_t n, const int32_t *rp, const int
     F.upper = upper;
     std::vector<double> ova, dg;
     PSK_TRY(split_factor(n, rp, ci, va, !upper, unit, F.rp, F.ci, ova, dg));
+    if (upper && !unit && nat.empty()) detect_fd5(n, F.rp, F.ci, ova, dg, T);
     std::vector<int32_t> order, lev;
     int64_t nlev = 0;
     level_order(F, order, lev, nlev);

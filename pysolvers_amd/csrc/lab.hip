@@ -158,3 +158,15 @@ extern "C" int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_
     return PSK_OK;
 }
 
+extern "C" int psk_lab_amg_gs_pair(psk_prec *M, int32_t set, int32_t *levels_on, int32_t *levels_eligible) {
+    using namespace psk;
+    if (set < -1 || set > 1) return fail(PSK_ERR_ARG, "psk_lab_amg_gs_pair: set must be -1, 0 or 1");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    PSK_HIP(hipStreamSynchronize(c->stream));   // queued applies keep the setting they were enqueued with
+    int on = 0, el = 0;
+    PSK_TRY(amg_gs_pair(M, set, &on, &el));
+    if (levels_on) *levels_on = on;
+    if (levels_eligible) *levels_eligible = el;
+    return PSK_OK;
+}

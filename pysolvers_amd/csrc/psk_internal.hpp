@@ -301,6 +301,12 @@ struct TriFactor {
     int lv_W = 0, lv_R = 0, lv_KM = 0;
     double est_syncfree_us = 0.0, est_band_us = 0.0, est_lds_us = -1.0, est_grid_us = -1.0, est_part_us = -1.0;
     double est_level_us = -1.0;
+    // 5-point grid signature of an upper factor (make_factor; amg.hip's paired Gauss-Seidel sweeps): n = fd5_m * H,
+    // row i's off-diagonal entries exactly columns i + 1 (i % m < m - 1) and i + m (i + m < n), values fd5_a1 / fd5_am,
+    // every diagonal fd5_d, fd5_mfirst = the +m entry stored before the +1 entry. fd5_m = 0: no such signature.
+    int64_t fd5_m = 0;
+    double fd5_d = 0.0, fd5_a1 = 0.0, fd5_am = 0.0;
+    int fd5_mfirst = 0;
     void release();
 };
 }  // namespace psk
@@ -908,7 +914,9 @@ int fd2d_fill(psk_csr *A, int64_t m, double a, double b, int64_t row_begin, int6
 // generic preconditioner apply (device pointers, out must not alias v): identity copy, Jacobi, ILU
 int prec_apply_dev(const psk_prec *M, int64_t n, const double *v, double *out, hipStream_t s);
 int ilu_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
-int ilu_apply_add(const psk_prec *M, const double *v, double *x, hipStream_t s);   // x += M^-1 v
+int ilu_apply_add(const psk_prec *M, const double *v, double *x, hipStream_t s);
+// AMG paired Gauss-Seidel sweeps (amg.hip; the lab library's switch): set -1 / 0 / 1, counts out
+int amg_gs_pair(psk_prec *M, int set, int *on, int *eligible);   // x += M^-1 v
 int ilu_check_error(const psk_prec *M, hipStream_t s);
 int amg_apply(const psk_prec *M, const double *v, double *out, hipStream_t s);
 void amg_free(AmgHierarchy *h);
