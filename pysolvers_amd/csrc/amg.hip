@@ -90,7 +90,7 @@ void amg_free(AmgHierarchy *h) {
 // announcements and waits (the band below trails by its publication latency plus up to one of these)
 constexpr int kGpOwn = 63, kGpRing = 32, kGpRW = 66, kGpExt = 256, kGpBlk = 8, kGpC = 16, kGpNB = 3, kGpSR = 65;
 constexpr size_t kGpStage = (size_t)kGpNB * kGpC * kGpSR;   // doubles of one streamed array's slots
-constexpr size_t kGpOffRing = 4 * kGpStage * 8, kGpOffExt = kGpOffRing + (size_t)kGpRing * kGpRW * 16,
+constexpr size_t kGpOffRing = 4 * kGpStage * 8, kGpOffExt = kGpOffRing + (size_t)kGpRing * kGpRW * 24,
                  kGpOffCtl = kGpOffExt + 3 * (size_t)kGpExt * 8, kGpLds = kGpOffCtl + 8 * 8;
 static_assert(kGpLds <= 160 * 1024, "one workgroup's LDS");
 // the waves' roles: the three compute waves on waves 1..3, the light polling (0) and streaming waves (4) (the
@@ -168,22 +168,20 @@ __device__ __forceinline__ double gp_shl1(double v) {
 // U's off-diagonal sum of one row as the serialized schedule forms it: LANES = false, the grid / band / levels
 // kernels' fma chain over the stored order from 0.0; LANES = true, the sync-free / LDS / partitioned kernels'
 // lane partials (entry k's product in lane k, fma(v, x, 0.0)) added by the wave reduction (ilu.hip row_total:
-// with two entries the one sum p0 + p1, the other lanes' zeros adding exactly nothing)
+// with two entries the one sum p0 + p1, the other lanes' zeros adding exactly nothing). An absent entry comes
+// with coefficient 0: fma(0, v, acc) = acc for a finite v and an acc that is not -0 (acc starts at +0, and an
+// fma onto +0 never rounds to -0), exactly the grid kernel's padding entries; the selects stay off the chain.
 template <bool LANES, bool MF>
-__device__ __forceinline__ double gp_uacc(const GsPairArgs &g, bool p1, double left, bool pm, double up) {
+__device__ __forceinline__ double gp_uacc(double c1, double left, double cm, double up) {
     if (LANES) {
-        const double q1 = p1 ? fma(g.a1, left, 0.0) : 0.0, qm = pm ? fma(g.am, up, 0.0) : 0.0;
+        const double q1 = fma(c1, left, 0.0), qm = fma(cm, up, 0.0);
         return MF ? qm + q1 : q1 + qm;
     }
-    double acc = 0.0;
-    if (MF) {
-        acc = pm ? fma(g.am, up, acc) : acc;
-        acc = p1 ? fma(g.a1, left, acc) : acc;
-    } else {
-        acc = p1 ? fma(g.a1, left, acc) : acc;
-        acc = pm ? fma(g.am, up, acc) : acc;
-    }
-    return acc;
+    return MF ? fma(c1, left, fma(cm, up, 0.0)) : fma(cm, up, fma(c1, left, 0.0));
+}
+// relaxed look at a progress word (the fast path of a block's waits; an acquire fence follows)
+__device__ __forceinline__ int gp_ready(const int64_t *c, int64_t want) {
+    return (int)(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= want);   // combined with &
 }
 
 #ifdef PSK_GP_PROF   // profile build (scripts/build_variant.sh gpprof -DPSK_GP_PROF): per band, s_memrealtime (100 MHz)
@@ -208,9 +206,10 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
     extern __shared__ __align__(16) unsigned char gsm[];
     double *st_r = reinterpret_cast<double *>(gsm), *st_x = st_r + kGpStage, *st_f = st_x + kGpStage,
            *st_o = st_f + kGpStage;   // [slot][step][line], row stride kGpSR
-    // x1 (ring1) and the second sweep's residual r2 (ring2) of step s, lane j at [s % kGpRing][j + 1]
+    // ring1: x1 of step s, lane j at [s % kGpRing][j + 1] (first sweep -> residual wave); ring2: (x1, r2) of step s
+    // at [s % kGpRing][2 (j + 1)] (residual wave -> second sweep)
     double(*ring1)[kGpRW] = reinterpret_cast<double(*)[kGpRW]>(gsm + kGpOffRing);
-    double(*ring2)[kGpRW] = ring1 + kGpRing;
+    double(*ring2)[2 * kGpRW] = reinterpret_cast<double(*)[2 * kGpRW]>(gsm + kGpOffRing + (size_t)kGpRing * kGpRW * 8);
     double *e1d = reinterpret_cast<double *>(gsm + kGpOffExt), *e1x = e1d + kGpExt, *e2d = e1x + kGpExt;
     // done through step: [0] first sweep, [1] second; known through position: [2] dx1 and x1, [3] all three;
     // chunks: [4] loaded through, [5] stored through; [6] the band; [7] residuals done through step
@@ -230,7 +229,8 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
             ctl[2] = ctl[3] = t > 0 ? -1 : kGpDone;
             ctl[4] = ctl[5] = ctl[7] = -1;
         }
-        __syncthreads();
+        for (int i = threadIdx.x; i < 3 * kGpExt; i += blockDim.x) e1d[i] = 0.0;   // finite values at positions
+        __syncthreads();                                                           // no band publishes
         const int64_t b = ctl[6];
         if (b >= g.nbands) break;
         const int64_t Y0 = b * kGpOwn, Y = Y0 + j;
@@ -250,13 +250,20 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
             double prev = 0.0;
             for (int64_t s0 = 0; s0 < S; s0 += kGpBlk) {
                 const int64_t c = s0 / kGpC;
-                if (s0 % kGpC == 0) wait(&ctl[4], c, 10);   // the chunk's r and x0 in LDS
                 if (s0 > 0) {
                     __builtin_amdgcn_s_waitcnt(0xc07f);   // the ring writes before the announcement
                     if (j == 0) gp_set(&ctl[0], s0 - 1);
                 }
-                wait(&ctl[1], s0 + kGpBlk - kGpRing, 5);   // ring rows free
-                if (b > 0) wait(&ctl[2], (s0 + kGpBlk - 1 < m - 1) ? s0 + kGpBlk - 1 : m - 1, 6);
+                {   // the chunk's r and x0 in LDS, ring1 rows free (read by the residual wave), the band above's dx1
+                    const int64_t w2 = b > 0 ? ((s0 + kGpBlk - 1 < m - 1) ? s0 + kGpBlk - 1 : m - 1) : -1;
+                    if (!__builtin_amdgcn_readfirstlane((int)(gp_ready(&ctl[4], c) & gp_ready(&ctl[7], s0 + kGpBlk - kGpRing) &
+                                                              gp_ready(&ctl[2], w2)))) {
+                        wait(&ctl[4], c, 10);
+                        wait(&ctl[7], s0 + kGpBlk - kGpRing, 5);
+                        wait(&ctl[2], w2, 6);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
                 double rr[kGpBlk], xx[kGpBlk], e1[kGpBlk];
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
@@ -270,7 +277,7 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                     const int64_t t = s0 + k, a = t - j;
                     const bool act = line && (uint64_t)a < (uint64_t)m;
                     const double up = gp_shr1(prev, e1[k]);   // dx1 of (Y - 1, a): lane j - 1, step t - 1
-                    const double acc = gp_uacc<LANES, MF>(g, a > 0, prev, Y > 0, up);
+                    const double acc = gp_uacc<LANES, MF>(a > 0 ? g.a1 : 0.0, prev, Y > 0 ? g.am : 0.0, up);
                     const double dx = (rr[k] - acc) / g.d;
                     const double x1 = xx[k] + dx;
                     ring1[t & (kGpRing - 1)][j + 1] = x1;
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                         gp_store(pb + a, dx);
                         gp_store(pb + m + a, x1);
                     }
-                    prev = act ? dx : 0.0;
+                    prev = dx;   // finite on every lane (absent neighbours carry coefficient 0)
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -300,8 +307,17 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                     __builtin_amdgcn_s_waitcnt(0xc07f);
                     if (j == 0) gp_set(&ctl[7], s0 - 1);
                 }
-                wait(&ctl[0], (s0 + kGpBlk - 1 < S - 1) ? s0 + kGpBlk - 1 : S - 1, 14);   // ring rows through s0 + 7
-                if (b > 0) wait(&ctl[2], (s0 + kGpBlk - 2 < m - 1) ? s0 + kGpBlk - 2 : m - 1, 15);
+                {   // ring1 rows through s0 + 7, ring2 rows free, the band above's x1
+                    const int64_t w0 = (s0 + kGpBlk - 1 < S - 1) ? s0 + kGpBlk - 1 : S - 1;
+                    const int64_t w2 = b > 0 ? ((s0 + kGpBlk - 2 < m - 1) ? s0 + kGpBlk - 2 : m - 1) : -1;
+                    if (!__builtin_amdgcn_readfirstlane((int)(gp_ready(&ctl[0], w0) & gp_ready(&ctl[1], s0 + kGpBlk - kGpRing) &
+                                                              gp_ready(&ctl[2], w2)))) {
+                        wait(&ctl[0], w0, 14);
+                        wait(&ctl[1], s0 + kGpBlk - kGpRing, 16);
+                        wait(&ctl[2], w2, 15);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
                 double xc[kGpBlk], ff[kGpBlk], ex[kGpBlk];
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
@@ -324,7 +340,10 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                         const double u = sum + g.v[q] * xr[ro];
                         sum = pr[ro] ? u : sum;
                     }
-                    ring2[(t - 1) & (kGpRing - 1)][j + 1] = ff[k] - sum;
+                    dv2 w;
+                    w.x = x1p;
+                    w.y = ff[k] - sum;
+                    *reinterpret_cast<dv2 *>(&ring2[(t - 1) & (kGpRing - 1)][2 * (j + 1)]) = w;
                     x1pp = x1p;
                     x1p = x1;
                 }
@@ -343,18 +362,27 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
             double prev = 0.0;
             for (int64_t s0 = 0; s0 < S1; s0 += kGpBlk) {
                 const int64_t c = s0 / kGpC;
-                if (s0 % kGpC == 0) wait(&ctl[5], c - kGpNB, 12);   // the chunk's output slot stored
                 if (s0 > 0) {
                     __builtin_amdgcn_s_waitcnt(0xc07f);   // the x2 slot writes before the announcement
                     if (j == 0) gp_set(&ctl[1], s0 - 1);
                 }
-                wait(&ctl[7], (s0 + kGpBlk < S - 1) ? s0 + kGpBlk : S - 1, 7);   // r2 rows through s0 + 7
-                if (b > 0) wait(&ctl[3], (s0 + kGpBlk - 1 < m - 1) ? s0 + kGpBlk - 1 : m - 1, 8);
+                {   // the chunk's output slot stored, r2 rows through s0 + 7, the band above's dx2
+                    const int64_t w7 = (s0 + kGpBlk < S - 1) ? s0 + kGpBlk : S - 1;
+                    const int64_t w3 = b > 0 ? ((s0 + kGpBlk - 1 < m - 1) ? s0 + kGpBlk - 1 : m - 1) : -1;
+                    if (!__builtin_amdgcn_readfirstlane((int)(gp_ready(&ctl[5], c - kGpNB) & gp_ready(&ctl[7], w7) &
+                                                              gp_ready(&ctl[3], w3)))) {
+                        wait(&ctl[5], c - kGpNB, 12);
+                        wait(&ctl[7], w7, 7);
+                        wait(&ctl[3], w3, 8);
+                    }
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+                }
                 double xv[kGpBlk], rv[kGpBlk], e2[kGpBlk];
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
-                    xv[k] = ring1[(s0 + k) & (kGpRing - 1)][j + 1];
-                    rv[k] = ring2[(s0 + k) & (kGpRing - 1)][j + 1];
+                    const dv2 w = *reinterpret_cast<const dv2 *>(&ring2[(s0 + k) & (kGpRing - 1)][2 * (j + 1)]);
+                    xv[k] = w.x;
+                    rv[k] = w.y;
                     e2[k] = e2d[(s0 + k) & (kGpExt - 1)];
                 }
 #pragma unroll
@@ -362,11 +390,11 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                     const int64_t s = s0 + k, a = s - j;
                     const bool act = line && (uint64_t)a < (uint64_t)m;
                     const double up = gp_shr1(prev, e2[k]);
-                    const double acc = gp_uacc<LANES, MF>(g, a > 0, prev, Y > 0, up);
+                    const double acc = gp_uacc<LANES, MF>(a > 0 ? g.a1 : 0.0, prev, Y > 0 ? g.am : 0.0, up);
                     const double dx = (rv[k] - acc) / g.d;
                     st_o[slot(c, (int)(s % kGpC), j)] = xv[k] + dx;   // x2
                     if (j == kGpOwn - 1 && act) gp_store(pb + 2 * m + a, dx);
-                    prev = act ? dx : 0.0;
+                    prev = dx;   // finite on every lane (absent neighbours carry coefficient 0)
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);

@@ -45,6 +45,12 @@ def main():
            "sweep2_end_after_sweep1_us_median": float(np.median(e1 - e0)),
            "wait_cycles_median": {k: float(np.median(r[:, i])) for k, i in
                                   (("ring", 3), ("ext_dx1", 4), ("sweep1_progress", 5), ("ext_dx2", 6))},
+           "residual_wave": {"busy_frac_median": float(np.median(1 - (r[:, 11] + r[:, 12]) / np.maximum(r[:, 10], 1))),
+                             "wait_sweep1_cycles_median": float(np.median(r[:, 11])),
+                             "wait_ext_cycles_median": float(np.median(r[:, 12]))},
+           "sweep1_busy_frac_band0": float(1 - (r[0, 3] + r[0, 4]) / max(r[0, 8], 1)),
+           "sweep2_busy_frac_band0": float(1 - (r[0, 5] + r[0, 6]) / max(r[0, 9], 1)),
+           "residual_busy_frac_band0": float(1 - (r[0, 11] + r[0, 12]) / max(r[0, 10], 1)),
            "xcd_counts": np.bincount(r[:, 7].astype(int), minlength=8).tolist(),
            "band0_raw": [int(x) for x in r[0]], "band1_raw": [int(x) for x in r[1]],
            "first_bands": [[round(float(x), 1) for x in (start[i], e0[i], e1[i])] for i in range(min(6, nb))]}
