@@ -1013,11 +1013,13 @@ def pcg_amg(N, m=8192, levels=5, cycles=2, iters=6, repeats=3):
     S = M._S[-1].operator
     fine_levels = S.device_info()["levels_u"]
     sweep_ms = timed(lambda: S.apply(v))
+    # one serialized sweep (the smoother's own apply); inside the V-cycle the fine level's sweeps run two per launch
+    # (amg.hip gs_pair_kernel: nuPre = nuPost = 2 -> one launch each), bit-identical to these
     out["fine_gs_sweep"] = {"bound": "latency (dependency chain)", "ms": sweep_ms, "dep_levels": fine_levels,
                             "us_per_level": sweep_ms * 1e3 / max(1, fine_levels),
                             "schedule": S.schedule("U")["schedule"],
                             "sweeps_per_apply": cycles * 4,
-                            "share_of_apply": cycles * 4 * sweep_ms / out["amg_apply_ms"]}
+                            "in_apply": "two sweeps per launch (gs_pair_kernel), %d launches" % (cycles * 2)}
     co = M._coarse
     v0 = psk.DeviceVector.from_numpy(np.random.default_rng(0).standard_normal(M.levels()[0]))
     out["coarse_solve_ms"] = timed(lambda: co.apply(v0))
