@@ -21,7 +21,7 @@ import statistics
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
-    ap.add_argument("--kernel", default="spmv_diag_kernel<1,")
+    ap.add_argument("--kernel", default="spmv_diagp_kernel<1,")
     ap.add_argument("--workgroups", type=int, default=19541)
     ap.add_argument("--settle", type=int, default=1999)
     ap.add_argument("--warmup", type=int, default=5)
