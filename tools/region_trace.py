@@ -22,7 +22,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--kernel", default="spmv_diagp_kernel<1,")
-    ap.add_argument("--workgroups", type=int, default=19541)
+    ap.add_argument("--workgroups", type=int, default=9771)
     ap.add_argument("--settle", type=int, default=1999)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--steps", type=int, default=20)
