@@ -116,6 +116,22 @@ def test_configs4_amg_hierarchy_and_pcg_fd8192(psk):
     yu, yv, yuv = M.applyRight(u), M.applyRight(v), M.applyRight(u + 2.0 * v)
     assert np.all(np.isfinite(yuv))
     assert np.linalg.norm(yuv - (yu + 2.0 * yv)) <= 1e-10 * np.linalg.norm(yuv)
+    # round 6: the fine level's Gauss-Seidel sweeps run two per launch (amg.hip gs_pair_kernel); at full size the
+    # apply and the PCG+AMG trajectory equal the serialized sweeps' bit for bit (psk_lab_amg_gs_pair switches)
+    import ctypes
+    from pysolvers_amd import _native as N
+    lab = N.load_lab()
+    on, el = ctypes.c_int32(), ctypes.c_int32()
+    N.check(lab.psk_lab_amg_gs_pair(M.device_handle, -1, ctypes.byref(on), ctypes.byref(el)), "gs_pair")
+    assert (on.value, el.value) == (1, 1)
+    N.check(lab.psk_lab_amg_gs_pair(M.device_handle, 0, None, None), "gs_pair off")
+    try:
+        yu_serial = M.applyRight(u)
+        st_serial = s.solve(dA, b)
+    finally:
+        N.check(lab.psk_lab_amg_gs_pair(M.device_handle, 1, None, None), "gs_pair on")
+    assert np.array_equal(yu_serial, yu)
+    assert np.array_equal(st_serial.info["hist"], st1.info["hist"]) and np.array_equal(st_serial.soln(), st1.soln())
 
 
 def test_configs4_amg_apply_and_pcg_vs_oracle_fd2048(psk):
