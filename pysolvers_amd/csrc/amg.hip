@@ -159,6 +159,10 @@ __device__ __forceinline__ double gp_shr1(double v, double edge) {
     const int hi = __builtin_amdgcn_update_dpp(__double2hiint(edge), __double2hiint(v), 0x138, 0xF, 0xF, false);
     return __hiloint2double(hi, lo);
 }
+// lane l's value, to every lane (two readlanes: no branch, no exec change)
+__device__ __forceinline__ double gp_lane(double v, int l) {
+    return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 // lane l <- lane l + 1 (wave_shl:1); lane 63 <- 0
 __device__ __forceinline__ double gp_shl1(double v) {
     const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, false);
@@ -246,7 +250,6 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
         };
         if (wave == kGpW1st) {
             // ---------------- first sweep: lanes 0..63 (lane 63: the next band's first line)
-            const bool line = Y < g.H;
             double prev = 0.0;
             for (int64_t s0 = 0; s0 < S; s0 += kGpBlk) {
                 const int64_t c = s0 / kGpC;
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
-                double rr[kGpBlk], xx[kGpBlk], e1[kGpBlk];
+                double rr[kGpBlk], xx[kGpBlk], e1[kGpBlk], pdx[kGpBlk];
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
                     const int e = (int)((s0 + k) % kGpC);
@@ -275,17 +278,25 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
                     const int64_t t = s0 + k, a = t - j;
-                    const bool act = line && (uint64_t)a < (uint64_t)m;
                     const double up = gp_shr1(prev, e1[k]);   // dx1 of (Y - 1, a): lane j - 1, step t - 1
                     const double acc = gp_uacc<LANES, MF>(a > 0 ? g.a1 : 0.0, prev, Y > 0 ? g.am : 0.0, up);
                     const double dx = (rr[k] - acc) / g.d;
                     const double x1 = xx[k] + dx;
                     ring1[t & (kGpRing - 1)][j + 1] = x1;
-                    if (j == kGpOwn - 1 && act) {   // one lane: the band below's line above
-                        gp_store(pb + a, dx);
-                        gp_store(pb + m + a, x1);
-                    }
+                    pdx[k] = gp_lane(dx, kGpOwn - 1);
                     prev = dx;   // finite on every lane (absent neighbours carry coefficient 0)
+                }
+                // the band below's line above: lane 62's dx1 and x1 of the block's steps, stored by lanes 0..7 once per
+                // block (one store each instead of a one-lane branch per step)
+                {
+                    double pd = pdx[0];
+#pragma unroll
+                    for (int k = 1; k < kGpBlk; ++k) pd = j == k ? pdx[k] : pd;
+                    const int64_t a = s0 + j - (kGpOwn - 1);
+                    if (j < kGpBlk && Y0 + kGpOwn - 1 < g.H && (uint64_t)a < (uint64_t)m) {
+                        gp_store(pb + a, pd);
+                        gp_store(pb + m + a, ring1[(s0 + j) & (kGpRing - 1)][kGpOwn]);
+                    }
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);
@@ -357,7 +368,6 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
             })
         } else if (wave == kGpW2nd) {
             // ---------------- second sweep: lanes 0..62, x1 and r2 from the rings
-            const bool line = j < kGpOwn && Y < g.H;
             const int64_t S1 = m + kGpOwn - 1;
             double prev = 0.0;
             for (int64_t s0 = 0; s0 < S1; s0 += kGpBlk) {
@@ -377,7 +387,7 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
                     }
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
-                double xv[kGpBlk], rv[kGpBlk], e2[kGpBlk];
+                double xv[kGpBlk], rv[kGpBlk], e2[kGpBlk], pdx[kGpBlk];
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
                     const dv2 w = *reinterpret_cast<const dv2 *>(&ring2[(s0 + k) & (kGpRing - 1)][2 * (j + 1)]);
@@ -388,13 +398,19 @@ __global__ __launch_bounds__(320) void gs_pair_kernel(GsPairArgs g) {
 #pragma unroll
                 for (int k = 0; k < kGpBlk; ++k) {
                     const int64_t s = s0 + k, a = s - j;
-                    const bool act = line && (uint64_t)a < (uint64_t)m;
                     const double up = gp_shr1(prev, e2[k]);
                     const double acc = gp_uacc<LANES, MF>(a > 0 ? g.a1 : 0.0, prev, Y > 0 ? g.am : 0.0, up);
                     const double dx = (rv[k] - acc) / g.d;
                     st_o[slot(c, (int)(s % kGpC), j)] = xv[k] + dx;   // x2
-                    if (j == kGpOwn - 1 && act) gp_store(pb + 2 * m + a, dx);
+                    pdx[k] = gp_lane(dx, kGpOwn - 1);
                     prev = dx;   // finite on every lane (absent neighbours carry coefficient 0)
+                }
+                {   // lane 62's dx2 of the block's steps, stored by lanes 0..7
+                    double pd = pdx[0];
+#pragma unroll
+                    for (int k = 1; k < kGpBlk; ++k) pd = j == k ? pdx[k] : pd;
+                    const int64_t a = s0 + j - (kGpOwn - 1);
+                    if (j < kGpBlk && Y0 + kGpOwn - 1 < g.H && (uint64_t)a < (uint64_t)m) gp_store(pb + 2 * m + a, pd);
                 }
             }
             __builtin_amdgcn_s_waitcnt(0xc07f);
