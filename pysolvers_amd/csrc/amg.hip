@@ -65,21 +65,21 @@ void amg_free(AmgHierarchy *h) {
 //     x1 = x0 + U^-1 (f - A x0),   x2 = x1 + U^-1 (f - A x1)           (ClassicSmoothers.py:31-36, twice)
 // runs as ONE launch after the first residual r = f - A x0 (launch_spmv). The upper solve goes from row n - 1
 // backwards: solve-order line Y = H - 1 - iy, position a = m - 1 - ix; (Y, a) depends on (Y, a - 1) (column
-// i + 1) and (Y - 1, a) (column i + m). A band of 63 lines is one workgroup of three waves, lane j on line
-// Y0 + j, stepping a skewed wavefront (step s: position a = s - j):
-//  * wave 0, the first sweep: dx1 from its own previous step (a - 1) and lane j - 1's previous step (line above)
-//    by a DPP wave shift — no memory on the dependency chain; x1 = x0 + dx1 into an LDS ring of steps. Lane 63
-//    recomputes the next band's first line, which the second sweep's residual needs (its -m neighbour).
-//  * wave 1, the second sweep, trailing wave 0: r2 = f - A x1 from the ring (the row's five entries in A's
-//    stored order from 0.0 with rounded products, absent entries skipped: the SpMV's bits), dx2 by the same
-//    DPP recurrence, x2 = x1 + dx2 stored to x.
-//  * wave 2 polls the band above's publications (dx1, x1, dx2 of its last owned line, sentinel-armed) into
-//    LDS for the lanes 0 of waves 0 and 1.
-//  * wave 3 streams: r, x0 and f into LDS ahead of the sweeps, 16 steps x 64 lines a chunk, and x2 back out
+// i + 1) and (Y - 1, a) (column i + m). A band of 63 lines is one workgroup of five waves (one per CU: its LDS),
+// lane j on line Y0 + j, stepping a skewed wavefront (step s: position a = s - j):
+//  * first sweep (kGpW1st): dx1 from its own previous step (a - 1) and lane j - 1's previous step (line above) by a
+//    DPP wave shift — no memory on the dependency chain; x1 = x0 + dx1 into ring1. Lane 63 recomputes the next
+//    band's first line, which the second sweep's residual needs (its -m neighbour).
+//  * residual (kGpWRes): at step t, r2 = f - A x1 of the lane's row of step t - 1, from x1 of three steps of its own
+//    line and of lanes j -/+ 1 (DPP), the row's five entries in A's stored order from 0.0 with rounded products,
+//    absent entries skipped (the SpMV's bits); (x1, r2) into ring2.
+//  * second sweep (kGpW2nd): dx2 by the same DPP recurrence on r2, x2 = x1 + dx2 into an output slot.
+//  * stream (kGpWStream): r, x0 and f into LDS ahead of the sweeps, 16 steps x 64 lines a chunk, and x2 back out
 //    once the second sweep has passed a chunk. A line's 16 steps are 16 consecutive rows, so each load and store
 //    instruction covers four lines' 128 B with 16 lanes each; read straight by the sweep lanes (one row of 64
-//    distinct lines per instruction, ~0.1 us of the CU's address path each) the same traffic held a step to
-//    ~0.8 us (profiles/r6_gs_pair_ab.txt).
+//    distinct lines per instruction) the same traffic held a step to ~0.8 us.
+//  * poller (wave 0): the band above's publications (dx1, x1, dx2 of its last owned line, sentinel-armed, stored
+//    once per 8-step block) into LDS for the lanes 0 of the other waves.
 // Every value is the serialized path's: U's off-diagonal sum formed as the factor's current schedule forms it
 // (gp_uacc: the grid / band / levels fma chain, or the sync-free / LDS / partitioned lane partials),
 // (r - acc) / d by IEEE division (the grid kernel's Markstein quotient is the IEEE one), x + dx. Bands are drawn
