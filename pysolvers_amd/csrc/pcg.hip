@@ -95,9 +95,17 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     int64_t n, double *__restrict__ r, const double *__restrict__ b, const double *__restrict__ Ap,
     const double *__restrict__ dinv, double ds, const double *__restrict__ pap, int nparts, GridSum gs, PcgState *st,
     const double *__restrict__ udr, int64_t k, TileMap tm) {
-    if (st->done) return;
+    // the done flag, p.Ap and udr[k] loaded together (one scalar round trip, not three in a chain): every
+    // address is valid whatever the flag says, and the asm keeps the loads above the branch (round 6: +0.5-1.8%
+    // PCG it/s at N = 10M, profiles/r6_prologue_ab.txt)
+    const double udk = udr[k];
+    const int32_t dn = st->done;
+    const double pap0 = pap[0];
+    __asm__ volatile("" ::"s"(dn), "s"(pap0), "s"(udk));
+    if (dn) return;
+    double pTAp = pap0;                                      // np.dot(p, Ap)  :113 (K1's grid sum; rank_sum)
+    for (int q = 1; q < nparts; ++q) pTAp += pap[q];
     __shared__ double sh[kWaves];
-    const double pTAp = rank_sum(pap, nparts, 1, 0);         // np.dot(p, Ap)  :113 (K1's grid sum)
     if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
@@ -106,7 +114,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         }
         return;
     }
-    const double alpha = udr[k] / pTAp;                      // :118
+    const double alpha = udk / pTAp;                         // :118
     // K3 (x update) runs iff this K2 did: it tests `live`, written by the previous kernel, never its
     // own done flag, which its first workgroup may set while later ones are still starting
     if (blockIdx.x == 0 && threadIdx.x == 0) st->live = k;
@@ -154,7 +162,18 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     double ds, const double *__restrict__ pap, const double *__restrict__ rrur, int nparts, PcgState *st,
     double *__restrict__ udr, double *__restrict__ hist, double *__restrict__ alphas, int64_t k, int64_t maxiter,
     int fail_on_maxiter, int64_t tile_base, TileMap tm) {
-    if (st->live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
+    // every solver scalar loaded together with the live flag (one scalar round trip; see K2)
+    const double udk = udr[k];
+    const int64_t live = st->live;
+    const double tauNB = st->tauNormB, pap0 = pap[0], rr0 = rrur[0], ur0 = rrur[1];
+    __asm__ volatile("" ::"s"(live), "s"(pap0), "s"(rr0), "s"(ur0), "s"(udk), "s"(tauNB));
+    if (live != k) return;   // K2 returned (stopped earlier, or breakdown at :114)
+    double pTAp = pap0, rr = rr0, ur = ur0;   // rank_sum's order
+    for (int q = 1; q < nparts; ++q) {
+        pTAp += pap[q];
+        rr += rrur[2 * q];
+        ur += rrur[2 * q + 1];
+    }
     // tile_base: a sharded solve launches the tiles holding the rows its neighbours need first (the
     // halo exchange then overlaps the rest); tile 0 alone writes the solver state. tm: XCD bands
     // over the launch's tiles (see K2)
@@ -165,9 +184,8 @@ __global__ __launch_bounds__(kBlock) void pcg_direction_kernel(
     double *pnext = pr.b[(k + 1) % kPcgDefer];
     const int q = pcg_pending(k);
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, pcur, rank_sum(pap, nparts, 1, 0), rank_sum(rrur, nparts, 2, 0),
-                               rank_sum(rrur, nparts, 2, 1), st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta, tile, &pr, alphas))
+    if (!pcg_direction_scalars(n, x, pcur, pTAp, rr, ur, udk, tauNB, st, udr, hist, k, maxiter, fail_on_maxiter,
+                               alpha, beta, tile, &pr, alphas))
         return;
     const bool flush = q == kPcgDefer - 1 || k == maxiter - 1;
     const bool x0 = k < kPcgDefer;   // no flush yet: x is the implicit x0 = 0 (never loaded)
@@ -301,8 +319,8 @@ __global__ __launch_bounds__(kBlock) void pcg_gen_direction_kernel(
     double *__restrict__ udr, double *__restrict__ hist, int64_t k, int64_t maxiter, int fail_on_maxiter) {
     if (st->live != k) return;
     double alpha, beta;
-    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, st, udr, hist, k, maxiter, fail_on_maxiter, alpha,
-                               beta, blockIdx.x))
+    if (!pcg_direction_scalars(n, x, p, *pap, rrur[0], *ur_gen, udr[k], st->tauNormB, st, udr, hist, k, maxiter,
+                               fail_on_maxiter, alpha, beta, blockIdx.x))
         return;
     const int64_t i = (int64_t)blockIdx.x * kVecTile + 2 * threadIdx.x;
     for (int64_t j = i; j < i + 2 && j < n; ++j) {

@@ -111,18 +111,18 @@ __device__ __forceinline__ double pcg_catch_up(double xj, const PRing *pr, int q
 // solve stopped at this iteration; x (which K3 owns) is then still advanced over the tile.
 // pr != nullptr: the q = pcg_pending(k) deferred x updates are applied first.
 __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, const double *__restrict__ p,
-                                             double pTAp, double rr, double ur, PcgState *st,
-                                             double *__restrict__ udr, double *__restrict__ hist, int64_t k,
+                                             double pTAp, double rr, double ur, double udk, double tauNB,
+                                             PcgState *st, double *__restrict__ udr, double *__restrict__ hist, int64_t k,
                                              int64_t maxiter, int fail_on_maxiter, double &alpha, double &beta,
                                              int64_t tile, const PRing *pr = nullptr,
                                              const double *__restrict__ alphas = nullptr) {
-    alpha = udr[k] / pTAp;                                   // :118
+    alpha = udk / pTAp;                                      // :118 (udk = udr[k])
     const double normR = sqrt(rr);                           // self.norm(r)  :125
     if (tile == 0 && threadIdx.x == 0) {
         hist[k] = normR;                                     // reportIter  :126
         st->last_hist = normR;
     }
-    if (normR <= st->tauNormB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131
+    if (normR <= tauNB || (!fail_on_maxiter && k == maxiter - 1)) {   // :129-131 (tauNB = st->tauNormB)
         const int64_t i = tile * kVecTile + 2 * threadIdx.x;
         // deferred updates (pr): before the first flush (k < kPcgDefer) x is still the implicit x0 = 0
         const bool x0 = pr && k < kPcgDefer;
@@ -139,7 +139,7 @@ __device__ inline bool pcg_direction_scalars(int64_t n, double *__restrict__ x, 
         }
         return false;
     }
-    beta = ur / udr[k];                                      // :134-135
+    beta = ur / udk;                                         // :134-135
     if (tile == 0 && threadIdx.x == 0) udr[k + 1] = ur;   // :136
     return true;
 }
