@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     if (dn) return;
     double pTAp = pap0;                                      // np.dot(p, Ap)  :113 (K1's grid sum; rank_sum)
     for (int q = 1; q < nparts; ++q) pTAp += pap[q];
-    __shared__ double sh[kWaves];
+    __shared__ double sh[2 * kWaves];
     if (pTAp == 0.0) {                                       // :114-115 handleBreakdown(k, ...)
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             st->brk_kind = 2;
@@ -122,9 +122,11 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     // written through the same XCD's L2; the grid sums are published by tile (order-independent)
     const int64_t tile = tile_of_block(tm);
     const int64_t i = tile * kVecTile + 2 * threadIdx.x;
+    const bool pair = i + 1 < n;
     uint32_t ticket = 0;   // gridsum ticket, drawn by thread 0 once its loads are issued
     double rr = 0.0, ur = 0.0;
-    if (i + 1 < n) {
+    if (pair) {
+        // (issued after the done test: issued before it, K2 measured 1-5% slower, profiles/r6_k2_early_sum2_ab.txt)
         const dv2 ro = FIRST ? ld2nt(b + i) : ld2(r + i), a = ld2nt(Ap + i);
         dv2 d{ds, ds};
         if (JAC == 1) d = ld2(dinv + i);
@@ -150,7 +152,8 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
         rr = rn * rn;
         ur = u0 * rn;
     }
-    const double v[2] = {block_sum(rr, sh), block_sum(ur, sh)};
+    block_sum2(rr, ur, sh);   // both sums in one barrier pair (same bits as two block_sums; round 6: +0.3%)
+    const double v[2] = {rr, ur};
     gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
 }
 

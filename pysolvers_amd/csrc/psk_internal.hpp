@@ -376,6 +376,31 @@ __device__ __forceinline__ double block_sum(double v, double *sh) {
     return r;
 }
 
+// block_sum of two values at once: each gets exactly block_sum's butterflies and wave-order sum (the same bits as
+// two calls), with one barrier pair instead of two and the two butterflies interleaved. `sh` holds 2 * kWaves doubles.
+__device__ __forceinline__ void block_sum2(double &a, double &b, double *sh) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        a += __shfl_xor(a, o, 64);
+        b += __shfl_xor(b, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) {
+        sh[2 * w] = a;
+        sh[2 * w + 1] = b;
+    }
+    __syncthreads();
+    double ra = sh[0], rb = sh[1];
+#pragma unroll
+    for (int i = 1; i < kWaves; ++i) {
+        ra += sh[2 * i];
+        rb += sh[2 * i + 1];
+    }
+    a = ra;
+    b = rb;
+}
+
 // Sum over the ranks of a gathered [nparts][W] array, component c, in rank order: every rank of a
 // sharded solve gets the same bits from its allgather'd copy (nparts == 1: the value itself).
 __device__ __forceinline__ double rank_sum(const double *g, int nparts, int W, int c) {
