@@ -269,7 +269,8 @@ def mvmult(A, x):
     """IterativeLinearSolver.py:94-106, on the device for sparse (and DeviceCSR) A. A dense ndarray A
     (the reference's `np.dot(A, x)`, :105-106, a BLAS dgemv) goes through CSR here: its row sums run in
     stored order, which rounds differently from dgemv's blocked order by a few ulps — dense-A results
-    match the reference to rounding, not bit for bit (parity unpinned for that case)."""
+    match the reference to rounding, not bit for bit (pinned by the reference's own dense PCG/GMRES runs,
+    tests/golden/make_dense.py, at the solver cases' bars)."""
     if isinstance(A, DeviceCSR) or sp.issparse(A):
         return spmv(A, x)
     return spmv(sp.csr_matrix(np.asarray(A, dtype=np.float64)), x)

@@ -77,3 +77,9 @@ def direct_manifest():
     """DefaultDirect / Newton-with-default-solver fixtures (tests/golden/make_direct.py)."""
     with open(os.path.join(GOLDEN, "manifest_direct.json")) as f:
         return json.load(f)
+
+
+def dense_cases():
+    """Dense-ndarray-A solver fixtures (tests/golden/make_dense.py: the reference's np.dot path)."""
+    with open(os.path.join(GOLDEN, "manifest_dense.json")) as f:
+        return json.load(f)["cases"]

@@ -20,8 +20,8 @@ import numpy as np
 import pytest
 import scipy.sparse as sp
 
-from conftest import (case_precond, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type, restarted_cases,
-                      solver_cases)
+from conftest import (case_precond, dense_cases, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type,
+                      restarted_cases, solver_cases)
 
 pytestmark = pytest.mark.gpu
 
@@ -163,6 +163,22 @@ def test_solver_matches_reference(psk, case):
     ctl = _ctl(maxiter=case["maxiter"], tau=case["tau"], failOnMaxiter=bool(case["fail_on_maxiter"]))
     pt = product_prec_type(psk, case_precond(case))
     factory = psk.PCG if case["kind"] == "pcg" else psk.GMRES
+    st = factory(control=ctl, precond=pt).makeSolver().solve(A, d["b"])
+    _check_against_golden(st, d, case)
+
+
+@pytest.mark.parametrize("case", dense_cases(), ids=lambda c: c["file"][:-4])
+def test_dense_solver_matches_reference(psk, case):
+    """A dense ndarray A (the reference's np.dot, IterativeLinearSolver.py:105-106 — a BLAS dgemv) runs on the
+    device as CSR with stored-order row sums: the reference's own dense runs (tests/golden/make_dense.py) pin it
+    with the solver cases' bars — identical iteration counts, residual history and solution within 1e-10 (or 10x
+    the reference's own 1-ulp sensitivity)."""
+    d = load_golden(case["file"])
+    ctl = _ctl(maxiter=case["maxiter"], tau=case["tau"], failOnMaxiter=bool(case["fail_on_maxiter"]))
+    pt = product_prec_type(psk, case_precond(case))
+    factory = psk.PCG if case["kind"] == "pcg" else psk.GMRES
+    A = d["A"]
+    assert isinstance(A, np.ndarray)
     st = factory(control=ctl, precond=pt).makeSolver().solve(A, d["b"])
     _check_against_golden(st, d, case)
 

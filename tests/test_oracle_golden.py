@@ -11,8 +11,8 @@ import hashlib
 import numpy as np
 import pytest
 
-from conftest import (case_precond, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type, restarted_cases,
-                      solver_cases)
+from conftest import (case_precond, dense_cases, golden_matrix, load_golden, manifest, oracle_prec, product_prec_type,
+                      restarted_cases, solver_cases)
 from oracle import fdlap, krylov, native
 
 
@@ -177,3 +177,21 @@ def test_direct_singular_fixture_is_spsolve():
             x = spla.spsolve(sp.csr_matrix(np.array(case["dense"])), np.array(case["b"]))
         assert case["success"] and bool(np.all(np.isnan(x))) == case["soln_all_nan"]
         assert sorted({type(i.message).__name__ for i in w}) == case["warnings"]
+
+
+@pytest.mark.parametrize("case", dense_cases(), ids=lambda c: c["file"][:-4])
+def test_oracle_dense_solvers_match_reference(case):
+    """A dense ndarray A (IterativeLinearSolver.py:105-106, np.dot): the oracle's A @ x path against the
+    reference's run (make_dense.py asserted bit-identity in the build container; here to 1e-10)."""
+    d = load_golden(case["file"])
+    A, b = d["A"], d["b"]
+    assert isinstance(A, np.ndarray) and A.ndim == 2
+    assert np.allclose(A @ d["x_exact"], b, rtol=1e-14, atol=1e-14 * np.abs(b).max())
+    prec = oracle_prec(A, case_precond(case))
+    fn = krylov.pcg if case["kind"] == "pcg" else krylov.gmres
+    st = fn(A, b, maxiter=case["maxiter"], tau=case["tau"], fail_on_maxiter=bool(case["fail_on_maxiter"]),
+            precond=prec)
+    assert st["iters"] == case["iters"] and bool(st["success"]) == case["success"]
+    assert len(st["hist"]) == len(d["hist"])
+    np.testing.assert_allclose(st["hist"], d["hist"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(st["soln"], d["soln"], rtol=1e-9, atol=1e-12 * np.abs(d["soln"]).max())
