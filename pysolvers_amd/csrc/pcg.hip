@@ -154,7 +154,36 @@ __global__ __launch_bounds__(kBlock) void pcg_update_kernel(
     }
     block_sum2(rr, ur, sh);   // both sums in one barrier pair (same bits as two block_sums; round 6: +0.3%)
     const double v[2] = {rr, ur};
-    gridsum_publish_tile<2>(gs, v, sh, ticket, tile);
+    // wave 0 alone publishes the tile and, holding its group's last ticket, reduces the group and takes part in the
+    // final stage in the wave forms (gridsum_take<2, 64>, gridsum_final_wave): no barrier after the totals (round 6:
+    // +0.3-0.7% PCG it/s at N = 10M, profiles/r6_k2_wpub_ab.txt; the group and final sums run in the wave order)
+    if (threadIdx.x >= 64) return;
+    const bool lane0 = threadIdx.x == 0;
+    if (gs.grp_log2 < 0) {
+        if (lane0) {
+            gridsum_put(gs.gslots + tile * 2, v[0]);
+            gridsum_put(gs.gslots + tile * 2 + 1, v[1]);
+        }
+        gridsum_final_wave<2>(gs);
+        return;
+    }
+    if (lane0) {
+        gridsum_put(gs.slots + gridsum_slot(gs, tile) * 2, v[0]);
+        gridsum_put(gs.slots + gridsum_slot(gs, tile) * 2 + 1, v[1]);
+    }
+    const uint32_t tk = __builtin_amdgcn_readfirstlane(ticket);
+    const int64_t g = gridsum_group_of(tile, gs.grp_log2);
+    int64_t base;
+    const int64_t cnt = gridsum_members(gs, g, base);
+    if (tk != (uint32_t)(cnt - 1)) return;
+    double gr[2];
+    gridsum_take<2, 64>(gs.slots, g << gs.grp_log2, cnt, gs.err, nullptr, gr);
+    if (lane0) {
+        gridsum_reset(gridsum_counter(gs, g));
+        gridsum_put(gs.gslots + g * 2, gr[0]);
+        gridsum_put(gs.gslots + g * 2 + 1, gr[1]);
+    }
+    gridsum_final_wave<2>(gs);
 }
 
 // ---- K3: x += alpha p (deferred, above), convergence test, beta, p = u + beta p (one-shot, as K2) --
