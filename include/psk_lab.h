@@ -32,6 +32,12 @@ int psk_lab_trisolve_workers(const psk_prec *M, int32_t which, int32_t *enrolled
  * every level's sweeps one launch each (the serialized path), 1 pairs them on the levels that qualify, -1
  * leaves the setting; *levels_on = the levels pairing now, *levels_eligible = the levels that qualify. */
 int psk_lab_amg_gs_pair(psk_prec *M, int32_t set, int32_t *levels_on, int32_t *levels_eligible);
+/* Lab (round 6): back-to-back SpMV launches (dot = 0: plain y = A x; 1: the PCG loop's kSpmvDot launch) that cycle
+ * through nbuf (x, y) device buffer pairs, one warm launch per pair first, then reps timed launches between two
+ * events; *avg_ms = the mean launch. nbuf = 1 is psk_spmv_timed; nbuf > 1 with more bytes than the Infinity Cache
+ * holds prices the launch without a cache-resident x (tools/mall_probe.py). */
+int psk_lab_spmv_rotate(const psk_csr *A, const double *const *xs, double *const *ys, int32_t nbuf, int32_t reps,
+                        int32_t dot, double *avg_ms);
 #ifdef __cplusplus
 }
 #endif

@@ -170,3 +170,36 @@ extern "C" int psk_lab_amg_gs_pair(psk_prec *M, int32_t set, int32_t *levels_on,
     if (levels_eligible) *levels_eligible = el;
     return PSK_OK;
 }
+
+extern "C" int psk_lab_spmv_rotate(const psk_csr *A, const double *const *xs, double *const *ys, int32_t nbuf,
+                                   int32_t reps, int32_t dot, double *avg_ms) {
+    using namespace psk;
+    if (!A || !xs || !ys || nbuf < 1 || reps < 1 || !avg_ms) return fail(PSK_ERR_ARG, "psk_lab_spmv_rotate: bad arguments");
+    if (A->comm) return fail(PSK_ERR_UNSUPPORTED, "psk_lab_spmv_rotate: sharded matrix");
+    for (int32_t i = 0; i < nbuf; ++i)
+        if (!xs[i] || !ys[i]) return fail(PSK_ERR_ARG, "psk_lab_spmv_rotate: NULL buffer");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    hipEvent_t e0, e1;
+    PSK_HIP(hipEventCreateWithFlags(&e0, hipEventDisableSystemFence));
+    PSK_HIP(hipEventCreateWithFlags(&e1, hipEventDisableSystemFence));
+    const int mode = dot ? kSpmvDot : kSpmvPlain;
+    DevBuf part;
+    int rc = part.ensure(64);
+    double *pp = dot ? part.as<double>() : nullptr;
+    for (int32_t i = 0; i < nbuf && rc == PSK_OK; ++i)   // warm: every pair once
+        rc = launch_spmv(A, mode, xs[i], ys[i], nullptr, nullptr, pp, nullptr, c->stream);
+    if (rc == PSK_OK && hipEventRecord(e0, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
+    for (int32_t r = 0; r < reps && rc == PSK_OK; ++r)
+        rc = launch_spmv(A, mode, xs[r % nbuf], ys[r % nbuf], nullptr, nullptr, pp, nullptr, c->stream);
+    if (rc == PSK_OK && hipEventRecord(e1, c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "event record");
+    float ms = 0.f;
+    if (rc == PSK_OK && hipEventSynchronize(e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event sync");
+    if (rc == PSK_OK && hipEventElapsedTime(&ms, e0, e1) != hipSuccess) rc = fail(PSK_ERR_HIP, "event time");
+    (void)hipStreamSynchronize(c->stream);   // before `part` is freed
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    part.release();
+    if (rc == PSK_OK) *avg_ms = (double)ms / reps;
+    return rc;
+}
