@@ -38,6 +38,11 @@ int psk_lab_amg_gs_pair(psk_prec *M, int32_t set, int32_t *levels_on, int32_t *l
  * holds prices the launch without a cache-resident x (tools/mall_probe.py). */
 int psk_lab_spmv_rotate(const psk_csr *A, const double *const *xs, double *const *ys, int32_t nbuf, int32_t reps,
                         int32_t dot, double *avg_ms);
+/* Lab (round 6): the SpMV launch's own time (dispatch-recorded events) when each launch follows a streaming write
+ * kernel (scratch = src, 16-B accesses): target 0 = no writer, 1 = the writer writes the SpMV's x (as K3 writes the
+ * p the next SpMV gathers), 2 = it writes `scratch` (another buffer of n doubles). reps <= 256. */
+int psk_lab_spmv_after_write(const psk_csr *A, double *x, double *y, const double *src, double *scratch,
+                             int32_t target, int32_t reps, int32_t dot, double *avg_ms);
 #ifdef __cplusplus
 }
 #endif

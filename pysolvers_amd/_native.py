@@ -117,6 +117,7 @@ LAB_SIGNATURES = {
     "psk_lab_trisolve_workers": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "psk_lab_amg_gs_pair": (ctypes.c_int, [P, I32, ctypes.POINTER(I32), ctypes.POINTER(I32)]),
     "psk_lab_spmv_rotate": (ctypes.c_int, [P, ctypes.POINTER(P), ctypes.POINTER(P), I32, I32, I32, ctypes.POINTER(F64)]),
+    "psk_lab_spmv_after_write": (ctypes.c_int, [P, P, P, P, P, I32, I32, I32, ctypes.POINTER(F64)]),
 }
 _lab = None
 

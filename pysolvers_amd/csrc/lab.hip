@@ -171,6 +171,17 @@ extern "C" int psk_lab_amg_gs_pair(psk_prec *M, int32_t set, int32_t *levels_on,
     return PSK_OK;
 }
 
+// the probe's writer: dst = src with 16-B accesses (the shape of K3 writing p_{k+1}, which the next SpMV gathers)
+__global__ __launch_bounds__(256) void lab_copy_kernel(int64_t n, const double *__restrict__ src, double *__restrict__ dst) {
+    const int64_t i = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 2;
+    if (i + 1 < n) {
+        const double2 v = *reinterpret_cast<const double2 *>(src + i);
+        *reinterpret_cast<double2 *>(dst + i) = v;
+    } else if (i < n) {
+        dst[i] = src[i];
+    }
+}
+
 extern "C" int psk_lab_spmv_rotate(const psk_csr *A, const double *const *xs, double *const *ys, int32_t nbuf,
                                    int32_t reps, int32_t dot, double *avg_ms) {
     using namespace psk;
@@ -201,5 +212,51 @@ extern "C" int psk_lab_spmv_rotate(const psk_csr *A, const double *const *xs, do
     (void)hipEventDestroy(e1);
     part.release();
     if (rc == PSK_OK) *avg_ms = (double)ms / reps;
+    return rc;
+}
+
+extern "C" int psk_lab_spmv_after_write(const psk_csr *A, double *x, double *y, const double *src, double *scratch,
+                                        int32_t target, int32_t reps, int32_t dot, double *avg_ms) {
+    using namespace psk;
+    if (!A || !x || !y || !src || !scratch || reps < 1 || reps > 256 || !avg_ms)
+        return fail(PSK_ERR_ARG, "psk_lab_spmv_after_write: bad arguments");
+    if (A->comm || A->ncols != A->n) return fail(PSK_ERR_UNSUPPORTED, "psk_lab_spmv_after_write: square unsharded only");
+    Context *c;
+    PSK_TRY(ctx(&c));
+    std::vector<hipEvent_t> ea((size_t)reps), eb((size_t)reps);
+    for (int32_t r = 0; r < reps; ++r) {
+        PSK_HIP(hipEventCreateWithFlags(&ea[(size_t)r], hipEventDisableSystemFence));
+        PSK_HIP(hipEventCreateWithFlags(&eb[(size_t)r], hipEventDisableSystemFence));
+    }
+    const int mode = dot ? kSpmvDot : kSpmvPlain;
+    DevBuf part;
+    int rc = part.ensure(64);
+    double *pp = dot ? part.as<double>() : nullptr;
+    const int64_t n = A->n;
+    const unsigned g = (unsigned)((n + 511) / 512);
+    double *dst = target == 1 ? x : scratch;   // 1: the writer writes the SpMV's x (as K3 writes p); 2: another buffer
+    rc = launch_spmv(A, mode, x, y, nullptr, nullptr, pp, nullptr, c->stream);   // warm
+    for (int32_t r = 0; r < reps && rc == PSK_OK; ++r) {
+        if (target > 0) {
+            hipLaunchKernelGGL(lab_copy_kernel, dim3(g), dim3(256), 0, c->stream, n, src, dst);
+            if (hipGetLastError() != hipSuccess) rc = fail(PSK_ERR_HIP, "lab copy");
+        }
+        if (rc == PSK_OK)
+            rc = launch_spmv(A, mode, x, y, nullptr, nullptr, pp, nullptr, c->stream, ea[(size_t)r], eb[(size_t)r]);
+    }
+    double tot = 0.0;
+    if (rc == PSK_OK && hipStreamSynchronize(c->stream) != hipSuccess) rc = fail(PSK_ERR_HIP, "sync");
+    for (int32_t r = 0; r < reps && rc == PSK_OK; ++r) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, ea[(size_t)r], eb[(size_t)r]) != hipSuccess) rc = fail(PSK_ERR_HIP, "event time");
+        tot += ms;
+    }
+    (void)hipStreamSynchronize(c->stream);
+    for (int32_t r = 0; r < reps; ++r) {
+        (void)hipEventDestroy(ea[(size_t)r]);
+        (void)hipEventDestroy(eb[(size_t)r]);
+    }
+    part.release();
+    if (rc == PSK_OK) *avg_ms = tot / reps;
     return rc;
 }

@@ -7,6 +7,9 @@ just written while ~650 MB stream per iteration. This times back-to-back launche
 pairs: nbuf = 1 is the batch; at nbuf >= 2 the x of a launch was last read nbuf launches earlier, with
 nbuf * 160 MB streamed in between.
 
+A second probe times the SpMV launch alone (dispatch-recorded events) when every launch follows a streaming write of
+n doubles: into nothing, into the SpMV's own x (as K3 writes the p the next SpMV gathers), or into another buffer.
+
     python tools/mall_probe.py [m] [reps]
 """
 import ctypes
@@ -48,6 +51,20 @@ def main(m=3163, reps=120):
                 vals.append(ms.value)
             key = "%s_nbuf%d" % ("dot" if dot else "plain", nbuf)
             out[key] = {"avg_ms": vals, "frac_of_8TBps": [17 * n / (v * 1e-3) / 8e12 for v in vals]}
+            print(key, " ".join("%.4f" % v for v in vals), flush=True)
+    # each SpMV after a streaming write kernel (16-B copy of n doubles): none / into the SpMV's x / into another buffer
+    src, scr = bufs[6][1], bufs[7][1]
+    x, y = bufs[0]
+    for dot in (0, 1):
+        for target, tname in ((0, "none"), (1, "x"), (2, "other")):
+            vals = []
+            for _ in range(3):
+                ms = ctypes.c_double()
+                N.check(lab.psk_lab_spmv_after_write(A, x, y, src, scr, target, min(reps, 200), dot, ctypes.byref(ms)),
+                        "after_write")
+                vals.append(ms.value)
+            key = "%s_after_write_%s" % ("dot" if dot else "plain", tname)
+            out[key] = {"avg_ms": vals}
             print(key, " ".join("%.4f" % v for v in vals), flush=True)
     print(json.dumps(out))
 
